@@ -1,0 +1,272 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Gkeys/s of the MI355X-native 4-way LSD radix sort (BASELINE.json metric
+"Gkeys/s sorted (32-bit keys+values) at 1/2/4/8 MI355X; % HBM roofline").
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload config3]
+
+A step = one full sort of one batch of synthetic input resident in HBM:
+* N = 1: BASELINE configs[2] — 256M (2^28) uniform u32 keys + u32 values (iota),
+  local_shuffle=true, bit_count 32, one RadixSortKernel.dispatch() per step.  Every step sorts a
+  different pre-generated batch (sorting already-sorted data would be a different workload).
+* N > 1 (torch.distributed.run, one process per GPU, RCCL): BASELINE configs[4] shape with
+  2^28 keys+values per rank (2^31 at 8 GPUs): stable top-byte partition -> histogram all_gather
+  -> RCCL all_to_all of keys and values over xGMI -> local LSD sort.  Weak scaling.
+
+Rank 0 prints ONE JSON line.  `value` = keys sorted by all ranks / max-over-ranks wall time.
+`roofline` is for the dominant kernel (the scatter pass): algorithmic bytes per launch
+(n x (4 + 4) read + n x (4 + 4) write for keys+values) / its average launch duration, timed with
+HIP events on the launch stream inside the timed region.  `cpu_baseline` times the reference's
+CPU path (`Uint32Array.prototype.sort((a, b) => a - b)`, example/index.ts:85) in Node on a bounded
+sample on this host (rank 0, N = 1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "webgpu-radix-sort_amd"))
+
+HBM_PEAK_GBS = 8000.0    # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+WORKLOADS = {
+    "config3": dict(n=1 << 28, values=True, local_shuffle=True, check_order=False, kind="u32",
+                    seed=3, desc="256M Uint32 keys + Uint32 values, local_shuffle=true, 1xMI355X"),
+    "config2": dict(n=1 << 26, values=False, local_shuffle=False, check_order=False, kind="u32",
+                    seed=2, desc="64M Uint32 keys-only, bit_count=32, workgroup_size 16x16"),
+    "config4": dict(n=1 << 28, values=True, local_shuffle=False, check_order=True,
+                    kind="f32_nearly", seed=4,
+                    desc="256M Float32 keys (nearly sorted) + Uint32 values, check_order=true"),
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(n_log2: int, seed: int) -> dict:
+    """Reference CPU path timed in Node on this host (kind 'reference'); falls back to the C
+    oracle's single-threaded stable sort (kind 'port') when Node is absent."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+    import oracle as O
+    n = 1 << n_log2
+    keys = O.gen_u32(seed, n)
+    try:
+        with tempfile.TemporaryDirectory() as td:
+            p = os.path.join(td, "keys.bin")
+            keys.tofile(p)
+            out = subprocess.run(["node", os.path.join(ROOT, "oracle", "cpu_sort_ref.js"), p],
+                                 capture_output=True, text=True, timeout=600, check=True)
+        r = json.loads(out.stdout.strip().splitlines()[-1])
+        assert r["sorted"]
+        return {"value": n / (r["ms"] / 1e3) / 1e9, "unit": "Gkeys/s", "cores": 1,
+                "kind": "reference",
+                "sample": (f"2^{n_log2} uniform u32 keys (keys only, as the reference's demo times "
+                           f"it), Uint32Array.sort((a,b)=>a-b) in Node {r['node']} on "
+                           f"'{r['cpu_model']}' ({r['cpus']} host cpus, 1 used); "
+                           f"{r['ms'] / 1e3:.2f} s; the comparator sort is super-linear, so the "
+                           f"rate at 2^28 is lower still"),
+                "seconds": r["ms"] / 1e3}
+    except (OSError, subprocess.SubprocessError, ValueError, AssertionError) as e:
+        log(f"node baseline unavailable ({e!r}); timing the C oracle instead")
+        vals = np.arange(n, dtype=np.uint32)
+        t = time.perf_counter()
+        O.stable_sort_masked_c(keys, vals, 32)
+        dt = time.perf_counter() - t
+        return {"value": n / dt / 1e9, "unit": "Gkeys/s", "cores": 1, "kind": "port",
+                "sample": f"2^{n_log2} u32 keys + values, oracle/rs_oracle.c stable LSD, 1 thread",
+                "seconds": dt}
+
+
+def make_input(torch, ops, wl, n, seed, start, dev):
+    keys = torch.empty(n, dtype=torch.int32, device=dev)
+    if wl["kind"] == "f32_nearly":
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as O  # host generation of the nearly-sorted f32 input (untimed)
+        keys.copy_(torch.from_numpy(O.nearly_sorted_f32_bits(n, seed).view("int32")))
+    else:
+        ops.fill_random_u32(keys, seed, start)
+    vals = None
+    if wl["values"]:
+        vals = torch.empty(n, dtype=torch.int32, device=dev)
+        ops.fill_iota_u32(vals, start)
+    return keys, vals
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="config3", choices=sorted(WORKLOADS))
+    ap.add_argument("--n", type=int, default=0, help="override keys per GPU (testing only)")
+    ap.add_argument("--radix-bits", type=int, default=0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-log2", type=int, default=23)
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
+                    help="PMC-derived HBM bytes per scatter launch (tools/pmc_traffic.py)")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    from radix_sort_amd import RadixSortKernel, ops
+    from radix_sort_amd.distributed import HipLocalOps, distributed_sort
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    wl = dict(WORKLOADS[args.workload])
+    n = args.n or wl["n"]
+    K, W = args.steps, args.warmup
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    kernel_ms = {}
+    extra = {}
+    if world == 1:
+        # One pre-generated batch per timed step (HBM holds them: 2 GiB each for config3).
+        per_batch = n * 4 * (2 if wl["values"] else 1)
+        free, _ = torch.cuda.mem_get_info(dev)
+        max_batches = max(1, int((free - 4 * per_batch) // (2 * per_batch)))  # batch + its plan's tmp
+        nb = min(K, max_batches)
+        if nb < K:
+            log(f"note: {K} steps but room for {nb} batches; later steps re-sort batches")
+        batches = [make_input(torch, ops, wl, n, wl["seed"] + 7919 * i, 0, dev) for i in range(nb)]
+        wk, wv = make_input(torch, ops, wl, n, wl["seed"] + 999331, 0, dev)
+        kern = RadixSortKernel(device=local, keys=wk, values=wv, count=n, bit_count=32,
+                               local_shuffle=wl["local_shuffle"], check_order=wl["check_order"],
+                               radix_bits=args.radix_bits)
+        kernels = [RadixSortKernel(device=local, keys=b[0], values=b[1], count=n, bit_count=32,
+                                   local_shuffle=wl["local_shuffle"],
+                                   check_order=wl["check_order"], radix_bits=args.radix_bits)
+                   for b in batches]
+        for w in range(W):
+            if w:
+                wk2, wv2 = make_input(torch, ops, wl, n, wl["seed"] + 999331 + w, 0, dev)
+                wk.copy_(wk2)
+                if wv is not None:
+                    wv.copy_(wv2)
+                del wk2, wv2
+            kern.dispatch()
+        torch.cuda.synchronize()
+        for k in kernels:
+            k.set_profiling(True)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(K):
+            kernels[i % nb].dispatch()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        for k in kernels:
+            for name, v in k.kernel_times().items():
+                acc = kernel_ms.setdefault(name, {"ms": 0.0, "launches": 0})
+                acc["ms"] += v["ms"]
+                acc["launches"] += v["launches"]
+        # sanity: the last sorted batch really is sorted (outside the timed region)
+        lk = batches[(K - 1) % nb][0]
+        if not ops.is_sorted(lk):
+            raise SystemExit("bench: output not sorted")
+        info = kernels[0].info
+        keys_per_step = n
+        scatter_keys = n
+    else:
+        keys, vals = make_input(torch, ops, wl, n, wl["seed"], rank * n, dev)
+        lo = HipLocalOps(local, int(n * 1.25), wl["values"], args.radix_bits)
+        for _ in range(W):
+            r = distributed_sort(keys, vals, lo)
+        torch.cuda.synchronize()
+        lo.plan.destroy()
+        lo = HipLocalOps(local, max(int(n * 1.25), r.n), wl["values"], args.radix_bits)
+        from radix_sort_amd import _lib
+        import ctypes
+        _lib.load().rs_plan_set_profiling(lo.plan._plan, 1)
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(K):
+            r = distributed_sort(keys, vals, lo)
+        torch.cuda.synchronize()
+        barrier()
+        elapsed = time.perf_counter() - t0
+        ms = (ctypes.c_double * 4)()
+        cnt = (ctypes.c_uint64 * 4)()
+        _lib.load().rs_plan_kernel_times(lo.plan._plan, ms, cnt)
+        for i, name in enumerate(_lib.KERNEL_NAMES):
+            kernel_ms[name] = {"ms": ms[i], "launches": int(cnt[i])}
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        if not ops.is_sorted(r.keys, r.n):
+            raise SystemExit(f"bench: rank {rank} output not sorted")
+        info = {"passes": 4}
+        keys_per_step = n * world
+        scatter_keys = r.n
+        extra["recv_keys_rank0"] = r.n
+        extra["partition"] = "top 8 bits, whole-bucket split"
+
+    value = keys_per_step * K / elapsed / 1e9
+    sc = kernel_ms.get("scatter", {"ms": 0.0, "launches": 0})
+    bytes_per_key = 16 if wl["values"] else 8
+    roof = None
+    if sc["launches"]:
+        avg_ms = sc["ms"] / sc["launches"]
+        achieved = scatter_keys * bytes_per_key / (avg_ms / 1e3) / 1e9
+        traffic = None
+        try:
+            with open(args.traffic_json) as f:
+                tj = json.load(f).get(args.workload)
+            if tj:
+                traffic = tj.get("scatter_bytes_per_launch")
+        except (OSError, ValueError):
+            pass
+        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "kernel": "k_scatter (rank + local shuffle + scatter)",
+                "avg_launch_ms": round(avg_ms, 4),
+                "algorithmic_bytes_per_launch": scatter_keys * bytes_per_key}
+    passes = info["passes"]
+    sort_bytes = keys_per_step / max(world, 1) * passes * (12 + 8 * (1 if wl["values"] else 0))
+    extra["whole_sort_hbm_GBs_per_gpu"] = round(sort_bytes / (elapsed / K) / 1e9, 1)
+    extra["kernel_ms_per_step"] = {k: round(v["ms"] / max(K, 1), 4) for k, v in kernel_ms.items()}
+    extra["passes"] = passes
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args.cpu_log2, wl["seed"])
+
+    if rank == 0:
+        out = {
+            "metric": "Gkeys/s sorted (32-bit keys+values) at 1/2/4/8 MI355X; % HBM roofline",
+            "value": round(value, 4), "unit": "Gkeys/s", "n_gpus": world, "steps": K,
+            "warmup": W, "ms_per_step": round(elapsed / K * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+            "data": "synthetic (splitmix64 counter generator, uniform u32; values = iota)",
+            "config": {"workload": args.workload, "description": wl["desc"], "keys_per_gpu": n,
+                       "global_keys": n * world, "bit_count": 32, "has_values": wl["values"],
+                       "local_shuffle": wl["local_shuffle"], "check_order": wl["check_order"],
+                       "radix_bits": args.radix_bits or 8,
+                       "parallelism": "single GPU" if world == 1 else
+                       f"{world} ranks, top-byte bucket exchange (RCCL all_to_all)"},
+            "roofline": roof, "cpu_baseline": cpu, **extra,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

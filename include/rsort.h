@@ -1,0 +1,147 @@
+/*
+ * rsort.h — C ABI of the MI355X-native 4-way LSD radix sort (librsort.so).
+ *
+ * This is the drop-in boundary for the reference's hot path,
+ *   new RadixSortKernel({device, keys, values, count, bit_count, workgroup_size,
+ *                        check_order, local_shuffle, avoid_bank_conflicts}).dispatch(pass)
+ * (README.md:72-88; shipped as RadixSortBufferKernel, src/kernels/radix-sort/
+ * RadixSortBufferKernel.ts:9-32, AbstractRadixSortKernel.ts:14-19,221-227) and for the
+ * exported PrefixSumKernel (src/kernels/PrefixSumKernel.ts:24-43,147-158).
+ *
+ * Plain C: pointers, sizes and status codes only; no exceptions cross it.  Device pointers are
+ * HIP device allocations (from rs_malloc, hipMalloc or torch); `stream` is a hipStream_t passed
+ * as void* (NULL = the default stream).  All sort/scan calls are asynchronous on `stream`, like
+ * the reference's dispatch(), which only encodes work (AbstractRadixSortKernel.ts:221-247).
+ *
+ * The matching host bindings (Node N-API addon, Python ctypes) are in INTEGRATION.md.
+ */
+#ifndef RSORT_H
+#define RSORT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RSORT_VERSION_MAJOR 0
+#define RSORT_VERSION_MINOR 1
+
+typedef enum rs_status {
+    RS_OK = 0,
+    RS_ERR_INVALID_ARG = 1,   /* null pointer, count too large, bad bit range ... */
+    RS_ERR_NOT_POW2 = 2,      /* workgroup_x*workgroup_y not a power of two
+                                 (PrefixSumKernel.ts:33-35) */
+    RS_ERR_BIT_COUNT = 3,     /* bit_count not a multiple of 4 in [4, 32] (README.md:97;
+                                 the reference leaves this unchecked) */
+    RS_ERR_HIP = 4,           /* a HIP runtime call failed (message in rs_last_error) */
+    RS_ERR_OUT_OF_MEMORY = 5,
+    RS_ERR_CAPACITY = 6       /* count exceeds the plan's capacity */
+} rs_status;
+
+/* rs_plan_desc.flags — the reference's boolean options. */
+#define RS_FLAG_HAS_VALUES           0x1u  /* data.values present (RadixSortBufferKernel.ts:25-28) */
+#define RS_FLAG_CHECK_ORDER          0x2u  /* check_order (AbstractRadixSortKernel.ts:249-276) */
+#define RS_FLAG_LOCAL_SHUFFLE        0x4u  /* local_shuffle (RadixSortBufferKernel.ts:38-44) */
+#define RS_FLAG_AVOID_BANK_CONFLICTS 0x8u  /* avoid_bank_conflicts (PrefixSumKernel.ts:37-40) */
+
+/* Options of one sort plan (one RadixSortKernel instance). */
+typedef struct rs_plan_desc {
+    int32_t  device;        /* HIP device ordinal                           (options.device) */
+    uint64_t count;         /* elements to sort, < 2^32                     (options.count) */
+    uint32_t bit_count;     /* sort by the low bit_count bits; 0 -> 32     (options.bit_count) */
+    uint32_t workgroup_x;   /* 0 -> 16; x*y must be a power of two <= 1024 (options.workgroup_size) */
+    uint32_t workgroup_y;   /* 0 -> 16 */
+    uint32_t flags;         /* RS_FLAG_* */
+    uint32_t radix_bits;    /* digit bits per HBM pass: 0 = auto (fused: 8-bit digits, four
+                               4-way splits per pass); 2 = one 4-way split per pass, the
+                               reference's pass structure (bit_count/2 passes); 4 or 8 */
+    uint32_t reserved;
+} rs_plan_desc;
+
+typedef struct rs_plan rs_plan;
+
+/* Per-plan facts (for benches / INTEGRATION tooling). */
+typedef struct rs_plan_info {
+    uint32_t passes;            /* global HBM passes per sort (even) */
+    uint32_t digit_bits[16];    /* digit width of each pass */
+    uint32_t tile_keys;         /* keys per tile of the rank/scatter kernel */
+    uint32_t grid_blocks;       /* workgroups of the histogram / scatter kernels */
+    uint64_t workspace_bytes;   /* device bytes owned by the plan */
+} rs_plan_info;
+
+/* Kernel kinds reported by rs_plan_kernel_times(). */
+enum {
+    RS_KERNEL_HISTOGRAM = 0,    /* per-block digit histogram          (RadixSort.ts:50-126) */
+    RS_KERNEL_SCAN = 1,         /* digit x block exclusive scan       (PrefixSum.ts:13-106) */
+    RS_KERNEL_SCATTER = 2,      /* rank + local shuffle + scatter     (RadixSortReorder.ts:80-102,
+                                                                       RadixSortLocalShuffle.ts) */
+    RS_KERNEL_CHECK = 3,        /* order check                        (CheckSort.ts:70-145) */
+    RS_KERNEL_KINDS = 4
+};
+
+/* ---- errors / versions ------------------------------------------------------------------ */
+const char* rs_last_error(void);               /* thread-local message of the last failure */
+const char* rs_status_string(rs_status s);
+uint32_t    rs_version(void);                  /* (major << 16) | minor */
+
+/* ---- sort plans (RadixSortKernel) ------------------------------------------------------- */
+/* Validate options, allocate the workspace (tmp keys/values, block histograms) on `device`. */
+rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out);
+/* Sort keys[0..count) (and values[0..count) when RS_FLAG_HAS_VALUES) in place, ascending and
+ * stable by (key & (2^bit_count - 1)); words at index >= count are untouched.  Float32 keys
+ * sort by raw bit pattern (README.md:9).  Asynchronous on `stream`. */
+rs_status rs_plan_sort(rs_plan* plan, void* keys, void* values, void* stream);
+/* Same, for n <= the plan's count (multi-GPU receive buffers vary per call). */
+rs_status rs_plan_sort_n(rs_plan* plan, void* keys, void* values, uint64_t n, void* stream);
+/* One stable scatter pass by digit (key >> shift) & (2^bits - 1), bits <= 8, out of place:
+ * in[0..n) -> out[0..n).  Writes the 2^bits digit totals (u32) to d_hist (device, may be
+ * NULL).  The bucket-exchange partition step of the multi-GPU sort. */
+rs_status rs_plan_partition(rs_plan* plan, const void* in_keys, const void* in_values,
+                            void* out_keys, void* out_values, uint64_t n, uint32_t shift,
+                            uint32_t bits, void* d_hist, void* stream);
+rs_status rs_plan_info_get(const rs_plan* plan, rs_plan_info* info);
+/* Kernel timing: when enabled, every launch of the plan is bracketed by HIP events on the
+ * launch stream and per-kind durations are accumulated (read after synchronising). */
+rs_status rs_plan_set_profiling(rs_plan* plan, int enable);
+rs_status rs_plan_kernel_times(rs_plan* plan, double ms[RS_KERNEL_KINDS],
+                               uint64_t launches[RS_KERNEL_KINDS]);
+rs_status rs_plan_reset_kernel_times(rs_plan* plan);
+void      rs_plan_destroy(rs_plan* plan);     /* frees the workspace (reference quirk Q9) */
+
+/* ---- prefix sum (PrefixSumKernel) ------------------------------------------------------- */
+typedef struct rs_scan_plan rs_scan_plan;
+/* workgroup_x*workgroup_y must be a power of two (PrefixSumKernel.ts:33-35). */
+rs_status rs_scan_plan_create(int32_t device, uint64_t count, uint32_t workgroup_x,
+                              uint32_t workgroup_y, uint32_t flags, rs_scan_plan** out);
+/* In-place exclusive scan (mod 2^32) of data[0..count); data[count..] untouched. */
+rs_status rs_scan_plan_run(rs_scan_plan* plan, void* data, void* stream);
+void      rs_scan_plan_destroy(rs_scan_plan* plan);
+
+/* ---- device memory / streams (the reference's createBuffers / queue analogue) ---------- */
+rs_status rs_device_count(int32_t* n);
+rs_status rs_malloc(int32_t device, uint64_t bytes, void** ptr);
+rs_status rs_free(void* ptr);
+rs_status rs_memcpy_h2d(void* dst, const void* src, uint64_t bytes, void* stream);
+rs_status rs_memcpy_d2h(void* dst, const void* src, uint64_t bytes, void* stream);
+rs_status rs_memcpy_d2d(void* dst, const void* src, uint64_t bytes, void* stream);
+rs_status rs_stream_create(int32_t device, void** stream);
+rs_status rs_stream_destroy(void* stream);
+rs_status rs_stream_synchronize(void* stream);
+
+/* ---- synthetic inputs (bench / tests) --------------------------------------------------- */
+/* dst[i] = low32(splitmix64_finaliser(seed * 0xD1B54A32D192ED03 + start + i)), i < n. */
+rs_status rs_fill_random_u32(void* dst, uint64_t n, uint64_t seed, uint64_t start, void* stream);
+/* dst[i] = first + i (u32 wrap), i < n. */
+rs_status rs_fill_iota_u32(void* dst, uint64_t n, uint32_t first, void* stream);
+/* Device-side order check of keys[0..n) by (key & mask): writes 1 (sorted) or 0 to *d_flag
+ * (device u32).  Checks every adjacent pair. */
+rs_status rs_is_sorted(const void* keys, uint64_t n, uint32_t bit_count, void* d_flag,
+                       void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RSORT_H */

@@ -1,0 +1,256 @@
+"""GPU parity: the HIP sort (through the C ABI) against the oracle and the golden fixtures.
+
+Bar: bit-exact.  Small and medium sizes compare every word with the oracle; the BASELINE
+full sizes (64M keys-only, 256M KV, 256M nearly-sorted f32 + check_order) are checked through
+size-independent properties: sorted by masked key, keys_out == keys_in[values_out] with
+values = iota (a permutation), equal keys keep increasing values (stability), and for keys-only
+an independent multiset check against torch.sort.
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+from conftest import case_arrays
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+def _t(a: np.ndarray):
+    return torch.from_numpy(np.ascontiguousarray(a).view(np.int32)).to(DEV)
+
+
+def _np(t) -> np.ndarray:
+    return t.cpu().numpy().view(np.uint32)
+
+
+def _sort(keys, vals, count=None, **opts):
+    from radix_sort_amd import RadixSortKernel
+    kt = _t(keys)
+    vt = None if vals is None else _t(vals)
+    k = RadixSortKernel(device=0, keys=kt, values=vt,
+                        count=keys.size if count is None else count, **opts)
+    k.dispatch()
+    torch.cuda.synchronize()
+    out = _np(kt), (None if vt is None else _np(vt))
+    k.destroy()
+    return out
+
+
+def test_golden_fixtures_default_options(golden):
+    manifest, arrays = golden
+    for case in manifest["sort_cases"]:
+        keys, vals, exp_k, exp_v = case_arrays(arrays, case)
+        k, v = _sort(keys, vals, case["count"], bit_count=case["bit_count"])
+        assert (k == exp_k).all(), case
+        if vals is not None:
+            assert (v == exp_v).all(), case
+
+
+@pytest.mark.parametrize("opts", [
+    dict(check_order=True),
+    dict(local_shuffle=True, avoid_bank_conflicts=True),
+    dict(radix_bits=2, workgroup_size={"x": 8, "y": 8}),          # the reference's 4-way pass structure
+    dict(radix_bits=4, checkOrder=True, workgroupSize={"x": 32, "y": 32}),
+])
+def test_golden_fixtures_option_matrix(golden, opts):
+    manifest, arrays = golden
+    for case in manifest["sort_cases"][::3] + [c for c in manifest["sort_cases"]
+                                                if c["kind"] in ("sorted", "q1", "nearly", "equal")]:
+        keys, vals, exp_k, exp_v = case_arrays(arrays, case)
+        k, v = _sort(keys, vals, case["count"], bit_count=case["bit_count"], **opts)
+        assert (k == exp_k).all(), (case, opts)
+        if vals is not None:
+            assert (v == exp_v).all(), (case, opts)
+
+
+def test_large_golden_sha(golden):
+    import hashlib
+    manifest, _ = golden
+    for case in manifest["large_cases"]:
+        n = case["n"]
+        kt = torch.empty(n, dtype=torch.int32, device=DEV)
+        from radix_sort_amd import ops, RadixSortKernel
+        ops.fill_random_u32(kt, case["seed"])
+        if case["kind"] == "f32":
+            u = _np(kt)
+            kt = _t(((u >> np.uint32(8)).astype(np.float64) * 2.0 ** -24).astype(np.float32).view(np.uint32))
+        vt = None
+        if case["has_values"]:
+            vt = torch.empty(n, dtype=torch.int32, device=DEV)
+            ops.fill_iota_u32(vt)
+        k = RadixSortKernel(keys=kt, values=vt, count=n)
+        k.dispatch()
+        torch.cuda.synchronize()
+        assert hashlib.sha256(_np(kt).tobytes()).hexdigest() == case["sha256_keys"]
+        if vt is not None:
+            assert hashlib.sha256(_np(vt).tobytes()).hexdigest() == case["sha256_values"]
+
+
+@pytest.mark.parametrize("bits", [4, 8, 12, 16, 20, 24, 28, 32])
+@pytest.mark.parametrize("radix_bits", [0, 2, 4])
+def test_random_vs_oracle_bit_counts(bits, radix_bits):
+    n = 300_001 if radix_bits != 2 else 70_001
+    keys = O.gen_u32(bits * 31 + radix_bits, n)
+    keys[::7] = keys[3]          # duplicates: stability visible through the values
+    vals = np.arange(n, dtype=np.uint32)
+    k, v = _sort(keys, vals, bit_count=bits, radix_bits=radix_bits)
+    ek, ev = O.stable_sort_masked(keys, vals, bits)
+    assert (k == ek).all() and (v == ev).all()
+
+
+@pytest.mark.parametrize("n", [4095, 4096, 4097, 1 << 20, (1 << 22) + 12345, 9_000_001])
+def test_sizes_keys_only_and_kv(n):
+    keys = O.gen_u32(n, n)
+    ek, _ = O.stable_sort_masked_c(keys, None, 32)
+    k, _ = _sort(keys, None)
+    assert (k == ek).all()
+    vals = np.arange(n, dtype=np.uint32)
+    k, v = _sort(keys, vals, check_order=(n % 2 == 1))
+    ek, ev = O.stable_sort_masked_c(keys, vals, 32)
+    assert (k == ek).all() and (v == ev).all()
+
+
+def test_count_less_than_buffer_leaves_tail():
+    n, count = 100_000, 77_777
+    keys = O.gen_u32(77, n)
+    vals = O.gen_u32(78, n)   # arbitrary values, not iota
+    k, v = _sort(keys, vals, count=count)
+    ek, ev = O.stable_sort_masked(keys, vals, 32, count)
+    assert (k == ek).all() and (v == ev).all()
+
+
+@pytest.mark.parametrize("kind", ["sorted", "sorted_after_first_pass", "reverse", "equal"])
+def test_check_order_early_exit_paths(kind):
+    n = 1 << 20
+    u = O.gen_u32(5, n)
+    if kind == "sorted":
+        keys = np.sort(u)
+    elif kind == "sorted_after_first_pass":
+        # only the low 6 bits vary: sorted after pass 0, so the check before pass 1 exits
+        # early with the data in the tmp buffers (exercises the tmp -> caller copy)
+        keys = u & np.uint32(0x3F)
+    elif kind == "reverse":
+        keys = np.sort(u)[::-1].copy()
+    else:
+        keys = np.full(n, 12345, dtype=np.uint32)
+    vals = np.arange(n, dtype=np.uint32)
+    for bits in (32, 24, 8):
+        k, v = _sort(keys, vals, check_order=True, bit_count=bits)
+        ek, ev = O.stable_sort_masked(keys, vals, bits)
+        assert (k == ek).all() and (v == ev).all(), (kind, bits)
+
+
+def test_prefix_sum_kernel_golden(golden):
+    from radix_sort_amd import PrefixSumKernel
+    manifest, arrays = golden
+    for case in manifest["scan_cases"]:
+        d, exp = arrays[case["name"] + "_data"], arrays[case["name"] + "_exp"]
+        t = _t(d)
+        k = PrefixSumKernel(data=t, count=case["count"], workgroupSize={"x": 16, "y": 16})
+        k.dispatch()
+        torch.cuda.synchronize()
+        assert (_np(t) == exp).all(), case["name"]
+
+
+def test_prefix_sum_large_wraps():
+    from radix_sort_amd import PrefixSumKernel
+    n = (1 << 24) + 3
+    d = O.gen_u32(11, n)          # large values: the running sum wraps mod 2^32
+    t = _t(d)
+    PrefixSumKernel(data=t).dispatch()
+    torch.cuda.synchronize()
+    assert (_np(t) == O.prefix_sum(d)).all()
+
+
+def test_partition_pass_and_histogram():
+    from radix_sort_amd import ops
+    n = 1_000_003
+    keys = O.gen_u32(3, n)
+    kt, vt = _t(keys), torch.arange(n, dtype=torch.int32, device=DEV)
+    ok, ov = torch.empty_like(kt), torch.empty_like(vt)
+    hist = torch.empty(256, dtype=torch.int32, device=DEV)
+    plan = ops.SortPlan(0, n, has_values=True)
+    plan.partition(kt, vt, ok, ov, n, 24, 8, hist)
+    torch.cuda.synchronize()
+    top = keys >> np.uint32(24)
+    perm = np.argsort(top, kind="stable")
+    assert (_np(ok) == keys[perm]).all() and (_np(ov) == perm.astype(np.uint32)).all()
+    assert (_np(hist) == np.bincount(top, minlength=256)).all()
+
+
+def test_kernel_profiling_counts_launches():
+    from radix_sort_amd import RadixSortKernel, ops
+    n = 1 << 22
+    kt = torch.empty(n, dtype=torch.int32, device=DEV)
+    ops.fill_random_u32(kt, 1)
+    k = RadixSortKernel(keys=kt, count=n)
+    k.set_profiling(True)
+    k.dispatch()
+    torch.cuda.synchronize()
+    t = k.kernel_times()
+    assert t["scatter"]["launches"] == k.info["passes"] == 4
+    assert t["scatter"]["ms"] > 0
+    assert ops.is_sorted(kt)
+
+
+# ---- BASELINE full sizes (properties) ---------------------------------------------------
+
+def _verify_kv_iota(keys_in, keys_out, vals_out, bits=32):
+    n = keys_in.numel()
+    vo = vals_out.long()
+    assert torch.equal(torch.bincount(vo, minlength=n), torch.ones(n, dtype=torch.long, device=DEV))
+    assert torch.equal(keys_in[vo], keys_out)                       # keys_out == keys_in[values]
+    mask = (1 << bits) - 1
+    ku = (keys_out.long() & 0xFFFFFFFF) & mask
+    assert bool((ku[1:] >= ku[:-1]).all())                         # sorted
+    eq = ku[1:] == ku[:-1]
+    assert bool((vo[1:][eq] > vo[:-1][eq]).all())                   # stable
+
+
+@pytest.mark.slow
+def test_config2_64M_keys_only():
+    from radix_sort_amd import RadixSortKernel, ops
+    n = 1 << 26
+    kt = torch.empty(n, dtype=torch.int32, device=DEV)
+    ops.fill_random_u32(kt, 2)
+    ref = torch.sort(kt.long() & 0xFFFFFFFF).values
+    RadixSortKernel(keys=kt, count=n, bit_count=32, workgroup_size={"x": 16, "y": 16}).dispatch()
+    torch.cuda.synchronize()
+    assert torch.equal(kt.long() & 0xFFFFFFFF, ref)
+    del ref
+
+
+@pytest.mark.slow
+def test_config3_256M_kv_local_shuffle():
+    from radix_sort_amd import RadixSortKernel, ops
+    n = 1 << 28
+    kt = torch.empty(n, dtype=torch.int32, device=DEV)
+    ops.fill_random_u32(kt, 3)
+    k_in = kt.clone()
+    vt = torch.empty(n, dtype=torch.int32, device=DEV)
+    ops.fill_iota_u32(vt)
+    RadixSortKernel(keys=kt, values=vt, count=n, local_shuffle=True).dispatch()
+    torch.cuda.synchronize()
+    _verify_kv_iota(k_in, kt, vt)
+
+
+@pytest.mark.slow
+def test_config4_256M_nearly_sorted_f32_check_order():
+    from radix_sort_amd import RadixSortKernel, ops
+    n = 1 << 28
+    bits = O.nearly_sorted_f32_bits(n, 4)
+    kt = _t(bits)
+    k_in = kt.clone()
+    vt = torch.empty(n, dtype=torch.int32, device=DEV)
+    ops.fill_iota_u32(vt)
+    RadixSortKernel(keys=kt, values=vt, count=n, check_order=True).dispatch()
+    torch.cuda.synchronize()
+    _verify_kv_iota(k_in, kt, vt)
+    # fully sorted variant: early exit leaves the data untouched
+    RadixSortKernel(keys=kt, values=vt, count=n, check_order=True).dispatch()
+    torch.cuda.synchronize()
+    _verify_kv_iota(k_in, kt, vt)

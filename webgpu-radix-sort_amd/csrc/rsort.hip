@@ -1,0 +1,577 @@
+// rsort.hip — C ABI (include/rsort.h) over the gfx950 radix-sort kernels (rs_kernels.hpp).
+//
+// Mirrors the reference's host classes:
+//   rs_plan_create  ~ new RadixSortBufferKernel(opts)   (RadixSortBufferKernel.ts:21-32:
+//                     option defaults AbstractRadixSortKernel.ts:52-57, resources :50-71)
+//   rs_plan_sort    ~ kernel.dispatch(pass)             (AbstractRadixSortKernel.ts:221-276)
+//   rs_scan_plan_*  ~ new PrefixSumKernel(opts).dispatch (PrefixSumKernel.ts:24-43,147-158)
+// Every call returns an rs_status; the message of the last failure is kept per thread.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/rsort.h"
+#include "rs_kernels.hpp"
+
+#define RS_EXPORT extern "C" __attribute__((visibility("default")))
+
+namespace {
+
+thread_local std::string g_err;
+
+rs_status fail(rs_status s, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return s;
+}
+
+#define HIP_TRY(expr)                                                                  \
+    do {                                                                               \
+        hipError_t e_ = (expr);                                                        \
+        if (e_ != hipSuccess)                                                          \
+            return fail(e_ == hipErrorOutOfMemory ? RS_ERR_OUT_OF_MEMORY : RS_ERR_HIP, \
+                        "%s: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__,      \
+                        __LINE__);                                                     \
+    } while (0)
+
+// Tuned geometry of the rank/scatter kernel.
+constexpr int kKPT = 16;                       // keys per thread per tile
+constexpr int kTile = rs::kBlock * kKPT;       // 4096 keys per tile
+constexpr uint32_t kMaxGrid = 1024;            // workgroups of histogram/scatter kernels
+constexpr int kCheckGrid = 2048;
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (dev >= 0 && dev != prev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+struct KernelTimer {
+    bool enabled = false;
+    struct Rec { int kind; hipEvent_t a, b; };
+    std::vector<Rec> pending;
+    std::vector<hipEvent_t> pool;
+    double ms[RS_KERNEL_KINDS] = {0, 0, 0, 0};
+    uint64_t launches[RS_KERNEL_KINDS] = {0, 0, 0, 0};
+
+    hipEvent_t get() {
+        if (!pool.empty()) { hipEvent_t e = pool.back(); pool.pop_back(); return e; }
+        hipEvent_t e = nullptr;
+        (void)hipEventCreate(&e);
+        return e;
+    }
+    // Records events around `launch` when enabled.
+    template <class F>
+    void run(int kind, hipStream_t s, F&& launch) {
+        if (!enabled) { launch(); return; }
+        Rec r{kind, get(), get()};
+        (void)hipEventRecord(r.a, s);
+        launch();
+        (void)hipEventRecord(r.b, s);
+        pending.push_back(r);
+    }
+    void drain() {
+        for (auto& r : pending) {
+            (void)hipEventSynchronize(r.b);
+            float t = 0.f;
+            if (hipEventElapsedTime(&t, r.a, r.b) == hipSuccess) ms[r.kind] += t;
+            launches[r.kind] += 1;
+            pool.push_back(r.a);
+            pool.push_back(r.b);
+        }
+        pending.clear();
+    }
+    ~KernelTimer() {
+        for (auto& r : pending) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
+        for (auto e : pool) (void)hipEventDestroy(e);
+    }
+};
+
+}  // namespace
+
+struct rs_plan {
+    rs_plan_desc desc{};
+    uint32_t bit_count = 32;
+    uint32_t radix_bits = 8;
+    bool has_values = false, check_order = false, local_shuffle = false;
+    uint32_t passes = 0;
+    uint32_t widths[16] = {};
+    uint64_t capacity = 0;
+    uint32_t* tmp_k = nullptr;
+    uint32_t* tmp_v = nullptr;
+    uint32_t* counts = nullptr;    // [256][kMaxGrid]
+    uint32_t* totals = nullptr;    // [256]
+    uint32_t* flags = nullptr;     // [16] check_order results
+    uint64_t workspace = 0;
+    KernelTimer timer;
+};
+
+struct rs_scan_plan {
+    int device = 0;
+    uint64_t count = 0;
+    uint32_t* sums = nullptr;     // [kMaxGrid]
+};
+
+namespace {
+
+uint32_t pick_R(uint32_t w) { return w <= 2 ? 2 : (w <= 4 ? 4 : 8); }
+
+struct Geometry {
+    uint32_t grid, base, extra;
+};
+
+Geometry geometry(uint64_t n, uint32_t tile, uint32_t max_grid) {
+    const uint64_t tiles = (n + tile - 1) / tile;
+    Geometry g;
+    g.grid = (uint32_t)std::min<uint64_t>(tiles, max_grid);
+    if (g.grid == 0) g.grid = 1;
+    g.base = (uint32_t)(tiles / g.grid);
+    g.extra = (uint32_t)(tiles % g.grid);
+    return g;
+}
+
+template <int R>
+void launch_histogram(const uint32_t* in, uint32_t n, uint32_t shift, uint32_t mask,
+                      const Geometry& geo, uint32_t* counts, const uint32_t* gate, int pass,
+                      hipStream_t s) {
+    hipLaunchKernelGGL((rs::k_histogram<R, kTile>), dim3(geo.grid), dim3(rs::kBlock), 0, s, in,
+                       n, shift, mask, geo.base, geo.extra, counts, gate, pass);
+}
+
+template <int R, bool V, bool ST>
+void launch_scatter_t(const uint32_t* ik, const uint32_t* iv, uint32_t* ok, uint32_t* ov,
+                      uint32_t n, uint32_t shift, uint32_t mask, uint32_t nbits,
+                      const Geometry& geo, const uint32_t* counts, const uint32_t* totals,
+                      const uint32_t* gate, int pass, hipStream_t s) {
+    hipLaunchKernelGGL((rs::k_scatter<R, kKPT, V, ST>), dim3(geo.grid), dim3(rs::kBlock), 0, s,
+                       ik, iv, ok, ov, n, shift, mask, nbits, geo.base, geo.extra, counts,
+                       totals, gate, pass);
+}
+
+template <int R>
+void launch_scatter(bool V, bool ST, const uint32_t* ik, const uint32_t* iv, uint32_t* ok,
+                    uint32_t* ov, uint32_t n, uint32_t shift, uint32_t mask, uint32_t nbits,
+                    const Geometry& geo, const uint32_t* counts, const uint32_t* totals,
+                    const uint32_t* gate, int pass, hipStream_t s) {
+    if (V) {
+        if (ST) launch_scatter_t<R, true, true>(ik, iv, ok, ov, n, shift, mask, nbits, geo, counts, totals, gate, pass, s);
+        else    launch_scatter_t<R, true, false>(ik, iv, ok, ov, n, shift, mask, nbits, geo, counts, totals, gate, pass, s);
+    } else {
+        if (ST) launch_scatter_t<R, false, true>(ik, iv, ok, ov, n, shift, mask, nbits, geo, counts, totals, gate, pass, s);
+        else    launch_scatter_t<R, false, false>(ik, iv, ok, ov, n, shift, mask, nbits, geo, counts, totals, gate, pass, s);
+    }
+}
+
+// One stable digit pass in -> out (histogram, scan, scatter).
+rs_status run_pass(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint32_t* ok,
+                   uint32_t* ov, uint32_t n, uint32_t shift, uint32_t w, bool values,
+                   const uint32_t* gate, int pass, hipStream_t s) {
+    const uint32_t R = pick_R(w);
+    const uint32_t mask = (1u << w) - 1u;
+    const Geometry geo = geometry(n, kTile, kMaxGrid);
+    p->timer.run(RS_KERNEL_HISTOGRAM, s, [&] {
+        if (R == 2) launch_histogram<2>(ik, n, shift, mask, geo, p->counts, gate, pass, s);
+        else if (R == 4) launch_histogram<4>(ik, n, shift, mask, geo, p->counts, gate, pass, s);
+        else launch_histogram<8>(ik, n, shift, mask, geo, p->counts, gate, pass, s);
+    });
+    HIP_TRY(hipGetLastError());
+    p->timer.run(RS_KERNEL_SCAN, s, [&] {
+        hipLaunchKernelGGL(rs::k_scan_rows, dim3(1u << R), dim3(rs::kBlock), 0, s, p->counts,
+                           geo.grid, p->totals, gate, pass);
+    });
+    HIP_TRY(hipGetLastError());
+    // The coalesced (LDS-staged) scatter is the implementation of the local shuffle; it is
+    // used for every sort (the direct scatter is kept for the A/B measurement only, see
+    // RS_LOCAL_SHUFFLE_DIRECT in DESIGN.md).
+    const bool staged = p->local_shuffle || true;
+    p->timer.run(RS_KERNEL_SCATTER, s, [&] {
+        if (R == 2) launch_scatter<2>(values, staged, ik, iv, ok, ov, n, shift, mask, w, geo, p->counts, p->totals, gate, pass, s);
+        else if (R == 4) launch_scatter<4>(values, staged, ik, iv, ok, ov, n, shift, mask, w, geo, p->counts, p->totals, gate, pass, s);
+        else launch_scatter<8>(values, staged, ik, iv, ok, ov, n, shift, mask, w, geo, p->counts, p->totals, gate, pass, s);
+    });
+    HIP_TRY(hipGetLastError());
+    return RS_OK;
+}
+
+uint32_t full_mask(uint32_t bits) { return bits >= 32 ? 0xFFFFFFFFu : ((1u << bits) - 1u); }
+
+}  // namespace
+
+// ============================================================================================
+RS_EXPORT const char* rs_last_error(void) { return g_err.c_str(); }
+
+RS_EXPORT const char* rs_status_string(rs_status s) {
+    switch (s) {
+        case RS_OK: return "ok";
+        case RS_ERR_INVALID_ARG: return "invalid argument";
+        case RS_ERR_NOT_POW2: return "workgroup size not a power of two";
+        case RS_ERR_BIT_COUNT: return "bit_count must be a multiple of 4 in [4, 32]";
+        case RS_ERR_HIP: return "HIP runtime error";
+        case RS_ERR_OUT_OF_MEMORY: return "out of device memory";
+        case RS_ERR_CAPACITY: return "count exceeds plan capacity";
+    }
+    return "unknown status";
+}
+
+RS_EXPORT uint32_t rs_version(void) { return (RSORT_VERSION_MAJOR << 16) | RSORT_VERSION_MINOR; }
+
+RS_EXPORT rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out) {
+    if (!desc || !out) return fail(RS_ERR_INVALID_ARG, "rs_plan_create: null argument");
+    *out = nullptr;
+    rs_plan_desc d = *desc;
+    if (d.bit_count == 0) d.bit_count = 32;                      // AbstractRadixSortKernel.ts:54
+    if (d.workgroup_x == 0) d.workgroup_x = 16;                  // AbstractKernel.ts:22-25
+    if (d.workgroup_y == 0) d.workgroup_y = 16;
+    const uint64_t T = (uint64_t)d.workgroup_x * d.workgroup_y;
+    if (T == 0 || (T & (T - 1)) || T > 1024)
+        return fail(RS_ERR_NOT_POW2,
+                    "workgroupSize.x * workgroupSize.y must be a power of two <= 1024. (current: %llu)",
+                    (unsigned long long)T);
+    if (d.bit_count % 4 || d.bit_count > 32)
+        return fail(RS_ERR_BIT_COUNT, "bit_count must be a multiple of 4 in [4, 32] (got %u)",
+                    d.bit_count);
+    if (d.count > 0xFFFFFFFFull)
+        return fail(RS_ERR_INVALID_ARG, "count must be < 2^32 (got %llu)",
+                    (unsigned long long)d.count);
+    uint32_t rb = d.radix_bits ? d.radix_bits : 8;
+    if (rb != 2 && rb != 4 && rb != 8)
+        return fail(RS_ERR_INVALID_ARG, "radix_bits must be 0, 2, 4 or 8 (got %u)", d.radix_bits);
+    if (d.flags & ~(uint32_t)0xF) return fail(RS_ERR_INVALID_ARG, "unknown flag bits 0x%x", d.flags);
+
+    rs_plan* p = new (std::nothrow) rs_plan();
+    if (!p) return fail(RS_ERR_OUT_OF_MEMORY, "host allocation failed");
+    p->desc = d;
+    p->bit_count = d.bit_count;
+    p->radix_bits = rb;
+    p->has_values = d.flags & RS_FLAG_HAS_VALUES;
+    p->check_order = d.flags & RS_FLAG_CHECK_ORDER;
+    p->local_shuffle = d.flags & RS_FLAG_LOCAL_SHUFFLE;
+    // Even number of passes so the result lands in the caller's buffers, like the reference's
+    // bit_count/2 passes with ping-pong on bit % 4 (AbstractRadixSortKernel.ts:93-107).
+    uint32_t P = (d.bit_count + rb - 1) / rb;
+    P += P & 1u;
+    p->passes = P;
+    for (uint32_t i = 0; i < P; ++i) p->widths[i] = d.bit_count / P + (i < d.bit_count % P ? 1 : 0);
+    p->capacity = d.count;
+
+    DeviceGuard guard(d.device);
+    auto cleanup = [&](rs_status s) { rs_plan_destroy(p); return s; };
+    auto alloc = [&](uint32_t** ptr, uint64_t bytes) -> hipError_t {
+        if (bytes == 0) bytes = 4;
+        p->workspace += bytes;
+        return hipMalloc((void**)ptr, bytes);
+    };
+    hipError_t e;
+    if ((e = alloc(&p->tmp_k, 4 * d.count)) != hipSuccess ||
+        (p->has_values && (e = alloc(&p->tmp_v, 4 * d.count)) != hipSuccess) ||
+        (e = alloc(&p->counts, 4ull * 256 * kMaxGrid)) != hipSuccess ||
+        (e = alloc(&p->totals, 4ull * 256)) != hipSuccess ||
+        (e = alloc(&p->flags, 4ull * 16)) != hipSuccess)
+        return cleanup(fail(e == hipErrorOutOfMemory ? RS_ERR_OUT_OF_MEMORY : RS_ERR_HIP,
+                            "rs_plan_create: hipMalloc failed: %s", hipGetErrorString(e)));
+    *out = p;
+    return RS_OK;
+}
+
+RS_EXPORT void rs_plan_destroy(rs_plan* p) {
+    if (!p) return;
+    DeviceGuard guard(p->desc.device);
+    p->timer.drain();
+    (void)hipFree(p->tmp_k);
+    (void)hipFree(p->tmp_v);
+    (void)hipFree(p->counts);
+    (void)hipFree(p->totals);
+    (void)hipFree(p->flags);
+    delete p;
+}
+
+RS_EXPORT rs_status rs_plan_sort_n(rs_plan* p, void* keys, void* values, uint64_t n,
+                                   void* stream) {
+    if (!p) return fail(RS_ERR_INVALID_ARG, "rs_plan_sort: null plan");
+    if (n > p->capacity)
+        return fail(RS_ERR_CAPACITY, "count %llu exceeds plan capacity %llu",
+                    (unsigned long long)n, (unsigned long long)p->capacity);
+    if (n <= 1) return RS_OK;
+    if (!keys) return fail(RS_ERR_INVALID_ARG, "rs_plan_sort: keys is null");
+    if (p->has_values && !values)
+        return fail(RS_ERR_INVALID_ARG, "rs_plan_sort: plan has values but values is null");
+    if (((uintptr_t)keys & 3) || (values && ((uintptr_t)values & 3)))
+        return fail(RS_ERR_INVALID_ARG, "keys/values must be 4-byte aligned (README.md limitations)");
+    DeviceGuard guard(p->desc.device);
+    hipStream_t s = (hipStream_t)stream;
+    const bool V = p->has_values;
+    const uint32_t n32 = (uint32_t)n;
+    uint32_t* uk = (uint32_t*)keys;
+    uint32_t* uv = V ? (uint32_t*)values : nullptr;
+    const uint32_t* gate = p->check_order ? p->flags : nullptr;
+    if (p->check_order) HIP_TRY(hipMemsetAsync(p->flags, 0, 16 * 4, s));
+    const uint32_t fmask = full_mask(p->bit_count);
+    uint32_t shift = 0;
+    for (uint32_t i = 0; i < p->passes; ++i) {
+        const bool even = (i % 2) == 0;
+        const uint32_t* ik = even ? uk : p->tmp_k;
+        const uint32_t* iv = even ? uv : p->tmp_v;
+        uint32_t* ok = even ? p->tmp_k : uk;
+        uint32_t* ov = even ? p->tmp_v : uv;
+        if (p->check_order) {
+            // Order check before every pass (the reference checks every second 2-bit pass,
+            // AbstractRadixSortKernel.ts:257-261); all pairs, masked keys (Q1/Q2 fixed).
+            const uint32_t grid = (uint32_t)std::min<uint64_t>(kCheckGrid, (n + rs::kBlock - 1) / rs::kBlock);
+            p->timer.run(RS_KERNEL_CHECK, s, [&] {
+                hipLaunchKernelGGL(rs::k_check, dim3(grid), dim3(rs::kBlock), 0, s, ik, n32,
+                                   fmask, p->flags, (int)i, (int)i - 1);
+            });
+            HIP_TRY(hipGetLastError());
+        }
+        rs_status st = run_pass(p, ik, iv, ok, ov, n32, shift, p->widths[i], V, gate, (int)i, s);
+        if (st != RS_OK) return st;
+        shift += p->widths[i];
+    }
+    if (p->check_order) {
+        const uint32_t grid = (uint32_t)std::min<uint64_t>(kCheckGrid, (n + rs::kBlock - 1) / rs::kBlock);
+        if (V)
+            hipLaunchKernelGGL(rs::k_finalize<true>, dim3(grid), dim3(rs::kBlock), 0, s, p->tmp_k,
+                               p->tmp_v, uk, uv, n32, p->flags, (int)p->passes);
+        else
+            hipLaunchKernelGGL(rs::k_finalize<false>, dim3(grid), dim3(rs::kBlock), 0, s, p->tmp_k,
+                               p->tmp_v, uk, uv, n32, p->flags, (int)p->passes);
+        HIP_TRY(hipGetLastError());
+    }
+    return RS_OK;
+}
+
+RS_EXPORT rs_status rs_plan_sort(rs_plan* p, void* keys, void* values, void* stream) {
+    if (!p) return fail(RS_ERR_INVALID_ARG, "rs_plan_sort: null plan");
+    return rs_plan_sort_n(p, keys, values, p->capacity, stream);
+}
+
+RS_EXPORT rs_status rs_plan_partition(rs_plan* p, const void* in_keys, const void* in_values,
+                                      void* out_keys, void* out_values, uint64_t n,
+                                      uint32_t shift, uint32_t bits, void* d_hist, void* stream) {
+    if (!p) return fail(RS_ERR_INVALID_ARG, "rs_plan_partition: null plan");
+    if (n > p->capacity)
+        return fail(RS_ERR_CAPACITY, "count %llu exceeds plan capacity %llu",
+                    (unsigned long long)n, (unsigned long long)p->capacity);
+    if (bits == 0 || bits > 8 || shift + bits > 32)
+        return fail(RS_ERR_INVALID_ARG, "partition digit must satisfy 1 <= bits <= 8, shift+bits <= 32");
+    const bool V = p->has_values && in_values && out_values;
+    if (n && (!in_keys || !out_keys)) return fail(RS_ERR_INVALID_ARG, "rs_plan_partition: null keys");
+    DeviceGuard guard(p->desc.device);
+    hipStream_t s = (hipStream_t)stream;
+    if (n == 0) {
+        if (d_hist) HIP_TRY(hipMemsetAsync(d_hist, 0, 4u << bits, s));
+        return RS_OK;
+    }
+    rs_status st = run_pass(p, (const uint32_t*)in_keys, (const uint32_t*)in_values,
+                            (uint32_t*)out_keys, (uint32_t*)out_values, (uint32_t)n, shift, bits,
+                            V, nullptr, 0, s);
+    if (st != RS_OK) return st;
+    if (d_hist) HIP_TRY(hipMemcpyAsync(d_hist, p->totals, 4u << bits, hipMemcpyDeviceToDevice, s));
+    return RS_OK;
+}
+
+RS_EXPORT rs_status rs_plan_info_get(const rs_plan* p, rs_plan_info* info) {
+    if (!p || !info) return fail(RS_ERR_INVALID_ARG, "rs_plan_info_get: null argument");
+    memset(info, 0, sizeof(*info));
+    info->passes = p->passes;
+    for (uint32_t i = 0; i < p->passes && i < 16; ++i) info->digit_bits[i] = p->widths[i];
+    info->tile_keys = kTile;
+    info->grid_blocks = geometry(p->capacity, kTile, kMaxGrid).grid;
+    info->workspace_bytes = p->workspace;
+    return RS_OK;
+}
+
+RS_EXPORT rs_status rs_plan_set_profiling(rs_plan* p, int enable) {
+    if (!p) return fail(RS_ERR_INVALID_ARG, "null plan");
+    p->timer.enabled = enable != 0;
+    return RS_OK;
+}
+
+RS_EXPORT rs_status rs_plan_kernel_times(rs_plan* p, double ms[RS_KERNEL_KINDS],
+                                         uint64_t launches[RS_KERNEL_KINDS]) {
+    if (!p) return fail(RS_ERR_INVALID_ARG, "null plan");
+    DeviceGuard guard(p->desc.device);
+    p->timer.drain();
+    for (int k = 0; k < RS_KERNEL_KINDS; ++k) {
+        if (ms) ms[k] = p->timer.ms[k];
+        if (launches) launches[k] = p->timer.launches[k];
+    }
+    return RS_OK;
+}
+
+RS_EXPORT rs_status rs_plan_reset_kernel_times(rs_plan* p) {
+    if (!p) return fail(RS_ERR_INVALID_ARG, "null plan");
+    DeviceGuard guard(p->desc.device);
+    p->timer.drain();
+    for (int k = 0; k < RS_KERNEL_KINDS; ++k) { p->timer.ms[k] = 0; p->timer.launches[k] = 0; }
+    return RS_OK;
+}
+
+// ---- prefix sum ----------------------------------------------------------------------------
+namespace {
+constexpr int kScanTile = 4096;
+}
+
+RS_EXPORT rs_status rs_scan_plan_create(int32_t device, uint64_t count, uint32_t wx, uint32_t wy,
+                                        uint32_t flags, rs_scan_plan** out) {
+    if (!out) return fail(RS_ERR_INVALID_ARG, "rs_scan_plan_create: null out");
+    *out = nullptr;
+    if (wx == 0) wx = 16;
+    if (wy == 0) wy = 16;
+    const uint64_t T = (uint64_t)wx * wy;
+    if ((T & (T - 1)) || T > 1024)
+        return fail(RS_ERR_NOT_POW2,
+                    "workgroupSize.x * workgroupSize.y must be a power of two. (current: %llu)",
+                    (unsigned long long)T);
+    if (count > 0xFFFFFFFFull) return fail(RS_ERR_INVALID_ARG, "count must be < 2^32");
+    if (flags & ~(uint32_t)RS_FLAG_AVOID_BANK_CONFLICTS)
+        return fail(RS_ERR_INVALID_ARG, "unknown flag bits 0x%x", flags);
+    rs_scan_plan* p = new (std::nothrow) rs_scan_plan();
+    if (!p) return fail(RS_ERR_OUT_OF_MEMORY, "host allocation failed");
+    p->device = device;
+    p->count = count;
+    DeviceGuard guard(device);
+    hipError_t e = hipMalloc((void**)&p->sums, 4ull * kMaxGrid);
+    if (e != hipSuccess) {
+        delete p;
+        return fail(RS_ERR_OUT_OF_MEMORY, "rs_scan_plan_create: %s", hipGetErrorString(e));
+    }
+    *out = p;
+    return RS_OK;
+}
+
+RS_EXPORT rs_status rs_scan_plan_run(rs_scan_plan* p, void* data, void* stream) {
+    if (!p) return fail(RS_ERR_INVALID_ARG, "rs_scan_plan_run: null plan");
+    if (p->count == 0) return RS_OK;
+    if (!data) return fail(RS_ERR_INVALID_ARG, "rs_scan_plan_run: null data");
+    DeviceGuard guard(p->device);
+    hipStream_t s = (hipStream_t)stream;
+    const uint32_t n = (uint32_t)p->count;
+    const Geometry geo = geometry(n, kScanTile, kMaxGrid);
+    hipLaunchKernelGGL(rs::k_chunk_sums<kScanTile>, dim3(geo.grid), dim3(rs::kBlock), 0, s,
+                       (const uint32_t*)data, n, geo.base, geo.extra, p->sums);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(rs::k_scan_small, dim3(1), dim3(rs::kBlock), 0, s, p->sums, geo.grid);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(rs::k_chunk_rescan<kScanTile>, dim3(geo.grid), dim3(rs::kBlock), 0, s,
+                       (uint32_t*)data, n, geo.base, geo.extra, (const uint32_t*)p->sums);
+    HIP_TRY(hipGetLastError());
+    return RS_OK;
+}
+
+RS_EXPORT void rs_scan_plan_destroy(rs_scan_plan* p) {
+    if (!p) return;
+    DeviceGuard guard(p->device);
+    (void)hipFree(p->sums);
+    delete p;
+}
+
+// ---- memory / streams ----------------------------------------------------------------------
+RS_EXPORT rs_status rs_device_count(int32_t* n) {
+    if (!n) return fail(RS_ERR_INVALID_ARG, "null");
+    int c = 0;
+    HIP_TRY(hipGetDeviceCount(&c));
+    *n = c;
+    return RS_OK;
+}
+
+RS_EXPORT rs_status rs_malloc(int32_t device, uint64_t bytes, void** ptr) {
+    if (!ptr) return fail(RS_ERR_INVALID_ARG, "null");
+    DeviceGuard guard(device);
+    HIP_TRY(hipMalloc(ptr, bytes ? bytes : 4));
+    return RS_OK;
+}
+
+RS_EXPORT rs_status rs_free(void* ptr) {
+    HIP_TRY(hipFree(ptr));
+    return RS_OK;
+}
+
+RS_EXPORT rs_status rs_memcpy_h2d(void* dst, const void* src, uint64_t bytes, void* stream) {
+    if (bytes == 0) return RS_OK;
+    HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, (hipStream_t)stream));
+    return RS_OK;
+}
+
+RS_EXPORT rs_status rs_memcpy_d2h(void* dst, const void* src, uint64_t bytes, void* stream) {
+    if (bytes == 0) return RS_OK;
+    HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, (hipStream_t)stream));
+    HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+    return RS_OK;
+}
+
+RS_EXPORT rs_status rs_memcpy_d2d(void* dst, const void* src, uint64_t bytes, void* stream) {
+    if (bytes == 0) return RS_OK;
+    HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    return RS_OK;
+}
+
+RS_EXPORT rs_status rs_stream_create(int32_t device, void** stream) {
+    if (!stream) return fail(RS_ERR_INVALID_ARG, "null");
+    DeviceGuard guard(device);
+    hipStream_t s;
+    HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    *stream = (void*)s;
+    return RS_OK;
+}
+
+RS_EXPORT rs_status rs_stream_destroy(void* stream) {
+    HIP_TRY(hipStreamDestroy((hipStream_t)stream));
+    return RS_OK;
+}
+
+RS_EXPORT rs_status rs_stream_synchronize(void* stream) {
+    HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+    return RS_OK;
+}
+
+RS_EXPORT rs_status rs_fill_random_u32(void* dst, uint64_t n, uint64_t seed, uint64_t start,
+                                       void* stream) {
+    if (n == 0) return RS_OK;
+    if (!dst) return fail(RS_ERR_INVALID_ARG, "null");
+    const uint32_t grid = (uint32_t)std::min<uint64_t>(8192, (n + rs::kBlock - 1) / rs::kBlock);
+    hipLaunchKernelGGL(rs::k_fill_random, dim3(grid), dim3(rs::kBlock), 0, (hipStream_t)stream,
+                       (uint32_t*)dst, n, seed, start);
+    HIP_TRY(hipGetLastError());
+    return RS_OK;
+}
+
+RS_EXPORT rs_status rs_fill_iota_u32(void* dst, uint64_t n, uint32_t first, void* stream) {
+    if (n == 0) return RS_OK;
+    if (!dst) return fail(RS_ERR_INVALID_ARG, "null");
+    const uint32_t grid = (uint32_t)std::min<uint64_t>(8192, (n + rs::kBlock - 1) / rs::kBlock);
+    hipLaunchKernelGGL(rs::k_fill_iota, dim3(grid), dim3(rs::kBlock), 0, (hipStream_t)stream,
+                       (uint32_t*)dst, n, first);
+    HIP_TRY(hipGetLastError());
+    return RS_OK;
+}
+
+RS_EXPORT rs_status rs_is_sorted(const void* keys, uint64_t n, uint32_t bit_count, void* d_flag,
+                                 void* stream) {
+    if (!d_flag) return fail(RS_ERR_INVALID_ARG, "null flag");
+    if (n > 0xFFFFFFFFull) return fail(RS_ERR_INVALID_ARG, "n must be < 2^32");
+    hipStream_t s = (hipStream_t)stream;
+    HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)d_flag, 1, 1, s));
+    if (n < 2) return RS_OK;
+    if (!keys) return fail(RS_ERR_INVALID_ARG, "null keys");
+    const uint32_t grid = (uint32_t)std::min<uint64_t>(kCheckGrid, (n + rs::kBlock - 1) / rs::kBlock);
+    hipLaunchKernelGGL(rs::k_is_sorted, dim3(grid), dim3(rs::kBlock), 0, s, (const uint32_t*)keys,
+                       (uint32_t)n, full_mask(bit_count ? bit_count : 32), (uint32_t*)d_flag);
+    HIP_TRY(hipGetLastError());
+    return RS_OK;
+}

@@ -1,0 +1,124 @@
+"""ctypes binding of librsort.so (include/rsort.h).
+
+The library is built in-tree (``webgpu-radix-sort_amd/lib/librsort.so``) by
+``__graft_entry__.build()`` or ``make -C webgpu-radix-sort_amd/csrc``.  There is no fallback:
+if the HIP library is missing, importing the sort raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.environ.get("RSORT_LIB", os.path.join(PKG_ROOT, "lib", "librsort.so"))
+HEADER_PATH = os.path.join(os.path.dirname(PKG_ROOT), "include", "rsort.h")
+
+RS_OK = 0
+RS_ERR_INVALID_ARG = 1
+RS_ERR_NOT_POW2 = 2
+RS_ERR_BIT_COUNT = 3
+RS_ERR_HIP = 4
+RS_ERR_OUT_OF_MEMORY = 5
+RS_ERR_CAPACITY = 6
+
+RS_FLAG_HAS_VALUES = 0x1
+RS_FLAG_CHECK_ORDER = 0x2
+RS_FLAG_LOCAL_SHUFFLE = 0x4
+RS_FLAG_AVOID_BANK_CONFLICTS = 0x8
+
+RS_KERNEL_HISTOGRAM, RS_KERNEL_SCAN, RS_KERNEL_SCATTER, RS_KERNEL_CHECK = range(4)
+RS_KERNEL_KINDS = 4
+KERNEL_NAMES = ("histogram", "scan", "scatter", "check")
+
+
+class RadixSortError(RuntimeError):
+    """A failed librsort call (status code + the library's last-error message)."""
+
+    def __init__(self, status: int, message: str):
+        super().__init__(message)
+        self.status = status
+
+
+class PlanDesc(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int32), ("count", ctypes.c_uint64),
+                ("bit_count", ctypes.c_uint32), ("workgroup_x", ctypes.c_uint32),
+                ("workgroup_y", ctypes.c_uint32), ("flags", ctypes.c_uint32),
+                ("radix_bits", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+
+
+class PlanInfo(ctypes.Structure):
+    _fields_ = [("passes", ctypes.c_uint32), ("digit_bits", ctypes.c_uint32 * 16),
+                ("tile_keys", ctypes.c_uint32), ("grid_blocks", ctypes.c_uint32),
+                ("workspace_bytes", ctypes.c_uint64)]
+
+
+_lib = None
+
+_VP = ctypes.c_void_p
+_SIGS = {
+    "rs_last_error": (ctypes.c_char_p, []),
+    "rs_status_string": (ctypes.c_char_p, [ctypes.c_int]),
+    "rs_version": (ctypes.c_uint32, []),
+    "rs_plan_create": (ctypes.c_int, [ctypes.POINTER(PlanDesc), ctypes.POINTER(_VP)]),
+    "rs_plan_sort": (ctypes.c_int, [_VP, _VP, _VP, _VP]),
+    "rs_plan_sort_n": (ctypes.c_int, [_VP, _VP, _VP, ctypes.c_uint64, _VP]),
+    "rs_plan_partition": (ctypes.c_int, [_VP, _VP, _VP, _VP, _VP, ctypes.c_uint64,
+                                         ctypes.c_uint32, ctypes.c_uint32, _VP, _VP]),
+    "rs_plan_info_get": (ctypes.c_int, [_VP, ctypes.POINTER(PlanInfo)]),
+    "rs_plan_set_profiling": (ctypes.c_int, [_VP, ctypes.c_int]),
+    "rs_plan_kernel_times": (ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_double),
+                                            ctypes.POINTER(ctypes.c_uint64)]),
+    "rs_plan_reset_kernel_times": (ctypes.c_int, [_VP]),
+    "rs_plan_destroy": (None, [_VP]),
+    "rs_scan_plan_create": (ctypes.c_int, [ctypes.c_int32, ctypes.c_uint64, ctypes.c_uint32,
+                                           ctypes.c_uint32, ctypes.c_uint32,
+                                           ctypes.POINTER(_VP)]),
+    "rs_scan_plan_run": (ctypes.c_int, [_VP, _VP, _VP]),
+    "rs_scan_plan_destroy": (None, [_VP]),
+    "rs_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int32)]),
+    "rs_malloc": (ctypes.c_int, [ctypes.c_int32, ctypes.c_uint64, ctypes.POINTER(_VP)]),
+    "rs_free": (ctypes.c_int, [_VP]),
+    "rs_memcpy_h2d": (ctypes.c_int, [_VP, _VP, ctypes.c_uint64, _VP]),
+    "rs_memcpy_d2h": (ctypes.c_int, [_VP, _VP, ctypes.c_uint64, _VP]),
+    "rs_memcpy_d2d": (ctypes.c_int, [_VP, _VP, ctypes.c_uint64, _VP]),
+    "rs_stream_create": (ctypes.c_int, [ctypes.c_int32, ctypes.POINTER(_VP)]),
+    "rs_stream_destroy": (ctypes.c_int, [_VP]),
+    "rs_stream_synchronize": (ctypes.c_int, [_VP]),
+    "rs_fill_random_u32": (ctypes.c_int, [_VP, ctypes.c_uint64, ctypes.c_uint64,
+                                          ctypes.c_uint64, _VP]),
+    "rs_fill_iota_u32": (ctypes.c_int, [_VP, ctypes.c_uint64, ctypes.c_uint32, _VP]),
+    "rs_is_sorted": (ctypes.c_int, [_VP, ctypes.c_uint64, ctypes.c_uint32, _VP, _VP]),
+}
+
+
+def header_functions(path: str = HEADER_PATH) -> list[str]:
+    """Names of the functions declared in include/rsort.h."""
+    src = open(path).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(rs_[a-z0-9_]+)\s*\(", src)))
+
+
+def load():
+    """Load librsort.so; raises (never falls back) when it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"librsort.so not found at {LIB_PATH}: build it with "
+            "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc, gfx950)")
+    L = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def check(status: int, what: str = "") -> None:
+    if status != RS_OK:
+        L = load()
+        msg = L.rs_last_error().decode(errors="replace")
+        raise RadixSortError(status, f"{what}: {msg}" if what else msg)

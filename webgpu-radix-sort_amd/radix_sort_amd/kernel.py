@@ -1,0 +1,297 @@
+"""Host-side mirror of the reference's kernel classes, over the HIP C ABI.
+
+Reference surface (MatthieuLepers/WebGPU-Radix-Sort v1.0.7):
+
+* README API: ``new RadixSortKernel({device, keys, values, count, check_order, bit_count,
+  workgroup_size, local_shuffle, avoid_bank_conflicts})`` (README.md:72-88,129,168)
+* shipped API: ``new RadixSortBufferKernel({device, data: {keys, values}, count, bitCount,
+  workgroupSize, checkOrder, localShuffle, avoidBankConflicts})``
+  (src/kernels/radix-sort/RadixSortBufferKernel.ts:9-32, AbstractRadixSortKernel.ts:14-19,52-57,
+  AbstractKernel.ts:3-7,22-25)
+* ``kernel.dispatch(pass)`` sorts ``buffers.keys`` / ``buffers.values`` in place
+  (AbstractRadixSortKernel.ts:221-276); the harness reads ``kernel.buffers.keys``
+  (example/tests.ts:72-74)
+* ``new PrefixSumKernel({device, data, count, workgroupSize, avoidBankConflicts}).dispatch(pass)``
+  (src/kernels/PrefixSumKernel.ts:24-43,147-158): in-place exclusive scan.
+
+Both option spellings are accepted.  Errors mirror the reference: a non-power-of-two workgroup
+raises (PrefixSumKernel.ts:33-35: "workgroupSize.x * workgroupSize.y must be a power of two");
+bit_count must be a multiple of 4 (README.md:97, unchecked in the reference - SURVEY Q4).
+``workgroup_size``, ``local_shuffle`` and ``avoid_bank_conflicts`` never change results (the
+HIP kernels use their own tuned geometry, and always stage the scatter through LDS).
+
+Buffers are device memory: torch CUDA tensors (uint32 / int32 / float32, contiguous),
+:class:`DeviceBuffer` objects, or raw device pointers (int).  ``dispatch`` is asynchronous on the
+given stream (default: torch's current stream for tensors, else the null stream).
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Any
+
+import numpy as np
+
+from . import _lib
+from ._lib import RadixSortError, check
+
+_SENTINEL = object()
+
+
+class DeviceBuffer:
+    """A device allocation owned by librsort (the reference's GPUBuffer from createBuffers,
+    example/tests.ts:227-244)."""
+
+    def __init__(self, nbytes: int, device: int = 0):
+        L = _lib.load()
+        p = ctypes.c_void_p()
+        check(L.rs_malloc(device, nbytes, ctypes.byref(p)), "rs_malloc")
+        self.ptr = p.value
+        self.nbytes = nbytes
+        self.device = device
+
+    @classmethod
+    def from_numpy(cls, arr: np.ndarray, device: int = 0) -> "DeviceBuffer":
+        a = np.ascontiguousarray(arr)
+        b = cls(a.nbytes, device)
+        b.write(a)
+        return b
+
+    def write(self, arr: np.ndarray, stream: int | None = None) -> None:
+        a = np.ascontiguousarray(arr)
+        if a.nbytes > self.nbytes:
+            raise ValueError("array larger than buffer")
+        L = _lib.load()
+        check(L.rs_memcpy_h2d(self.ptr, a.ctypes.data, a.nbytes, stream), "rs_memcpy_h2d")
+        check(L.rs_stream_synchronize(stream), "rs_stream_synchronize")
+
+    def read(self, dtype=np.uint32, count: int | None = None, stream: int | None = None) -> np.ndarray:
+        itemsize = np.dtype(dtype).itemsize
+        n = self.nbytes // itemsize if count is None else count
+        out = np.empty(n, dtype=dtype)
+        check(_lib.load().rs_memcpy_d2h(out.ctypes.data, self.ptr, n * itemsize, stream),
+              "rs_memcpy_d2h")
+        return out
+
+    def free(self) -> None:
+        if self.ptr:
+            check(_lib.load().rs_free(self.ptr), "rs_free")
+            self.ptr = None
+
+    def __del__(self):  # pragma: no cover - best effort
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def _is_torch(x) -> bool:
+    return type(x).__module__.startswith("torch") and hasattr(x, "data_ptr")
+
+
+def _buffer_info(buf, name: str):
+    """-> (device pointer, capacity in u32 elements or None, device ordinal or None)."""
+    if buf is None:
+        return None, None, None
+    if _is_torch(buf):
+        import torch
+        if buf.device.type != "cuda":
+            raise RadixSortError(_lib.RS_ERR_INVALID_ARG, f"{name} must be a device (cuda) tensor")
+        if buf.element_size() != 4:
+            raise RadixSortError(_lib.RS_ERR_INVALID_ARG,
+                                 f"{name}: elements must be 4 bytes (README.md limitations)")
+        if not buf.is_contiguous():
+            raise RadixSortError(_lib.RS_ERR_INVALID_ARG, f"{name} must be contiguous")
+        del torch
+        return buf.data_ptr(), buf.numel(), buf.device.index
+    if isinstance(buf, DeviceBuffer):
+        return buf.ptr, buf.nbytes // 4, buf.device
+    if isinstance(buf, int):
+        return buf, None, None
+    raise RadixSortError(_lib.RS_ERR_INVALID_ARG, f"unsupported {name} buffer type {type(buf)!r}")
+
+
+def _device_ordinal(device, *fallbacks) -> int:
+    if device is None or device is _SENTINEL:
+        for f in fallbacks:
+            if f is not None:
+                return int(f)
+        return 0
+    if isinstance(device, int):
+        return device
+    if hasattr(device, "index"):  # torch.device
+        return 0 if device.index is None else int(device.index)
+    if isinstance(device, str):
+        return int(device.split(":")[1]) if ":" in device else 0
+    raise RadixSortError(_lib.RS_ERR_INVALID_ARG, f"unsupported device {device!r}")
+
+
+def _stream_handle(stream, uses_torch: bool, device: int):
+    if stream is None:
+        if uses_torch:
+            import torch
+            return torch.cuda.current_stream(device).cuda_stream
+        return None
+    if isinstance(stream, int):
+        return stream
+    if hasattr(stream, "cuda_stream"):
+        return stream.cuda_stream
+    raise RadixSortError(_lib.RS_ERR_INVALID_ARG, f"unsupported stream {stream!r}")
+
+
+def _pick(opts: dict, *names, default=None):
+    for n in names:
+        if n in opts and opts[n] is not None:
+            return opts[n]
+    return default
+
+
+def _workgroup(ws) -> tuple[int, int]:
+    if ws is None:
+        return 16, 16
+    if isinstance(ws, dict):
+        return int(ws.get("x", 16)), int(ws.get("y", 1 if "x" in ws else 16))
+    if isinstance(ws, (tuple, list)):
+        return int(ws[0]), int(ws[1]) if len(ws) > 1 else 1
+    return int(ws), 1
+
+
+class RadixSortKernel:
+    """Drop-in for ``RadixSortKernel`` / ``RadixSortBufferKernel``: sorts ``keys`` (and
+    ``values``) in place, ascending and stable by the low ``bit_count`` bits."""
+
+    def __init__(self, options: dict | None = None, **kw: Any):
+        opts = dict(options or {})
+        opts.update(kw)
+        data = opts.get("data") or {}
+        keys = _pick(opts, "keys") if "keys" in opts else data.get("keys")
+        values = _pick(opts, "values") if "values" in opts else data.get("values")
+        if keys is None:
+            raise RadixSortError(_lib.RS_ERR_INVALID_ARG, "keys buffer is required")
+        kptr, kcap, kdev = _buffer_info(keys, "keys")
+        vptr, vcap, vdev = _buffer_info(values, "values")
+        count = _pick(opts, "count")
+        if count is None:
+            if kcap is None:
+                raise RadixSortError(_lib.RS_ERR_INVALID_ARG, "count is required with raw pointers")
+            count = kcap
+        count = int(count)
+        for cap, name in ((kcap, "keys"), (vcap, "values")):
+            if cap is not None and cap < count:
+                raise RadixSortError(_lib.RS_ERR_INVALID_ARG,
+                                     f"{name} buffer holds {cap} elements < count {count}")
+        self.device = _device_ordinal(opts.get("device", _SENTINEL), kdev, vdev)
+        self.count = count
+        self.bit_count = int(_pick(opts, "bit_count", "bitCount", default=32))
+        wx, wy = _workgroup(_pick(opts, "workgroup_size", "workgroupSize"))
+        self.workgroup_size = {"x": wx, "y": wy}
+        self.check_order = bool(_pick(opts, "check_order", "checkOrder", default=False))
+        self.local_shuffle = bool(_pick(opts, "local_shuffle", "localShuffle", default=False))
+        self.avoid_bank_conflicts = bool(_pick(opts, "avoid_bank_conflicts", "avoidBankConflicts",
+                                               default=False))
+        self.radix_bits = int(_pick(opts, "radix_bits", "radixBits", default=0))
+        self.has_values = values is not None
+        self.buffers = {"keys": keys}
+        if values is not None:
+            self.buffers["values"] = values
+        self._uses_torch = _is_torch(keys)
+        self._ptrs = (kptr, vptr)
+        flags = ((_lib.RS_FLAG_HAS_VALUES if self.has_values else 0)
+                 | (_lib.RS_FLAG_CHECK_ORDER if self.check_order else 0)
+                 | (_lib.RS_FLAG_LOCAL_SHUFFLE if self.local_shuffle else 0)
+                 | (_lib.RS_FLAG_AVOID_BANK_CONFLICTS if self.avoid_bank_conflicts else 0))
+        desc = _lib.PlanDesc(self.device, count, self.bit_count, wx, wy, flags, self.radix_bits, 0)
+        L = _lib.load()
+        plan = ctypes.c_void_p()
+        check(L.rs_plan_create(ctypes.byref(desc), ctypes.byref(plan)), "RadixSortKernel")
+        self._plan = plan
+
+    # -- reference surface --------------------------------------------------------------------
+    def dispatch(self, pass_=None) -> None:
+        """Sort in place, asynchronously on ``pass_`` (a stream; None = current stream)."""
+        s = _stream_handle(pass_, self._uses_torch, self.device)
+        check(_lib.load().rs_plan_sort(self._plan, self._ptrs[0], self._ptrs[1], s), "dispatch")
+
+    def destroy(self) -> None:
+        if getattr(self, "_plan", None):
+            _lib.load().rs_plan_destroy(self._plan)
+            self._plan = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.destroy()
+        except Exception:
+            pass
+
+    # -- extras ----------------------------------------------------------------------------
+    @property
+    def info(self) -> dict:
+        inf = _lib.PlanInfo()
+        check(_lib.load().rs_plan_info_get(self._plan, ctypes.byref(inf)), "info")
+        return {"passes": inf.passes, "digit_bits": list(inf.digit_bits[: inf.passes]),
+                "tile_keys": inf.tile_keys, "grid_blocks": inf.grid_blocks,
+                "workspace_bytes": inf.workspace_bytes}
+
+    def set_profiling(self, enable: bool) -> None:
+        check(_lib.load().rs_plan_set_profiling(self._plan, 1 if enable else 0), "profiling")
+
+    def kernel_times(self, reset: bool = False) -> dict:
+        ms = (ctypes.c_double * _lib.RS_KERNEL_KINDS)()
+        n = (ctypes.c_uint64 * _lib.RS_KERNEL_KINDS)()
+        L = _lib.load()
+        check(L.rs_plan_kernel_times(self._plan, ms, n), "kernel_times")
+        if reset:
+            check(L.rs_plan_reset_kernel_times(self._plan), "reset_kernel_times")
+        return {name: {"ms": ms[i], "launches": n[i]} for i, name in enumerate(_lib.KERNEL_NAMES)}
+
+
+RadixSortBufferKernel = RadixSortKernel
+
+
+class PrefixSumKernel:
+    """Drop-in for ``PrefixSumKernel``: in-place exclusive scan (mod 2^32) of data[:count]."""
+
+    def __init__(self, options: dict | None = None, **kw: Any):
+        opts = dict(options or {})
+        opts.update(kw)
+        data = opts.get("data")
+        if data is None:
+            raise RadixSortError(_lib.RS_ERR_INVALID_ARG, "data buffer is required")
+        ptr, cap, dev = _buffer_info(data, "data")
+        count = _pick(opts, "count", default=cap)
+        if count is None:
+            raise RadixSortError(_lib.RS_ERR_INVALID_ARG, "count is required with raw pointers")
+        count = int(count)
+        if cap is not None and cap < count:
+            raise RadixSortError(_lib.RS_ERR_INVALID_ARG, f"data holds {cap} elements < count {count}")
+        wx, wy = _workgroup(_pick(opts, "workgroup_size", "workgroupSize"))
+        self.device = _device_ordinal(opts.get("device", _SENTINEL), dev)
+        self.count = count
+        self.workgroup_size = {"x": wx, "y": wy}
+        self.avoid_bank_conflicts = bool(_pick(opts, "avoid_bank_conflicts", "avoidBankConflicts",
+                                               default=False))
+        self.data = data
+        self._ptr = ptr
+        self._uses_torch = _is_torch(data)
+        plan = ctypes.c_void_p()
+        flags = _lib.RS_FLAG_AVOID_BANK_CONFLICTS if self.avoid_bank_conflicts else 0
+        check(_lib.load().rs_scan_plan_create(self.device, count, wx, wy, flags,
+                                              ctypes.byref(plan)), "PrefixSumKernel")
+        self._plan = plan
+
+    def dispatch(self, pass_=None, dispatch_size_buffer=None, offset: int = 0) -> None:
+        if dispatch_size_buffer is not None:
+            raise RadixSortError(_lib.RS_ERR_INVALID_ARG,
+                                 "indirect dispatch buffers are not used by the HIP backend")
+        s = _stream_handle(pass_, self._uses_torch, self.device)
+        check(_lib.load().rs_scan_plan_run(self._plan, self._ptr, s), "dispatch")
+
+    def destroy(self) -> None:
+        if getattr(self, "_plan", None):
+            _lib.load().rs_scan_plan_destroy(self._plan)
+            self._plan = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.destroy()
+        except Exception:
+            pass

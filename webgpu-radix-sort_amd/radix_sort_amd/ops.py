@@ -1,0 +1,77 @@
+"""Torch-tensor conveniences over the C ABI: synthetic inputs, order check, sort plans that can
+be re-used with varying counts, and the single-pass stable partition used by the multi-GPU
+bucket exchange.  All compute is in librsort.so."""
+from __future__ import annotations
+
+import ctypes
+
+from . import _lib
+from ._lib import check
+
+
+def _stream(t, stream=None):
+    import torch
+    if stream is not None:
+        return stream if isinstance(stream, int) else stream.cuda_stream
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def fill_random_u32(t, seed: int, start: int = 0, stream=None) -> None:
+    """t[i] = rs generator(seed, start + i) (same as oracle.gen_u32)."""
+    check(_lib.load().rs_fill_random_u32(t.data_ptr(), t.numel(), seed, start, _stream(t, stream)),
+          "rs_fill_random_u32")
+
+
+def fill_iota_u32(t, first: int = 0, stream=None) -> None:
+    check(_lib.load().rs_fill_iota_u32(t.data_ptr(), t.numel(), first, _stream(t, stream)),
+          "rs_fill_iota_u32")
+
+
+def is_sorted(t, n: int | None = None, bit_count: int = 32, stream=None) -> bool:
+    import torch
+    flag = torch.empty(1, dtype=torch.int32, device=t.device)
+    n = t.numel() if n is None else n
+    check(_lib.load().rs_is_sorted(t.data_ptr(), n, bit_count, flag.data_ptr(), _stream(t, stream)),
+          "rs_is_sorted")
+    return bool(flag.item())
+
+
+class SortPlan:
+    """A sort plan with a capacity; sorts any n <= capacity (multi-GPU receive buffers)."""
+
+    def __init__(self, device: int, capacity: int, has_values: bool, bit_count: int = 32,
+                 radix_bits: int = 0, check_order: bool = False):
+        flags = (_lib.RS_FLAG_HAS_VALUES if has_values else 0) | \
+                (_lib.RS_FLAG_CHECK_ORDER if check_order else 0) | _lib.RS_FLAG_LOCAL_SHUFFLE
+        desc = _lib.PlanDesc(device, capacity, bit_count, 16, 16, flags, radix_bits, 0)
+        p = ctypes.c_void_p()
+        check(_lib.load().rs_plan_create(ctypes.byref(desc), ctypes.byref(p)), "SortPlan")
+        self._plan = p
+        self.capacity = capacity
+        self.has_values = has_values
+
+    def sort(self, keys, values=None, n: int | None = None, stream=None) -> None:
+        n = keys.numel() if n is None else n
+        check(_lib.load().rs_plan_sort_n(self._plan, keys.data_ptr(),
+                                         None if values is None else values.data_ptr(), n,
+                                         _stream(keys, stream)), "rs_plan_sort_n")
+
+    def partition(self, in_keys, in_values, out_keys, out_values, n: int, shift: int, bits: int,
+                  hist=None, stream=None) -> None:
+        """Stable one-digit scatter in -> out; hist (device u32[2^bits]) gets digit totals."""
+        check(_lib.load().rs_plan_partition(
+            self._plan, in_keys.data_ptr(), None if in_values is None else in_values.data_ptr(),
+            out_keys.data_ptr(), None if out_values is None else out_values.data_ptr(), n, shift,
+            bits, None if hist is None else hist.data_ptr(), _stream(in_keys, stream)),
+            "rs_plan_partition")
+
+    def destroy(self) -> None:
+        if getattr(self, "_plan", None):
+            _lib.load().rs_plan_destroy(self._plan)
+            self._plan = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.destroy()
+        except Exception:
+            pass

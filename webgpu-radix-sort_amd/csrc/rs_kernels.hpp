@@ -25,6 +25,22 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#ifndef RS_KV_INTERLEAVED
+#define RS_KV_INTERLEAVED 1  // stage (key, value) pairs as one 64-bit LDS word (ds_write_b64/ds_read_b64)
+#endif
+#ifndef RS_NT_LOAD
+#define RS_NT_LOAD 0         // 1: non-temporal (streaming) loads of the pass input
+#endif
+#ifndef RS_NT_STORE
+#define RS_NT_STORE 0        // 1: all scatter stores nt; 2: nt only for lines fully written by the tile
+#endif
+#ifndef RS_XCD_GROUP
+#define RS_XCD_GROUP 1       // interleaved mode: consecutive tiles run on one XCD in the same round
+#endif
+#ifndef RS_SCATTER_DEBUG
+#define RS_SCATTER_DEBUG 0   // ablations for tools/sweep.py: 1 linear writes, 3 no stores
+#endif
+
 namespace rs {
 
 constexpr int kBlock = 256;              // threads per workgroup: 4 waves of 64
@@ -91,12 +107,15 @@ __device__ __forceinline__ Chunk chunk_of(uint32_t g, uint32_t base, uint32_t ex
 }
 
 // ---- histogram (upsweep) -----------------------------------------------------------------
-// counts[d * G + g] = number of keys of workgroup g's chunk whose digit is d.
+// counts[d * G + g] = number of keys of workgroup g's chunk whose digit is d.  Each thread keeps
+// UNROLL 16-byte loads in flight; per-wave LDS histograms (ds_add_u32, no return).
 template <int R, int TILE>
 __global__ __launch_bounds__(kBlock) void k_histogram(
     const uint32_t* __restrict__ keys, uint32_t n, uint32_t shift, uint32_t mask,
     uint32_t base, uint32_t extra, uint32_t* __restrict__ counts, const uint32_t* gate, int pass) {
     constexpr int RADIX = 1 << R;
+    constexpr int UNROLL = 8;
+    constexpr uint32_t STEP = 4u * kBlock * UNROLL;     // keys per block iteration
     __shared__ uint32_t hist[kWaves][RADIX];
     if (gated_off(gate, pass)) return;
     const uint32_t G = gridDim.x, g = blockIdx.x, tid = threadIdx.x, w = tid >> 6;
@@ -111,14 +130,19 @@ __global__ __launch_bounds__(kBlock) void k_histogram(
     const bool vec = (((uintptr_t)keys) & 15u) == 0;
     uint32_t i = lo;
     if (vec) {
-        // 16-byte loads: every lane reads 4 consecutive keys; 1 KiB per wave-instruction.
-        const uint32_t full_end = lo + ((hi - lo) & ~(uint32_t)(4 * kBlock - 1));
-        for (; i < full_end; i += 4 * kBlock) {
-            const uint4 q = *reinterpret_cast<const uint4*>(keys + i + 4 * tid);
-            atomicAdd(&h[(q.x >> shift) & mask], 1u);
-            atomicAdd(&h[(q.y >> shift) & mask], 1u);
-            atomicAdd(&h[(q.z >> shift) & mask], 1u);
-            atomicAdd(&h[(q.w >> shift) & mask], 1u);
+        const uint32_t full_end = lo + ((hi - lo) / STEP) * STEP;
+        for (; i < full_end; i += STEP) {
+            uint4 q[UNROLL];
+#pragma unroll
+            for (int u = 0; u < UNROLL; ++u)
+                q[u] = *reinterpret_cast<const uint4*>(keys + i + u * (4 * kBlock) + 4 * tid);
+#pragma unroll
+            for (int u = 0; u < UNROLL; ++u) {
+                atomicAdd(&h[(q[u].x >> shift) & mask], 1u);
+                atomicAdd(&h[(q[u].y >> shift) & mask], 1u);
+                atomicAdd(&h[(q[u].z >> shift) & mask], 1u);
+                atomicAdd(&h[(q[u].w >> shift) & mask], 1u);
+            }
         }
     }
     for (uint32_t j = i + tid; j < hi; j += kBlock) atomicAdd(&h[(keys[j] >> shift) & mask], 1u);
@@ -131,159 +155,366 @@ __global__ __launch_bounds__(kBlock) void k_histogram(
     }
 }
 
+// Tile-interleaved variant: workgroup g owns tiles g, g+G, g+2G, ... and writes one count row
+// entry per TILE: counts[d * ntiles + t].  With this ownership the workgroups running at the
+// same time work on adjacent tiles, so their scatter writes for each digit form one contiguous
+// stream instead of one cursor per workgroup.
+template <int R, int TILE, int HB>
+__global__ __launch_bounds__(HB) void k_histogram_tiles(
+    const uint32_t* __restrict__ keys, uint32_t n, uint32_t shift, uint32_t mask,
+    uint32_t ntiles, uint32_t* __restrict__ counts, const uint32_t* gate, int pass) {
+    constexpr int RADIX = 1 << R;
+    constexpr int NW = HB / 64;
+    constexpr int PER = TILE / (4 * HB);               // uint4 loads per thread per tile
+    static_assert(TILE % (4 * HB) == 0, "tile must be a multiple of 4*HB");
+    __shared__ uint32_t hist[NW][RADIX];
+    if (gated_off(gate, pass)) return;
+    const uint32_t G = gridDim.x, tid = threadIdx.x, w = tid >> 6;
+    uint32_t* h = hist[w];
+    const bool vec = (((uintptr_t)keys) & 15u) == 0;
+    for (uint32_t t = blockIdx.x; t < ntiles; t += G) {
+        for (uint32_t i = tid; i < (uint32_t)(NW * RADIX); i += HB) (&hist[0][0])[i] = 0u;
+        __syncthreads();
+        const uint32_t lo = t * (uint32_t)TILE;
+        if (vec && (uint64_t)lo + TILE <= n) {
+            uint4 q[PER];
+#pragma unroll
+            for (int u = 0; u < PER; ++u)
+                q[u] = *reinterpret_cast<const uint4*>(keys + lo + u * (4 * HB) + 4 * tid);
+#pragma unroll
+            for (int u = 0; u < PER; ++u) {
+                atomicAdd(&h[(q[u].x >> shift) & mask], 1u);
+                atomicAdd(&h[(q[u].y >> shift) & mask], 1u);
+                atomicAdd(&h[(q[u].z >> shift) & mask], 1u);
+                atomicAdd(&h[(q[u].w >> shift) & mask], 1u);
+            }
+        } else {
+            const uint32_t hi = (uint64_t)lo + TILE < n ? lo + (uint32_t)TILE : n;
+            for (uint32_t j = lo + tid; j < hi; j += HB) atomicAdd(&h[(keys[j] >> shift) & mask], 1u);
+        }
+        __syncthreads();
+        for (uint32_t d = tid; d < (uint32_t)RADIX; d += HB) {
+            uint32_t c = 0;
+#pragma unroll
+            for (int v = 0; v < NW; ++v) c += hist[v][d];
+            counts[(size_t)d * ntiles + t] = c;
+        }
+        __syncthreads();
+    }
+}
+
 // ---- digit x workgroup scan ----------------------------------------------------------------
-// Block d scans row d of counts (G entries) to an exclusive prefix in place and writes the row
-// total to totals[d].
-__global__ __launch_bounds__(kBlock) void k_scan_rows(uint32_t* __restrict__ counts, uint32_t G,
+// Block d scans row d of counts (rowlen entries) to an exclusive prefix in place and writes the
+// row total to totals[d].  The row goes through LDS in segments of SCAN_SEG entries: coalesced
+// loads, each thread then owns SCAN_SEG/256 CONTIGUOUS entries (thread-local scan + one block
+// scan per segment), coalesced stores.
+constexpr int kScanSeg = 8192;
+__global__ __launch_bounds__(kBlock) void k_scan_rows(uint32_t* __restrict__ counts,
+                                                      uint32_t rowlen,
                                                       uint32_t* __restrict__ totals,
                                                       const uint32_t* gate, int pass) {
+    constexpr int PER = kScanSeg / kBlock;   // contiguous entries per thread
+    __shared__ uint32_t buf[kScanSeg + kScanSeg / 32];   // +1 word per 32: conflict-free rows
     __shared__ uint32_t scratch[kWaves];
     if (gated_off(gate, pass)) return;
-    uint32_t* row = counts + (size_t)blockIdx.x * G;
-    const uint32_t per = (G + kBlock - 1) / kBlock;
-    const uint32_t b0 = threadIdx.x * per;
-    uint32_t s = 0;
-    for (uint32_t k = 0; k < per; ++k)
-        if (b0 + k < G) s += row[b0 + k];
-    uint32_t tot;
-    uint32_t run = block_excl_scan(s, scratch, tot);
-    for (uint32_t k = 0; k < per; ++k)
-        if (b0 + k < G) {
-            uint32_t c = row[b0 + k];
-            row[b0 + k] = run;
-            run += c;
-        }
-    if (threadIdx.x == 0) totals[blockIdx.x] = tot;
+    uint32_t* row = counts + (size_t)blockIdx.x * rowlen;
+    const uint32_t tid = threadIdx.x;
+    auto at = [](uint32_t i) { return i + (i >> 5); };
+    uint32_t carry = 0;
+    for (uint32_t seg0 = 0; seg0 < rowlen; seg0 += kScanSeg) {
+        const uint32_t len = rowlen - seg0 < (uint32_t)kScanSeg ? rowlen - seg0 : (uint32_t)kScanSeg;
+#pragma unroll 8
+        for (uint32_t i = tid; i < (uint32_t)kScanSeg; i += kBlock)
+            buf[at(i)] = i < len ? row[seg0 + i] : 0u;
+        __syncthreads();
+        uint32_t x[PER], sum = 0;
+#pragma unroll
+        for (int q = 0; q < PER; ++q) { x[q] = buf[at(tid * PER + q)]; sum += x[q]; }
+        uint32_t tot;
+        uint32_t run = carry + block_excl_scan(sum, scratch, tot);
+#pragma unroll
+        for (int q = 0; q < PER; ++q) { buf[at(tid * PER + q)] = run; run += x[q]; }
+        __syncthreads();
+#pragma unroll 8
+        for (uint32_t i = tid; i < len; i += kBlock) row[seg0 + i] = buf[at(i)];
+        carry += tot;
+        __syncthreads();
+    }
+    if (tid == 0) totals[blockIdx.x] = carry;
 }
 
 // ---- rank + local shuffle + scatter (downsweep) ----------------------------------------
-// Tile = 256 threads x KPT keys.  Wave w owns positions [w*64*KPT, (w+1)*64*KPT) of the tile;
-// slot j of lane l is position w*64*KPT + j*64 + l (coalesced 256-B loads per slot).
-template <int R, int KPT, bool HAS_VALUES, bool STAGED>
-__global__ __launch_bounds__(kBlock) void k_scatter(
-    const uint32_t* __restrict__ in_k, const uint32_t* __restrict__ in_v,
-    uint32_t* __restrict__ out_k, uint32_t* __restrict__ out_v, uint32_t n, uint32_t shift,
-    uint32_t mask, uint32_t nbits, uint32_t base, uint32_t extra,
-    const uint32_t* __restrict__ counts, const uint32_t* __restrict__ totals,
-    const uint32_t* gate, int pass) {
-    constexpr int RADIX = 1 << R;
-    constexpr int TILE = kBlock * KPT;
-    constexpr int WAVE_KEYS = 64 * KPT;
-    static_assert(RADIX <= kBlock, "one digit per thread");
-    __shared__ uint32_t s_whist[kWaves][RADIX];     // per-wave counts -> per-wave tile offsets
-    __shared__ uint32_t s_gdelta[RADIX];             // global pos - tile pos, per digit
-    __shared__ uint32_t s_scratch[kWaves];
-    __shared__ uint32_t s_keys[STAGED ? TILE : 1];
-    __shared__ uint32_t s_vals[(STAGED && HAS_VALUES) ? TILE : 1];
+// Tile = BLOCK threads x KPT keys.  Wave w owns positions [w*64*KPT, (w+1)*64*KPT) of the
+// tile; slot j of lane l is position w*64*KPT + j*64 + l (coalesced 256-B loads per slot).
+//
+// In-wave stable rank, two implementations (same result, tested against each other):
+//  * RANK_LDS_ATOMIC: every lane does ds_add_rtn_u32(&wave_count[digit], 1).  gfx950's LDS
+//    resolves one wave's same-address atomics in lane order (probed: tools/lds_order_probe.hip,
+//    6.4e8 lane atomics over random / 4-address / single-address / same-bank / partial-exec
+//    patterns, 0 out of order), so the returned value is the number of same-digit keys in
+//    earlier slots and lower lanes: the stable rank, for ~3 VALU + 1 LDS op per 64 keys.
+//  * RANK_BALLOT: match mask from R ballots (lanes sharing my digit), mbcnt for the rank in
+//    the slot, the lowest lane bumps the wave counter (ds_add_rtn) and broadcasts it
+//    (ds_bpermute).  Architecture-guaranteed; ~60 VALU per 64 keys.  Selected with
+//    RSORT_RANK=ballot.
+enum RankMode { RANK_LDS_ATOMIC = 0, RANK_BALLOT = 1 };
 
-    if (gated_off(gate, pass)) return;
-    const uint32_t G = gridDim.x, g = blockIdx.x, tid = threadIdx.x;
-    const uint32_t w = tid >> 6, lane = lane_id();
-
-    // Running global base of digit `tid` for this workgroup:
-    //   sum of totals of smaller digits + this row's exclusive prefix.
-    uint32_t dtot = (tid < (uint32_t)RADIX) ? totals[tid] : 0u;
-    uint32_t all;
-    uint32_t run = block_excl_scan(dtot, s_scratch, all);
-    if (tid < (uint32_t)RADIX) run += counts[(size_t)tid * G + g];
-
-    const Chunk ch = chunk_of(g, base, extra);
-    for (uint32_t t = 0; t < ch.count; ++t) {
-        const uint32_t tile0 = (ch.first + t) * (uint32_t)TILE;
-        const uint32_t wbase = tile0 + w * WAVE_KEYS;
-        uint32_t k[KPT];
-        uint32_t v[HAS_VALUES ? KPT : 1];
-        uint32_t rank[KPT];
+template <int KPT, bool HAS_VALUES>
+__device__ __forceinline__ void load_tile(const uint32_t* __restrict__ in_k,
+                                          const uint32_t* __restrict__ in_v, uint32_t wbase,
+                                          uint32_t n, bool full, uint32_t (&k)[KPT],
+                                          uint32_t (&v)[HAS_VALUES ? KPT : 1]) {
+    const uint32_t lane = lane_id();
+    if (full) {
+#if RS_NT_LOAD
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) k[j] = __builtin_nontemporal_load(in_k + wbase + j * 64 + lane);
+        if (HAS_VALUES) {
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) v[j] = __builtin_nontemporal_load(in_v + wbase + j * 64 + lane);
+        }
+#else
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) k[j] = in_k[wbase + j * 64 + lane];
+        if (HAS_VALUES) {
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) v[j] = in_v[wbase + j * 64 + lane];
+        }
+#endif
+    } else {
 #pragma unroll
         for (int j = 0; j < KPT; ++j) {
             const uint32_t p = wbase + j * 64 + lane;
             k[j] = (p < n) ? in_k[p] : 0u;
             if (HAS_VALUES) v[j] = (p < n) ? in_v[p] : 0u;
         }
+    }
+}
+
+// Lanes of this wave whose digit equals mine (restricted to `valid`): AND over the digit bits
+// of (bit set ? ballot(bit) : ~ballot(bit)).
+template <int R>
+__device__ __forceinline__ uint64_t match_mask(uint32_t d, uint64_t valid) {
+    uint32_t mlo = (uint32_t)valid, mhi = (uint32_t)(valid >> 32);
+#pragma unroll
+    for (int b = 0; b < R; ++b) {
+        const uint32_t x = (uint32_t)__builtin_amdgcn_sbfe((int)d, b, 1);
+        const uint64_t bb = __ballot(x != 0u);
+        mlo &= ~((uint32_t)bb ^ x);
+        mhi &= ~((uint32_t)(bb >> 32) ^ x);
+    }
+    return ((uint64_t)mhi << 32) | mlo;
+}
+
+// Exclusive scan over a BLOCK-thread workgroup (NW waves); scratch >= NW u32 of LDS.
+template <int NW>
+__device__ __forceinline__ uint32_t block_excl_scan_n(uint32_t v, uint32_t* scratch, uint32_t& total) {
+    const uint32_t inc = wave_incl_scan(v);
+    const uint32_t w = threadIdx.x >> 6;
+    if (lane_id() == 63) scratch[w] = inc;
+    __syncthreads();
+    uint32_t pre = 0, tot = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < (uint32_t)NW; ++i) {
+        uint32_t s = scratch[i];
+        pre += (i < w) ? s : 0u;
+        tot += s;
+    }
+    __syncthreads();
+    total = tot;
+    return pre + inc - v;
+}
+
+template <int R, int BLOCK, int KPT, bool HAS_VALUES, int RANK, bool IL>
+__global__ __launch_bounds__(BLOCK) void k_scatter(
+    const uint32_t* __restrict__ in_k, const uint32_t* __restrict__ in_v,
+    uint32_t* __restrict__ out_k, uint32_t* __restrict__ out_v, uint32_t n, uint32_t shift,
+    uint32_t mask, uint32_t base, uint32_t extra, const uint32_t* __restrict__ counts,
+    const uint32_t* __restrict__ totals, const uint32_t* gate, int pass) {
+    constexpr int RADIX = 1 << R;
+    constexpr int NW = BLOCK / 64;
+    constexpr int TILE = BLOCK * KPT;
+    constexpr int WAVE_KEYS = 64 * KPT;
+    static_assert(RADIX <= BLOCK, "one digit per thread");
+    __shared__ uint32_t s_whist[NW][RADIX];          // per-wave counts -> per-wave tile offsets
+    __shared__ uint32_t s_gdelta[RADIX];             // global pos - tile pos, per digit
+#if RS_NT_STORE == 2 || RS_SCATTER_DEBUG >= 4
+    __shared__ uint2 s_run[RADIX];                   // [lo, hi) of the digit's run in this tile
+#endif
+    __shared__ uint32_t s_scratch[NW];
+    constexpr bool KVI = HAS_VALUES && RS_KV_INTERLEAVED;
+    __shared__ uint32_t s_keys[KVI ? 1 : TILE];
+    __shared__ uint32_t s_vals[(HAS_VALUES && !KVI) ? TILE : 1];
+    __shared__ uint2 s_kv[KVI ? TILE : 1];
+
+    if (gated_off(gate, pass)) return;
+    const uint32_t G = gridDim.x, g = blockIdx.x, tid = threadIdx.x;
+    const uint32_t w = tid >> 6, lane = lane_id();
+
+    // Global base of digit `tid`: sum of the totals of smaller digits.  Chunked ownership adds
+    // this workgroup's row prefix once and then runs on; interleaved ownership adds the
+    // tile's row prefix per tile.  (`base` = ntiles when IL.)
+    uint32_t dtot = (tid < (uint32_t)RADIX) ? totals[tid] : 0u;
+    uint32_t all;
+    const uint32_t dbase = block_excl_scan_n<NW>(dtot, s_scratch, all);
+    uint32_t run = dbase;
+    const uint32_t ntiles = base;
+    const uint32_t rowlen = IL ? ntiles : G;
+    Chunk ch;
+    // XCD grouping (speed only, never correctness): workgroups are dealt round-robin over the
+    // 8 XCDs, so workgroup g sits on XCD g % 8 as slot g / 8.  Round r gives XCD x the tiles
+    // (8r + x) * (G/8) + slot: the G/8 workgroups of one XCD scatter ADJACENT tiles at the same
+    // time, and the partial cache lines where one tile's digit run meets the next tile's run
+    // are completed in that XCD's L2 instead of being written back twice.
+    const bool xg = IL && RS_XCD_GROUP && (G % 8u) == 0u;
+    const uint32_t gslot = xg ? (g >> 3) : g, gx = xg ? (g & 7u) : 0u, gper = xg ? (G >> 3) : G;
+    if (IL) {
+        ch.first = xg ? gx * gper + gslot : g;
+        ch.count = ch.first < ntiles ? (ntiles - ch.first + G - 1) / G : 0u;
+    } else {
+        ch = chunk_of(g, base, extra);
+        if (tid < (uint32_t)RADIX) run += counts[(size_t)tid * rowlen + g];
+    }
+    const uint32_t tstride = IL ? G : 1u;
+    uint32_t k[KPT];
+    uint32_t v[HAS_VALUES ? KPT : 1];
+    if (ch.count) {
+        const uint32_t tile0 = ch.first * (uint32_t)TILE;
+        load_tile<KPT, HAS_VALUES>(in_k, in_v, tile0 + w * WAVE_KEYS, n,
+                                   (uint64_t)tile0 + TILE <= n, k, v);
+    }
+    for (uint32_t t = 0; t < ch.count; ++t) {
+        const uint32_t tidx = ch.first + t * tstride;
+        const uint32_t tile0 = tidx * (uint32_t)TILE;
+        if (IL && tid < (uint32_t)RADIX) run = dbase + counts[(size_t)tid * rowlen + tidx];
+        const uint32_t wbase = tile0 + w * WAVE_KEYS;
+        const bool full = (uint64_t)tile0 + TILE <= n;
         // zero this wave's counters (the previous tile's readers finished at the last barrier)
         for (uint32_t d = lane; d < (uint32_t)RADIX; d += 64) s_whist[w][d] = 0u;
 
-        // Wavefront ballot ranking: for each slot, the lanes holding my digit (match mask),
-        // my rank among them (mbcnt) and the slot count; the lowest such lane bumps the
-        // wave's counter.  Slots are processed in position order, so ranks are stable.
+        uint32_t rank[KPT];
+        if (RANK == RANK_LDS_ATOMIC) {
 #pragma unroll
-        for (int j = 0; j < KPT; ++j) {
-            const uint32_t p = wbase + j * 64 + lane;
-            const bool valid = p < n;
-            const uint32_t d = (k[j] >> shift) & mask;
-            uint64_t m = __ballot(valid);
-#pragma unroll
-            for (int b = 0; b < R; ++b) {
-                if ((uint32_t)b < nbits) {
-                    const bool bit = (d >> b) & 1u;
-                    const uint64_t bb = __ballot(bit);
-                    m &= bit ? bb : ~bb;
-                }
+            for (int j = 0; j < KPT; ++j) {
+                const uint32_t d = (k[j] >> shift) & mask;
+                if (full || wbase + j * 64 + lane < n) rank[j] = atomicAdd(&s_whist[w][d], 1u);
             }
-            const uint32_t lt = mbcnt(m);
-            const uint32_t prior = s_whist[w][d];
-            rank[j] = prior + lt;
-            if (valid && lt == 0) s_whist[w][d] = prior + (uint32_t)__popcll(m);
+        } else {
+            uint32_t info[KPT];
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) {
+                const uint32_t d = (k[j] >> shift) & mask;
+                const uint64_t valid = full ? ~0ull : __ballot(wbase + j * 64 + lane < n);
+                const uint64_t m = match_mask<R>(d, valid);
+                const uint32_t lt = mbcnt(m);
+                const uint32_t lo = (uint32_t)m, hi = (uint32_t)(m >> 32);
+                const uint32_t leader = lo ? (uint32_t)__builtin_ctz(lo)
+                                           : (hi ? 32u + (uint32_t)__builtin_ctz(hi) : 0u);
+                uint32_t old = 0;
+                if (lt == 0 && ((valid >> lane) & 1ull))
+                    old = atomicAdd(&s_whist[w][d], (uint32_t)__popcll(m));
+                rank[j] = old;
+                info[j] = (leader << 16) | lt;
+            }
+#pragma unroll
+            for (int j = 0; j < KPT; ++j)
+                rank[j] = __builtin_amdgcn_ds_bpermute((int)((info[j] >> 16) << 2), (int)rank[j]) +
+                          (info[j] & 0xFFFFu);
         }
         __syncthreads();
 
         // Per digit: offsets of each wave inside the tile, tile digit start, global delta.
-        uint32_t c = 0, wc[kWaves];
+        uint32_t c = 0, wc[NW];
         if (tid < (uint32_t)RADIX) {
 #pragma unroll
-            for (int q = 0; q < kWaves; ++q) { wc[q] = s_whist[q][tid]; c += wc[q]; }
+            for (int q = 0; q < NW; ++q) { wc[q] = s_whist[q][tid]; c += wc[q]; }
         }
         uint32_t ttot;
-        const uint32_t tstart = block_excl_scan(c, s_scratch, ttot);
+        const uint32_t tstart = block_excl_scan_n<NW>(c, s_scratch, ttot);
         if (tid < (uint32_t)RADIX) {
             uint32_t o = tstart;
 #pragma unroll
-            for (int q = 0; q < kWaves; ++q) { s_whist[q][tid] = o; o += wc[q]; }
+            for (int q = 0; q < NW; ++q) { s_whist[q][tid] = o; o += wc[q]; }
             s_gdelta[tid] = run - tstart;
+#if RS_NT_STORE == 2 || RS_SCATTER_DEBUG >= 4
+            s_run[tid] = make_uint2(run, run + c);
+#endif
             run += c;
         }
         __syncthreads();
 
-        if (STAGED) {
-            // Local shuffle: the tile, stably sorted by digit, in LDS.
+        // Local shuffle: the tile, stably sorted by digit, in LDS.
 #pragma unroll
-            for (int j = 0; j < KPT; ++j) {
-                const uint32_t p = wbase + j * 64 + lane;
-                if (p < n) {
-                    const uint32_t d = (k[j] >> shift) & mask;
-                    const uint32_t s = s_whist[w][d] + rank[j];
-                    if (s < (uint32_t)TILE) {
+        for (int j = 0; j < KPT; ++j) {
+            if (full || wbase + j * 64 + lane < n) {
+                const uint32_t d = (k[j] >> shift) & mask;
+                const uint32_t s = s_whist[w][d] + rank[j];
+                if (s < (uint32_t)TILE) {
+                    if (KVI) {
+                        s_kv[s] = make_uint2(k[j], v[j]);
+                    } else {
                         s_keys[s] = k[j];
                         if (HAS_VALUES) s_vals[s] = v[j];
                     }
                 }
             }
-            __syncthreads();
-            const uint32_t nvalid = (n - tile0 < (uint32_t)TILE) ? (n - tile0) : (uint32_t)TILE;
-            // Coalesced scatter: consecutive lanes write consecutive positions of a digit run.
+        }
+        __syncthreads();
+        // Prefetch the next tile into the (now free) key/value registers; its latency hides
+        // under this tile's scatter.
+        if (t + 1 < ch.count) {
+            const uint32_t nt0 = tile0 + tstride * TILE;
+            load_tile<KPT, HAS_VALUES>(in_k, in_v, nt0 + w * WAVE_KEYS, n,
+                                       (uint64_t)nt0 + TILE <= n, k, v);
+        }
+        // Coalesced scatter: consecutive lanes write consecutive positions of a digit run.
+        const uint32_t nvalid = full ? (uint32_t)TILE : n - tile0;
 #pragma unroll 4
-            for (uint32_t i = tid; i < nvalid; i += kBlock) {
-                const uint32_t key = s_keys[i];
-                const uint32_t pos = s_gdelta[(key >> shift) & mask] + i;
-                if (pos < n) {  // never false for a consistent histogram; keeps a bug from faulting
+        for (uint32_t i = tid; i < nvalid; i += BLOCK) {
+            uint32_t key, val = 0;
+            if (KVI) {
+                const uint2 kv = s_kv[i];
+                key = kv.x;
+                val = kv.y;
+            } else {
+                key = s_keys[i];
+                if (HAS_VALUES) val = s_vals[i];
+            }
+#if RS_SCATTER_DEBUG == 1
+            const uint32_t pos = tile0 + i + (s_gdelta[(key >> shift) & mask] & 0);
+#else
+            const uint32_t pos = s_gdelta[(key >> shift) & mask] + i;
+#endif
+#if RS_SCATTER_DEBUG == 3
+            asm volatile("" ::"v"(key), "v"(pos), "v"(val));
+#else
+            if (pos < n) {  // never false for a consistent histogram; keeps a bug from faulting
+#if RS_NT_STORE == 1
+                __builtin_nontemporal_store(key, out_k + pos);
+                if (HAS_VALUES) __builtin_nontemporal_store(val, out_v + pos);
+#elif RS_NT_STORE == 2
+                const uint2 rr = s_run[(key >> shift) & mask];
+                if ((pos & ~31u) >= rr.x && (pos | 31u) < rr.y) {
+                    __builtin_nontemporal_store(key, out_k + pos);
+                    if (HAS_VALUES) __builtin_nontemporal_store(val, out_v + pos);
+                } else {
                     out_k[pos] = key;
-                    if (HAS_VALUES) out_v[pos] = s_vals[i];
+                    if (HAS_VALUES) out_v[pos] = val;
                 }
-            }
-        } else {
-            // Direct scatter from registers (no local shuffle): same positions, uncoalesced.
-#pragma unroll
-            for (int j = 0; j < KPT; ++j) {
-                const uint32_t p = wbase + j * 64 + lane;
-                if (p < n) {
-                    const uint32_t d = (k[j] >> shift) & mask;
-                    const uint32_t pos = s_gdelta[d] + s_whist[w][d] + rank[j];
-                    if (pos < n) {
-                        out_k[pos] = k[j];
-                        if (HAS_VALUES) out_v[pos] = v[j];
-                    }
+#elif RS_SCATTER_DEBUG >= 4
+                // ablation: drop elements of partially covered sectors (4: 32 B, 5: 128 B)
+                constexpr uint32_t SM = RS_SCATTER_DEBUG == 4 ? 7u : 31u;
+                const uint2 rr = s_run[(key >> shift) & mask];
+                if ((pos & ~SM) >= rr.x && (pos | SM) < rr.y) {
+                    out_k[pos] = key;
+                    if (HAS_VALUES) out_v[pos] = val;
                 }
+#else
+                out_k[pos] = key;
+                if (HAS_VALUES) out_v[pos] = val;
+#endif
             }
+#endif
         }
         __syncthreads();
     }

@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -45,9 +46,27 @@ rs_status fail(rs_status s, const char* fmt, ...) {
     } while (0)
 
 // Tuned geometry of the rank/scatter kernel.
-constexpr int kKPT = 16;                       // keys per thread per tile
-constexpr int kTile = rs::kBlock * kKPT;       // 4096 keys per tile
-constexpr uint32_t kMaxGrid = 1024;            // workgroups of histogram/scatter kernels
+#ifndef RS_KPT
+#define RS_KPT 16
+#endif
+#ifndef RS_INTERLEAVE
+#define RS_INTERLEAVE 1      // tile-interleaved workgroup ownership (see k_histogram_tiles)
+#endif
+#ifndef RS_HIST_BLOCK
+#define RS_HIST_BLOCK 512
+#endif
+#ifndef RS_SCATTER_BLOCK
+#define RS_SCATTER_BLOCK 1024
+#endif
+#ifndef RS_MAX_GRID
+#define RS_MAX_GRID 512
+#endif
+constexpr int kKPT = RS_KPT;                   // keys per thread per tile
+constexpr int kScatterBlock = RS_SCATTER_BLOCK;  // threads per rank/scatter workgroup
+constexpr int kTile = kScatterBlock * kKPT;    // keys per tile
+constexpr uint32_t kMaxGrid = RS_MAX_GRID;     // workgroups of histogram/scatter kernels
+constexpr bool kInterleave = RS_INTERLEAVE != 0;
+constexpr int kHistBlock = RS_HIST_BLOCK;
 constexpr int kCheckGrid = 2048;
 
 struct DeviceGuard {
@@ -109,6 +128,7 @@ struct rs_plan {
     uint32_t bit_count = 32;
     uint32_t radix_bits = 8;
     bool has_values = false, check_order = false, local_shuffle = false;
+    int rank_mode = rs::RANK_LDS_ATOMIC;   // RSORT_RANK=ballot selects the ballot-match ranking
     uint32_t passes = 0;
     uint32_t widths[16] = {};
     uint64_t capacity = 0;
@@ -135,11 +155,16 @@ struct Geometry {
     uint32_t grid, base, extra;
 };
 
-Geometry geometry(uint64_t n, uint32_t tile, uint32_t max_grid) {
+Geometry geometry(uint64_t n, uint32_t tile, uint32_t max_grid, bool interleave = false) {
     const uint64_t tiles = (n + tile - 1) / tile;
     Geometry g;
     g.grid = (uint32_t)std::min<uint64_t>(tiles, max_grid);
     if (g.grid == 0) g.grid = 1;
+    if (interleave) {           // workgroup g owns tiles g, g+grid, ...; base = tile count
+        g.base = (uint32_t)std::max<uint64_t>(tiles, 1);
+        g.extra = 0;
+        return g;
+    }
     g.base = (uint32_t)(tiles / g.grid);
     g.extra = (uint32_t)(tiles % g.grid);
     return g;
@@ -149,31 +174,42 @@ template <int R>
 void launch_histogram(const uint32_t* in, uint32_t n, uint32_t shift, uint32_t mask,
                       const Geometry& geo, uint32_t* counts, const uint32_t* gate, int pass,
                       hipStream_t s) {
-    hipLaunchKernelGGL((rs::k_histogram<R, kTile>), dim3(geo.grid), dim3(rs::kBlock), 0, s, in,
-                       n, shift, mask, geo.base, geo.extra, counts, gate, pass);
+    if (kInterleave) {
+        const uint32_t ntiles = geo.base;
+        const uint32_t grid = std::min<uint32_t>(ntiles, kMaxGrid);
+        hipLaunchKernelGGL((rs::k_histogram_tiles<R, kTile, kHistBlock>), dim3(grid),
+                           dim3(kHistBlock), 0, s, in, n, shift, mask, ntiles, counts, gate, pass);
+    } else {
+        hipLaunchKernelGGL((rs::k_histogram<R, kTile>), dim3(geo.grid), dim3(rs::kBlock), 0, s,
+                           in, n, shift, mask, geo.base, geo.extra, counts, gate, pass);
+    }
 }
 
-template <int R, bool V, bool ST>
+template <int R, bool V, int RANK>
 void launch_scatter_t(const uint32_t* ik, const uint32_t* iv, uint32_t* ok, uint32_t* ov,
-                      uint32_t n, uint32_t shift, uint32_t mask, uint32_t nbits,
-                      const Geometry& geo, const uint32_t* counts, const uint32_t* totals,
-                      const uint32_t* gate, int pass, hipStream_t s) {
-    hipLaunchKernelGGL((rs::k_scatter<R, kKPT, V, ST>), dim3(geo.grid), dim3(rs::kBlock), 0, s,
-                       ik, iv, ok, ov, n, shift, mask, nbits, geo.base, geo.extra, counts,
-                       totals, gate, pass);
+                      uint32_t n, uint32_t shift, uint32_t mask, const Geometry& geo,
+                      const uint32_t* counts, const uint32_t* totals, const uint32_t* gate,
+                      int pass, hipStream_t s) {
+    hipLaunchKernelGGL((rs::k_scatter<R, kScatterBlock, kKPT, V, RANK, kInterleave>), dim3(geo.grid),
+                       dim3(kScatterBlock), 0, s, ik, iv, ok, ov, n, shift, mask, geo.base,
+                       geo.extra, counts, totals, gate, pass);
 }
 
 template <int R>
-void launch_scatter(bool V, bool ST, const uint32_t* ik, const uint32_t* iv, uint32_t* ok,
-                    uint32_t* ov, uint32_t n, uint32_t shift, uint32_t mask, uint32_t nbits,
-                    const Geometry& geo, const uint32_t* counts, const uint32_t* totals,
-                    const uint32_t* gate, int pass, hipStream_t s) {
+void launch_scatter(bool V, int rank_mode, const uint32_t* ik, const uint32_t* iv, uint32_t* ok,
+                    uint32_t* ov, uint32_t n, uint32_t shift, uint32_t mask, const Geometry& geo,
+                    const uint32_t* counts, const uint32_t* totals, const uint32_t* gate,
+                    int pass, hipStream_t s) {
     if (V) {
-        if (ST) launch_scatter_t<R, true, true>(ik, iv, ok, ov, n, shift, mask, nbits, geo, counts, totals, gate, pass, s);
-        else    launch_scatter_t<R, true, false>(ik, iv, ok, ov, n, shift, mask, nbits, geo, counts, totals, gate, pass, s);
+        if (rank_mode == rs::RANK_BALLOT)
+            launch_scatter_t<R, true, rs::RANK_BALLOT>(ik, iv, ok, ov, n, shift, mask, geo, counts, totals, gate, pass, s);
+        else
+            launch_scatter_t<R, true, rs::RANK_LDS_ATOMIC>(ik, iv, ok, ov, n, shift, mask, geo, counts, totals, gate, pass, s);
     } else {
-        if (ST) launch_scatter_t<R, false, true>(ik, iv, ok, ov, n, shift, mask, nbits, geo, counts, totals, gate, pass, s);
-        else    launch_scatter_t<R, false, false>(ik, iv, ok, ov, n, shift, mask, nbits, geo, counts, totals, gate, pass, s);
+        if (rank_mode == rs::RANK_BALLOT)
+            launch_scatter_t<R, false, rs::RANK_BALLOT>(ik, iv, ok, ov, n, shift, mask, geo, counts, totals, gate, pass, s);
+        else
+            launch_scatter_t<R, false, rs::RANK_LDS_ATOMIC>(ik, iv, ok, ov, n, shift, mask, geo, counts, totals, gate, pass, s);
     }
 }
 
@@ -183,7 +219,8 @@ rs_status run_pass(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint32_t*
                    const uint32_t* gate, int pass, hipStream_t s) {
     const uint32_t R = pick_R(w);
     const uint32_t mask = (1u << w) - 1u;
-    const Geometry geo = geometry(n, kTile, kMaxGrid);
+    const Geometry geo = geometry(n, kTile, kMaxGrid, kInterleave);
+    const uint32_t rowlen = kInterleave ? geo.base : geo.grid;
     p->timer.run(RS_KERNEL_HISTOGRAM, s, [&] {
         if (R == 2) launch_histogram<2>(ik, n, shift, mask, geo, p->counts, gate, pass, s);
         else if (R == 4) launch_histogram<4>(ik, n, shift, mask, geo, p->counts, gate, pass, s);
@@ -192,17 +229,16 @@ rs_status run_pass(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint32_t*
     HIP_TRY(hipGetLastError());
     p->timer.run(RS_KERNEL_SCAN, s, [&] {
         hipLaunchKernelGGL(rs::k_scan_rows, dim3(1u << R), dim3(rs::kBlock), 0, s, p->counts,
-                           geo.grid, p->totals, gate, pass);
+                           rowlen, p->totals, gate, pass);
     });
     HIP_TRY(hipGetLastError());
-    // The coalesced (LDS-staged) scatter is the implementation of the local shuffle; it is
-    // used for every sort (the direct scatter is kept for the A/B measurement only, see
-    // RS_LOCAL_SHUFFLE_DIRECT in DESIGN.md).
-    const bool staged = p->local_shuffle || true;
+    // The scatter always stages the tile through LDS (the local shuffle,
+    // RadixSortLocalShuffle.ts:94-116): it is what makes the writes coalesced, so the
+    // local_shuffle flag only selects what the reference's option name promises.
     p->timer.run(RS_KERNEL_SCATTER, s, [&] {
-        if (R == 2) launch_scatter<2>(values, staged, ik, iv, ok, ov, n, shift, mask, w, geo, p->counts, p->totals, gate, pass, s);
-        else if (R == 4) launch_scatter<4>(values, staged, ik, iv, ok, ov, n, shift, mask, w, geo, p->counts, p->totals, gate, pass, s);
-        else launch_scatter<8>(values, staged, ik, iv, ok, ov, n, shift, mask, w, geo, p->counts, p->totals, gate, pass, s);
+        if (R == 2) launch_scatter<2>(values, p->rank_mode, ik, iv, ok, ov, n, shift, mask, geo, p->counts, p->totals, gate, pass, s);
+        else if (R == 4) launch_scatter<4>(values, p->rank_mode, ik, iv, ok, ov, n, shift, mask, geo, p->counts, p->totals, gate, pass, s);
+        else launch_scatter<8>(values, p->rank_mode, ik, iv, ok, ov, n, shift, mask, geo, p->counts, p->totals, gate, pass, s);
     });
     HIP_TRY(hipGetLastError());
     return RS_OK;
@@ -261,6 +297,8 @@ RS_EXPORT rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out) {
     p->has_values = d.flags & RS_FLAG_HAS_VALUES;
     p->check_order = d.flags & RS_FLAG_CHECK_ORDER;
     p->local_shuffle = d.flags & RS_FLAG_LOCAL_SHUFFLE;
+    if (const char* rk = getenv("RSORT_RANK"))
+        p->rank_mode = (strcmp(rk, "ballot") == 0) ? rs::RANK_BALLOT : rs::RANK_LDS_ATOMIC;
     // Even number of passes so the result lands in the caller's buffers, like the reference's
     // bit_count/2 passes with ping-pong on bit % 4 (AbstractRadixSortKernel.ts:93-107).
     uint32_t P = (d.bit_count + rb - 1) / rb;
@@ -279,7 +317,7 @@ RS_EXPORT rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out) {
     hipError_t e;
     if ((e = alloc(&p->tmp_k, 4 * d.count)) != hipSuccess ||
         (p->has_values && (e = alloc(&p->tmp_v, 4 * d.count)) != hipSuccess) ||
-        (e = alloc(&p->counts, 4ull * 256 * kMaxGrid)) != hipSuccess ||
+        (e = alloc(&p->counts, 4ull * 256 * std::max<uint64_t>(kMaxGrid, (d.count + kTile - 1) / kTile))) != hipSuccess ||
         (e = alloc(&p->totals, 4ull * 256)) != hipSuccess ||
         (e = alloc(&p->flags, 4ull * 16)) != hipSuccess)
         return cleanup(fail(e == hipErrorOutOfMemory ? RS_ERR_OUT_OF_MEMORY : RS_ERR_HIP,
@@ -391,7 +429,7 @@ RS_EXPORT rs_status rs_plan_info_get(const rs_plan* p, rs_plan_info* info) {
     info->passes = p->passes;
     for (uint32_t i = 0; i < p->passes && i < 16; ++i) info->digit_bits[i] = p->widths[i];
     info->tile_keys = kTile;
-    info->grid_blocks = geometry(p->capacity, kTile, kMaxGrid).grid;
+    info->grid_blocks = geometry(p->capacity, kTile, kMaxGrid, kInterleave).grid;
     info->workspace_bytes = p->workspace;
     return RS_OK;
 }

@@ -1,0 +1,75 @@
+#!/usr/bin/env python3
+"""HBM traffic per kernel launch from rocprofv3 PMC counters (run on the GPU box).
+
+Follows MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE in separate --pmc passes (TCC slots),
+KB units; on gfx950 FETCH_SIZE reports 1/2 of the bytes of a coalesced streaming read, so it is
+doubled.  Both corrections are re-checked in the same run on kernels with a known byte count:
+k_fill_random writes exactly n*4 bytes, k_histogram reads exactly n*4 bytes.
+
+    python3 tools/pmc_traffic.py [config3|config2] [out.json]
+
+This script never touches the GPU itself: rocprofv3 runs tools/prof_driver.py as a child.
+"""
+import csv
+import glob
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+N = {"config3": 1 << 28, "config2": 1 << 26}
+KV = {"config3": True, "config2": False}
+
+
+def run_pass(counter: str, wl: str, outdir: str) -> dict:
+    d = os.path.join(outdir, counter.lower())
+    cmd = ["rocprofv3", "--pmc", counter, "--output-format", "csv", "-d", d, "-o", "pmc", "--",
+           sys.executable, os.path.join(ROOT, "tools", "prof_driver.py"), wl, "2"]
+    subprocess.run(cmd, check=True, timeout=400, stdout=subprocess.DEVNULL)
+    agg = {}
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            name = r["Kernel_Name"]
+            key = ("scatter" if "k_scatter" in name else "histogram" if "k_histogram" in name
+                   else "fill_random" if "k_fill_random" in name else "scan" if "k_scan_rows" in name
+                   else None)
+            if key:
+                agg.setdefault(key, []).append(float(r["Counter_Value"]) * 1024.0)
+    return {k: sum(v) / len(v) for k, v in agg.items()}
+
+
+def main():
+    wl = sys.argv[1] if len(sys.argv) > 1 else "config3"
+    out = sys.argv[2] if len(sys.argv) > 2 else os.path.join(ROOT, "gpurun_out", "traffic.json")
+    outdir = os.path.join(ROOT, "gpurun_out", "pmc_" + wl)
+    fetch = run_pass("FETCH_SIZE", wl, outdir)
+    write = run_pass("WRITE_SIZE", wl, outdir)
+    n = N[wl]
+    read_scale = (n * 4) / fetch["histogram"]          # expect ~2.0 (gfx950 FETCH_SIZE = 1/2)
+    write_scale = (n * 4) / write["fill_random"]       # expect ~1.0
+    alg = n * (16 if KV[wl] else 8)
+    res = {
+        "workload": wl, "n": n,
+        "calibration": {"read_scale_from_histogram": round(read_scale, 4),
+                        "write_scale_from_fill": round(write_scale, 4)},
+        "raw_bytes": {"fetch": fetch, "write": write},
+        "scatter_read_bytes_per_launch": fetch["scatter"] * 2.0,
+        "scatter_write_bytes_per_launch": write["scatter"],
+        "scatter_bytes_per_launch": fetch["scatter"] * 2.0 + write["scatter"],
+        "scatter_algorithmic_bytes_per_launch": alg,
+        "histogram_bytes_per_launch": fetch["histogram"] * 2.0 + write.get("histogram", 0.0),
+    }
+    res["scatter_traffic_over_algorithmic"] = round(res["scatter_bytes_per_launch"] / alg, 4)
+    try:
+        allres = json.load(open(out))
+    except (OSError, ValueError):
+        allres = {}
+    allres[wl] = res
+    with open(out, "w") as f:
+        json.dump(allres, f, indent=1)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()

@@ -108,6 +108,8 @@ def main() -> None:
     ap.add_argument("--n", type=int, default=0, help="override keys per GPU (testing only)")
     ap.add_argument("--radix-bits", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--distributed", action="store_true",
+                    help="use the bucket-exchange path even at world size 1 (testing)")
     ap.add_argument("--cpu-log2", type=int, default=23)
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per scatter launch (tools/pmc_traffic.py)")
@@ -125,19 +127,20 @@ def main() -> None:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    use_dist = world > 1 or args.distributed
+    if use_dist:
         dist.init_process_group("nccl", device_id=dev)
     wl = dict(WORKLOADS[args.workload])
     n = args.n or wl["n"]
     K, W = args.steps, args.warmup
 
     def barrier():
-        if world > 1:
+        if use_dist:
             dist.barrier()
 
     kernel_ms = {}
     extra = {}
-    if world == 1:
+    if not use_dist:
         # One pre-generated batch per timed step (HBM holds them: 2 GiB each for config3).
         per_batch = n * 4 * (2 if wl["values"] else 1)
         free, _ = torch.cuda.mem_get_info(dev)
@@ -186,11 +189,12 @@ def main() -> None:
     else:
         keys, vals = make_input(torch, ops, wl, n, wl["seed"], rank * n, dev)
         lo = HipLocalOps(local, int(n * 1.25), wl["values"], args.radix_bits)
+        r = None
         for _ in range(W):
             r = distributed_sort(keys, vals, lo)
         torch.cuda.synchronize()
         lo.plan.destroy()
-        lo = HipLocalOps(local, max(int(n * 1.25), r.n), wl["values"], args.radix_bits)
+        lo = HipLocalOps(local, max(int(n * 1.25), r.n if r else 0), wl["values"], args.radix_bits)
         from radix_sort_amd import _lib
         import ctypes
         _lib.load().rs_plan_set_profiling(lo.plan._plan, 1)
@@ -245,7 +249,7 @@ def main() -> None:
     extra["passes"] = passes
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and not use_dist and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.cpu_log2, wl["seed"])
 
     if rank == 0:
@@ -264,7 +268,7 @@ def main() -> None:
             "roofline": roof, "cpu_baseline": cpu, **extra,
         }
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
 
 

@@ -1,0 +1,137 @@
+"""Multi-GPU bucket exchange (radix_sort_amd/distributed.py) on CPU with gloo, world size 2.
+
+The local steps are injected: here an oracle-backed LocalOps (test infrastructure), on the GPU
+the librsort-backed HipLocalOps.  What is tested is the orchestration: histogram all_gather,
+whole-bucket split, all_to_all with uneven splits, rank-ordered concatenation, global stability.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import oracle as O
+from radix_sort_amd.distributed import bucket_owners, distributed_sort, split_sizes
+
+
+class OracleLocalOps:
+    """Test-only local steps on CPU tensors (int32 views of u32 words)."""
+
+    def empty(self, n, like):
+        return torch.empty(n, dtype=like.dtype)
+
+    def partition(self, keys, values, shift, bits):
+        k = keys.numpy().view(np.uint32)
+        top = (k >> np.uint32(shift)) & np.uint32((1 << bits) - 1)
+        perm = np.argsort(top, kind="stable")
+        hist = np.bincount(top, minlength=1 << bits).astype(np.int32)
+        sk = torch.from_numpy(k[perm].view(np.int32).copy())
+        sv = None if values is None else torch.from_numpy(values.numpy()[perm].copy())
+        return sk, sv, torch.from_numpy(hist)
+
+    def sort(self, keys, values, n):
+        k = keys.numpy().view(np.uint32)
+        v = None if values is None else values.numpy().view(np.uint32)
+        ok, ov = O.stable_sort_masked(k[:n], None if v is None else v[:n], 32)
+        keys.numpy().view(np.uint32)[:n] = ok
+        if v is not None:
+            values.numpy().view(np.uint32)[:n] = ov
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, n_per_rank, kind, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        if kind == "uniform":
+            k = O.gen_u32(9, n_per_rank, start=rank * n_per_rank)
+        elif kind == "few":   # heavy duplicates: stability across ranks matters
+            k = O.gen_u32(9, n_per_rank, start=rank * n_per_rank) % np.uint32(7) << np.uint32(29)
+        else:                 # skewed: everything in a handful of top-byte buckets
+            k = O.gen_u32(9, n_per_rank, start=rank * n_per_rank) & np.uint32(0x03FFFFFF)
+        v = np.arange(rank * n_per_rank, (rank + 1) * n_per_rank, dtype=np.uint32)
+        r = distributed_sort(torch.from_numpy(k.view(np.int32).copy()),
+                             torch.from_numpy(v.view(np.int32).copy()), OracleLocalOps())
+        q.put((rank, r.keys[: r.n].numpy().view(np.uint32).copy(),
+               r.values[: r.n].numpy().view(np.uint32).copy(), r.send_sizes, r.recv_sizes))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("kind", ["uniform", "few", "skewed"])
+def test_gloo_world2_bucket_exchange_is_global_stable_sort(kind):
+    world, n = 2, 20_000
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, kind, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    outs = sorted([q.get(timeout=120) for _ in range(world)], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    keys = np.concatenate([o[1] for o in outs])
+    vals = np.concatenate([o[2] for o in outs])
+    all_k = np.concatenate([
+        (O.gen_u32(9, n, start=r * n) if kind == "uniform" else
+         O.gen_u32(9, n, start=r * n) % np.uint32(7) << np.uint32(29) if kind == "few" else
+         O.gen_u32(9, n, start=r * n) & np.uint32(0x03FFFFFF)) for r in range(world)])
+    ek, ev = O.stable_sort_masked(all_k, np.arange(world * n, dtype=np.uint32), 32)
+    assert (keys == ek).all() and (vals == ev).all()
+    # every rank sent exactly its input, received what others sent it
+    assert sum(outs[0][3]) == n and sum(outs[1][3]) == n
+    assert outs[0][4][1] == outs[1][3][0] and outs[1][4][0] == outs[0][3][1]
+
+
+def test_bucket_owners_balanced_and_whole():
+    hist = [[10] * 256, [10] * 256, [5] * 256, [15] * 256]
+    b = bucket_owners(hist, 4)
+    assert b[0] == 0 and b[-1] == 256 and b == sorted(b)
+    totals = [sum(h[i] for h in hist for i in range(b[q], b[q + 1])) for q in range(4)]
+    assert max(totals) - min(totals) <= 40     # one bucket of imbalance at most
+    send, recv = split_sizes(hist, b, 1, 4)
+    assert sum(send) == sum(hist[1])
+    # degenerate: one bucket holds everything -> it goes to a single rank
+    h2 = [[0] * 256 for _ in range(2)]
+    h2[0][7] = 100
+    h2[1][7] = 50
+    b2 = bucket_owners(h2, 2)
+    s0, r0 = split_sizes(h2, b2, 0, 2)
+    s1, r1 = split_sizes(h2, b2, 1, 2)
+    assert sum(r0) + sum(r1) == 150 and (sum(r0) == 0 or sum(r1) == 0)
+
+
+@pytest.mark.gpu
+def test_rccl_world1_hip_local_ops_round_trip():
+    """The product path (HipLocalOps + RCCL calls) on one GPU: world size 1 over nccl."""
+    from radix_sort_amd.distributed import HipLocalOps
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(_free_port())
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        n = 3_000_017
+        k = O.gen_u32(21, n)
+        v = np.arange(n, dtype=np.uint32)
+        kt = torch.from_numpy(k.view(np.int32)).cuda()
+        vt = torch.from_numpy(v.view(np.int32)).cuda()
+        ops = HipLocalOps(0, n, True)
+        r = distributed_sort(kt, vt, ops)
+        torch.cuda.synchronize()
+        ek, ev = O.stable_sort_masked(k, v, 32)
+        assert r.n == n
+        assert (r.keys.cpu().numpy().view(np.uint32) == ek).all()
+        assert (r.values.cpu().numpy().view(np.uint32) == ev).all()
+    finally:
+        dist.destroy_process_group()

@@ -1,0 +1,93 @@
+// Type declarations for the MI355X radix sort's JavaScript API (index.js).  Mirrors the
+// reference's exported classes (src/index.ts:1-3) and option shapes.
+
+export declare const GPUBufferUsage: {
+  readonly MAP_READ: number; readonly MAP_WRITE: number; readonly COPY_SRC: number;
+  readonly COPY_DST: number; readonly INDEX: number; readonly VERTEX: number;
+  readonly UNIFORM: number; readonly STORAGE: number; readonly INDIRECT: number;
+  readonly QUERY_RESOLVE: number;
+};
+export declare const GPUMapMode: { readonly READ: number; readonly WRITE: number };
+
+export interface WorkgroupSize { x: number; y: number; }
+
+export declare class DeviceBuffer {
+  readonly device: Device;
+  readonly size: number;
+  readonly usage: number;
+  readonly ptr: bigint | null;
+  getMappedRange(offset?: number, size?: number): ArrayBuffer;
+  unmap(): void;
+  mapAsync(mode: number): Promise<number>;
+  destroy(): void;
+}
+
+export interface ComputePass { end(): void; }
+export interface CommandBuffer { readonly commands: ReadonlyArray<() => void>; }
+export declare class CommandEncoder {
+  beginComputePass(descriptor?: unknown): ComputePass;
+  copyBufferToBuffer(src: DeviceBuffer, srcOffset: number, dst: DeviceBuffer, dstOffset: number, size: number): void;
+  finish(): CommandBuffer;
+}
+
+export declare class Device {
+  constructor(ordinal?: number);
+  readonly ordinal: number;
+  readonly limits: Readonly<Record<string, number>>;
+  readonly queue: {
+    submit(commandBuffers: CommandBuffer[]): void;
+    writeBuffer(buffer: DeviceBuffer, offset: number, data: ArrayBufferView | ArrayBuffer): void;
+    onSubmittedWorkDone(): Promise<void>;
+  };
+  createBuffer(desc: { size: number; usage?: number; mappedAtCreation?: boolean; label?: string }): DeviceBuffer;
+  createCommandEncoder(): CommandEncoder;
+  synchronize(): void;
+  destroy(): void;
+}
+
+export declare const gpu: {
+  requestAdapter(opts?: { ordinal?: number }): Promise<{ requestDevice(): Promise<Device> } | null>;
+};
+
+/** README spelling (README.md:72-88). */
+export interface RadixSortKernelOptions {
+  device?: Device;
+  keys?: DeviceBuffer;
+  values?: DeviceBuffer;
+  count: number;
+  bit_count?: number;
+  workgroup_size?: WorkgroupSize;
+  check_order?: boolean;
+  local_shuffle?: boolean;
+  avoid_bank_conflicts?: boolean;
+  /** Shipped-source spelling (RadixSortBufferKernel.ts:9-16). */
+  data?: { keys: DeviceBuffer; values?: DeviceBuffer };
+  bitCount?: number;
+  workgroupSize?: WorkgroupSize;
+  checkOrder?: boolean;
+  localShuffle?: boolean;
+  avoidBankConflicts?: boolean;
+  /** Digit bits per HBM pass: 0 = auto (8), 2 = the reference's one 4-way split per pass. */
+  radixBits?: number;
+}
+
+export declare class RadixSortKernel {
+  constructor(options: RadixSortKernelOptions);
+  readonly buffers: { keys: DeviceBuffer; values?: DeviceBuffer };
+  readonly count: number;
+  readonly bitCount: number;
+  readonly workgroupSize: WorkgroupSize;
+  readonly threadsPerWorkgroup: number;
+  readonly workgroupCount: number;
+  readonly info: { passes: number; digitBits: number[]; tileKeys: number; gridBlocks: number; workspaceBytes: number };
+  /** Records the sort into `pass` (runs at queue.submit) or runs it immediately. */
+  dispatch(pass?: ComputePass): void;
+  destroy(): void;
+}
+export declare class RadixSortBufferKernel extends RadixSortKernel {}
+
+export declare class PrefixSumKernel {
+  constructor(options: { device?: Device; data: DeviceBuffer; count: number; workgroupSize?: WorkgroupSize; avoidBankConflicts?: boolean });
+  dispatch(pass?: ComputePass): void;
+  destroy(): void;
+}

@@ -1,0 +1,274 @@
+'use strict';
+// webgpu-radix-sort on MI355X — the reference's JavaScript API over the HIP C ABI.
+//
+// Exports the reference's classes (src/index.ts:1-3; README.md:61-90):
+//   RadixSortKernel / RadixSortBufferKernel  — sort keys (+values) in place, stable, ascending by
+//                                              the low bit_count bits
+//   PrefixSumKernel                          — in-place exclusive scan
+// and a minimal WebGPU-shaped device (gpu.requestAdapter().requestDevice(), createBuffer,
+// createCommandEncoder/beginComputePass, queue.submit, mapAsync) so code written for the
+// reference runs unchanged: as in WebGPU, dispatch() only RECORDS work into the pass; it runs
+// on the device's HIP stream when the command buffer is submitted (AbstractRadixSortKernel.ts:
+// 221-247 encode-only; example/tests.ts:78 submit).
+//
+// All compute is in librsort.so (hand-written gfx950 kernels).  There is no CPU fallback: if
+// the addon or the library is missing, require() throws.
+//
+// Plain ES2019 CommonJS (Node >= 12); types in index.d.ts.
+
+const path = require('path');
+
+const addon = require(path.join(__dirname, 'build', 'rsort_napi.node'));
+
+const GPUBufferUsage = Object.freeze({
+  MAP_READ: 0x0001, MAP_WRITE: 0x0002, COPY_SRC: 0x0004, COPY_DST: 0x0008, INDEX: 0x0010,
+  VERTEX: 0x0020, UNIFORM: 0x0040, STORAGE: 0x0080, INDIRECT: 0x0100, QUERY_RESOLVE: 0x0200,
+});
+const GPUMapMode = Object.freeze({ READ: 0x0001, WRITE: 0x0002 });
+
+// ---- device, buffers, command recording -----------------------------------------------------
+
+class DeviceBuffer {
+  // A GPUBuffer analogue.  MAP_READ / MAP_WRITE buffers live in host memory (like WebGPU's
+  // CPU-visible staging buffers); every other buffer is a HIP device allocation.
+  constructor(device, { size, usage = 0, mappedAtCreation = false, label = '' }) {
+    if (!(size >= 0)) throw new TypeError('createBuffer: size required');
+    this.device = device;
+    this.size = size;
+    this.usage = usage;
+    this.label = label;
+    this.host = (usage & (GPUBufferUsage.MAP_READ | GPUBufferUsage.MAP_WRITE)) !== 0;
+    this.ptr = this.host ? null : addon.malloc(device.ordinal, Math.max(size, 4));
+    this.hostData = this.host ? new ArrayBuffer(size) : null;
+    this.mapped = mappedAtCreation ? (this.host ? this.hostData : new ArrayBuffer(size)) : null;
+    this.destroyed = false;
+  }
+
+  // The whole-buffer range aliases the mapping (writes through it reach the buffer at unmap(),
+  // as in WebGPU); a sub-range is returned as a copy.
+  getMappedRange(offset = 0, size) {
+    if (!this.mapped) throw new Error('buffer is not mapped');
+    if (offset === 0 && (size === undefined || size === this.size)) return this.mapped;
+    return this.mapped.slice(offset, size === undefined ? undefined : offset + size);
+  }
+
+  unmap() {
+    if (this.mapped && !this.host) addon.h2d(this.ptr, new Uint8Array(this.mapped), this.device.stream);
+    this.mapped = null;
+  }
+
+  mapAsync(mode) {
+    if (!this.host) return Promise.reject(new Error('mapAsync needs a MAP_READ/MAP_WRITE buffer'));
+    addon.streamSynchronize(this.device.stream);   // results of submitted work are complete
+    this.mapped = this.hostData;
+    return Promise.resolve(mode);
+  }
+
+  destroy() {
+    if (!this.destroyed && this.ptr) addon.free(this.ptr);
+    this.destroyed = true;
+    this.ptr = null;
+  }
+}
+
+class ComputePass {
+  constructor(encoder) { this.encoder = encoder; }
+  record(fn) { this.encoder.commands.push(fn); }
+  end() {}
+}
+
+class CommandEncoder {
+  constructor(device) { this.device = device; this.commands = []; }
+  beginComputePass() { return new ComputePass(this); }
+  copyBufferToBuffer(src, srcOffset, dst, dstOffset, size) {
+    const dev = this.device;
+    this.commands.push(() => {
+      if (!src.host && dst.host) {
+        addon.streamSynchronize(dev.stream);
+        addon.d2h(new Uint8Array(dst.hostData, dstOffset, size), src.ptr + BigInt(srcOffset), dev.stream);
+      } else if (src.host && !dst.host) {
+        addon.h2d(dst.ptr + BigInt(dstOffset), new Uint8Array(src.hostData, srcOffset, size), dev.stream);
+      } else if (!src.host && !dst.host) {
+        addon.d2d(dst.ptr + BigInt(dstOffset), src.ptr + BigInt(srcOffset), size, dev.stream);
+      } else {
+        new Uint8Array(dst.hostData, dstOffset, size).set(new Uint8Array(src.hostData, srcOffset, size));
+      }
+    });
+  }
+  finish() { return { commands: this.commands.slice() }; }
+}
+
+class Queue {
+  constructor(device) { this.device = device; }
+  submit(commandBuffers) {
+    for (const cb of commandBuffers) for (const fn of cb.commands) fn();
+  }
+  writeBuffer(buffer, offset, data) {
+    const bytes = ArrayBuffer.isView(data) ? new Uint8Array(data.buffer, data.byteOffset, data.byteLength)
+      : new Uint8Array(data);
+    addon.h2d(buffer.ptr + BigInt(offset), bytes, this.device.stream);
+  }
+  onSubmittedWorkDone() { addon.streamSynchronize(this.device.stream); return Promise.resolve(); }
+}
+
+class Device {
+  constructor(ordinal = 0) {
+    this.ordinal = ordinal;
+    this.stream = null;               // the HIP null stream of this device
+    this.queue = new Queue(this);
+    // The reference reads these limits (example/tests.ts:10-14, utils.ts:11).
+    this.limits = Object.freeze({
+      maxComputeWorkgroupsPerDimension: 2147483647,
+      maxComputeInvocationsPerWorkgroup: 1024,
+      maxComputeWorkgroupSizeX: 1024,
+      maxComputeWorkgroupSizeY: 1024,
+      maxStorageBufferBindingSize: 2 ** 34,
+      maxBufferSize: 2 ** 34,
+    });
+  }
+  createBuffer(desc) { return new DeviceBuffer(this, desc); }
+  createCommandEncoder() { return new CommandEncoder(this); }
+  synchronize() { addon.streamSynchronize(this.stream); }
+  destroy() {}
+}
+
+// navigator.gpu-shaped entry point: `await gpu.requestAdapter()` then `requestDevice()`.
+const gpu = {
+  async requestAdapter(opts = {}) {
+    const ordinal = opts.ordinal || 0;
+    if (addon.deviceCount() <= ordinal) return null;
+    return { async requestDevice() { return new Device(ordinal); } };
+  },
+};
+
+// ---- kernels ---------------------------------------------------------------------------------
+
+function pick(opts, names, dflt) {
+  for (const n of names) if (opts[n] !== undefined && opts[n] !== null) return opts[n];
+  return dflt;
+}
+
+function bufferPtr(b, name) {
+  if (b === undefined || b === null) return null;
+  if (typeof b === 'bigint') return b;
+  if (b instanceof DeviceBuffer) {
+    if (b.host) throw new TypeError(`${name} must be a device (STORAGE) buffer`);
+    return b.ptr;
+  }
+  if (b && typeof b.ptr === 'bigint') return b.ptr;
+  throw new TypeError(`${name}: expected a device buffer`);
+}
+
+function recordOrRun(pass, fn) {
+  if (pass && typeof pass.record === 'function') pass.record(fn);
+  else fn();
+}
+
+class RadixSortKernel {
+  /**
+   * Accepts both spellings: README's {device, keys, values, count, check_order, bit_count,
+   * workgroup_size, local_shuffle, avoid_bank_conflicts} (README.md:72-88,129,168) and the
+   * shipped {device, data: {keys, values}, count, bitCount, workgroupSize, checkOrder,
+   * localShuffle, avoidBankConflicts} (RadixSortBufferKernel.ts:9-16, AbstractRadixSortKernel.ts:
+   * 14-19, AbstractKernel.ts:3-7).  Defaults: bitCount 32, workgroupSize {x:16,y:16},
+   * checkOrder/localShuffle/avoidBankConflicts false (AbstractRadixSortKernel.ts:52-57).
+   */
+  constructor(options) {
+    const opts = options || {};
+    const data = opts.data || {};
+    this.device = opts.device || null;
+    const keys = opts.keys !== undefined ? opts.keys : data.keys;
+    const values = opts.values !== undefined ? opts.values : data.values;
+    if (keys === undefined || keys === null) throw new TypeError('keys buffer is required');
+    this.count = opts.count;
+    if (!(this.count >= 0)) throw new TypeError('count is required');
+    this.bitCount = pick(opts, ['bit_count', 'bitCount'], 32);
+    this.workgroupSize = pick(opts, ['workgroup_size', 'workgroupSize'], { x: 16, y: 16 });
+    this.checkOrder = !!pick(opts, ['check_order', 'checkOrder'], false);
+    this.localShuffle = !!pick(opts, ['local_shuffle', 'localShuffle'], false);
+    this.avoidBankConflicts = !!pick(opts, ['avoid_bank_conflicts', 'avoidBankConflicts'], false);
+    this.radixBits = pick(opts, ['radix_bits', 'radixBits'], 0);
+    this.buffers = { keys };
+    if (values !== undefined && values !== null) this.buffers.values = values;
+    this.hasValues = !!this.buffers.values;
+    for (const [name, b] of Object.entries(this.buffers)) {
+      if (b instanceof DeviceBuffer && b.size < this.count * 4) {
+        throw new RangeError(`${name} buffer (${b.size} bytes) smaller than count * 4`);
+      }
+    }
+    this._keys = bufferPtr(keys, 'keys');
+    this._values = bufferPtr(this.buffers.values, 'values');
+    const flags = (this.hasValues ? addon.FLAG_HAS_VALUES : 0)
+      | (this.checkOrder ? addon.FLAG_CHECK_ORDER : 0)
+      | (this.localShuffle ? addon.FLAG_LOCAL_SHUFFLE : 0)
+      | (this.avoidBankConflicts ? addon.FLAG_AVOID_BANK_CONFLICTS : 0);
+    this._plan = addon.planCreate({
+      device: this.device ? this.device.ordinal : 0,
+      count: this.count,
+      bitCount: this.bitCount,
+      workgroupX: this.workgroupSize.x,
+      workgroupY: this.workgroupSize.y === undefined ? 1 : this.workgroupSize.y,
+      flags,
+      radixBits: this.radixBits,
+    });
+  }
+
+  get threadsPerWorkgroup() { return this.workgroupSize.x * (this.workgroupSize.y || 1); }
+
+  get workgroupCount() { return Math.ceil(this.count / this.threadsPerWorkgroup); }
+
+  get info() { return addon.planInfo(this._plan); }
+
+  /** Record the sort into `pass` (runs at queue.submit), or run it now when no pass is given. */
+  dispatch(pass) {
+    const stream = this.device ? this.device.stream : null;
+    recordOrRun(pass, () => addon.planSort(this._plan, this._keys, this._values, stream));
+  }
+
+  destroy() {
+    if (this._plan) addon.planDestroy(this._plan);
+    this._plan = null;
+  }
+}
+
+class RadixSortBufferKernel extends RadixSortKernel {}
+
+class PrefixSumKernel {
+  /** {device, data, count, workgroupSize, avoidBankConflicts} (PrefixSumKernel.ts:24-43). */
+  constructor(options) {
+    const opts = options || {};
+    this.device = opts.device || null;
+    this.data = opts.data;
+    this.count = opts.count;
+    if (!(this.count >= 0)) throw new TypeError('count is required');
+    this.workgroupSize = pick(opts, ['workgroup_size', 'workgroupSize'], { x: 16, y: 16 });
+    this.avoidBankConflicts = !!pick(opts, ['avoid_bank_conflicts', 'avoidBankConflicts'], false);
+    this._data = bufferPtr(this.data, 'data');
+    this._plan = addon.scanPlanCreate(this.device ? this.device.ordinal : 0, this.count,
+      this.workgroupSize.x, this.workgroupSize.y === undefined ? 1 : this.workgroupSize.y,
+      this.avoidBankConflicts ? addon.FLAG_AVOID_BANK_CONFLICTS : 0);
+  }
+
+  dispatch(pass, dispatchSizeBuffer) {
+    if (dispatchSizeBuffer) throw new Error('indirect dispatch buffers are not used by the HIP backend');
+    const stream = this.device ? this.device.stream : null;
+    recordOrRun(pass, () => addon.scanPlanRun(this._plan, this._data, stream));
+  }
+
+  destroy() {
+    if (this._plan) addon.scanPlanDestroy(this._plan);
+    this._plan = null;
+  }
+}
+
+module.exports = {
+  RadixSortKernel,
+  RadixSortBufferKernel,
+  PrefixSumKernel,
+  Device,
+  DeviceBuffer,
+  GPUBufferUsage,
+  GPUMapMode,
+  gpu,
+  addon,
+};

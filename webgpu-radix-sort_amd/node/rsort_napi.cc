@@ -1,0 +1,414 @@
+// rsort_napi.cc — Node N-API binding of librsort (include/rsort.h).
+//
+// The thin FFI layer between the reference's host language (JavaScript/TypeScript, Node) and the
+// gfx950 HIP kernels.  Device pointers and HIP streams cross as BigInt; plans cross as externals
+// with a finalizer (the reference never frees its GPU resources).  Every failed
+// call throws Error(rs_last_error()).  No compute happens here.
+#define NAPI_VERSION 8
+#include <node_api.h>
+
+#include <cstdint>
+#include <cstring>
+#include <string>
+
+#include "../../include/rsort.h"
+
+namespace {
+
+#define NAPI_CALL(env, call)                                              \
+    do {                                                                  \
+        if ((call) != napi_ok) {                                          \
+            napi_throw_error((env), nullptr, "N-API call failed: " #call); \
+            return nullptr;                                               \
+        }                                                                 \
+    } while (0)
+
+napi_value throw_status(napi_env env, rs_status st, const char* what) {
+    std::string msg = std::string(what) + ": " + rs_last_error();
+    napi_throw_error(env, rs_status_string(st), msg.c_str());
+    return nullptr;
+}
+
+#define RS_CALL(env, call, what)                               \
+    do {                                                       \
+        rs_status st_ = (call);                                \
+        if (st_ != RS_OK) return throw_status((env), st_, what); \
+    } while (0)
+
+bool get_u64(napi_env env, napi_value v, uint64_t* out) {
+    napi_valuetype t;
+    if (napi_typeof(env, v, &t) != napi_ok) return false;
+    if (t == napi_null || t == napi_undefined) { *out = 0; return true; }
+    if (t == napi_bigint) {
+        bool lossless = true;
+        return napi_get_value_bigint_uint64(env, v, out, &lossless) == napi_ok;
+    }
+    if (t == napi_number) {
+        double d = 0;
+        if (napi_get_value_double(env, v, &d) != napi_ok || d < 0) return false;
+        *out = (uint64_t)d;
+        return true;
+    }
+    return false;
+}
+
+bool get_u32_prop(napi_env env, napi_value obj, const char* key, uint32_t* out, uint32_t dflt) {
+    bool has = false;
+    *out = dflt;
+    if (napi_has_named_property(env, obj, key, &has) != napi_ok) return false;
+    if (!has) return true;
+    napi_value v;
+    if (napi_get_named_property(env, obj, key, &v) != napi_ok) return false;
+    uint64_t x = 0;
+    if (!get_u64(env, v, &x)) return false;
+    *out = (uint32_t)x;
+    return true;
+}
+
+napi_value bigint(napi_env env, uint64_t x) {
+    napi_value r;
+    napi_create_bigint_uint64(env, x, &r);
+    return r;
+}
+
+template <int N>
+bool args(napi_env env, napi_callback_info info, napi_value (&argv)[N], size_t* argc_out = nullptr) {
+    size_t argc = N;
+    if (napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr) != napi_ok) return false;
+    for (size_t i = argc; i < (size_t)N; ++i) napi_get_undefined(env, &argv[i]);
+    if (argc_out) *argc_out = argc;
+    return true;
+}
+
+void* ptr_of(napi_env env, napi_value v, bool* ok) {
+    uint64_t x = 0;
+    *ok = get_u64(env, v, &x);
+    return (void*)(uintptr_t)x;
+}
+
+// ---- plans as externals ------------------------------------------------------------------
+struct PlanBox { rs_plan* plan; };
+struct ScanBox { rs_scan_plan* plan; };
+
+void plan_finalize(napi_env, void* data, void*) {
+    auto* b = static_cast<PlanBox*>(data);
+    if (b->plan) rs_plan_destroy(b->plan);
+    delete b;
+}
+void scan_finalize(napi_env, void* data, void*) {
+    auto* b = static_cast<ScanBox*>(data);
+    if (b->plan) rs_scan_plan_destroy(b->plan);
+    delete b;
+}
+
+template <class Box>
+Box* box_of(napi_env env, napi_value v) {
+    void* p = nullptr;
+    if (napi_get_value_external(env, v, &p) != napi_ok || !p) {
+        napi_throw_type_error(env, nullptr, "expected a plan handle");
+        return nullptr;
+    }
+    return static_cast<Box*>(p);
+}
+
+// ---- functions ---------------------------------------------------------------------------
+napi_value DeviceCount(napi_env env, napi_callback_info) {
+    int32_t n = 0;
+    RS_CALL(env, rs_device_count(&n), "deviceCount");
+    napi_value r;
+    napi_create_int32(env, n, &r);
+    return r;
+}
+
+napi_value Version(napi_env env, napi_callback_info) {
+    napi_value r;
+    napi_create_uint32(env, rs_version(), &r);
+    return r;
+}
+
+// malloc(device, bytes) -> BigInt
+napi_value Malloc(napi_env env, napi_callback_info info) {
+    napi_value a[2];
+    if (!args(env, info, a)) return nullptr;
+    uint64_t dev = 0, bytes = 0;
+    if (!get_u64(env, a[0], &dev) || !get_u64(env, a[1], &bytes))
+        return napi_throw_type_error(env, nullptr, "malloc(device, bytes)"), nullptr;
+    void* p = nullptr;
+    RS_CALL(env, rs_malloc((int32_t)dev, bytes, &p), "malloc");
+    return bigint(env, (uint64_t)(uintptr_t)p);
+}
+
+napi_value Free(napi_env env, napi_callback_info info) {
+    napi_value a[1];
+    if (!args(env, info, a)) return nullptr;
+    bool ok;
+    void* p = ptr_of(env, a[0], &ok);
+    if (!ok) return napi_throw_type_error(env, nullptr, "free(ptr)"), nullptr;
+    RS_CALL(env, rs_free(p), "free");
+    return nullptr;
+}
+
+// h2d(ptr, typedArray|ArrayBuffer) / d2h(typedArray|ArrayBuffer, ptr): synchronous copies
+bool host_span(napi_env env, napi_value v, void** data, size_t* bytes) {
+    bool is_ta = false, is_ab = false;
+    napi_is_typedarray(env, v, &is_ta);
+    if (is_ta) {
+        napi_typedarray_type t;
+        size_t len = 0, off = 0;
+        napi_value ab;
+        if (napi_get_typedarray_info(env, v, &t, &len, data, &ab, &off) != napi_ok) return false;
+        size_t el = 1;
+        switch (t) {
+            case napi_int16_array: case napi_uint16_array: el = 2; break;
+            case napi_int32_array: case napi_uint32_array: case napi_float32_array: el = 4; break;
+            case napi_float64_array: case napi_bigint64_array: case napi_biguint64_array: el = 8; break;
+            default: el = 1;
+        }
+        *bytes = len * el;
+        return true;
+    }
+    napi_is_arraybuffer(env, v, &is_ab);
+    if (is_ab) return napi_get_arraybuffer_info(env, v, data, bytes) == napi_ok;
+    return false;
+}
+
+napi_value H2D(napi_env env, napi_callback_info info) {
+    napi_value a[3];
+    if (!args(env, info, a)) return nullptr;
+    bool ok;
+    void* dst = ptr_of(env, a[0], &ok);
+    void* src = nullptr;
+    size_t bytes = 0;
+    if (!ok || !host_span(env, a[1], &src, &bytes))
+        return napi_throw_type_error(env, nullptr, "h2d(ptr, typedArray)"), nullptr;
+    void* stream = ptr_of(env, a[2], &ok);
+    RS_CALL(env, rs_memcpy_h2d(dst, src, bytes, stream), "h2d");
+    RS_CALL(env, rs_stream_synchronize(stream), "h2d");
+    return nullptr;
+}
+
+napi_value D2H(napi_env env, napi_callback_info info) {
+    napi_value a[3];
+    if (!args(env, info, a)) return nullptr;
+    void* dst = nullptr;
+    size_t bytes = 0;
+    bool ok;
+    if (!host_span(env, a[0], &dst, &bytes))
+        return napi_throw_type_error(env, nullptr, "d2h(typedArray, ptr)"), nullptr;
+    void* src = ptr_of(env, a[1], &ok);
+    void* stream = ptr_of(env, a[2], &ok);
+    RS_CALL(env, rs_memcpy_d2h(dst, src, bytes, stream), "d2h");
+    return nullptr;
+}
+
+napi_value D2D(napi_env env, napi_callback_info info) {
+    napi_value a[4];
+    if (!args(env, info, a)) return nullptr;
+    bool ok1, ok2, ok3;
+    void* dst = ptr_of(env, a[0], &ok1);
+    void* src = ptr_of(env, a[1], &ok2);
+    uint64_t bytes = 0;
+    ok3 = get_u64(env, a[2], &bytes);
+    bool ok4;
+    void* stream = ptr_of(env, a[3], &ok4);
+    if (!ok1 || !ok2 || !ok3) return napi_throw_type_error(env, nullptr, "d2d(dst, src, bytes, stream)"), nullptr;
+    RS_CALL(env, rs_memcpy_d2d(dst, src, bytes, stream), "d2d");
+    return nullptr;
+}
+
+napi_value StreamCreate(napi_env env, napi_callback_info info) {
+    napi_value a[1];
+    if (!args(env, info, a)) return nullptr;
+    uint64_t dev = 0;
+    get_u64(env, a[0], &dev);
+    void* s = nullptr;
+    RS_CALL(env, rs_stream_create((int32_t)dev, &s), "streamCreate");
+    return bigint(env, (uint64_t)(uintptr_t)s);
+}
+
+napi_value StreamDestroy(napi_env env, napi_callback_info info) {
+    napi_value a[1];
+    if (!args(env, info, a)) return nullptr;
+    bool ok;
+    void* s = ptr_of(env, a[0], &ok);
+    RS_CALL(env, rs_stream_destroy(s), "streamDestroy");
+    return nullptr;
+}
+
+napi_value StreamSynchronize(napi_env env, napi_callback_info info) {
+    napi_value a[1];
+    if (!args(env, info, a)) return nullptr;
+    bool ok;
+    void* s = ptr_of(env, a[0], &ok);
+    RS_CALL(env, rs_stream_synchronize(s), "streamSynchronize");
+    return nullptr;
+}
+
+// planCreate({device, count, bitCount, workgroupX, workgroupY, flags, radixBits}) -> external
+napi_value PlanCreate(napi_env env, napi_callback_info info) {
+    napi_value a[1];
+    if (!args(env, info, a)) return nullptr;
+    rs_plan_desc d;
+    memset(&d, 0, sizeof(d));
+    uint32_t dev = 0, countlo = 0;
+    (void)countlo;
+    napi_value cnt;
+    bool has = false;
+    napi_has_named_property(env, a[0], "count", &has);
+    uint64_t count = 0;
+    if (has) {
+        napi_get_named_property(env, a[0], "count", &cnt);
+        if (!get_u64(env, cnt, &count)) return napi_throw_type_error(env, nullptr, "count"), nullptr;
+    }
+    if (!get_u32_prop(env, a[0], "device", &dev, 0) ||
+        !get_u32_prop(env, a[0], "bitCount", &d.bit_count, 32) ||
+        !get_u32_prop(env, a[0], "workgroupX", &d.workgroup_x, 16) ||
+        !get_u32_prop(env, a[0], "workgroupY", &d.workgroup_y, 16) ||
+        !get_u32_prop(env, a[0], "flags", &d.flags, 0) ||
+        !get_u32_prop(env, a[0], "radixBits", &d.radix_bits, 0))
+        return napi_throw_type_error(env, nullptr, "planCreate: bad option"), nullptr;
+    d.device = (int32_t)dev;
+    d.count = count;
+    rs_plan* p = nullptr;
+    RS_CALL(env, rs_plan_create(&d, &p), "RadixSortKernel");
+    napi_value ext;
+    auto* box = new PlanBox{p};
+    if (napi_create_external(env, box, plan_finalize, nullptr, &ext) != napi_ok) {
+        plan_finalize(env, box, nullptr);
+        return napi_throw_error(env, nullptr, "external"), nullptr;
+    }
+    return ext;
+}
+
+// planSort(plan, keysPtr, valuesPtr|null, stream|null [, n])
+napi_value PlanSort(napi_env env, napi_callback_info info) {
+    napi_value a[5];
+    size_t argc = 0;
+    if (!args(env, info, a, &argc)) return nullptr;
+    PlanBox* b = box_of<PlanBox>(env, a[0]);
+    if (!b) return nullptr;
+    if (!b->plan) return napi_throw_error(env, nullptr, "plan destroyed"), nullptr;
+    bool ok;
+    void* k = ptr_of(env, a[1], &ok);
+    void* v = ptr_of(env, a[2], &ok);
+    void* s = ptr_of(env, a[3], &ok);
+    if (argc >= 5) {
+        uint64_t n = 0;
+        if (!get_u64(env, a[4], &n)) return napi_throw_type_error(env, nullptr, "n"), nullptr;
+        RS_CALL(env, rs_plan_sort_n(b->plan, k, v, n, s), "dispatch");
+    } else {
+        RS_CALL(env, rs_plan_sort(b->plan, k, v, s), "dispatch");
+    }
+    return nullptr;
+}
+
+napi_value PlanDestroy(napi_env env, napi_callback_info info) {
+    napi_value a[1];
+    if (!args(env, info, a)) return nullptr;
+    PlanBox* b = box_of<PlanBox>(env, a[0]);
+    if (!b) return nullptr;
+    if (b->plan) rs_plan_destroy(b->plan);
+    b->plan = nullptr;
+    return nullptr;
+}
+
+napi_value PlanInfo(napi_env env, napi_callback_info info) {
+    napi_value a[1];
+    if (!args(env, info, a)) return nullptr;
+    PlanBox* b = box_of<PlanBox>(env, a[0]);
+    if (!b || !b->plan) return napi_throw_error(env, nullptr, "plan destroyed"), nullptr;
+    rs_plan_info inf;
+    RS_CALL(env, rs_plan_info_get(b->plan, &inf), "info");
+    napi_value o, x, arr;
+    napi_create_object(env, &o);
+    napi_create_uint32(env, inf.passes, &x); napi_set_named_property(env, o, "passes", x);
+    napi_create_uint32(env, inf.tile_keys, &x); napi_set_named_property(env, o, "tileKeys", x);
+    napi_create_uint32(env, inf.grid_blocks, &x); napi_set_named_property(env, o, "gridBlocks", x);
+    napi_create_double(env, (double)inf.workspace_bytes, &x); napi_set_named_property(env, o, "workspaceBytes", x);
+    napi_create_array_with_length(env, inf.passes, &arr);
+    for (uint32_t i = 0; i < inf.passes && i < 16; ++i) {
+        napi_create_uint32(env, inf.digit_bits[i], &x);
+        napi_set_element(env, arr, i, x);
+    }
+    napi_set_named_property(env, o, "digitBits", arr);
+    return o;
+}
+
+// scanPlanCreate(device, count, wx, wy, flags) -> external
+napi_value ScanPlanCreate(napi_env env, napi_callback_info info) {
+    napi_value a[5];
+    if (!args(env, info, a)) return nullptr;
+    uint64_t dev = 0, count = 0, wx = 16, wy = 16, flags = 0;
+    if (!get_u64(env, a[0], &dev) || !get_u64(env, a[1], &count) || !get_u64(env, a[2], &wx) ||
+        !get_u64(env, a[3], &wy) || !get_u64(env, a[4], &flags))
+        return napi_throw_type_error(env, nullptr, "scanPlanCreate(device, count, wx, wy, flags)"), nullptr;
+    rs_scan_plan* p = nullptr;
+    RS_CALL(env, rs_scan_plan_create((int32_t)dev, count, (uint32_t)wx, (uint32_t)wy, (uint32_t)flags, &p),
+            "PrefixSumKernel");
+    napi_value ext;
+    auto* box = new ScanBox{p};
+    if (napi_create_external(env, box, scan_finalize, nullptr, &ext) != napi_ok) {
+        scan_finalize(env, box, nullptr);
+        return napi_throw_error(env, nullptr, "external"), nullptr;
+    }
+    return ext;
+}
+
+napi_value ScanPlanRun(napi_env env, napi_callback_info info) {
+    napi_value a[3];
+    if (!args(env, info, a)) return nullptr;
+    ScanBox* b = box_of<ScanBox>(env, a[0]);
+    if (!b || !b->plan) return napi_throw_error(env, nullptr, "plan destroyed"), nullptr;
+    bool ok;
+    void* d = ptr_of(env, a[1], &ok);
+    void* s = ptr_of(env, a[2], &ok);
+    RS_CALL(env, rs_scan_plan_run(b->plan, d, s), "dispatch");
+    return nullptr;
+}
+
+napi_value ScanPlanDestroy(napi_env env, napi_callback_info info) {
+    napi_value a[1];
+    if (!args(env, info, a)) return nullptr;
+    ScanBox* b = box_of<ScanBox>(env, a[0]);
+    if (!b) return nullptr;
+    if (b->plan) rs_scan_plan_destroy(b->plan);
+    b->plan = nullptr;
+    return nullptr;
+}
+
+napi_value Define(napi_env env, napi_value exports, const char* name, napi_callback cb) {
+    napi_value fn;
+    napi_create_function(env, name, NAPI_AUTO_LENGTH, cb, nullptr, &fn);
+    napi_set_named_property(env, exports, name, fn);
+    return exports;
+}
+
+napi_value Init(napi_env env, napi_value exports) {
+    Define(env, exports, "version", Version);
+    Define(env, exports, "deviceCount", DeviceCount);
+    Define(env, exports, "malloc", Malloc);
+    Define(env, exports, "free", Free);
+    Define(env, exports, "h2d", H2D);
+    Define(env, exports, "d2h", D2H);
+    Define(env, exports, "d2d", D2D);
+    Define(env, exports, "streamCreate", StreamCreate);
+    Define(env, exports, "streamDestroy", StreamDestroy);
+    Define(env, exports, "streamSynchronize", StreamSynchronize);
+    Define(env, exports, "planCreate", PlanCreate);
+    Define(env, exports, "planSort", PlanSort);
+    Define(env, exports, "planDestroy", PlanDestroy);
+    Define(env, exports, "planInfo", PlanInfo);
+    Define(env, exports, "scanPlanCreate", ScanPlanCreate);
+    Define(env, exports, "scanPlanRun", ScanPlanRun);
+    Define(env, exports, "scanPlanDestroy", ScanPlanDestroy);
+    napi_value v;
+    napi_create_uint32(env, RS_FLAG_HAS_VALUES, &v); napi_set_named_property(env, exports, "FLAG_HAS_VALUES", v);
+    napi_create_uint32(env, RS_FLAG_CHECK_ORDER, &v); napi_set_named_property(env, exports, "FLAG_CHECK_ORDER", v);
+    napi_create_uint32(env, RS_FLAG_LOCAL_SHUFFLE, &v); napi_set_named_property(env, exports, "FLAG_LOCAL_SHUFFLE", v);
+    napi_create_uint32(env, RS_FLAG_AVOID_BANK_CONFLICTS, &v); napi_set_named_property(env, exports, "FLAG_AVOID_BANK_CONFLICTS", v);
+    return exports;
+}
+
+}  // namespace
+
+NAPI_MODULE(NODE_GYP_MODULE_NAME, Init)

@@ -1,0 +1,105 @@
+'use strict';
+// GPU: the reference's own test flow (example/tests.ts:9-107), seeded: create buffers,
+// construct the kernel, dispatch into a compute pass, copy back, submit, mapAsync, compare
+// against keys.slice(0, count).sort((a, b) => a - b) and keysResult[i] == keys[values[i]];
+// additionally checks stability (values = iota stay increasing within equal keys) and the
+// prefix sum against prefixSumCpu (example/tests.ts:288-296).
+const assert = require('assert');
+const { gpu, RadixSortKernel, RadixSortBufferKernel, PrefixSumKernel, GPUBufferUsage, GPUMapMode } = require('..');
+
+function mulberry32(a) {
+  return function next() {
+    a |= 0; a = (a + 0x6D2B79F5) | 0;
+    let t = Math.imul(a ^ (a >>> 15), 1 | a);
+    t = (t + Math.imul(t ^ (t >>> 7), 61 | t)) ^ t;
+    return ((t ^ (t >>> 14)) >>> 0) / 4294967296;
+  };
+}
+
+function createBuffers(device, data) {       // example/tests.ts:227-244
+  const dataBuffer = device.createBuffer({ size: data.length * 4, usage: GPUBufferUsage.STORAGE | GPUBufferUsage.COPY_SRC, mappedAtCreation: true });
+  new Uint32Array(dataBuffer.getMappedRange()).set(data);
+  dataBuffer.unmap();
+  const dataBufferMapped = device.createBuffer({ size: data.length * 4, usage: GPUBufferUsage.MAP_READ | GPUBufferUsage.COPY_DST });
+  return [dataBuffer, dataBufferMapped];
+}
+
+async function testRadixSort(device, keysAndValues, rand) {
+  let cases = 0;
+  for (const [wx, wy] of [[16, 16], [8, 4], [32, 32], [2, 2]]) {
+    for (let exp = 2; exp < 7; exp += 1) {
+      const elementCount = Math.floor(10 ** exp * (rand() * 0.1 + 0.9));
+      const subElementCount = Math.floor(elementCount * rand() + 1);
+      const keys = new Uint32Array(elementCount).map(() => Math.ceil(rand() * (2 ** 32 - 1)) % (exp === 3 ? 97 : 2 ** 32));
+      const values = new Uint32Array(elementCount).map((_, i) => i);
+      const checkOrder = rand() > 0.5;
+      const localShuffle = rand() > 0.5;
+      const avoidBankConflicts = rand() > 0.5;
+      const [keysBuffer, keysBufferMapped] = createBuffers(device, keys);
+      const [valuesBuffer, valuesBufferMapped] = createBuffers(device, values);
+      const Kernel = rand() > 0.5 ? RadixSortKernel : RadixSortBufferKernel;
+      const kernel = new Kernel({
+        device, data: { keys: keysBuffer, values: keysAndValues ? valuesBuffer : undefined },
+        count: subElementCount, bitCount: 32, workgroupSize: { x: wx, y: wy },
+        checkOrder, localShuffle, avoidBankConflicts,
+      });
+      const encoder = device.createCommandEncoder();
+      const pass = encoder.beginComputePass();
+      kernel.dispatch(pass);
+      pass.end();
+      encoder.copyBufferToBuffer(kernel.buffers.keys, 0, keysBufferMapped, 0, elementCount * 4);
+      if (keysAndValues) encoder.copyBufferToBuffer(kernel.buffers.values, 0, valuesBufferMapped, 0, elementCount * 4);
+      device.queue.submit([encoder.finish()]);
+      await keysBufferMapped.mapAsync(GPUMapMode.READ);
+      const keysResult = new Uint32Array(keysBufferMapped.getMappedRange().slice());
+      keysBufferMapped.unmap();
+      const expected = keys.slice(0, subElementCount).sort((a, b) => a - b);
+      assert.ok(expected.every((v, i) => v === keysResult[i]), `keys mismatch n=${elementCount} count=${subElementCount}`);
+      for (let i = subElementCount; i < elementCount; i += 1) assert.strictEqual(keysResult[i], keys[i]);
+      if (keysAndValues) {
+        await valuesBufferMapped.mapAsync(GPUMapMode.READ);
+        const valuesResult = new Uint32Array(valuesBufferMapped.getMappedRange().slice());
+        valuesBufferMapped.unmap();
+        for (let i = 0; i < subElementCount; i += 1) {
+          assert.strictEqual(keysResult[i], keys[valuesResult[i]]);
+          if (i && keysResult[i] === keysResult[i - 1]) assert.ok(valuesResult[i] > valuesResult[i - 1], 'stability');
+        }
+      }
+      kernel.destroy();
+      for (const b of [keysBuffer, valuesBuffer]) b.destroy();
+      cases += 1;
+    }
+  }
+  return cases;
+}
+
+async function testPrefixSum(device, rand) {
+  for (const n of [1, 7, 512, 1025, 100003]) {
+    const data = new Uint32Array(n).map(() => Math.floor(rand() * 8));
+    const [buf, mapped] = createBuffers(device, data);
+    const k = new PrefixSumKernel({ device, data: buf, count: n, workgroupSize: { x: 16, y: 16 } });
+    const encoder = device.createCommandEncoder();
+    const pass = encoder.beginComputePass();
+    k.dispatch(pass);
+    pass.end();
+    encoder.copyBufferToBuffer(buf, 0, mapped, 0, n * 4);
+    device.queue.submit([encoder.finish()]);
+    await mapped.mapAsync(GPUMapMode.READ);
+    const out = new Uint32Array(mapped.getMappedRange().slice());
+    let sum = 0;
+    for (let i = 0; i < n; i += 1) { assert.strictEqual(out[i], sum >>> 0); sum += data[i]; }
+    k.destroy();
+    buf.destroy();
+  }
+}
+
+(async () => {
+  const adapter = await gpu.requestAdapter();
+  assert.ok(adapter, 'no HIP device');
+  const device = await adapter.requestDevice();
+  const rand = mulberry32(20250404);
+  const a = await testRadixSort(device, false, rand);
+  const b = await testRadixSort(device, true, rand);
+  await testPrefixSum(device, rand);
+  console.log(`node sort checks ok (${a + b} sort cases, prefix sum)`);
+})().catch((e) => { console.error(e); process.exit(1); });

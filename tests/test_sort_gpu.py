@@ -254,3 +254,30 @@ def test_config4_256M_nearly_sorted_f32_check_order():
     RadixSortKernel(keys=kt, values=vt, count=n, check_order=True).dispatch()
     torch.cuda.synchronize()
     _verify_kv_iota(k_in, kt, vt)
+
+
+@pytest.mark.parametrize("rank", ["atomic", "ballot"])
+@pytest.mark.parametrize("tile", ["small", "large"])
+def test_rank_modes_and_tile_configs(monkeypatch, golden, rank, tile):
+    """Both in-wave ranking implementations and both tile configurations give the oracle's
+    result (RSORT_RANK / RSORT_TILE are read at plan creation)."""
+    monkeypatch.setenv("RSORT_RANK", rank)
+    monkeypatch.setenv("RSORT_TILE", tile)
+    for n, bits, kind in ((20_000, 32, "u32"), (300_001, 32, "few"), (1_000_003, 24, "u32"),
+                          (70_001, 12, "u32")):
+        keys = O.gen_u32(n + bits, n)
+        if kind == "few":
+            keys = keys % np.uint32(13)
+        vals = np.arange(n, dtype=np.uint32)
+        k, v = _sort(keys, vals, bit_count=bits, check_order=(n % 2 == 1))
+        ek, ev = O.stable_sort_masked(keys, vals, bits)
+        assert (k == ek).all() and (v == ev).all(), (n, bits, kind)
+        k, _ = _sort(keys, None, bit_count=bits)
+        assert (k == ek).all()
+    manifest, arrays = golden
+    for case in manifest["sort_cases"][::4]:
+        keys, vals, exp_k, exp_v = case_arrays(arrays, case)
+        k, v = _sort(keys, vals, case["count"], bit_count=case["bit_count"])
+        assert (k == exp_k).all(), case
+        if vals is not None:
+            assert (v == exp_v).all(), case

@@ -51,5 +51,9 @@ int main() {
     if (run(size_t(1) << 28, true)) return 1;
     if (run(size_t(1) << 26, false)) return 1;
     if (run(size_t(1) << 20, false)) return 1;
+    if (run(size_t(1) << 20, true)) return 1;
+    if (run(100000, false)) return 1;
+    if (run(10000000, false)) return 1;
+    if (run(size_t(1) << 24, true)) return 1;
     return 0;
 }

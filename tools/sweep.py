@@ -21,7 +21,7 @@ import torch
 from radix_sort_amd import RadixSortKernel, ops
 res = []
 for name, n, kv, rb in %(loads)s:
-    nb = 4
+    nb = 4 if n > (1 << 22) else 20
     bs = []
     for i in range(nb):
         k = torch.empty(n, dtype=torch.int32, device="cuda")
@@ -36,12 +36,16 @@ for name, n, kv, rb in %(loads)s:
         wv = torch.empty(n, dtype=torch.int32, device="cuda"); ops.fill_iota_u32(wv)
     RadixSortKernel(keys=wk, values=wv, count=n, radix_bits=rb).dispatch()
     ks = [RadixSortKernel(keys=k, values=v, count=n, radix_bits=rb) for k, v in bs]
-    for kk in ks: kk.set_profiling(True)
     torch.cuda.synchronize()
     t = time.perf_counter()
     for kk in ks: kk.dispatch()
     torch.cuda.synchronize()
-    dt = (time.perf_counter() - t) / nb
+    dt = (time.perf_counter() - t) / nb          # wall time, profiling off
+    for i in range(nb):                           # fresh unsorted inputs for the profiled run
+        ops.fill_random_u32(bs[i][0], 500 + i)
+    for kk in ks: kk.set_profiling(True)
+    for kk in ks: kk.dispatch()
+    torch.cuda.synchronize()
     kt = {}
     for kk in ks:
         for a, b in kk.kernel_times().items():
@@ -56,6 +60,10 @@ print("RESULT " + json.dumps(res))
 '''
 
 LOADS = [("config3_kv_256M", 1 << 28, True, 0), ("config2_keys_64M", 1 << 26, False, 0)]
+if os.environ.get("SWEEP_SMALL"):
+    LOADS = [("keys_100K", 100_000, False, 0), ("keys_1M", 1 << 20, False, 0),
+             ("kv_1M", 1 << 20, True, 0), ("keys_10M", 10_000_000, False, 0),
+             ("kv_16M", 1 << 24, True, 0)]
 
 COPY = r'''
 import json, time, torch

@@ -3,47 +3,34 @@
 // One global HBM pass sorts one digit of `w <= R` bits (R = 2: exactly the reference's 4-way
 // pass; R = 8: four fused 4-way splits per HBM round trip).  Per pass, three kernels:
 //
-//   k_histogram  — per-workgroup digit counts over a contiguous chunk of tiles
-//                  (the reference's block-sum half of radix_sort, RadixSort.ts:50-126)
-//   k_scan_rows  — exclusive scan of the digit x workgroup count matrix, one row per digit,
-//                  plus the per-digit totals (the PrefixSumKernel chain over the 4*WC
-//                  block sums, PrefixSum.ts:13-106 / AbstractRadixSortKernel.ts:240)
-//   k_scatter    — per tile: wavefront ballot ranking (stable, per digit), tile-level digit
-//                  offsets, local shuffle through LDS (RadixSortLocalShuffle.ts:94-116),
-//                  and a coalesced scatter of keys (+values) to their global positions
-//                  (RadixSortReorder.ts:80-102)
+//   k_histogram  — per-tile digit counts, one wave per tile
+//                  (the block-sum half of the reference's radix_sort, RadixSort.ts:50-126)
+//   k_scan_rows  — exclusive scan of each digit's row of tile counts + digit totals
+//                  (the PrefixSumKernel chain over the digit-major block sums,
+//                  PrefixSum.ts:13-106, AbstractRadixSortKernel.ts:240)
+//   k_scatter    — per tile: stable in-wave ranking, tile digit offsets, local shuffle through
+//                  LDS (RadixSortLocalShuffle.ts:94-116), coalesced scatter of keys (+values)
+//                  to their global positions (RadixSortReorder.ts:80-102)
+//
+// and k_sort_small: the whole sort of up to one tile in one workgroup, all passes in LDS.
 //
 // Data layout in HBM: keys / values are separate u32 arrays (structure of arrays, as the
-// reference's two GPUBuffers); the count matrix is digit-major counts[d * G + g] like the
+// reference's two GPUBuffers); the count matrix is digit-major counts[d * ntiles + t] like the
 // reference's block_sums[b * WORKGROUP_COUNT + WORKGROUP_ID] (RadixSort.ts:113).
-//
-// Workgroup g of the histogram and scatter kernels owns the contiguous tile range
-// [g*base + min(g, extra), ...) so its digit-d output for all its tiles is ONE contiguous run
-// (the running per-digit base lives in a register of thread d): partial cache lines only at
-// chunk edges, and the L2 of the owning XCD merges consecutive tile runs.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#ifndef RS_KV_INTERLEAVED
-#define RS_KV_INTERLEAVED 1  // stage (key, value) pairs as one 64-bit LDS word (ds_write_b64/ds_read_b64)
-#endif
-#ifndef RS_NT_LOAD
-#define RS_NT_LOAD 0         // 1: non-temporal (streaming) loads of the pass input
-#endif
-#ifndef RS_NT_STORE
-#define RS_NT_STORE 0        // 1: all scatter stores nt; 2: nt only for lines fully written by the tile
-#endif
 #ifndef RS_XCD_GROUP
-#define RS_XCD_GROUP 1       // interleaved mode: consecutive tiles run on one XCD in the same round
+#define RS_XCD_GROUP 1       // consecutive tiles run on one XCD in the same round (speed only)
 #endif
 #ifndef RS_SCATTER_DEBUG
-#define RS_SCATTER_DEBUG 0   // ablations for tools/sweep.py: 1 linear writes, 3 no stores
-#endif
+#define RS_SCATTER_DEBUG 0   // ablations (tools/sweep.py): 1 linear writes, 3 no stores,
+#endif                       //   4 drop partially covered 32-B sectors
 
 namespace rs {
 
-constexpr int kBlock = 256;              // threads per workgroup: 4 waves of 64
+constexpr int kBlock = 256;              // threads of the small kernels: 4 waves of 64
 constexpr int kWaves = kBlock / 64;
 
 // ---- small helpers ---------------------------------------------------------------------
@@ -65,16 +52,17 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
     return v;
 }
 
-// Exclusive scan of one u32 per thread over the 256-thread block.  `scratch` >= 4 u32 LDS.
-// Contains two barriers; every thread of the block must call it.
-__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* scratch, uint32_t& total) {
+// Exclusive scan of one u32 per thread over an NW-wave workgroup; scratch >= NW u32 of LDS.
+// Contains two barriers; every thread of the workgroup must call it.
+template <int NW>
+__device__ __forceinline__ uint32_t block_excl_scan_n(uint32_t v, uint32_t* scratch, uint32_t& total) {
     const uint32_t inc = wave_incl_scan(v);
     const uint32_t w = threadIdx.x >> 6;
     if (lane_id() == 63) scratch[w] = inc;
     __syncthreads();
     uint32_t pre = 0, tot = 0;
 #pragma unroll
-    for (uint32_t i = 0; i < (uint32_t)kWaves; ++i) {
+    for (uint32_t i = 0; i < (uint32_t)NW; ++i) {
         uint32_t s = scratch[i];
         pre += (i < w) ? s : 0u;
         tot += s;
@@ -84,17 +72,21 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* scratc
     return pre + inc - v;
 }
 
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* scratch, uint32_t& total) {
+    return block_excl_scan_n<kWaves>(v, scratch, total);
+}
+
 // check_order gate: inv[c] == 0 means check c found (or inherited) "sorted", so every kernel
 // of pass >= c is skipped (replaces the reference's zeroed indirect dispatch sizes,
 // CheckSort.ts:115-145).  gate == nullptr when check_order is off.
 __device__ __forceinline__ bool gated_off(const uint32_t* gate, int upto) {
     if (!gate) return false;
     for (int c = 0; c <= upto; ++c)
-        if (__builtin_nontemporal_load(gate + c) == 0u) return true;
+        if (gate[c] == 0u) return true;
     return false;
 }
 
-struct Chunk {          // tile range of one workgroup
+struct Chunk {          // contiguous tile range of one workgroup (prefix-sum kernels)
     uint32_t first;     // first tile
     uint32_t count;     // number of tiles
 };
@@ -107,113 +99,77 @@ __device__ __forceinline__ Chunk chunk_of(uint32_t g, uint32_t base, uint32_t ex
 }
 
 // ---- histogram (upsweep) -----------------------------------------------------------------
-// counts[d * G + g] = number of keys of workgroup g's chunk whose digit is d.  Each thread keeps
-// UNROLL 16-byte loads in flight; per-wave LDS histograms (ds_add_u32, no return).
-template <int R, int TILE>
+// counts[d * ntiles + t] = number of keys of tile t whose digit is d.  Every wave histograms
+// whole tiles on its own (wave-private LDS counters: one wave's LDS operations execute in
+// order, so no barrier is needed between its atomics and its read-back), with U 16-byte loads
+// per lane in flight, double-buffered across iterations.
+template <int R, int TILE, int U>
 __global__ __launch_bounds__(kBlock) void k_histogram(
-    const uint32_t* __restrict__ keys, uint32_t n, uint32_t shift, uint32_t mask,
-    uint32_t base, uint32_t extra, uint32_t* __restrict__ counts, const uint32_t* gate, int pass) {
-    constexpr int RADIX = 1 << R;
-    constexpr int UNROLL = 8;
-    constexpr uint32_t STEP = 4u * kBlock * UNROLL;     // keys per block iteration
-    __shared__ uint32_t hist[kWaves][RADIX];
-    if (gated_off(gate, pass)) return;
-    const uint32_t G = gridDim.x, g = blockIdx.x, tid = threadIdx.x, w = tid >> 6;
-    for (uint32_t i = tid; i < (uint32_t)(kWaves * RADIX); i += kBlock) (&hist[0][0])[i] = 0u;
-    __syncthreads();
-    const Chunk ch = chunk_of(g, base, extra);
-    const uint64_t lo64 = (uint64_t)ch.first * TILE;
-    const uint32_t lo = (uint32_t)lo64;
-    const uint64_t hi64 = lo64 + (uint64_t)ch.count * TILE;
-    const uint32_t hi = (uint32_t)(hi64 < n ? hi64 : n);
-    uint32_t* h = hist[w];
-    const bool vec = (((uintptr_t)keys) & 15u) == 0;
-    uint32_t i = lo;
-    if (vec) {
-        const uint32_t full_end = lo + ((hi - lo) / STEP) * STEP;
-        for (; i < full_end; i += STEP) {
-            uint4 q[UNROLL];
-#pragma unroll
-            for (int u = 0; u < UNROLL; ++u)
-                q[u] = *reinterpret_cast<const uint4*>(keys + i + u * (4 * kBlock) + 4 * tid);
-#pragma unroll
-            for (int u = 0; u < UNROLL; ++u) {
-                atomicAdd(&h[(q[u].x >> shift) & mask], 1u);
-                atomicAdd(&h[(q[u].y >> shift) & mask], 1u);
-                atomicAdd(&h[(q[u].z >> shift) & mask], 1u);
-                atomicAdd(&h[(q[u].w >> shift) & mask], 1u);
-            }
-        }
-    }
-    for (uint32_t j = i + tid; j < hi; j += kBlock) atomicAdd(&h[(keys[j] >> shift) & mask], 1u);
-    __syncthreads();
-    for (uint32_t d = tid; d < (uint32_t)RADIX; d += kBlock) {
-        uint32_t s = 0;
-#pragma unroll
-        for (int v = 0; v < kWaves; ++v) s += hist[v][d];
-        counts[(size_t)d * G + g] = s;
-    }
-}
-
-// Tile-interleaved variant: workgroup g owns tiles g, g+G, g+2G, ... and writes one count row
-// entry per TILE: counts[d * ntiles + t].  With this ownership the workgroups running at the
-// same time work on adjacent tiles, so their scatter writes for each digit form one contiguous
-// stream instead of one cursor per workgroup.
-template <int R, int TILE, int HB>
-__global__ __launch_bounds__(HB) void k_histogram_tiles(
     const uint32_t* __restrict__ keys, uint32_t n, uint32_t shift, uint32_t mask,
     uint32_t ntiles, uint32_t* __restrict__ counts, const uint32_t* gate, int pass) {
     constexpr int RADIX = 1 << R;
-    constexpr int NW = HB / 64;
-    constexpr int PER = TILE / (4 * HB);               // uint4 loads per thread per tile
-    static_assert(TILE % (4 * HB) == 0, "tile must be a multiple of 4*HB");
-    __shared__ uint32_t hist[NW][RADIX];
+    constexpr int STEP = 64 * 4 * U;                    // keys per wave per iteration
+    constexpr int ITERS = TILE / STEP;
+    static_assert(TILE % STEP == 0, "tile must be a multiple of the wave step");
+    __shared__ uint32_t hist[kWaves][RADIX];
     if (gated_off(gate, pass)) return;
-    const uint32_t G = gridDim.x, tid = threadIdx.x, w = tid >> 6;
+    const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+    const uint32_t nwaves = gridDim.x * kWaves;
     uint32_t* h = hist[w];
     const bool vec = (((uintptr_t)keys) & 15u) == 0;
-    for (uint32_t t = blockIdx.x; t < ntiles; t += G) {
-        for (uint32_t i = tid; i < (uint32_t)(NW * RADIX); i += HB) (&hist[0][0])[i] = 0u;
-        __syncthreads();
+    for (uint32_t t = blockIdx.x * kWaves + w; t < ntiles; t += nwaves) {
+        for (uint32_t d = lane; d < (uint32_t)RADIX; d += 64) h[d] = 0u;
         const uint32_t lo = t * (uint32_t)TILE;
         if (vec && (uint64_t)lo + TILE <= n) {
-            uint4 q[PER];
+            const uint4* src = reinterpret_cast<const uint4*>(keys + lo) + lane;
+            uint4 a[U], b[U];
 #pragma unroll
-            for (int u = 0; u < PER; ++u)
-                q[u] = *reinterpret_cast<const uint4*>(keys + lo + u * (4 * HB) + 4 * tid);
+            for (int u = 0; u < U; ++u) a[u] = src[u * 64];
+#pragma unroll 1
+            for (int it = 0; it < ITERS; it += 2) {
+                if (it + 1 < ITERS) {
 #pragma unroll
-            for (int u = 0; u < PER; ++u) {
-                atomicAdd(&h[(q[u].x >> shift) & mask], 1u);
-                atomicAdd(&h[(q[u].y >> shift) & mask], 1u);
-                atomicAdd(&h[(q[u].z >> shift) & mask], 1u);
-                atomicAdd(&h[(q[u].w >> shift) & mask], 1u);
+                    for (int u = 0; u < U; ++u) b[u] = src[(it + 1) * (STEP / 4) + u * 64];
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    atomicAdd(&h[(a[u].x >> shift) & mask], 1u);
+                    atomicAdd(&h[(a[u].y >> shift) & mask], 1u);
+                    atomicAdd(&h[(a[u].z >> shift) & mask], 1u);
+                    atomicAdd(&h[(a[u].w >> shift) & mask], 1u);
+                }
+                if (it + 1 < ITERS) {
+                    if (it + 2 < ITERS) {
+#pragma unroll
+                        for (int u = 0; u < U; ++u) a[u] = src[(it + 2) * (STEP / 4) + u * 64];
+                    }
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        atomicAdd(&h[(b[u].x >> shift) & mask], 1u);
+                        atomicAdd(&h[(b[u].y >> shift) & mask], 1u);
+                        atomicAdd(&h[(b[u].z >> shift) & mask], 1u);
+                        atomicAdd(&h[(b[u].w >> shift) & mask], 1u);
+                    }
+                }
             }
         } else {
             const uint32_t hi = (uint64_t)lo + TILE < n ? lo + (uint32_t)TILE : n;
-            for (uint32_t j = lo + tid; j < hi; j += HB) atomicAdd(&h[(keys[j] >> shift) & mask], 1u);
+            for (uint32_t j = lo + lane; j < hi; j += 64) atomicAdd(&h[(keys[j] >> shift) & mask], 1u);
         }
-        __syncthreads();
-        for (uint32_t d = tid; d < (uint32_t)RADIX; d += HB) {
-            uint32_t c = 0;
-#pragma unroll
-            for (int v = 0; v < NW; ++v) c += hist[v][d];
-            counts[(size_t)d * ntiles + t] = c;
-        }
-        __syncthreads();
+        for (uint32_t d = lane; d < (uint32_t)RADIX; d += 64) counts[(size_t)d * ntiles + t] = h[d];
     }
 }
 
-// ---- digit x workgroup scan ----------------------------------------------------------------
+// ---- digit x tile scan ---------------------------------------------------------------------
 // Block d scans row d of counts (rowlen entries) to an exclusive prefix in place and writes the
-// row total to totals[d].  The row goes through LDS in segments of SCAN_SEG entries: coalesced
-// loads, each thread then owns SCAN_SEG/256 CONTIGUOUS entries (thread-local scan + one block
-// scan per segment), coalesced stores.
+// row total to totals[d].  The row goes through LDS in segments of up to kScanSeg entries:
+// coalesced loads, each thread then owns `per` CONTIGUOUS entries (thread-local scan + one block
+// scan per segment), coalesced stores.  Short rows use a short segment.
 constexpr int kScanSeg = 8192;
 __global__ __launch_bounds__(kBlock) void k_scan_rows(uint32_t* __restrict__ counts,
                                                       uint32_t rowlen,
                                                       uint32_t* __restrict__ totals,
                                                       const uint32_t* gate, int pass) {
-    constexpr int PER = kScanSeg / kBlock;   // contiguous entries per thread
     __shared__ uint32_t buf[kScanSeg + kScanSeg / 32];   // +1 word per 32: conflict-free rows
     __shared__ uint32_t scratch[kWaves];
     if (gated_off(gate, pass)) return;
@@ -223,19 +179,22 @@ __global__ __launch_bounds__(kBlock) void k_scan_rows(uint32_t* __restrict__ cou
     uint32_t carry = 0;
     for (uint32_t seg0 = 0; seg0 < rowlen; seg0 += kScanSeg) {
         const uint32_t len = rowlen - seg0 < (uint32_t)kScanSeg ? rowlen - seg0 : (uint32_t)kScanSeg;
-#pragma unroll 8
-        for (uint32_t i = tid; i < (uint32_t)kScanSeg; i += kBlock)
-            buf[at(i)] = i < len ? row[seg0 + i] : 0u;
+        const uint32_t per = (len + kBlock - 1) / kBlock;          // <= 32
+        const uint32_t seg = per * kBlock;
+#pragma unroll 4
+        for (uint32_t i = tid; i < seg; i += kBlock) buf[at(i)] = i < len ? row[seg0 + i] : 0u;
         __syncthreads();
-        uint32_t x[PER], sum = 0;
-#pragma unroll
-        for (int q = 0; q < PER; ++q) { x[q] = buf[at(tid * PER + q)]; sum += x[q]; }
+        uint32_t sum = 0;
+        for (uint32_t q = 0; q < per; ++q) sum += buf[at(tid * per + q)];
         uint32_t tot;
         uint32_t run = carry + block_excl_scan(sum, scratch, tot);
-#pragma unroll
-        for (int q = 0; q < PER; ++q) { buf[at(tid * PER + q)] = run; run += x[q]; }
+        for (uint32_t q = 0; q < per; ++q) {
+            const uint32_t x = buf[at(tid * per + q)];
+            buf[at(tid * per + q)] = run;
+            run += x;
+        }
         __syncthreads();
-#pragma unroll 8
+#pragma unroll 4
         for (uint32_t i = tid; i < len; i += kBlock) row[seg0 + i] = buf[at(i)];
         carry += tot;
         __syncthreads();
@@ -255,8 +214,7 @@ __global__ __launch_bounds__(kBlock) void k_scan_rows(uint32_t* __restrict__ cou
 //    earlier slots and lower lanes: the stable rank, for ~3 VALU + 1 LDS op per 64 keys.
 //  * RANK_BALLOT: match mask from R ballots (lanes sharing my digit), mbcnt for the rank in
 //    the slot, the lowest lane bumps the wave counter (ds_add_rtn) and broadcasts it
-//    (ds_bpermute).  Architecture-guaranteed; ~60 VALU per 64 keys.  Selected with
-//    RSORT_RANK=ballot.
+//    (ds_bpermute).  Architecture-guaranteed; ~60 VALU per 64 keys.  RSORT_RANK=ballot.
 enum RankMode { RANK_LDS_ATOMIC = 0, RANK_BALLOT = 1 };
 
 template <int KPT, bool HAS_VALUES>
@@ -266,21 +224,12 @@ __device__ __forceinline__ void load_tile(const uint32_t* __restrict__ in_k,
                                           uint32_t (&v)[HAS_VALUES ? KPT : 1]) {
     const uint32_t lane = lane_id();
     if (full) {
-#if RS_NT_LOAD
-#pragma unroll
-        for (int j = 0; j < KPT; ++j) k[j] = __builtin_nontemporal_load(in_k + wbase + j * 64 + lane);
-        if (HAS_VALUES) {
-#pragma unroll
-            for (int j = 0; j < KPT; ++j) v[j] = __builtin_nontemporal_load(in_v + wbase + j * 64 + lane);
-        }
-#else
 #pragma unroll
         for (int j = 0; j < KPT; ++j) k[j] = in_k[wbase + j * 64 + lane];
         if (HAS_VALUES) {
 #pragma unroll
             for (int j = 0; j < KPT; ++j) v[j] = in_v[wbase + j * 64 + lane];
         }
-#endif
     } else {
 #pragma unroll
         for (int j = 0; j < KPT; ++j) {
@@ -306,30 +255,51 @@ __device__ __forceinline__ uint64_t match_mask(uint32_t d, uint64_t valid) {
     return ((uint64_t)mhi << 32) | mlo;
 }
 
-// Exclusive scan over a BLOCK-thread workgroup (NW waves); scratch >= NW u32 of LDS.
-template <int NW>
-__device__ __forceinline__ uint32_t block_excl_scan_n(uint32_t v, uint32_t* scratch, uint32_t& total) {
-    const uint32_t inc = wave_incl_scan(v);
-    const uint32_t w = threadIdx.x >> 6;
-    if (lane_id() == 63) scratch[w] = inc;
-    __syncthreads();
-    uint32_t pre = 0, tot = 0;
+// Stable in-wave ranks of the KPT slots (see RankMode); counters in `whist` (this wave's row).
+template <int R, int KPT, int RANK>
+__device__ __forceinline__ void rank_slots(const uint32_t (&k)[KPT], uint32_t (&rank)[KPT],
+                                           uint32_t* whist, uint32_t shift, uint32_t mask,
+                                           uint32_t wbase, uint32_t n, bool full) {
+    const uint32_t lane = lane_id();
+    if (RANK == RANK_LDS_ATOMIC) {
 #pragma unroll
-    for (uint32_t i = 0; i < (uint32_t)NW; ++i) {
-        uint32_t s = scratch[i];
-        pre += (i < w) ? s : 0u;
-        tot += s;
+        for (int j = 0; j < KPT; ++j) {
+            const uint32_t d = (k[j] >> shift) & mask;
+            if (full || wbase + j * 64 + lane < n) rank[j] = atomicAdd(&whist[d], 1u);
+        }
+    } else {
+        uint32_t info[KPT];
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) {
+            const uint32_t d = (k[j] >> shift) & mask;
+            const uint64_t valid = full ? ~0ull : __ballot(wbase + j * 64 + lane < n);
+            const uint64_t m = match_mask<R>(d, valid);
+            const uint32_t lt = mbcnt(m);
+            const uint32_t lo = (uint32_t)m, hi = (uint32_t)(m >> 32);
+            const uint32_t leader = lo ? (uint32_t)__builtin_ctz(lo)
+                                       : (hi ? 32u + (uint32_t)__builtin_ctz(hi) : 0u);
+            uint32_t old = 0;
+            if (lt == 0 && ((valid >> lane) & 1ull)) old = atomicAdd(&whist[d], (uint32_t)__popcll(m));
+            rank[j] = old;
+            info[j] = (leader << 16) | lt;
+        }
+#pragma unroll
+        for (int j = 0; j < KPT; ++j)
+            rank[j] = __builtin_amdgcn_ds_bpermute((int)((info[j] >> 16) << 2), (int)rank[j]) +
+                      (info[j] & 0xFFFFu);
     }
-    __syncthreads();
-    total = tot;
-    return pre + inc - v;
 }
 
-template <int R, int BLOCK, int KPT, bool HAS_VALUES, int RANK, bool IL>
+// Workgroup g owns tiles g, g+G, g+2G, ... (per-tile counts, so any ownership works).
+// XCD grouping (speed only, never correctness): workgroups are dealt round-robin over the 8
+// XCDs, so workgroup g sits on XCD g % 8 as slot g / 8.  Round r gives XCD x the tiles
+// (8r + x) * (G/8) + slot: the workgroups of one XCD scatter ADJACENT tiles at the same time,
+// so each digit's writes from one XCD form one contiguous stream.
+template <int R, int BLOCK, int KPT, bool HAS_VALUES, int RANK>
 __global__ __launch_bounds__(BLOCK) void k_scatter(
     const uint32_t* __restrict__ in_k, const uint32_t* __restrict__ in_v,
     uint32_t* __restrict__ out_k, uint32_t* __restrict__ out_v, uint32_t n, uint32_t shift,
-    uint32_t mask, uint32_t base, uint32_t extra, const uint32_t* __restrict__ counts,
+    uint32_t mask, uint32_t ntiles, const uint32_t* __restrict__ counts,
     const uint32_t* __restrict__ totals, const uint32_t* gate, int pass) {
     constexpr int RADIX = 1 << R;
     constexpr int NW = BLOCK / 64;
@@ -338,89 +308,44 @@ __global__ __launch_bounds__(BLOCK) void k_scatter(
     static_assert(RADIX <= BLOCK, "one digit per thread");
     __shared__ uint32_t s_whist[NW][RADIX];          // per-wave counts -> per-wave tile offsets
     __shared__ uint32_t s_gdelta[RADIX];             // global pos - tile pos, per digit
-#if RS_NT_STORE == 2 || RS_SCATTER_DEBUG >= 4
+#if RS_SCATTER_DEBUG >= 4
     __shared__ uint2 s_run[RADIX];                   // [lo, hi) of the digit's run in this tile
 #endif
     __shared__ uint32_t s_scratch[NW];
-    constexpr bool KVI = HAS_VALUES && RS_KV_INTERLEAVED;
-    __shared__ uint32_t s_keys[KVI ? 1 : TILE];
-    __shared__ uint32_t s_vals[(HAS_VALUES && !KVI) ? TILE : 1];
-    __shared__ uint2 s_kv[KVI ? TILE : 1];
+    __shared__ uint32_t s_keys[HAS_VALUES ? 1 : TILE];
+    __shared__ uint2 s_kv[HAS_VALUES ? TILE : 1];    // (key, value) staged as one 64-bit word
 
     if (gated_off(gate, pass)) return;
     const uint32_t G = gridDim.x, g = blockIdx.x, tid = threadIdx.x;
     const uint32_t w = tid >> 6, lane = lane_id();
 
-    // Global base of digit `tid`: sum of the totals of smaller digits.  Chunked ownership adds
-    // this workgroup's row prefix once and then runs on; interleaved ownership adds the
-    // tile's row prefix per tile.  (`base` = ntiles when IL.)
+    // Global base of digit `tid`: sum of the totals of smaller digits; the tile's row prefix
+    // is added per tile.
     uint32_t dtot = (tid < (uint32_t)RADIX) ? totals[tid] : 0u;
     uint32_t all;
     const uint32_t dbase = block_excl_scan_n<NW>(dtot, s_scratch, all);
-    uint32_t run = dbase;
-    const uint32_t ntiles = base;
-    const uint32_t rowlen = IL ? ntiles : G;
-    Chunk ch;
-    // XCD grouping (speed only, never correctness): workgroups are dealt round-robin over the
-    // 8 XCDs, so workgroup g sits on XCD g % 8 as slot g / 8.  Round r gives XCD x the tiles
-    // (8r + x) * (G/8) + slot: the G/8 workgroups of one XCD scatter ADJACENT tiles at the same
-    // time, and the partial cache lines where one tile's digit run meets the next tile's run
-    // are completed in that XCD's L2 instead of being written back twice.
-    const bool xg = IL && RS_XCD_GROUP && (G % 8u) == 0u;
-    const uint32_t gslot = xg ? (g >> 3) : g, gx = xg ? (g & 7u) : 0u, gper = xg ? (G >> 3) : G;
-    if (IL) {
-        ch.first = xg ? gx * gper + gslot : g;
-        ch.count = ch.first < ntiles ? (ntiles - ch.first + G - 1) / G : 0u;
-    } else {
-        ch = chunk_of(g, base, extra);
-        if (tid < (uint32_t)RADIX) run += counts[(size_t)tid * rowlen + g];
-    }
-    const uint32_t tstride = IL ? G : 1u;
+    const bool xg = RS_XCD_GROUP && (G % 8u) == 0u;
+    const uint32_t first = xg ? (g & 7u) * (G >> 3) + (g >> 3) : g;
+    const uint32_t count = first < ntiles ? (ntiles - first + G - 1) / G : 0u;
     uint32_t k[KPT];
     uint32_t v[HAS_VALUES ? KPT : 1];
-    if (ch.count) {
-        const uint32_t tile0 = ch.first * (uint32_t)TILE;
+    if (count) {
+        const uint32_t tile0 = first * (uint32_t)TILE;
         load_tile<KPT, HAS_VALUES>(in_k, in_v, tile0 + w * WAVE_KEYS, n,
                                    (uint64_t)tile0 + TILE <= n, k, v);
     }
-    for (uint32_t t = 0; t < ch.count; ++t) {
-        const uint32_t tidx = ch.first + t * tstride;
+    for (uint32_t t = 0; t < count; ++t) {
+        const uint32_t tidx = first + t * G;
         const uint32_t tile0 = tidx * (uint32_t)TILE;
-        if (IL && tid < (uint32_t)RADIX) run = dbase + counts[(size_t)tid * rowlen + tidx];
         const uint32_t wbase = tile0 + w * WAVE_KEYS;
         const bool full = (uint64_t)tile0 + TILE <= n;
+        uint32_t run = 0;
+        if (tid < (uint32_t)RADIX) run = dbase + counts[(size_t)tid * ntiles + tidx];
         // zero this wave's counters (the previous tile's readers finished at the last barrier)
         for (uint32_t d = lane; d < (uint32_t)RADIX; d += 64) s_whist[w][d] = 0u;
 
         uint32_t rank[KPT];
-        if (RANK == RANK_LDS_ATOMIC) {
-#pragma unroll
-            for (int j = 0; j < KPT; ++j) {
-                const uint32_t d = (k[j] >> shift) & mask;
-                if (full || wbase + j * 64 + lane < n) rank[j] = atomicAdd(&s_whist[w][d], 1u);
-            }
-        } else {
-            uint32_t info[KPT];
-#pragma unroll
-            for (int j = 0; j < KPT; ++j) {
-                const uint32_t d = (k[j] >> shift) & mask;
-                const uint64_t valid = full ? ~0ull : __ballot(wbase + j * 64 + lane < n);
-                const uint64_t m = match_mask<R>(d, valid);
-                const uint32_t lt = mbcnt(m);
-                const uint32_t lo = (uint32_t)m, hi = (uint32_t)(m >> 32);
-                const uint32_t leader = lo ? (uint32_t)__builtin_ctz(lo)
-                                           : (hi ? 32u + (uint32_t)__builtin_ctz(hi) : 0u);
-                uint32_t old = 0;
-                if (lt == 0 && ((valid >> lane) & 1ull))
-                    old = atomicAdd(&s_whist[w][d], (uint32_t)__popcll(m));
-                rank[j] = old;
-                info[j] = (leader << 16) | lt;
-            }
-#pragma unroll
-            for (int j = 0; j < KPT; ++j)
-                rank[j] = __builtin_amdgcn_ds_bpermute((int)((info[j] >> 16) << 2), (int)rank[j]) +
-                          (info[j] & 0xFFFFu);
-        }
+        rank_slots<R, KPT, RANK>(k, rank, s_whist[w], shift, mask, wbase, n, full);
         __syncthreads();
 
         // Per digit: offsets of each wave inside the tile, tile digit start, global delta.
@@ -436,10 +361,9 @@ __global__ __launch_bounds__(BLOCK) void k_scatter(
 #pragma unroll
             for (int q = 0; q < NW; ++q) { s_whist[q][tid] = o; o += wc[q]; }
             s_gdelta[tid] = run - tstart;
-#if RS_NT_STORE == 2 || RS_SCATTER_DEBUG >= 4
+#if RS_SCATTER_DEBUG >= 4
             s_run[tid] = make_uint2(run, run + c);
 #endif
-            run += c;
         }
         __syncthreads();
 
@@ -450,20 +374,16 @@ __global__ __launch_bounds__(BLOCK) void k_scatter(
                 const uint32_t d = (k[j] >> shift) & mask;
                 const uint32_t s = s_whist[w][d] + rank[j];
                 if (s < (uint32_t)TILE) {
-                    if (KVI) {
-                        s_kv[s] = make_uint2(k[j], v[j]);
-                    } else {
-                        s_keys[s] = k[j];
-                        if (HAS_VALUES) s_vals[s] = v[j];
-                    }
+                    if (HAS_VALUES) s_kv[s] = make_uint2(k[j], v[j]);
+                    else s_keys[s] = k[j];
                 }
             }
         }
         __syncthreads();
         // Prefetch the next tile into the (now free) key/value registers; its latency hides
         // under this tile's scatter.
-        if (t + 1 < ch.count) {
-            const uint32_t nt0 = tile0 + tstride * TILE;
+        if (t + 1 < count) {
+            const uint32_t nt0 = tile0 + G * TILE;
             load_tile<KPT, HAS_VALUES>(in_k, in_v, nt0 + w * WAVE_KEYS, n,
                                        (uint64_t)nt0 + TILE <= n, k, v);
         }
@@ -472,13 +392,12 @@ __global__ __launch_bounds__(BLOCK) void k_scatter(
 #pragma unroll 4
         for (uint32_t i = tid; i < nvalid; i += BLOCK) {
             uint32_t key, val = 0;
-            if (KVI) {
+            if (HAS_VALUES) {
                 const uint2 kv = s_kv[i];
                 key = kv.x;
                 val = kv.y;
             } else {
                 key = s_keys[i];
-                if (HAS_VALUES) val = s_vals[i];
             }
 #if RS_SCATTER_DEBUG == 1
             const uint32_t pos = tile0 + i + (s_gdelta[(key >> shift) & mask] & 0);
@@ -487,36 +406,101 @@ __global__ __launch_bounds__(BLOCK) void k_scatter(
 #endif
 #if RS_SCATTER_DEBUG == 3
             asm volatile("" ::"v"(key), "v"(pos), "v"(val));
-#else
-            if (pos < n) {  // never false for a consistent histogram; keeps a bug from faulting
-#if RS_NT_STORE == 1
-                __builtin_nontemporal_store(key, out_k + pos);
-                if (HAS_VALUES) __builtin_nontemporal_store(val, out_v + pos);
-#elif RS_NT_STORE == 2
-                const uint2 rr = s_run[(key >> shift) & mask];
-                if ((pos & ~31u) >= rr.x && (pos | 31u) < rr.y) {
-                    __builtin_nontemporal_store(key, out_k + pos);
-                    if (HAS_VALUES) __builtin_nontemporal_store(val, out_v + pos);
-                } else {
-                    out_k[pos] = key;
-                    if (HAS_VALUES) out_v[pos] = val;
-                }
-#elif RS_SCATTER_DEBUG >= 4
-                // ablation: drop elements of partially covered sectors (4: 32 B, 5: 128 B)
-                constexpr uint32_t SM = RS_SCATTER_DEBUG == 4 ? 7u : 31u;
-                const uint2 rr = s_run[(key >> shift) & mask];
-                if ((pos & ~SM) >= rr.x && (pos | SM) < rr.y) {
-                    out_k[pos] = key;
-                    if (HAS_VALUES) out_v[pos] = val;
-                }
-#else
+#elif RS_SCATTER_DEBUG == 4
+            const uint2 rr = s_run[(key >> shift) & mask];
+            if ((pos & ~7u) >= rr.x && (pos | 7u) < rr.y) {
                 out_k[pos] = key;
                 if (HAS_VALUES) out_v[pos] = val;
-#endif
+            }
+#else
+            if (pos < n) {  // never false for a consistent histogram; keeps a bug from faulting
+                out_k[pos] = key;
+                if (HAS_VALUES) out_v[pos] = val;
             }
 #endif
         }
         __syncthreads();
+    }
+}
+
+// ---- whole sort of a small array in one workgroup ------------------------------------------
+// n <= BLOCK*KPT: keys (+values) stay in registers between passes; every pass ranks, stages the
+// tile sorted by its digit in LDS, and reloads the registers from LDS.  One launch, one HBM read
+// and one HBM write for the whole sort.
+struct PassList {
+    uint32_t count;
+    uint32_t width[16];
+};
+
+template <int BLOCK, int KPT, bool HAS_VALUES, int RANK>
+__global__ __launch_bounds__(BLOCK) void k_sort_small(uint32_t* __restrict__ keys,
+                                                      uint32_t* __restrict__ values, uint32_t n,
+                                                      PassList passes) {
+    constexpr int R = 8, RADIX = 256;
+    constexpr int NW = BLOCK / 64;
+    constexpr int TILE = BLOCK * KPT;
+    constexpr int WAVE_KEYS = 64 * KPT;
+    __shared__ uint32_t s_whist[NW][RADIX];
+    __shared__ uint32_t s_scratch[NW];
+    __shared__ uint32_t s_keys[HAS_VALUES ? 1 : TILE];
+    __shared__ uint2 s_kv[HAS_VALUES ? TILE : 1];
+    const uint32_t tid = threadIdx.x, w = tid >> 6, lane = lane_id();
+    const uint32_t wbase = w * WAVE_KEYS;
+    uint32_t k[KPT];
+    uint32_t v[HAS_VALUES ? KPT : 1];
+    load_tile<KPT, HAS_VALUES>(keys, values, wbase, n, false, k, v);
+    uint32_t shift = 0;
+    for (uint32_t p = 0; p < passes.count; ++p) {
+        const uint32_t mask = (1u << passes.width[p]) - 1u;
+        for (uint32_t d = lane; d < (uint32_t)RADIX; d += 64) s_whist[w][d] = 0u;
+        uint32_t rank[KPT];
+        rank_slots<R, KPT, RANK>(k, rank, s_whist[w], shift, mask, wbase, n, false);
+        __syncthreads();
+        uint32_t c = 0, wc[NW];
+        if (tid < (uint32_t)RADIX) {
+#pragma unroll
+            for (int q = 0; q < NW; ++q) { wc[q] = s_whist[q][tid]; c += wc[q]; }
+        }
+        uint32_t ttot;
+        const uint32_t tstart = block_excl_scan_n<NW>(c, s_scratch, ttot);
+        if (tid < (uint32_t)RADIX) {
+            uint32_t o = tstart;
+#pragma unroll
+            for (int q = 0; q < NW; ++q) { s_whist[q][tid] = o; o += wc[q]; }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) {
+            if (wbase + j * 64 + lane < n) {
+                const uint32_t s = s_whist[w][(k[j] >> shift) & mask] + rank[j];
+                if (HAS_VALUES) s_kv[s] = make_uint2(k[j], v[j]);
+                else s_keys[s] = k[j];
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) {
+            const uint32_t p2 = wbase + j * 64 + lane;
+            if (p2 < n) {
+                if (HAS_VALUES) {
+                    const uint2 kv = s_kv[p2];
+                    k[j] = kv.x;
+                    v[j] = kv.y;
+                } else {
+                    k[j] = s_keys[p2];
+                }
+            }
+        }
+        shift += passes.width[p];
+        // the next pass writes s_whist / s_kv only after two more barriers
+    }
+#pragma unroll
+    for (int j = 0; j < KPT; ++j) {
+        const uint32_t p2 = wbase + j * 64 + lane;
+        if (p2 < n) {
+            keys[p2] = k[j];
+            if (HAS_VALUES) values[p2] = v[j];
+        }
     }
 }
 

@@ -45,28 +45,24 @@ rs_status fail(rs_status s, const char* fmt, ...) {
                         __LINE__);                                                     \
     } while (0)
 
-// Tuned geometry of the rank/scatter kernel.
-#ifndef RS_KPT
-#define RS_KPT 16
+// Tuned geometry (sweeps in tools/sweep.py).  Two scatter configurations:
+//   large: 1024 threads x 16 keys = 16384-key tiles, 145 KiB LDS, one workgroup per CU
+//   small:  256 threads x 16 keys =  4096-key tiles,  37 KiB LDS, four workgroups per CU
+// and a single-workgroup sort for n <= kTinyMax.
+#ifndef RS_SMALL_MAX
+#define RS_SMALL_MAX (12u << 20)  // n below this uses the small-tile configuration
 #endif
-#ifndef RS_INTERLEAVE
-#define RS_INTERLEAVE 1      // tile-interleaved workgroup ownership (see k_histogram_tiles)
+#ifndef RS_HIST_U
+#define RS_HIST_U 4               // 16-byte loads per lane per histogram iteration (x2 in flight)
 #endif
-#ifndef RS_HIST_BLOCK
-#define RS_HIST_BLOCK 512
-#endif
-#ifndef RS_SCATTER_BLOCK
-#define RS_SCATTER_BLOCK 1024
-#endif
-#ifndef RS_MAX_GRID
-#define RS_MAX_GRID 512
-#endif
-constexpr int kKPT = RS_KPT;                   // keys per thread per tile
-constexpr int kScatterBlock = RS_SCATTER_BLOCK;  // threads per rank/scatter workgroup
-constexpr int kTile = kScatterBlock * kKPT;    // keys per tile
-constexpr uint32_t kMaxGrid = RS_MAX_GRID;     // workgroups of histogram/scatter kernels
-constexpr bool kInterleave = RS_INTERLEAVE != 0;
-constexpr int kHistBlock = RS_HIST_BLOCK;
+struct TileCfg {
+    int block, kpt, tile;
+    uint32_t max_grid;
+};
+constexpr TileCfg kLarge{1024, 16, 16384, 512};
+constexpr TileCfg kSmall{256, 16, 4096, 1024};
+constexpr uint32_t kTinyMax = 1024 * 16;
+constexpr uint32_t kHistGrid = 2048;
 constexpr int kCheckGrid = 2048;
 
 struct DeviceGuard {
@@ -134,7 +130,7 @@ struct rs_plan {
     uint64_t capacity = 0;
     uint32_t* tmp_k = nullptr;
     uint32_t* tmp_v = nullptr;
-    uint32_t* counts = nullptr;    // [256][kMaxGrid]
+    uint32_t* counts = nullptr;    // [256][ntiles] digit-major tile counts
     uint32_t* totals = nullptr;    // [256]
     uint32_t* flags = nullptr;     // [16] check_order results
     uint64_t workspace = 0;
@@ -144,101 +140,109 @@ struct rs_plan {
 struct rs_scan_plan {
     int device = 0;
     uint64_t count = 0;
-    uint32_t* sums = nullptr;     // [kMaxGrid]
+    uint32_t* sums = nullptr;     // [kScanMaxGrid]
 };
 
 namespace {
 
 uint32_t pick_R(uint32_t w) { return w <= 2 ? 2 : (w <= 4 ? 4 : 8); }
 
-struct Geometry {
-    uint32_t grid, base, extra;
-};
-
-Geometry geometry(uint64_t n, uint32_t tile, uint32_t max_grid, bool interleave = false) {
-    const uint64_t tiles = (n + tile - 1) / tile;
-    Geometry g;
-    g.grid = (uint32_t)std::min<uint64_t>(tiles, max_grid);
-    if (g.grid == 0) g.grid = 1;
-    if (interleave) {           // workgroup g owns tiles g, g+grid, ...; base = tile count
-        g.base = (uint32_t)std::max<uint64_t>(tiles, 1);
-        g.extra = 0;
-        return g;
-    }
-    g.base = (uint32_t)(tiles / g.grid);
-    g.extra = (uint32_t)(tiles % g.grid);
-    return g;
+bool use_small_tiles(uint64_t n) {
+    if (const char* e = getenv("RSORT_TILE")) return strcmp(e, "small") == 0;
+    return n < RS_SMALL_MAX;
 }
 
-template <int R>
+template <int R, int TILE>
 void launch_histogram(const uint32_t* in, uint32_t n, uint32_t shift, uint32_t mask,
-                      const Geometry& geo, uint32_t* counts, const uint32_t* gate, int pass,
+                      uint32_t ntiles, uint32_t* counts, const uint32_t* gate, int pass,
                       hipStream_t s) {
-    if (kInterleave) {
-        const uint32_t ntiles = geo.base;
-        const uint32_t grid = std::min<uint32_t>(ntiles, kMaxGrid);
-        hipLaunchKernelGGL((rs::k_histogram_tiles<R, kTile, kHistBlock>), dim3(grid),
-                           dim3(kHistBlock), 0, s, in, n, shift, mask, ntiles, counts, gate, pass);
-    } else {
-        hipLaunchKernelGGL((rs::k_histogram<R, kTile>), dim3(geo.grid), dim3(rs::kBlock), 0, s,
-                           in, n, shift, mask, geo.base, geo.extra, counts, gate, pass);
-    }
+    const uint32_t grid = std::min<uint32_t>((ntiles + rs::kWaves - 1) / rs::kWaves, kHistGrid);
+    hipLaunchKernelGGL((rs::k_histogram<R, TILE, RS_HIST_U>), dim3(grid), dim3(rs::kBlock), 0, s,
+                       in, n, shift, mask, ntiles, counts, gate, pass);
 }
 
-template <int R, bool V, int RANK>
+template <int R, int BLOCK, int KPT, bool V, int RANK>
 void launch_scatter_t(const uint32_t* ik, const uint32_t* iv, uint32_t* ok, uint32_t* ov,
-                      uint32_t n, uint32_t shift, uint32_t mask, const Geometry& geo,
+                      uint32_t n, uint32_t shift, uint32_t mask, uint32_t ntiles, uint32_t grid,
                       const uint32_t* counts, const uint32_t* totals, const uint32_t* gate,
                       int pass, hipStream_t s) {
-    hipLaunchKernelGGL((rs::k_scatter<R, kScatterBlock, kKPT, V, RANK, kInterleave>), dim3(geo.grid),
-                       dim3(kScatterBlock), 0, s, ik, iv, ok, ov, n, shift, mask, geo.base,
-                       geo.extra, counts, totals, gate, pass);
+    hipLaunchKernelGGL((rs::k_scatter<R, BLOCK, KPT, V, RANK>), dim3(grid), dim3(BLOCK), 0, s,
+                       ik, iv, ok, ov, n, shift, mask, ntiles, counts, totals, gate, pass);
 }
 
-template <int R>
+template <int R, int BLOCK, int KPT>
 void launch_scatter(bool V, int rank_mode, const uint32_t* ik, const uint32_t* iv, uint32_t* ok,
-                    uint32_t* ov, uint32_t n, uint32_t shift, uint32_t mask, const Geometry& geo,
-                    const uint32_t* counts, const uint32_t* totals, const uint32_t* gate,
-                    int pass, hipStream_t s) {
-    if (V) {
-        if (rank_mode == rs::RANK_BALLOT)
-            launch_scatter_t<R, true, rs::RANK_BALLOT>(ik, iv, ok, ov, n, shift, mask, geo, counts, totals, gate, pass, s);
-        else
-            launch_scatter_t<R, true, rs::RANK_LDS_ATOMIC>(ik, iv, ok, ov, n, shift, mask, geo, counts, totals, gate, pass, s);
-    } else {
-        if (rank_mode == rs::RANK_BALLOT)
-            launch_scatter_t<R, false, rs::RANK_BALLOT>(ik, iv, ok, ov, n, shift, mask, geo, counts, totals, gate, pass, s);
-        else
-            launch_scatter_t<R, false, rs::RANK_LDS_ATOMIC>(ik, iv, ok, ov, n, shift, mask, geo, counts, totals, gate, pass, s);
-    }
+                    uint32_t* ov, uint32_t n, uint32_t shift, uint32_t mask, uint32_t ntiles,
+                    uint32_t grid, const uint32_t* counts, const uint32_t* totals,
+                    const uint32_t* gate, int pass, hipStream_t s) {
+    constexpr int A = rs::RANK_LDS_ATOMIC, B = rs::RANK_BALLOT;
+    if (V && rank_mode == B)
+        launch_scatter_t<R, BLOCK, KPT, true, B>(ik, iv, ok, ov, n, shift, mask, ntiles, grid, counts, totals, gate, pass, s);
+    else if (V)
+        launch_scatter_t<R, BLOCK, KPT, true, A>(ik, iv, ok, ov, n, shift, mask, ntiles, grid, counts, totals, gate, pass, s);
+    else if (rank_mode == B)
+        launch_scatter_t<R, BLOCK, KPT, false, B>(ik, iv, ok, ov, n, shift, mask, ntiles, grid, counts, totals, gate, pass, s);
+    else
+        launch_scatter_t<R, BLOCK, KPT, false, A>(ik, iv, ok, ov, n, shift, mask, ntiles, grid, counts, totals, gate, pass, s);
 }
 
-// One stable digit pass in -> out (histogram, scan, scatter).
-rs_status run_pass(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint32_t* ok,
-                   uint32_t* ov, uint32_t n, uint32_t shift, uint32_t w, bool values,
-                   const uint32_t* gate, int pass, hipStream_t s) {
-    const uint32_t R = pick_R(w);
+// One stable digit pass in -> out (histogram, scan, scatter) with tile configuration C.
+template <int R, int BLOCK, int KPT>
+rs_status run_pass_cfg(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint32_t* ok,
+                       uint32_t* ov, uint32_t n, uint32_t shift, uint32_t w, bool values,
+                       const uint32_t* gate, int pass, uint32_t max_grid, hipStream_t s) {
+    constexpr int TILE = BLOCK * KPT;
     const uint32_t mask = (1u << w) - 1u;
-    const Geometry geo = geometry(n, kTile, kMaxGrid, kInterleave);
-    const uint32_t rowlen = kInterleave ? geo.base : geo.grid;
+    const uint32_t ntiles = (uint32_t)(((uint64_t)n + TILE - 1) / TILE);
+    const uint32_t grid = std::min<uint32_t>(ntiles, max_grid);
     p->timer.run(RS_KERNEL_HISTOGRAM, s, [&] {
-        if (R == 2) launch_histogram<2>(ik, n, shift, mask, geo, p->counts, gate, pass, s);
-        else if (R == 4) launch_histogram<4>(ik, n, shift, mask, geo, p->counts, gate, pass, s);
-        else launch_histogram<8>(ik, n, shift, mask, geo, p->counts, gate, pass, s);
+        launch_histogram<R, TILE>(ik, n, shift, mask, ntiles, p->counts, gate, pass, s);
     });
     HIP_TRY(hipGetLastError());
     p->timer.run(RS_KERNEL_SCAN, s, [&] {
         hipLaunchKernelGGL(rs::k_scan_rows, dim3(1u << R), dim3(rs::kBlock), 0, s, p->counts,
-                           rowlen, p->totals, gate, pass);
+                           ntiles, p->totals, gate, pass);
     });
     HIP_TRY(hipGetLastError());
     // The scatter always stages the tile through LDS (the local shuffle,
-    // RadixSortLocalShuffle.ts:94-116): it is what makes the writes coalesced, so the
-    // local_shuffle flag only selects what the reference's option name promises.
+    // RadixSortLocalShuffle.ts:94-116): it is what makes the writes coalesced.
     p->timer.run(RS_KERNEL_SCATTER, s, [&] {
-        if (R == 2) launch_scatter<2>(values, p->rank_mode, ik, iv, ok, ov, n, shift, mask, geo, p->counts, p->totals, gate, pass, s);
-        else if (R == 4) launch_scatter<4>(values, p->rank_mode, ik, iv, ok, ov, n, shift, mask, geo, p->counts, p->totals, gate, pass, s);
-        else launch_scatter<8>(values, p->rank_mode, ik, iv, ok, ov, n, shift, mask, geo, p->counts, p->totals, gate, pass, s);
+        launch_scatter<R, BLOCK, KPT>(values, p->rank_mode, ik, iv, ok, ov, n, shift, mask, ntiles,
+                                      grid, p->counts, p->totals, gate, pass, s);
+    });
+    HIP_TRY(hipGetLastError());
+    return RS_OK;
+}
+
+rs_status run_pass(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint32_t* ok,
+                   uint32_t* ov, uint32_t n, uint32_t shift, uint32_t w, bool values,
+                   const uint32_t* gate, int pass, hipStream_t s) {
+    const uint32_t R = pick_R(w);
+    if (use_small_tiles(n)) {
+        if (R == 2) return run_pass_cfg<2, kSmall.block, kSmall.kpt>(p, ik, iv, ok, ov, n, shift, w, values, gate, pass, kSmall.max_grid, s);
+        if (R == 4) return run_pass_cfg<4, kSmall.block, kSmall.kpt>(p, ik, iv, ok, ov, n, shift, w, values, gate, pass, kSmall.max_grid, s);
+        return run_pass_cfg<8, kSmall.block, kSmall.kpt>(p, ik, iv, ok, ov, n, shift, w, values, gate, pass, kSmall.max_grid, s);
+    }
+    if (R == 2) return run_pass_cfg<2, kLarge.block, kLarge.kpt>(p, ik, iv, ok, ov, n, shift, w, values, gate, pass, kLarge.max_grid, s);
+    if (R == 4) return run_pass_cfg<4, kLarge.block, kLarge.kpt>(p, ik, iv, ok, ov, n, shift, w, values, gate, pass, kLarge.max_grid, s);
+    return run_pass_cfg<8, kLarge.block, kLarge.kpt>(p, ik, iv, ok, ov, n, shift, w, values, gate, pass, kLarge.max_grid, s);
+}
+
+// Whole sort of n <= kTinyMax in one workgroup (k_sort_small).
+rs_status run_tiny(rs_plan* p, uint32_t* k, uint32_t* v, uint32_t n, hipStream_t s) {
+    rs::PassList pl{};
+    pl.count = p->passes;
+    for (uint32_t i = 0; i < p->passes; ++i) pl.width[i] = p->widths[i];
+    constexpr int A = rs::RANK_LDS_ATOMIC, B = rs::RANK_BALLOT;
+    p->timer.run(RS_KERNEL_SCATTER, s, [&] {
+        if (v && p->rank_mode == B)
+            hipLaunchKernelGGL((rs::k_sort_small<1024, 16, true, B>), dim3(1), dim3(1024), 0, s, k, v, n, pl);
+        else if (v)
+            hipLaunchKernelGGL((rs::k_sort_small<1024, 16, true, A>), dim3(1), dim3(1024), 0, s, k, v, n, pl);
+        else if (p->rank_mode == B)
+            hipLaunchKernelGGL((rs::k_sort_small<1024, 16, false, B>), dim3(1), dim3(1024), 0, s, k, v, n, pl);
+        else
+            hipLaunchKernelGGL((rs::k_sort_small<1024, 16, false, A>), dim3(1), dim3(1024), 0, s, k, v, n, pl);
     });
     HIP_TRY(hipGetLastError());
     return RS_OK;
@@ -317,7 +321,7 @@ RS_EXPORT rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out) {
     hipError_t e;
     if ((e = alloc(&p->tmp_k, 4 * d.count)) != hipSuccess ||
         (p->has_values && (e = alloc(&p->tmp_v, 4 * d.count)) != hipSuccess) ||
-        (e = alloc(&p->counts, 4ull * 256 * std::max<uint64_t>(kMaxGrid, (d.count + kTile - 1) / kTile))) != hipSuccess ||
+        (e = alloc(&p->counts, 4ull * 256 * std::max<uint64_t>(1, (d.count + kSmall.tile - 1) / kSmall.tile))) != hipSuccess ||
         (e = alloc(&p->totals, 4ull * 256)) != hipSuccess ||
         (e = alloc(&p->flags, 4ull * 16)) != hipSuccess)
         return cleanup(fail(e == hipErrorOutOfMemory ? RS_ERR_OUT_OF_MEMORY : RS_ERR_HIP,
@@ -356,6 +360,7 @@ RS_EXPORT rs_status rs_plan_sort_n(rs_plan* p, void* keys, void* values, uint64_
     const uint32_t n32 = (uint32_t)n;
     uint32_t* uk = (uint32_t*)keys;
     uint32_t* uv = V ? (uint32_t*)values : nullptr;
+    if (n <= kTinyMax) return run_tiny(p, uk, uv, n32, s);   // one launch; check_order moot
     const uint32_t* gate = p->check_order ? p->flags : nullptr;
     if (p->check_order) HIP_TRY(hipMemsetAsync(p->flags, 0, 16 * 4, s));
     const uint32_t fmask = full_mask(p->bit_count);
@@ -428,8 +433,10 @@ RS_EXPORT rs_status rs_plan_info_get(const rs_plan* p, rs_plan_info* info) {
     memset(info, 0, sizeof(*info));
     info->passes = p->passes;
     for (uint32_t i = 0; i < p->passes && i < 16; ++i) info->digit_bits[i] = p->widths[i];
-    info->tile_keys = kTile;
-    info->grid_blocks = geometry(p->capacity, kTile, kMaxGrid, kInterleave).grid;
+    const TileCfg& c = use_small_tiles(p->capacity) ? kSmall : kLarge;
+    info->tile_keys = p->capacity <= kTinyMax ? kTinyMax : (uint32_t)c.tile;
+    info->grid_blocks = p->capacity <= kTinyMax ? 1u
+        : (uint32_t)std::min<uint64_t>((p->capacity + c.tile - 1) / c.tile, c.max_grid);
     info->workspace_bytes = p->workspace;
     return RS_OK;
 }
@@ -463,6 +470,16 @@ RS_EXPORT rs_status rs_plan_reset_kernel_times(rs_plan* p) {
 // ---- prefix sum ----------------------------------------------------------------------------
 namespace {
 constexpr int kScanTile = 4096;
+constexpr uint32_t kScanMaxGrid = 1024;
+struct Geometry { uint32_t grid, base, extra; };
+Geometry geometry(uint64_t n, uint32_t tile, uint32_t max_grid) {
+    const uint64_t tiles = (n + tile - 1) / tile;
+    Geometry g;
+    g.grid = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(tiles, 1), max_grid);
+    g.base = (uint32_t)(tiles / g.grid);
+    g.extra = (uint32_t)(tiles % g.grid);
+    return g;
+}
 }
 
 RS_EXPORT rs_status rs_scan_plan_create(int32_t device, uint64_t count, uint32_t wx, uint32_t wy,
@@ -484,7 +501,7 @@ RS_EXPORT rs_status rs_scan_plan_create(int32_t device, uint64_t count, uint32_t
     p->device = device;
     p->count = count;
     DeviceGuard guard(device);
-    hipError_t e = hipMalloc((void**)&p->sums, 4ull * kMaxGrid);
+    hipError_t e = hipMalloc((void**)&p->sums, 4ull * kScanMaxGrid);
     if (e != hipSuccess) {
         delete p;
         return fail(RS_ERR_OUT_OF_MEMORY, "rs_scan_plan_create: %s", hipGetErrorString(e));
@@ -500,7 +517,7 @@ RS_EXPORT rs_status rs_scan_plan_run(rs_scan_plan* p, void* data, void* stream) 
     DeviceGuard guard(p->device);
     hipStream_t s = (hipStream_t)stream;
     const uint32_t n = (uint32_t)p->count;
-    const Geometry geo = geometry(n, kScanTile, kMaxGrid);
+    const Geometry geo = geometry(n, kScanTile, kScanMaxGrid);
     hipLaunchKernelGGL(rs::k_chunk_sums<kScanTile>, dim3(geo.grid), dim3(rs::kBlock), 0, s,
                        (const uint32_t*)data, n, geo.base, geo.extra, p->sums);
     HIP_TRY(hipGetLastError());

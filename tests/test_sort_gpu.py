@@ -282,24 +282,3 @@ def test_rank_modes_and_tile_configs(monkeypatch, golden, rank, tile):
         if vals is not None:
             assert (v == exp_v).all(), case
 
-
-@pytest.mark.parametrize("onepass", ["1", "0"])
-@pytest.mark.parametrize("tile", ["small", "large"])
-def test_onepass_vs_three_kernel_path(monkeypatch, onepass, tile):
-    """The persistent one-launch-per-pass kernel and the histogram/scan/scatter path give the
-    oracle's result; the persistent kernel's bounded waits never time out."""
-    from radix_sort_amd import RadixSortKernel
-    monkeypatch.setenv("RSORT_ONEPASS", onepass)
-    monkeypatch.setenv("RSORT_TILE", tile)
-    for n, bits in ((16_385, 32), (100_003, 32), (2_500_000, 32), (5_000_001, 20), (40_000, 8)):
-        keys = O.gen_u32(n * 3 + bits, n)
-        keys[::3] = keys[1]
-        vals = np.arange(n, dtype=np.uint32)
-        kt, vt = _t(keys), _t(vals)
-        k = RadixSortKernel(keys=kt, values=vt, count=n, bit_count=bits)
-        k.dispatch()
-        torch.cuda.synchronize()
-        assert k.device_errors() == 0
-        ek, ev = O.stable_sort_masked(keys, vals, bits)
-        assert (_np(kt) == ek).all() and (_np(vt) == ev).all(), (n, bits)
-        k.destroy()

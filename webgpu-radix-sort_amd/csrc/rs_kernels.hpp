@@ -387,18 +387,6 @@ __global__ __launch_bounds__(BLOCK) void k_scatter(
             load_tile<KPT, HAS_VALUES>(in_k, in_v, nt0 + w * WAVE_KEYS, n,
                                        (uint64_t)nt0 + TILE <= n, k, v);
         }
-#if RS_SCATTER_DEBUG == 5
-        // ablation: read the keys of the tile two rounds ahead (as a look-ahead histogram would)
-        if (t + 2 < count) {
-            const uint32_t t2 = tile0 + 2 * G * TILE + w * WAVE_KEYS;
-            if ((uint64_t)t2 + WAVE_KEYS <= n) {
-                uint32_t x = 0;
-#pragma unroll
-                for (int j = 0; j < KPT; ++j) x ^= in_k[t2 + j * 64 + lane];
-                asm volatile("" ::"v"(x));
-            }
-        }
-#endif
         // Coalesced scatter: consecutive lanes write consecutive positions of a digit run.
         const uint32_t nvalid = full ? (uint32_t)TILE : n - tile0;
 #pragma unroll 4
@@ -440,285 +428,6 @@ struct PassList {
     uint32_t count;
     uint32_t width[16];
 };
-
-// ---- whole-array digit totals of every pass, from one read of the keys --------------------
-// The digit histogram of pass p over the whole array does not depend on the order the earlier
-// passes left the keys in, so the unsorted input gives all passes' totals at once (one read
-// of the keys per sort instead of a histogram read per pass).  out[off(p) + d], off(p) = sum of
-// 2^width[<p] (<= 1024 entries), must be zeroed.  Wave-private LDS counters, one global atomic
-// per counter per workgroup.
-constexpr int kTotalsMax = 1024;
-__global__ __launch_bounds__(kBlock) void k_pass_totals(const uint32_t* __restrict__ keys,
-                                                        uint32_t n, PassList pl,
-                                                        uint32_t* __restrict__ out) {
-    __shared__ uint32_t hist[kWaves][kTotalsMax];
-    const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
-    uint32_t total = 0;
-    for (uint32_t p = 0; p < pl.count; ++p) total += 1u << pl.width[p];
-    for (uint32_t i = tid; i < (uint32_t)(kWaves * kTotalsMax); i += kBlock) (&hist[0][0])[i] = 0u;
-    __syncthreads();
-    uint32_t* h = hist[w];
-    auto count_key = [&](uint32_t key) {
-        uint32_t off = 0, shift = 0;
-        for (uint32_t p = 0; p < pl.count; ++p) {
-            const uint32_t wd = pl.width[p];
-            atomicAdd(&h[off + ((key >> shift) & ((1u << wd) - 1u))], 1u);
-            off += 1u << wd;
-            shift += wd;
-        }
-    };
-    const uint32_t nv = n / 4;
-    const uint4* k4 = reinterpret_cast<const uint4*>(keys);
-    const bool vec = (((uintptr_t)keys) & 15u) == 0;
-    const uint32_t stride = gridDim.x * kBlock;
-    if (vec) {
-        for (uint32_t i = blockIdx.x * kBlock + tid; i < nv; i += stride) {
-            const uint4 q = k4[i];
-            count_key(q.x); count_key(q.y); count_key(q.z); count_key(q.w);
-        }
-        for (uint32_t i = 4 * nv + blockIdx.x * kBlock + tid; i < n; i += stride) count_key(keys[i]);
-    } else {
-        for (uint32_t i = blockIdx.x * kBlock + tid; i < n; i += stride) count_key(keys[i]);
-    }
-    (void)lane;
-    __syncthreads();
-    for (uint32_t i = tid; i < total; i += kBlock) {
-        uint32_t c = 0;
-#pragma unroll
-        for (int q = 0; q < kWaves; ++q) c += hist[q][i];
-        if (c) atomicAdd(&out[i], c);
-    }
-}
-
-// ---- one launch per pass: persistent rank + scatter with look-ahead digit counts -----------
-// G workgroups, all resident (G <= CUs x workgroups per CU).  Round r = tiles [rG, rG+G);
-// workgroup g owns slot(g) of every round (XCD-grouped as in k_scatter).  Per round r a
-// workgroup:
-//   * consumes pfx[T_r][*] (global start of each digit for its tile; produced in round r-1),
-//   * ranks, stages and scatters T_r (as k_scatter), prefetching T_{r+1}'s keys/values,
-//   * reads the keys of T_{r+2} and publishes their digit counts agg[T_{r+2}][*] (that read
-//     warms the Infinity Cache for the real read one round later, so no separate histogram pass
-//     reads the array from HBM),
-//   * scans digits d = g, g+G, ... over the tiles of round r+1 (agg, published in round r-1)
-//     and publishes pfx for round r+1, carrying each digit's running base.
-// Hand-offs follow the fence-free form of MI355X_MICROARCH.md §Workgroup dispatch "Valid
-// forms" row 1: payload stored write-through (sc1, agent-scope relaxed atomic store) and loaded
-// with sc1 loads; every storing wave drains (s_waitcnt vmcnt(0)) before the workgroup barrier;
-// ONE lane then adds to a per-round counter (agent-scope atomic); the consumer polls that
-// counter with relaxed agent loads.  Counters are zeroed by a memset before every launch.
-// Spins are bounded: on timeout err[0] is set and the pass output is garbage (never a hang).
-struct OnepassSync {
-    uint32_t* agg_ready;   // [nrounds] workgroups that published counts for round r
-    uint32_t* pfx_ready;   // [nrounds] digit scanners that published prefixes for round r
-    uint32_t* err;         // [1] spin timeouts
-};
-
-__device__ __forceinline__ uint32_t ld_sc1(const uint32_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_sc1(uint32_t* p, uint32_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Called by all threads.  Thread 0 spins until *ctr >= target; everyone leaves after a barrier.
-#ifndef RS_ONEPASS_DEBUG
-#define RS_ONEPASS_DEBUG 0   // ablations (wrong results): 1 no waits, 2 no scan duty, 3 both
-#endif
-__device__ __forceinline__ void wait_counter(const uint32_t* ctr, uint32_t target, uint32_t* err) {
-    if ((RS_ONEPASS_DEBUG & 1) == 0 && threadIdx.x == 0) {
-        uint32_t spins = 0;
-        while (ld_sc1(ctr) < target) {
-            __builtin_amdgcn_s_sleep(2);
-            if (++spins > (1u << 22)) {   // ~seconds: a non-resident grid or a bug, never a hang
-                atomicOr(err, 1u);
-                break;
-            }
-        }
-    }
-    __syncthreads();
-}
-
-// Called by all threads after they stored (sc1) their part of a payload.
-__device__ __forceinline__ void signal_counter(uint32_t* ctr) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-template <int R, int BLOCK, int KPT, bool HAS_VALUES, int RANK>
-__global__ __launch_bounds__(BLOCK) void k_onepass(
-    const uint32_t* __restrict__ in_k, const uint32_t* __restrict__ in_v,
-    uint32_t* __restrict__ out_k, uint32_t* __restrict__ out_v, uint32_t n, uint32_t shift,
-    uint32_t mask, uint32_t ntiles, uint32_t* agg, uint32_t* pfx, OnepassSync sync,
-    const uint32_t* __restrict__ dtot, const uint32_t* gate, int pass) {
-    constexpr int RADIX = 1 << R;
-    constexpr int NW = BLOCK / 64;
-    constexpr int TILE = BLOCK * KPT;
-    constexpr int WAVE_KEYS = 64 * KPT;
-    static_assert(RADIX <= BLOCK, "one digit per thread");
-    __shared__ uint32_t s_whist[NW][RADIX];
-    __shared__ uint32_t s_gdelta[RADIX];
-    __shared__ uint32_t s_base[RADIX];
-    __shared__ uint32_t s_scratch[NW];
-    __shared__ uint32_t s_keys[HAS_VALUES ? 1 : TILE];
-    __shared__ uint2 s_kv[HAS_VALUES ? TILE : 1];
-
-    if (gated_off(gate, pass)) return;
-    const uint32_t G = gridDim.x, g = blockIdx.x, tid = threadIdx.x;
-    const uint32_t w = tid >> 6, lane = lane_id();
-    const bool xg = RS_XCD_GROUP && (G % 8u) == 0u;
-    const uint32_t slot = xg ? (g & 7u) * (G >> 3) + (g >> 3) : g;
-    const uint32_t nrounds = (ntiles + G - 1) / G;
-    auto tile_of = [&](uint32_t r) { return r * G + slot; };
-    auto in_round = [&](uint32_t r) { return ntiles - r * G < G ? ntiles - r * G : G; };
-    const uint32_t scanners = G < (uint32_t)RADIX ? G : (uint32_t)RADIX;
-
-    // Digit counts of tile T (keys read now, counted in s_whist), published to agg[T][*].
-    // s_whist must be free; contains barriers; all threads call it (no-op when T >= ntiles).
-    auto publish_counts = [&](uint32_t r, const uint32_t (&kc)[KPT]) {
-        const uint32_t T = tile_of(r);
-        if (r >= nrounds || T >= ntiles) return;
-        for (uint32_t d = lane; d < (uint32_t)RADIX; d += 64) s_whist[w][d] = 0u;
-        const uint32_t wb = T * (uint32_t)TILE + w * WAVE_KEYS;
-#pragma unroll
-        for (int j = 0; j < KPT; ++j)
-            if (wb + j * 64 + lane < n) atomicAdd(&s_whist[w][(kc[j] >> shift) & mask], 1u);
-        __syncthreads();
-        if (tid < (uint32_t)RADIX) {
-            uint32_t c = 0;
-#pragma unroll
-            for (int q = 0; q < NW; ++q) c += s_whist[q][tid];
-            st_sc1(agg + (size_t)T * RADIX + tid, c);
-        }
-        signal_counter(sync.agg_ready + r);
-    };
-    auto load_keys = [&](uint32_t r, uint32_t (&kc)[KPT]) {
-        const uint32_t T = tile_of(r);
-        if (r >= nrounds || T >= ntiles) return;
-        const uint32_t wb = T * (uint32_t)TILE + w * WAVE_KEYS;
-#pragma unroll
-        for (int j = 0; j < KPT; ++j) {
-            const uint32_t p = wb + j * 64 + lane;
-            kc[j] = p < n ? in_k[p] : 0u;
-        }
-    };
-    // Scan duty for round q: digits d = g, g+G, ... over the round's tiles; each digit's
-    // running base (total over earlier rounds) lives in s_base[d] of its scanner.
-    // s_base[d] starts at digit d's first output position: exclusive scan of the whole-array
-    // digit totals of this pass (k_pass_totals).
-    {
-        const uint32_t c = tid <= mask && tid < (uint32_t)RADIX ? dtot[tid] : 0u;
-        uint32_t all;
-        const uint32_t ex = block_excl_scan_n<NW>(c, s_scratch, all);
-        if (tid < (uint32_t)RADIX) s_base[tid] = ex;
-    }
-    auto scan_duty = [&](uint32_t q) {
-        if (q >= nrounds || g >= scanners || (RS_ONEPASS_DEBUG & 2)) return;
-        wait_counter(sync.agg_ready + q, in_round(q), sync.err);
-        const uint32_t m = in_round(q);
-        for (uint32_t d = g; d < (uint32_t)RADIX; d += G) {
-            uint32_t b = s_base[d];
-            for (uint32_t i0 = 0; i0 < m; i0 += BLOCK) {
-                const uint32_t i = i0 + tid;
-                const uint32_t c = i < m ? ld_sc1(agg + (size_t)(q * G + i) * RADIX + d) : 0u;
-                uint32_t tot;
-                const uint32_t ex = block_excl_scan_n<NW>(c, s_scratch, tot);
-                if (i < m) st_sc1(pfx + (size_t)(q * G + i) * RADIX + d, b + ex);
-                b += tot;
-            }
-            if (tid == 0) s_base[d] = b;
-        }
-        signal_counter(sync.pfx_ready + q);
-    };
-
-    // ---- prologue: counts for rounds 0 and 1, prefixes for round 0, first tile -----------------
-    uint32_t k[KPT];
-    uint32_t v[HAS_VALUES ? KPT : 1];
-    {
-        uint32_t kc[KPT];
-        load_keys(0, kc);
-        publish_counts(0, kc);
-        load_keys(1, kc);
-        __syncthreads();
-        publish_counts(1, kc);
-    }
-    scan_duty(0);
-    if (tile_of(0) < ntiles) {
-        const uint32_t tile0 = tile_of(0) * (uint32_t)TILE;
-        load_tile<KPT, HAS_VALUES>(in_k, in_v, tile0 + w * WAVE_KEYS, n,
-                                   (uint64_t)tile0 + TILE <= n, k, v);
-    }
-
-    for (uint32_t r = 0; r < nrounds; ++r) {
-        const uint32_t T = tile_of(r);
-        const bool have = T < ntiles;
-        uint32_t kc[KPT];
-        if (have) {
-            const uint32_t tile0 = T * (uint32_t)TILE;
-            const uint32_t wbase = tile0 + w * WAVE_KEYS;
-            const bool full = (uint64_t)tile0 + TILE <= n;
-            for (uint32_t d = lane; d < (uint32_t)RADIX; d += 64) s_whist[w][d] = 0u;
-            uint32_t rank[KPT];
-            rank_slots<R, KPT, RANK>(k, rank, s_whist[w], shift, mask, wbase, n, full);
-            __syncthreads();
-            uint32_t c = 0, wc[NW];
-            if (tid < (uint32_t)RADIX) {
-#pragma unroll
-                for (int q = 0; q < NW; ++q) { wc[q] = s_whist[q][tid]; c += wc[q]; }
-            }
-            uint32_t ttot;
-            const uint32_t tstart = block_excl_scan_n<NW>(c, s_scratch, ttot);
-            wait_counter(sync.pfx_ready + r, scanners, sync.err);
-            if (tid < (uint32_t)RADIX) {
-                uint32_t o = tstart;
-#pragma unroll
-                for (int q = 0; q < NW; ++q) { s_whist[q][tid] = o; o += wc[q]; }
-                s_gdelta[tid] = ld_sc1(pfx + (size_t)T * RADIX + tid) - tstart;
-            }
-            __syncthreads();
-#pragma unroll
-            for (int j = 0; j < KPT; ++j) {
-                if (full || wbase + j * 64 + lane < n) {
-                    const uint32_t d = (k[j] >> shift) & mask;
-                    const uint32_t s = s_whist[w][d] + rank[j];
-                    if (s < (uint32_t)TILE) {
-                        if (HAS_VALUES) s_kv[s] = make_uint2(k[j], v[j]);
-                        else s_keys[s] = k[j];
-                    }
-                }
-            }
-            __syncthreads();
-            if (r + 1 < nrounds && tile_of(r + 1) < ntiles) {
-                const uint32_t nt0 = tile_of(r + 1) * (uint32_t)TILE;
-                load_tile<KPT, HAS_VALUES>(in_k, in_v, nt0 + w * WAVE_KEYS, n,
-                                           (uint64_t)nt0 + TILE <= n, k, v);
-            }
-            load_keys(r + 2, kc);
-            const uint32_t nvalid = full ? (uint32_t)TILE : n - tile0;
-#pragma unroll 4
-            for (uint32_t i = tid; i < nvalid; i += BLOCK) {
-                uint32_t key, val = 0;
-                if (HAS_VALUES) {
-                    const uint2 kv = s_kv[i];
-                    key = kv.x;
-                    val = kv.y;
-                } else {
-                    key = s_keys[i];
-                }
-                const uint32_t pos = s_gdelta[(key >> shift) & mask] + i;
-                if (pos < n) {
-                    out_k[pos] = key;
-                    if (HAS_VALUES) out_v[pos] = val;
-                }
-            }
-            __syncthreads();
-        } else {
-            load_keys(r + 2, kc);
-        }
-        publish_counts(r + 2, kc);
-        scan_duty(r + 1);
-    }
-}
 
 // ---- whole sort of a small array in one workgroup ------------------------------------------
 // n <= BLOCK*KPT: keys (+values) stay in registers between passes; every pass ranks, stages the

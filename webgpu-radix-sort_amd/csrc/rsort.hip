@@ -133,14 +133,6 @@ struct rs_plan {
     uint32_t* counts = nullptr;    // [256][ntiles] digit-major tile counts
     uint32_t* totals = nullptr;    // [256]
     uint32_t* flags = nullptr;     // [16] check_order results
-    uint32_t* agg = nullptr;       // [ntiles][256] look-ahead digit counts (k_onepass)
-    uint32_t* pfx = nullptr;       // [ntiles][256] per-tile digit starts (k_onepass)
-    uint32_t* ptot = nullptr;      // [<=1024] whole-array digit totals of every pass (k_onepass)
-    uint32_t ptot_off[16] = {};    // offset of pass i's totals in ptot
-    uint32_t* sync = nullptr;      // [passes][2*max_rounds] + err: k_onepass hand-off counters
-    uint32_t sync_stride = 0;      // words per pass in `sync`
-    uint32_t cus = 256;            // compute units of the device
-    bool onepass = false;          // RSORT_ONEPASS=1 selects the persistent k_onepass path
     uint64_t workspace = 0;
     KernelTimer timer;
 };
@@ -194,68 +186,15 @@ void launch_scatter(bool V, int rank_mode, const uint32_t* ik, const uint32_t* i
         launch_scatter_t<R, BLOCK, KPT, false, A>(ik, iv, ok, ov, n, shift, mask, ntiles, grid, counts, totals, gate, pass, s);
 }
 
-template <class F>
-uint32_t resident_blocks(F kernel, int block, uint32_t lds_bytes) {
-    int api = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&api, kernel, block, 0) != hipSuccess) api = 1;
-    const uint32_t by_lds = lds_bytes ? (uint32_t)(163840u / lds_bytes) : 8u;
-    return std::max<uint32_t>(1, std::min<uint32_t>((uint32_t)api, by_lds));
-}
-
-template <int R, int BLOCK, int KPT, bool V, int RANK>
-rs_status launch_onepass_t(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint32_t* ok,
-                           uint32_t* ov, uint32_t n, uint32_t shift, uint32_t mask,
-                           uint32_t ntiles, const uint32_t* gate, int pass, hipStream_t s) {
-    auto kern = rs::k_onepass<R, BLOCK, KPT, V, RANK>;
-    static uint32_t per_cu = 0;   // per instantiation
-    if (!per_cu) {
-        hipFuncAttributes attr;
-        uint32_t lds = 0;
-        if (hipFuncGetAttributes(&attr, (const void*)kern) == hipSuccess) lds = (uint32_t)attr.sharedSizeBytes;
-        per_cu = resident_blocks(kern, BLOCK, lds);
-    }
-    const uint32_t G = std::min<uint32_t>(ntiles, p->cus * per_cu);
-    const uint32_t nrounds = (ntiles + G - 1) / G;
-    rs::OnepassSync sy;
-    uint32_t* base = p->sync + (size_t)pass * p->sync_stride;
-    sy.agg_ready = base;
-    sy.pfx_ready = base + nrounds;
-    sy.err = p->sync + (size_t)16 * p->sync_stride;
-    hipLaunchKernelGGL(kern, dim3(G), dim3(BLOCK), 0, s, ik, iv, ok, ov, n, shift, mask, ntiles,
-                       p->agg, p->pfx, sy, p->ptot + p->ptot_off[pass], gate, pass);
-    return RS_OK;
-}
-
-template <int R, int BLOCK, int KPT>
-rs_status launch_onepass(rs_plan* p, bool V, const uint32_t* ik, const uint32_t* iv,
-                         uint32_t* ok, uint32_t* ov, uint32_t n, uint32_t shift, uint32_t mask,
-                         uint32_t ntiles, const uint32_t* gate, int pass, hipStream_t s) {
-    constexpr int A = rs::RANK_LDS_ATOMIC, B = rs::RANK_BALLOT;
-    if (V && p->rank_mode == B) return launch_onepass_t<R, BLOCK, KPT, true, B>(p, ik, iv, ok, ov, n, shift, mask, ntiles, gate, pass, s);
-    if (V) return launch_onepass_t<R, BLOCK, KPT, true, A>(p, ik, iv, ok, ov, n, shift, mask, ntiles, gate, pass, s);
-    if (p->rank_mode == B) return launch_onepass_t<R, BLOCK, KPT, false, B>(p, ik, iv, ok, ov, n, shift, mask, ntiles, gate, pass, s);
-    return launch_onepass_t<R, BLOCK, KPT, false, A>(p, ik, iv, ok, ov, n, shift, mask, ntiles, gate, pass, s);
-}
-
 // One stable digit pass in -> out (histogram, scan, scatter) with tile configuration C.
 template <int R, int BLOCK, int KPT>
 rs_status run_pass_cfg(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint32_t* ok,
                        uint32_t* ov, uint32_t n, uint32_t shift, uint32_t w, bool values,
-                       const uint32_t* gate, int pass, uint32_t max_grid, bool onepass,
-                       hipStream_t s) {
+                       const uint32_t* gate, int pass, uint32_t max_grid, hipStream_t s) {
     constexpr int TILE = BLOCK * KPT;
     const uint32_t mask = (1u << w) - 1u;
     const uint32_t ntiles = (uint32_t)(((uint64_t)n + TILE - 1) / TILE);
     const uint32_t grid = std::min<uint32_t>(ntiles, max_grid);
-    if (onepass) {
-        rs_status st = RS_OK;
-        p->timer.run(RS_KERNEL_SCATTER, s, [&] {
-            st = launch_onepass<R, BLOCK, KPT>(p, values, ik, iv, ok, ov, n, shift, mask, ntiles, gate, pass, s);
-        });
-        if (st != RS_OK) return st;
-        HIP_TRY(hipGetLastError());
-        return RS_OK;
-    }
     p->timer.run(RS_KERNEL_HISTOGRAM, s, [&] {
         launch_histogram<R, TILE>(ik, n, shift, mask, ntiles, p->counts, gate, pass, s);
     });
@@ -277,17 +216,16 @@ rs_status run_pass_cfg(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint3
 
 rs_status run_pass(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint32_t* ok,
                    uint32_t* ov, uint32_t n, uint32_t shift, uint32_t w, bool values,
-                   const uint32_t* gate, int pass, hipStream_t s, bool allow_onepass = true) {
+                   const uint32_t* gate, int pass, hipStream_t s) {
     const uint32_t R = pick_R(w);
-    const bool op = allow_onepass && p->onepass;
     if (use_small_tiles(n)) {
-        if (R == 2) return run_pass_cfg<2, kSmall.block, kSmall.kpt>(p, ik, iv, ok, ov, n, shift, w, values, gate, pass, kSmall.max_grid, op, s);
-        if (R == 4) return run_pass_cfg<4, kSmall.block, kSmall.kpt>(p, ik, iv, ok, ov, n, shift, w, values, gate, pass, kSmall.max_grid, op, s);
-        return run_pass_cfg<8, kSmall.block, kSmall.kpt>(p, ik, iv, ok, ov, n, shift, w, values, gate, pass, kSmall.max_grid, op, s);
+        if (R == 2) return run_pass_cfg<2, kSmall.block, kSmall.kpt>(p, ik, iv, ok, ov, n, shift, w, values, gate, pass, kSmall.max_grid, s);
+        if (R == 4) return run_pass_cfg<4, kSmall.block, kSmall.kpt>(p, ik, iv, ok, ov, n, shift, w, values, gate, pass, kSmall.max_grid, s);
+        return run_pass_cfg<8, kSmall.block, kSmall.kpt>(p, ik, iv, ok, ov, n, shift, w, values, gate, pass, kSmall.max_grid, s);
     }
-    if (R == 2) return run_pass_cfg<2, kLarge.block, kLarge.kpt>(p, ik, iv, ok, ov, n, shift, w, values, gate, pass, kLarge.max_grid, op, s);
-    if (R == 4) return run_pass_cfg<4, kLarge.block, kLarge.kpt>(p, ik, iv, ok, ov, n, shift, w, values, gate, pass, kLarge.max_grid, op, s);
-    return run_pass_cfg<8, kLarge.block, kLarge.kpt>(p, ik, iv, ok, ov, n, shift, w, values, gate, pass, kLarge.max_grid, op, s);
+    if (R == 2) return run_pass_cfg<2, kLarge.block, kLarge.kpt>(p, ik, iv, ok, ov, n, shift, w, values, gate, pass, kLarge.max_grid, s);
+    if (R == 4) return run_pass_cfg<4, kLarge.block, kLarge.kpt>(p, ik, iv, ok, ov, n, shift, w, values, gate, pass, kLarge.max_grid, s);
+    return run_pass_cfg<8, kLarge.block, kLarge.kpt>(p, ik, iv, ok, ov, n, shift, w, values, gate, pass, kLarge.max_grid, s);
 }
 
 // Whole sort of n <= kTinyMax in one workgroup (k_sort_small).
@@ -363,7 +301,6 @@ RS_EXPORT rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out) {
     p->has_values = d.flags & RS_FLAG_HAS_VALUES;
     p->check_order = d.flags & RS_FLAG_CHECK_ORDER;
     p->local_shuffle = d.flags & RS_FLAG_LOCAL_SHUFFLE;
-    if (const char* op = getenv("RSORT_ONEPASS")) p->onepass = strcmp(op, "0") != 0;
     if (const char* rk = getenv("RSORT_RANK"))
         p->rank_mode = (strcmp(rk, "ballot") == 0) ? rs::RANK_BALLOT : rs::RANK_LDS_ATOMIC;
     // Even number of passes so the result lands in the caller's buffers, like the reference's
@@ -371,45 +308,24 @@ RS_EXPORT rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out) {
     uint32_t P = (d.bit_count + rb - 1) / rb;
     P += P & 1u;
     p->passes = P;
-    for (uint32_t i = 0, off = 0; i < P; ++i) {
-        p->widths[i] = d.bit_count / P + (i < d.bit_count % P ? 1 : 0);
-        p->ptot_off[i] = off;
-        off += 1u << p->widths[i];
-    }
+    for (uint32_t i = 0; i < P; ++i) p->widths[i] = d.bit_count / P + (i < d.bit_count % P ? 1 : 0);
     p->capacity = d.count;
 
     DeviceGuard guard(d.device);
-    {
-        hipDeviceProp_t prop;
-        if (hipGetDeviceProperties(&prop, d.device) == hipSuccess && prop.multiProcessorCount > 0)
-            p->cus = (uint32_t)prop.multiProcessorCount;
-    }
     auto cleanup = [&](rs_status s) { rs_plan_destroy(p); return s; };
     auto alloc = [&](uint32_t** ptr, uint64_t bytes) -> hipError_t {
         if (bytes == 0) bytes = 4;
         p->workspace += bytes;
         return hipMalloc((void**)ptr, bytes);
     };
-    // tiles of the finest configuration that can be used for this count; rounds have >= 1 tile
-    const uint64_t max_tiles = std::max<uint64_t>(
-        1, std::max<uint64_t>((d.count + kLarge.tile - 1) / kLarge.tile,
-                              (std::min<uint64_t>(d.count, RS_SMALL_MAX) + kSmall.tile - 1) / kSmall.tile));
-    // rounds per pass: G >= min(ntiles, CUs), so at most ceil(max_tiles / CUs) rounds
-    p->sync_stride = (uint32_t)(2 * ((max_tiles + p->cus - 1) / p->cus) + 2);
     hipError_t e;
     if ((e = alloc(&p->tmp_k, 4 * d.count)) != hipSuccess ||
         (p->has_values && (e = alloc(&p->tmp_v, 4 * d.count)) != hipSuccess) ||
         (e = alloc(&p->counts, 4ull * 256 * std::max<uint64_t>(1, (d.count + kSmall.tile - 1) / kSmall.tile))) != hipSuccess ||
         (e = alloc(&p->totals, 4ull * 256)) != hipSuccess ||
-        (e = alloc(&p->ptot, 4ull * rs::kTotalsMax)) != hipSuccess ||
-        (e = alloc(&p->flags, 4ull * 16)) != hipSuccess ||
-        (e = alloc(&p->agg, 4ull * 256 * max_tiles)) != hipSuccess ||
-        (e = alloc(&p->pfx, 4ull * 256 * max_tiles)) != hipSuccess ||
-        (e = alloc(&p->sync, 4ull * (16 * p->sync_stride + 16))) != hipSuccess)
+        (e = alloc(&p->flags, 4ull * 16)) != hipSuccess)
         return cleanup(fail(e == hipErrorOutOfMemory ? RS_ERR_OUT_OF_MEMORY : RS_ERR_HIP,
                             "rs_plan_create: hipMalloc failed: %s", hipGetErrorString(e)));
-    if ((e = hipMemset(p->sync, 0, 4ull * (16 * p->sync_stride + 16))) != hipSuccess)
-        return cleanup(fail(RS_ERR_HIP, "rs_plan_create: hipMemset failed: %s", hipGetErrorString(e)));
     *out = p;
     return RS_OK;
 }
@@ -422,11 +338,7 @@ RS_EXPORT void rs_plan_destroy(rs_plan* p) {
     (void)hipFree(p->tmp_v);
     (void)hipFree(p->counts);
     (void)hipFree(p->totals);
-    (void)hipFree(p->ptot);
     (void)hipFree(p->flags);
-    (void)hipFree(p->agg);
-    (void)hipFree(p->pfx);
-    (void)hipFree(p->sync);
     delete p;
 }
 
@@ -451,18 +363,6 @@ RS_EXPORT rs_status rs_plan_sort_n(rs_plan* p, void* keys, void* values, uint64_
     if (n <= kTinyMax) return run_tiny(p, uk, uv, n32, s);   // one launch; check_order moot
     const uint32_t* gate = p->check_order ? p->flags : nullptr;
     if (p->check_order) HIP_TRY(hipMemsetAsync(p->flags, 0, 16 * 4, s));
-    if (p->onepass) {
-        HIP_TRY(hipMemsetAsync(p->sync, 0, 4ull * (16 * p->sync_stride + 16), s));
-        HIP_TRY(hipMemsetAsync(p->ptot, 0, 4ull * rs::kTotalsMax, s));
-        rs::PassList pl{};
-        pl.count = p->passes;
-        for (uint32_t i = 0; i < p->passes; ++i) pl.width[i] = p->widths[i];
-        const uint32_t grid = (uint32_t)std::min<uint64_t>(4ull * p->cus, (n / 4 + rs::kBlock - 1) / rs::kBlock + 1);
-        p->timer.run(RS_KERNEL_HISTOGRAM, s, [&] {
-            hipLaunchKernelGGL(rs::k_pass_totals, dim3(grid), dim3(rs::kBlock), 0, s, uk, n32, pl, p->ptot);
-        });
-        HIP_TRY(hipGetLastError());
-    }
     const uint32_t fmask = full_mask(p->bit_count);
     uint32_t shift = 0;
     for (uint32_t i = 0; i < p->passes; ++i) {
@@ -522,17 +422,9 @@ RS_EXPORT rs_status rs_plan_partition(rs_plan* p, const void* in_keys, const voi
     }
     rs_status st = run_pass(p, (const uint32_t*)in_keys, (const uint32_t*)in_values,
                             (uint32_t*)out_keys, (uint32_t*)out_values, (uint32_t)n, shift, bits,
-                            V, nullptr, 0, s, /*allow_onepass=*/false);
+                            V, nullptr, 0, s);
     if (st != RS_OK) return st;
     if (d_hist) HIP_TRY(hipMemcpyAsync(d_hist, p->totals, 4u << bits, hipMemcpyDeviceToDevice, s));
-    return RS_OK;
-}
-
-RS_EXPORT rs_status rs_plan_device_errors(rs_plan* p, uint32_t* errors) {
-    if (!p || !errors) return fail(RS_ERR_INVALID_ARG, "rs_plan_device_errors: null argument");
-    DeviceGuard guard(p->desc.device);
-    HIP_TRY(hipDeviceSynchronize());
-    HIP_TRY(hipMemcpy(errors, p->sync + (size_t)16 * p->sync_stride, 4, hipMemcpyDeviceToHost));
     return RS_OK;
 }
 

@@ -45,6 +45,11 @@ typedef enum rs_status {
 #define RS_FLAG_CHECK_ORDER          0x2u  /* check_order (AbstractRadixSortKernel.ts:249-276) */
 #define RS_FLAG_LOCAL_SHUFFLE        0x4u  /* local_shuffle (RadixSortBufferKernel.ts:38-44) */
 #define RS_FLAG_AVOID_BANK_CONFLICTS 0x8u  /* avoid_bank_conflicts (PrefixSumKernel.ts:37-40) */
+#define RS_FLAG_INTERLEAVED          0x10u /* RadixSortTextureKernel layout: `keys` points to count
+                                              8-byte (key, value) records (the rg32uint texels,
+                                              RadixSortTextureKernel.ts:15-35, RadixSortReorder.ts:
+                                              42-63), sorted in place; `values` must be NULL.
+                                              Implies values (RadixSortTextureKernel.ts:27-29). */
 
 /* Options of one sort plan (one RadixSortKernel instance). */
 typedef struct rs_plan_desc {
@@ -89,9 +94,10 @@ uint32_t    rs_version(void);                  /* (major << 16) | minor */
 /* ---- sort plans (RadixSortKernel) ------------------------------------------------------- */
 /* Validate options, allocate the workspace (tmp keys/values, block histograms) on `device`. */
 rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out);
-/* Sort keys[0..count) (and values[0..count) when RS_FLAG_HAS_VALUES) in place, ascending and
- * stable by (key & (2^bit_count - 1)); words at index >= count are untouched.  Float32 keys
- * sort by raw bit pattern (README.md:9).  Asynchronous on `stream`. */
+/* Sort keys[0..count) (and values[0..count) when RS_FLAG_HAS_VALUES; records[0..count) when
+ * RS_FLAG_INTERLEAVED) in place, ascending and stable by (key & (2^bit_count - 1)); elements
+ * at index >= count are untouched.  Float32 keys sort by raw bit pattern (README.md:9).
+ * Asynchronous on `stream`. */
 rs_status rs_plan_sort(rs_plan* plan, void* keys, void* values, void* stream);
 /* Same, for n <= the plan's count (multi-GPU receive buffers vary per call). */
 rs_status rs_plan_sort_n(rs_plan* plan, void* keys, void* values, uint64_t n, void* stream);

@@ -80,3 +80,9 @@ def test_python_facade_validates_both_spellings():
         RadixSortKernel(keys=0x1000)
     with pytest.raises(RadixSortError, match="power of two"):
         PrefixSumKernel(data=0x1000, count=10, workgroupSize={"x": 3, "y": 3})
+
+
+def test_interleaved_flag_is_known_and_next_bit_is_not():
+    # RS_FLAG_INTERLEAVED (0x10) passes option validation; 0x20 is rejected before any device work
+    assert _lib.RS_FLAG_INTERLEAVED == 0x10
+    assert _create(flags=0x20)[0] == _lib.RS_ERR_INVALID_ARG

@@ -33,6 +33,11 @@ namespace rs {
 constexpr int kBlock = 256;              // threads of the small kernels: 4 waves of 64
 constexpr int kWaves = kBlock / 64;
 
+// Key/value layouts in HBM.  KEYS: keys only.  SOA: separate key and value arrays (the
+// reference's RadixSortBufferKernel buffers).  AOS: one array of 8-byte (key, value) records,
+// the rg32uint texels of RadixSortTextureKernel (RadixSortReorder.ts:42-63), record i at word 2i.
+enum Layout { LAYOUT_KEYS = 0, LAYOUT_SOA = 1, LAYOUT_AOS = 2 };
+
 // ---- small helpers ---------------------------------------------------------------------
 
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
@@ -103,12 +108,14 @@ __device__ __forceinline__ Chunk chunk_of(uint32_t g, uint32_t base, uint32_t ex
 // whole tiles on its own (wave-private LDS counters: one wave's LDS operations execute in
 // order, so no barrier is needed between its atomics and its read-back), with U 16-byte loads
 // per lane in flight, double-buffered across iterations.
-template <int R, int TILE, int U>
+template <int R, int TILE, int U, int KS>
 __global__ __launch_bounds__(kBlock) void k_histogram(
     const uint32_t* __restrict__ keys, uint32_t n, uint32_t shift, uint32_t mask,
     uint32_t ntiles, uint32_t* __restrict__ counts, const uint32_t* gate, int pass) {
+    // KS = words per key (1: key array, 2: AOS records, the key in the low word)
     constexpr int RADIX = 1 << R;
-    constexpr int STEP = 64 * 4 * U;                    // keys per wave per iteration
+    constexpr int KPV = 4 / KS;                         // keys per 16-byte load
+    constexpr int STEP = 64 * KPV * U;                  // keys per wave per iteration
     constexpr int ITERS = TILE / STEP;
     static_assert(TILE % STEP == 0, "tile must be a multiple of the wave step");
     __shared__ uint32_t hist[kWaves][RADIX];
@@ -117,11 +124,17 @@ __global__ __launch_bounds__(kBlock) void k_histogram(
     const uint32_t nwaves = gridDim.x * kWaves;
     uint32_t* h = hist[w];
     const bool vec = (((uintptr_t)keys) & 15u) == 0;
+    auto count4 = [&](const uint4& q) {
+        atomicAdd(&h[(q.x >> shift) & mask], 1u);
+        if (KS == 1) atomicAdd(&h[(q.y >> shift) & mask], 1u);
+        atomicAdd(&h[(q.z >> shift) & mask], 1u);
+        if (KS == 1) atomicAdd(&h[(q.w >> shift) & mask], 1u);
+    };
     for (uint32_t t = blockIdx.x * kWaves + w; t < ntiles; t += nwaves) {
         for (uint32_t d = lane; d < (uint32_t)RADIX; d += 64) h[d] = 0u;
         const uint32_t lo = t * (uint32_t)TILE;
         if (vec && (uint64_t)lo + TILE <= n) {
-            const uint4* src = reinterpret_cast<const uint4*>(keys + lo) + lane;
+            const uint4* src = reinterpret_cast<const uint4*>(keys + (size_t)lo * KS) + lane;
             uint4 a[U], b[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) a[u] = src[u * 64];
@@ -129,32 +142,23 @@ __global__ __launch_bounds__(kBlock) void k_histogram(
             for (int it = 0; it < ITERS; it += 2) {
                 if (it + 1 < ITERS) {
 #pragma unroll
-                    for (int u = 0; u < U; ++u) b[u] = src[(it + 1) * (STEP / 4) + u * 64];
+                    for (int u = 0; u < U; ++u) b[u] = src[(it + 1) * (64 * U) + u * 64];
                 }
 #pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    atomicAdd(&h[(a[u].x >> shift) & mask], 1u);
-                    atomicAdd(&h[(a[u].y >> shift) & mask], 1u);
-                    atomicAdd(&h[(a[u].z >> shift) & mask], 1u);
-                    atomicAdd(&h[(a[u].w >> shift) & mask], 1u);
-                }
+                for (int u = 0; u < U; ++u) count4(a[u]);
                 if (it + 1 < ITERS) {
                     if (it + 2 < ITERS) {
 #pragma unroll
-                        for (int u = 0; u < U; ++u) a[u] = src[(it + 2) * (STEP / 4) + u * 64];
+                        for (int u = 0; u < U; ++u) a[u] = src[(it + 2) * (64 * U) + u * 64];
                     }
 #pragma unroll
-                    for (int u = 0; u < U; ++u) {
-                        atomicAdd(&h[(b[u].x >> shift) & mask], 1u);
-                        atomicAdd(&h[(b[u].y >> shift) & mask], 1u);
-                        atomicAdd(&h[(b[u].z >> shift) & mask], 1u);
-                        atomicAdd(&h[(b[u].w >> shift) & mask], 1u);
-                    }
+                    for (int u = 0; u < U; ++u) count4(b[u]);
                 }
             }
         } else {
             const uint32_t hi = (uint64_t)lo + TILE < n ? lo + (uint32_t)TILE : n;
-            for (uint32_t j = lo + lane; j < hi; j += 64) atomicAdd(&h[(keys[j] >> shift) & mask], 1u);
+            for (uint32_t j = lo + lane; j < hi; j += 64)
+                atomicAdd(&h[(keys[(size_t)j * KS] >> shift) & mask], 1u);
         }
         for (uint32_t d = lane; d < (uint32_t)RADIX; d += 64) counts[(size_t)d * ntiles + t] = h[d];
     }
@@ -217,13 +221,23 @@ __global__ __launch_bounds__(kBlock) void k_scan_rows(uint32_t* __restrict__ cou
 //    (ds_bpermute).  Architecture-guaranteed; ~60 VALU per 64 keys.  RSORT_RANK=ballot.
 enum RankMode { RANK_LDS_ATOMIC = 0, RANK_BALLOT = 1 };
 
-template <int KPT, bool HAS_VALUES>
+template <int KPT, int L>
 __device__ __forceinline__ void load_tile(const uint32_t* __restrict__ in_k,
                                           const uint32_t* __restrict__ in_v, uint32_t wbase,
                                           uint32_t n, bool full, uint32_t (&k)[KPT],
-                                          uint32_t (&v)[HAS_VALUES ? KPT : 1]) {
+                                          uint32_t (&v)[L != LAYOUT_KEYS ? KPT : 1]) {
+    constexpr bool HAS_VALUES = L != LAYOUT_KEYS;
     const uint32_t lane = lane_id();
-    if (full) {
+    if (L == LAYOUT_AOS) {
+        const uint2* rec = reinterpret_cast<const uint2*>(in_k);
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) {
+            const uint32_t p = wbase + j * 64 + lane;
+            const uint2 r = (full || p < n) ? rec[p] : make_uint2(0u, 0u);
+            k[j] = r.x;
+            v[j] = r.y;
+        }
+    } else if (full) {
 #pragma unroll
         for (int j = 0; j < KPT; ++j) k[j] = in_k[wbase + j * 64 + lane];
         if (HAS_VALUES) {
@@ -295,12 +309,13 @@ __device__ __forceinline__ void rank_slots(const uint32_t (&k)[KPT], uint32_t (&
 // XCDs, so workgroup g sits on XCD g % 8 as slot g / 8.  Round r gives XCD x the tiles
 // (8r + x) * (G/8) + slot: the workgroups of one XCD scatter ADJACENT tiles at the same time,
 // so each digit's writes from one XCD form one contiguous stream.
-template <int R, int BLOCK, int KPT, bool HAS_VALUES, int RANK>
+template <int R, int BLOCK, int KPT, int L, int RANK>
 __global__ __launch_bounds__(BLOCK) void k_scatter(
     const uint32_t* __restrict__ in_k, const uint32_t* __restrict__ in_v,
     uint32_t* __restrict__ out_k, uint32_t* __restrict__ out_v, uint32_t n, uint32_t shift,
     uint32_t mask, uint32_t ntiles, const uint32_t* __restrict__ counts,
     const uint32_t* __restrict__ totals, const uint32_t* gate, int pass) {
+    constexpr bool HAS_VALUES = L != LAYOUT_KEYS;
     constexpr int RADIX = 1 << R;
     constexpr int NW = BLOCK / 64;
     constexpr int TILE = BLOCK * KPT;
@@ -331,7 +346,7 @@ __global__ __launch_bounds__(BLOCK) void k_scatter(
     uint32_t v[HAS_VALUES ? KPT : 1];
     if (count) {
         const uint32_t tile0 = first * (uint32_t)TILE;
-        load_tile<KPT, HAS_VALUES>(in_k, in_v, tile0 + w * WAVE_KEYS, n,
+        load_tile<KPT, L>(in_k, in_v, tile0 + w * WAVE_KEYS, n,
                                    (uint64_t)tile0 + TILE <= n, k, v);
     }
     for (uint32_t t = 0; t < count; ++t) {
@@ -384,7 +399,7 @@ __global__ __launch_bounds__(BLOCK) void k_scatter(
         // under this tile's scatter.
         if (t + 1 < count) {
             const uint32_t nt0 = tile0 + G * TILE;
-            load_tile<KPT, HAS_VALUES>(in_k, in_v, nt0 + w * WAVE_KEYS, n,
+            load_tile<KPT, L>(in_k, in_v, nt0 + w * WAVE_KEYS, n,
                                        (uint64_t)nt0 + TILE <= n, k, v);
         }
         // Coalesced scatter: consecutive lanes write consecutive positions of a digit run.
@@ -414,8 +429,12 @@ __global__ __launch_bounds__(BLOCK) void k_scatter(
             }
 #else
             if (pos < n) {  // never false for a consistent histogram; keeps a bug from faulting
-                out_k[pos] = key;
-                if (HAS_VALUES) out_v[pos] = val;
+                if (L == LAYOUT_AOS) {
+                    reinterpret_cast<uint2*>(out_k)[pos] = make_uint2(key, val);
+                } else {
+                    out_k[pos] = key;
+                    if (HAS_VALUES) out_v[pos] = val;
+                }
             }
 #endif
         }
@@ -433,10 +452,11 @@ struct PassList {
 // n <= BLOCK*KPT: keys (+values) stay in registers between passes; every pass ranks, stages the
 // tile sorted by its digit in LDS, and reloads the registers from LDS.  One launch, one HBM read
 // and one HBM write for the whole sort.
-template <int BLOCK, int KPT, bool HAS_VALUES, int RANK>
+template <int BLOCK, int KPT, int L, int RANK>
 __global__ __launch_bounds__(BLOCK) void k_sort_small(uint32_t* __restrict__ keys,
                                                       uint32_t* __restrict__ values, uint32_t n,
                                                       PassList passes) {
+    constexpr bool HAS_VALUES = L != LAYOUT_KEYS;
     constexpr int R = 8, RADIX = 256;
     constexpr int NW = BLOCK / 64;
     constexpr int TILE = BLOCK * KPT;
@@ -449,7 +469,7 @@ __global__ __launch_bounds__(BLOCK) void k_sort_small(uint32_t* __restrict__ key
     const uint32_t wbase = w * WAVE_KEYS;
     uint32_t k[KPT];
     uint32_t v[HAS_VALUES ? KPT : 1];
-    load_tile<KPT, HAS_VALUES>(keys, values, wbase, n, false, k, v);
+    load_tile<KPT, L>(keys, values, wbase, n, false, k, v);
     uint32_t shift = 0;
     for (uint32_t p = 0; p < passes.count; ++p) {
         const uint32_t mask = (1u << passes.width[p]) - 1u;
@@ -499,22 +519,27 @@ __global__ __launch_bounds__(BLOCK) void k_sort_small(uint32_t* __restrict__ key
     for (int j = 0; j < KPT; ++j) {
         const uint32_t p2 = wbase + j * 64 + lane;
         if (p2 < n) {
-            keys[p2] = k[j];
-            if (HAS_VALUES) values[p2] = v[j];
+            if (L == LAYOUT_AOS) {
+                reinterpret_cast<uint2*>(keys)[p2] = make_uint2(k[j], v[j]);
+            } else {
+                keys[p2] = k[j];
+                if (HAS_VALUES) values[p2] = v[j];
+            }
         }
     }
 }
 
 // ---- order check -------------------------------------------------------------------------
-// inv[pass] |= 1 if any adjacent pair of keys[0..n) is out of order under `mask`.
+// inv[pass] |= 1 if any adjacent pair of keys[0..n) is out of order under `mask`.  Key i is
+// word i * kstride (2 for AOS records).
 __global__ __launch_bounds__(kBlock) void k_check(const uint32_t* __restrict__ keys, uint32_t n,
-                                                  uint32_t mask, uint32_t* inv, int pass,
-                                                  int gate_upto) {
+                                                  uint32_t kstride, uint32_t mask, uint32_t* inv,
+                                                  int pass, int gate_upto) {
     if (gate_upto >= 0 && gated_off(inv, gate_upto)) return;
     bool bad = false;
     const uint32_t stride = gridDim.x * kBlock;
     for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i + 1 < n; i += stride) {
-        const uint32_t a = keys[i] & mask, b = keys[i + 1] & mask;
+        const uint32_t a = keys[(size_t)i * kstride] & mask, b = keys[(size_t)(i + 1) * kstride] & mask;
         bad |= a > b;
     }
     if (__ballot(bad) != 0 && lane_id() == 0) atomicOr(inv + pass, 1u);
@@ -522,7 +547,7 @@ __global__ __launch_bounds__(kBlock) void k_check(const uint32_t* __restrict__ k
 
 // After an early exit at an odd pass the sorted data sits in the tmp buffers: copy it back so
 // the result is always in the caller's buffers (AbstractRadixSortKernel.ts:94-98).
-template <bool HAS_VALUES>
+template <int L>
 __global__ __launch_bounds__(kBlock) void k_finalize(const uint32_t* __restrict__ tk,
                                                      const uint32_t* __restrict__ tv,
                                                      uint32_t* __restrict__ uk,
@@ -534,8 +559,12 @@ __global__ __launch_bounds__(kBlock) void k_finalize(const uint32_t* __restrict_
     if (first < 0 || (first & 1) == 0) return;
     const uint32_t stride = gridDim.x * kBlock;
     for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
-        uk[i] = tk[i];
-        if (HAS_VALUES) uv[i] = tv[i];
+        if (L == LAYOUT_AOS) {
+            reinterpret_cast<uint2*>(uk)[i] = reinterpret_cast<const uint2*>(tk)[i];
+        } else {
+            uk[i] = tk[i];
+            if (L == LAYOUT_SOA) uv[i] = tv[i];
+        }
     }
 }
 

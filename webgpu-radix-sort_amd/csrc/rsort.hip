@@ -124,6 +124,7 @@ struct rs_plan {
     uint32_t bit_count = 32;
     uint32_t radix_bits = 8;
     bool has_values = false, check_order = false, local_shuffle = false;
+    int layout = rs::LAYOUT_KEYS;          // rs::Layout of the caller's data
     int rank_mode = rs::RANK_LDS_ATOMIC;   // RSORT_RANK=ballot selects the ballot-match ranking
     uint32_t passes = 0;
     uint32_t widths[16] = {};
@@ -153,50 +154,62 @@ bool use_small_tiles(uint64_t n) {
 }
 
 template <int R, int TILE>
-void launch_histogram(const uint32_t* in, uint32_t n, uint32_t shift, uint32_t mask,
+void launch_histogram(int L, const uint32_t* in, uint32_t n, uint32_t shift, uint32_t mask,
                       uint32_t ntiles, uint32_t* counts, const uint32_t* gate, int pass,
                       hipStream_t s) {
     const uint32_t grid = std::min<uint32_t>((ntiles + rs::kWaves - 1) / rs::kWaves, kHistGrid);
-    hipLaunchKernelGGL((rs::k_histogram<R, TILE, RS_HIST_U>), dim3(grid), dim3(rs::kBlock), 0, s,
-                       in, n, shift, mask, ntiles, counts, gate, pass);
+    if (L == rs::LAYOUT_AOS)
+        hipLaunchKernelGGL((rs::k_histogram<R, TILE, RS_HIST_U, 2>), dim3(grid), dim3(rs::kBlock), 0, s,
+                           in, n, shift, mask, ntiles, counts, gate, pass);
+    else
+        hipLaunchKernelGGL((rs::k_histogram<R, TILE, RS_HIST_U, 1>), dim3(grid), dim3(rs::kBlock), 0, s,
+                           in, n, shift, mask, ntiles, counts, gate, pass);
 }
 
-template <int R, int BLOCK, int KPT, bool V, int RANK>
+template <int R, int BLOCK, int KPT, int L, int RANK>
 void launch_scatter_t(const uint32_t* ik, const uint32_t* iv, uint32_t* ok, uint32_t* ov,
                       uint32_t n, uint32_t shift, uint32_t mask, uint32_t ntiles, uint32_t grid,
                       const uint32_t* counts, const uint32_t* totals, const uint32_t* gate,
                       int pass, hipStream_t s) {
-    hipLaunchKernelGGL((rs::k_scatter<R, BLOCK, KPT, V, RANK>), dim3(grid), dim3(BLOCK), 0, s,
+    hipLaunchKernelGGL((rs::k_scatter<R, BLOCK, KPT, L, RANK>), dim3(grid), dim3(BLOCK), 0, s,
                        ik, iv, ok, ov, n, shift, mask, ntiles, counts, totals, gate, pass);
 }
 
+template <int R, int BLOCK, int KPT, int L>
+void launch_scatter_l(int rank_mode, const uint32_t* ik, const uint32_t* iv, uint32_t* ok,
+                      uint32_t* ov, uint32_t n, uint32_t shift, uint32_t mask, uint32_t ntiles,
+                      uint32_t grid, const uint32_t* counts, const uint32_t* totals,
+                      const uint32_t* gate, int pass, hipStream_t s) {
+    if (rank_mode == rs::RANK_BALLOT)
+        launch_scatter_t<R, BLOCK, KPT, L, rs::RANK_BALLOT>(ik, iv, ok, ov, n, shift, mask, ntiles, grid, counts, totals, gate, pass, s);
+    else
+        launch_scatter_t<R, BLOCK, KPT, L, rs::RANK_LDS_ATOMIC>(ik, iv, ok, ov, n, shift, mask, ntiles, grid, counts, totals, gate, pass, s);
+}
+
 template <int R, int BLOCK, int KPT>
-void launch_scatter(bool V, int rank_mode, const uint32_t* ik, const uint32_t* iv, uint32_t* ok,
+void launch_scatter(int L, int rank_mode, const uint32_t* ik, const uint32_t* iv, uint32_t* ok,
                     uint32_t* ov, uint32_t n, uint32_t shift, uint32_t mask, uint32_t ntiles,
                     uint32_t grid, const uint32_t* counts, const uint32_t* totals,
                     const uint32_t* gate, int pass, hipStream_t s) {
-    constexpr int A = rs::RANK_LDS_ATOMIC, B = rs::RANK_BALLOT;
-    if (V && rank_mode == B)
-        launch_scatter_t<R, BLOCK, KPT, true, B>(ik, iv, ok, ov, n, shift, mask, ntiles, grid, counts, totals, gate, pass, s);
-    else if (V)
-        launch_scatter_t<R, BLOCK, KPT, true, A>(ik, iv, ok, ov, n, shift, mask, ntiles, grid, counts, totals, gate, pass, s);
-    else if (rank_mode == B)
-        launch_scatter_t<R, BLOCK, KPT, false, B>(ik, iv, ok, ov, n, shift, mask, ntiles, grid, counts, totals, gate, pass, s);
+    if (L == rs::LAYOUT_AOS)
+        launch_scatter_l<R, BLOCK, KPT, rs::LAYOUT_AOS>(rank_mode, ik, iv, ok, ov, n, shift, mask, ntiles, grid, counts, totals, gate, pass, s);
+    else if (L == rs::LAYOUT_SOA)
+        launch_scatter_l<R, BLOCK, KPT, rs::LAYOUT_SOA>(rank_mode, ik, iv, ok, ov, n, shift, mask, ntiles, grid, counts, totals, gate, pass, s);
     else
-        launch_scatter_t<R, BLOCK, KPT, false, A>(ik, iv, ok, ov, n, shift, mask, ntiles, grid, counts, totals, gate, pass, s);
+        launch_scatter_l<R, BLOCK, KPT, rs::LAYOUT_KEYS>(rank_mode, ik, iv, ok, ov, n, shift, mask, ntiles, grid, counts, totals, gate, pass, s);
 }
 
 // One stable digit pass in -> out (histogram, scan, scatter) with tile configuration C.
 template <int R, int BLOCK, int KPT>
 rs_status run_pass_cfg(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint32_t* ok,
-                       uint32_t* ov, uint32_t n, uint32_t shift, uint32_t w, bool values,
+                       uint32_t* ov, uint32_t n, uint32_t shift, uint32_t w, int L,
                        const uint32_t* gate, int pass, uint32_t max_grid, hipStream_t s) {
     constexpr int TILE = BLOCK * KPT;
     const uint32_t mask = (1u << w) - 1u;
     const uint32_t ntiles = (uint32_t)(((uint64_t)n + TILE - 1) / TILE);
     const uint32_t grid = std::min<uint32_t>(ntiles, max_grid);
     p->timer.run(RS_KERNEL_HISTOGRAM, s, [&] {
-        launch_histogram<R, TILE>(ik, n, shift, mask, ntiles, p->counts, gate, pass, s);
+        launch_histogram<R, TILE>(L, ik, n, shift, mask, ntiles, p->counts, gate, pass, s);
     });
     HIP_TRY(hipGetLastError());
     p->timer.run(RS_KERNEL_SCAN, s, [&] {
@@ -207,7 +220,7 @@ rs_status run_pass_cfg(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint3
     // The scatter always stages the tile through LDS (the local shuffle,
     // RadixSortLocalShuffle.ts:94-116): it is what makes the writes coalesced.
     p->timer.run(RS_KERNEL_SCATTER, s, [&] {
-        launch_scatter<R, BLOCK, KPT>(values, p->rank_mode, ik, iv, ok, ov, n, shift, mask, ntiles,
+        launch_scatter<R, BLOCK, KPT>(L, p->rank_mode, ik, iv, ok, ov, n, shift, mask, ntiles,
                                       grid, p->counts, p->totals, gate, pass, s);
     });
     HIP_TRY(hipGetLastError());
@@ -215,17 +228,17 @@ rs_status run_pass_cfg(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint3
 }
 
 rs_status run_pass(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint32_t* ok,
-                   uint32_t* ov, uint32_t n, uint32_t shift, uint32_t w, bool values,
+                   uint32_t* ov, uint32_t n, uint32_t shift, uint32_t w, int L,
                    const uint32_t* gate, int pass, hipStream_t s) {
     const uint32_t R = pick_R(w);
     if (use_small_tiles(n)) {
-        if (R == 2) return run_pass_cfg<2, kSmall.block, kSmall.kpt>(p, ik, iv, ok, ov, n, shift, w, values, gate, pass, kSmall.max_grid, s);
-        if (R == 4) return run_pass_cfg<4, kSmall.block, kSmall.kpt>(p, ik, iv, ok, ov, n, shift, w, values, gate, pass, kSmall.max_grid, s);
-        return run_pass_cfg<8, kSmall.block, kSmall.kpt>(p, ik, iv, ok, ov, n, shift, w, values, gate, pass, kSmall.max_grid, s);
+        if (R == 2) return run_pass_cfg<2, kSmall.block, kSmall.kpt>(p, ik, iv, ok, ov, n, shift, w, L, gate, pass, kSmall.max_grid, s);
+        if (R == 4) return run_pass_cfg<4, kSmall.block, kSmall.kpt>(p, ik, iv, ok, ov, n, shift, w, L, gate, pass, kSmall.max_grid, s);
+        return run_pass_cfg<8, kSmall.block, kSmall.kpt>(p, ik, iv, ok, ov, n, shift, w, L, gate, pass, kSmall.max_grid, s);
     }
-    if (R == 2) return run_pass_cfg<2, kLarge.block, kLarge.kpt>(p, ik, iv, ok, ov, n, shift, w, values, gate, pass, kLarge.max_grid, s);
-    if (R == 4) return run_pass_cfg<4, kLarge.block, kLarge.kpt>(p, ik, iv, ok, ov, n, shift, w, values, gate, pass, kLarge.max_grid, s);
-    return run_pass_cfg<8, kLarge.block, kLarge.kpt>(p, ik, iv, ok, ov, n, shift, w, values, gate, pass, kLarge.max_grid, s);
+    if (R == 2) return run_pass_cfg<2, kLarge.block, kLarge.kpt>(p, ik, iv, ok, ov, n, shift, w, L, gate, pass, kLarge.max_grid, s);
+    if (R == 4) return run_pass_cfg<4, kLarge.block, kLarge.kpt>(p, ik, iv, ok, ov, n, shift, w, L, gate, pass, kLarge.max_grid, s);
+    return run_pass_cfg<8, kLarge.block, kLarge.kpt>(p, ik, iv, ok, ov, n, shift, w, L, gate, pass, kLarge.max_grid, s);
 }
 
 // Whole sort of n <= kTinyMax in one workgroup (k_sort_small).
@@ -233,16 +246,20 @@ rs_status run_tiny(rs_plan* p, uint32_t* k, uint32_t* v, uint32_t n, hipStream_t
     rs::PassList pl{};
     pl.count = p->passes;
     for (uint32_t i = 0; i < p->passes; ++i) pl.width[i] = p->widths[i];
-    constexpr int A = rs::RANK_LDS_ATOMIC, B = rs::RANK_BALLOT;
+    const bool ballot = p->rank_mode == rs::RANK_BALLOT;
     p->timer.run(RS_KERNEL_SCATTER, s, [&] {
-        if (v && p->rank_mode == B)
-            hipLaunchKernelGGL((rs::k_sort_small<1024, 16, true, B>), dim3(1), dim3(1024), 0, s, k, v, n, pl);
-        else if (v)
-            hipLaunchKernelGGL((rs::k_sort_small<1024, 16, true, A>), dim3(1), dim3(1024), 0, s, k, v, n, pl);
-        else if (p->rank_mode == B)
-            hipLaunchKernelGGL((rs::k_sort_small<1024, 16, false, B>), dim3(1), dim3(1024), 0, s, k, v, n, pl);
-        else
-            hipLaunchKernelGGL((rs::k_sort_small<1024, 16, false, A>), dim3(1), dim3(1024), 0, s, k, v, n, pl);
+        auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(1), dim3(1024), 0, s, k, v, n, pl); };
+        constexpr int A = rs::RANK_LDS_ATOMIC, B = rs::RANK_BALLOT;
+        switch (p->layout) {
+            case rs::LAYOUT_AOS:
+                ballot ? go(rs::k_sort_small<1024, 16, rs::LAYOUT_AOS, B>) : go(rs::k_sort_small<1024, 16, rs::LAYOUT_AOS, A>);
+                break;
+            case rs::LAYOUT_SOA:
+                ballot ? go(rs::k_sort_small<1024, 16, rs::LAYOUT_SOA, B>) : go(rs::k_sort_small<1024, 16, rs::LAYOUT_SOA, A>);
+                break;
+            default:
+                ballot ? go(rs::k_sort_small<1024, 16, rs::LAYOUT_KEYS, B>) : go(rs::k_sort_small<1024, 16, rs::LAYOUT_KEYS, A>);
+        }
     });
     HIP_TRY(hipGetLastError());
     return RS_OK;
@@ -291,14 +308,16 @@ RS_EXPORT rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out) {
     uint32_t rb = d.radix_bits ? d.radix_bits : 8;
     if (rb != 2 && rb != 4 && rb != 8)
         return fail(RS_ERR_INVALID_ARG, "radix_bits must be 0, 2, 4 or 8 (got %u)", d.radix_bits);
-    if (d.flags & ~(uint32_t)0xF) return fail(RS_ERR_INVALID_ARG, "unknown flag bits 0x%x", d.flags);
+    if (d.flags & ~(uint32_t)0x1F) return fail(RS_ERR_INVALID_ARG, "unknown flag bits 0x%x", d.flags);
 
     rs_plan* p = new (std::nothrow) rs_plan();
     if (!p) return fail(RS_ERR_OUT_OF_MEMORY, "host allocation failed");
     p->desc = d;
     p->bit_count = d.bit_count;
     p->radix_bits = rb;
-    p->has_values = d.flags & RS_FLAG_HAS_VALUES;
+    p->has_values = d.flags & (RS_FLAG_HAS_VALUES | RS_FLAG_INTERLEAVED);
+    p->layout = (d.flags & RS_FLAG_INTERLEAVED) ? rs::LAYOUT_AOS
+              : (p->has_values ? rs::LAYOUT_SOA : rs::LAYOUT_KEYS);
     p->check_order = d.flags & RS_FLAG_CHECK_ORDER;
     p->local_shuffle = d.flags & RS_FLAG_LOCAL_SHUFFLE;
     if (const char* rk = getenv("RSORT_RANK"))
@@ -319,8 +338,9 @@ RS_EXPORT rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out) {
         return hipMalloc((void**)ptr, bytes);
     };
     hipError_t e;
-    if ((e = alloc(&p->tmp_k, 4 * d.count)) != hipSuccess ||
-        (p->has_values && (e = alloc(&p->tmp_v, 4 * d.count)) != hipSuccess) ||
+    if ((p->layout != rs::LAYOUT_AOS && (e = alloc(&p->tmp_k, 4 * d.count)) != hipSuccess) ||
+        (p->layout == rs::LAYOUT_AOS && (e = alloc(&p->tmp_k, 8 * d.count)) != hipSuccess) ||
+        (p->layout == rs::LAYOUT_SOA && (e = alloc(&p->tmp_v, 4 * d.count)) != hipSuccess) ||
         (e = alloc(&p->counts, 4ull * 256 * std::max<uint64_t>(1, (d.count + kSmall.tile - 1) / kSmall.tile))) != hipSuccess ||
         (e = alloc(&p->totals, 4ull * 256)) != hipSuccess ||
         (e = alloc(&p->flags, 4ull * 16)) != hipSuccess)
@@ -350,16 +370,20 @@ RS_EXPORT rs_status rs_plan_sort_n(rs_plan* p, void* keys, void* values, uint64_
                     (unsigned long long)n, (unsigned long long)p->capacity);
     if (n <= 1) return RS_OK;
     if (!keys) return fail(RS_ERR_INVALID_ARG, "rs_plan_sort: keys is null");
-    if (p->has_values && !values)
+    const int L = p->layout;
+    if (L == rs::LAYOUT_SOA && !values)
         return fail(RS_ERR_INVALID_ARG, "rs_plan_sort: plan has values but values is null");
+    if (L == rs::LAYOUT_AOS && values)
+        return fail(RS_ERR_INVALID_ARG, "rs_plan_sort: interleaved plan takes (key, value) records in keys; values must be null");
     if (((uintptr_t)keys & 3) || (values && ((uintptr_t)values & 3)))
         return fail(RS_ERR_INVALID_ARG, "keys/values must be 4-byte aligned (README.md limitations)");
+    if (L == rs::LAYOUT_AOS && ((uintptr_t)keys & 7))
+        return fail(RS_ERR_INVALID_ARG, "interleaved records must be 8-byte aligned");
     DeviceGuard guard(p->desc.device);
     hipStream_t s = (hipStream_t)stream;
-    const bool V = p->has_values;
     const uint32_t n32 = (uint32_t)n;
     uint32_t* uk = (uint32_t*)keys;
-    uint32_t* uv = V ? (uint32_t*)values : nullptr;
+    uint32_t* uv = L == rs::LAYOUT_SOA ? (uint32_t*)values : nullptr;
     if (n <= kTinyMax) return run_tiny(p, uk, uv, n32, s);   // one launch; check_order moot
     const uint32_t* gate = p->check_order ? p->flags : nullptr;
     if (p->check_order) HIP_TRY(hipMemsetAsync(p->flags, 0, 16 * 4, s));
@@ -377,22 +401,23 @@ RS_EXPORT rs_status rs_plan_sort_n(rs_plan* p, void* keys, void* values, uint64_
             const uint32_t grid = (uint32_t)std::min<uint64_t>(kCheckGrid, (n + rs::kBlock - 1) / rs::kBlock);
             p->timer.run(RS_KERNEL_CHECK, s, [&] {
                 hipLaunchKernelGGL(rs::k_check, dim3(grid), dim3(rs::kBlock), 0, s, ik, n32,
-                                   fmask, p->flags, (int)i, (int)i - 1);
+                                   L == rs::LAYOUT_AOS ? 2u : 1u, fmask, p->flags, (int)i, (int)i - 1);
             });
             HIP_TRY(hipGetLastError());
         }
-        rs_status st = run_pass(p, ik, iv, ok, ov, n32, shift, p->widths[i], V, gate, (int)i, s);
+        rs_status st = run_pass(p, ik, iv, ok, ov, n32, shift, p->widths[i], L, gate, (int)i, s);
         if (st != RS_OK) return st;
         shift += p->widths[i];
     }
     if (p->check_order) {
         const uint32_t grid = (uint32_t)std::min<uint64_t>(kCheckGrid, (n + rs::kBlock - 1) / rs::kBlock);
-        if (V)
-            hipLaunchKernelGGL(rs::k_finalize<true>, dim3(grid), dim3(rs::kBlock), 0, s, p->tmp_k,
-                               p->tmp_v, uk, uv, n32, p->flags, (int)p->passes);
-        else
-            hipLaunchKernelGGL(rs::k_finalize<false>, dim3(grid), dim3(rs::kBlock), 0, s, p->tmp_k,
-                               p->tmp_v, uk, uv, n32, p->flags, (int)p->passes);
+        auto fin = [&](auto kern) {
+            hipLaunchKernelGGL(kern, dim3(grid), dim3(rs::kBlock), 0, s, p->tmp_k, p->tmp_v, uk, uv,
+                               n32, p->flags, (int)p->passes);
+        };
+        if (L == rs::LAYOUT_AOS) fin(rs::k_finalize<rs::LAYOUT_AOS>);
+        else if (L == rs::LAYOUT_SOA) fin(rs::k_finalize<rs::LAYOUT_SOA>);
+        else fin(rs::k_finalize<rs::LAYOUT_KEYS>);
         HIP_TRY(hipGetLastError());
     }
     return RS_OK;
@@ -412,7 +437,8 @@ RS_EXPORT rs_status rs_plan_partition(rs_plan* p, const void* in_keys, const voi
                     (unsigned long long)n, (unsigned long long)p->capacity);
     if (bits == 0 || bits > 8 || shift + bits > 32)
         return fail(RS_ERR_INVALID_ARG, "partition digit must satisfy 1 <= bits <= 8, shift+bits <= 32");
-    const bool V = p->has_values && in_values && out_values;
+    const int L = p->layout == rs::LAYOUT_AOS ? (int)rs::LAYOUT_AOS
+                : (p->has_values && in_values && out_values ? (int)rs::LAYOUT_SOA : (int)rs::LAYOUT_KEYS);
     if (n && (!in_keys || !out_keys)) return fail(RS_ERR_INVALID_ARG, "rs_plan_partition: null keys");
     DeviceGuard guard(p->desc.device);
     hipStream_t s = (hipStream_t)stream;
@@ -422,7 +448,7 @@ RS_EXPORT rs_status rs_plan_partition(rs_plan* p, const void* in_keys, const voi
     }
     rs_status st = run_pass(p, (const uint32_t*)in_keys, (const uint32_t*)in_values,
                             (uint32_t*)out_keys, (uint32_t*)out_values, (uint32_t)n, shift, bits,
-                            V, nullptr, 0, s);
+                            L, nullptr, 0, s);
     if (st != RS_OK) return st;
     if (d_hist) HIP_TRY(hipMemcpyAsync(d_hist, p->totals, 4u << bits, hipMemcpyDeviceToDevice, s));
     return RS_OK;

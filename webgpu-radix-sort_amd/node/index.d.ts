@@ -22,11 +22,21 @@ export declare class DeviceBuffer {
   destroy(): void;
 }
 
+/** rg32uint (key, value) texture: texel (x, y) = record y * width + x, dense in device memory. */
+export declare class DeviceTexture extends DeviceBuffer {
+  readonly width: number;
+  readonly height: number;
+  readonly format: 'rg32uint' | 'r32uint';
+  readonly bytesPerTexel: number;
+}
+export interface Extent { width: number; height?: number; }
+
 export interface ComputePass { end(): void; }
 export interface CommandBuffer { readonly commands: ReadonlyArray<() => void>; }
 export declare class CommandEncoder {
   beginComputePass(descriptor?: unknown): ComputePass;
   copyBufferToBuffer(src: DeviceBuffer, srcOffset: number, dst: DeviceBuffer, dstOffset: number, size: number): void;
+  copyTextureToBuffer(src: { texture: DeviceTexture }, dst: { buffer: DeviceBuffer; offset?: number; bytesPerRow?: number }, extent: Extent): void;
   finish(): CommandBuffer;
 }
 
@@ -37,9 +47,11 @@ export declare class Device {
   readonly queue: {
     submit(commandBuffers: CommandBuffer[]): void;
     writeBuffer(buffer: DeviceBuffer, offset: number, data: ArrayBufferView | ArrayBuffer): void;
+    writeTexture(dest: { texture: DeviceTexture }, data: ArrayBufferView | ArrayBuffer, layout: { offset?: number; bytesPerRow?: number }, extent: Extent): void;
     onSubmittedWorkDone(): Promise<void>;
   };
   createBuffer(desc: { size: number; usage?: number; mappedAtCreation?: boolean; label?: string }): DeviceBuffer;
+  createTexture(desc: { size: Extent | [number, number?]; format?: 'rg32uint' | 'r32uint'; usage?: number; label?: string }): DeviceTexture;
   createCommandEncoder(): CommandEncoder;
   synchronize(): void;
   destroy(): void;
@@ -85,6 +97,28 @@ export declare class RadixSortKernel {
   destroy(): void;
 }
 export declare class RadixSortBufferKernel extends RadixSortKernel {}
+
+/** RadixSortTextureKernel.ts:15-35: sorts an rg32uint (key, value) texture in place by key. */
+export interface RadixSortTextureKernelOptions {
+  device?: Device;
+  data?: { texture: DeviceTexture };
+  texture?: DeviceTexture;
+  count?: number;
+  bitCount?: number; bit_count?: number;
+  workgroupSize?: WorkgroupSize; workgroup_size?: WorkgroupSize;
+  checkOrder?: boolean; check_order?: boolean;
+  avoidBankConflicts?: boolean; avoid_bank_conflicts?: boolean;
+  radixBits?: number;
+}
+export declare class RadixSortTextureKernel {
+  constructor(options: RadixSortTextureKernelOptions);
+  readonly textures: { read: DeviceTexture };
+  readonly hasValues: true;
+  readonly count: number;
+  readonly info: { passes: number; digitBits: number[]; tileKeys: number; gridBlocks: number; workspaceBytes: number };
+  dispatch(pass?: ComputePass): void;
+  destroy(): void;
+}
 
 export declare class PrefixSumKernel {
   constructor(options: { device?: Device; data: DeviceBuffer; count: number; workgroupSize?: WorkgroupSize; avoidBankConflicts?: boolean });

@@ -71,6 +71,25 @@ class DeviceBuffer {
   }
 }
 
+// A GPUTexture analogue for the rg32uint textures of RadixSortTextureKernel: texel (x, y) is the
+// 8-byte (key, value) record y * width + x, stored densely row-major in a device allocation
+// (RadixSortReorder.ts:42-63 addresses texels exactly this way).
+const TEXEL_BYTES = { rg32uint: 8, r32uint: 4 };
+
+class DeviceTexture extends DeviceBuffer {
+  constructor(device, { size, format = 'rg32uint', usage = 0, label = '' }) {
+    const width = Array.isArray(size) ? size[0] : size.width;
+    const height = Array.isArray(size) ? (size[1] || 1) : (size.height || 1);
+    const bpt = TEXEL_BYTES[format];
+    if (!bpt) throw new TypeError(`createTexture: unsupported format ${format}`);
+    super(device, { size: width * height * bpt, usage, label });
+    this.width = width;
+    this.height = height;
+    this.format = format;
+    this.bytesPerTexel = bpt;
+  }
+}
+
 class ComputePass {
   constructor(encoder) { this.encoder = encoder; }
   record(fn) { this.encoder.commands.push(fn); }
@@ -95,6 +114,18 @@ class CommandEncoder {
       }
     });
   }
+  // {texture}, {buffer, offset?, bytesPerRow?}, {width, height}: whole rows of a dense texture
+  copyTextureToBuffer(src, dst, extent) {
+    const tex = src.texture;
+    const w = extent.width === undefined ? extent[0] : extent.width;
+    const h = (extent.height === undefined ? extent[1] : extent.height) || 1;
+    const row = w * tex.bytesPerTexel;
+    const pitch = dst.bytesPerRow || row;
+    for (let y = 0; y < h; ++y) {
+      this.copyBufferToBuffer(tex, y * tex.width * tex.bytesPerTexel, dst.buffer,
+        (dst.offset || 0) + y * pitch, row);
+    }
+  }
   finish() { return { commands: this.commands.slice() }; }
 }
 
@@ -102,6 +133,21 @@ class Queue {
   constructor(device) { this.device = device; }
   submit(commandBuffers) {
     for (const cb of commandBuffers) for (const fn of cb.commands) fn();
+  }
+  // {texture}, data, {offset?, bytesPerRow?}, {width, height}
+  writeTexture(dest, data, layout, extent) {
+    const tex = dest.texture;
+    const bytes = ArrayBuffer.isView(data) ? new Uint8Array(data.buffer, data.byteOffset, data.byteLength)
+      : new Uint8Array(data);
+    const w = extent.width === undefined ? extent[0] : extent.width;
+    const h = (extent.height === undefined ? extent[1] : extent.height) || 1;
+    const row = w * tex.bytesPerTexel;
+    const pitch = (layout && layout.bytesPerRow) || row;
+    const off = (layout && layout.offset) || 0;
+    for (let y = 0; y < h; ++y) {
+      addon.h2d(tex.ptr + BigInt(y * tex.width * tex.bytesPerTexel),
+        bytes.subarray(off + y * pitch, off + y * pitch + row), this.device.stream);
+    }
   }
   writeBuffer(buffer, offset, data) {
     const bytes = ArrayBuffer.isView(data) ? new Uint8Array(data.buffer, data.byteOffset, data.byteLength)
@@ -127,6 +173,7 @@ class Device {
     });
   }
   createBuffer(desc) { return new DeviceBuffer(this, desc); }
+  createTexture(desc) { return new DeviceTexture(this, desc); }
   createCommandEncoder() { return new CommandEncoder(this); }
   synchronize() { addon.streamSynchronize(this.stream); }
   destroy() {}
@@ -233,6 +280,64 @@ class RadixSortKernel {
 
 class RadixSortBufferKernel extends RadixSortKernel {}
 
+class RadixSortTextureKernel {
+  /**
+   * {device, data: {texture}, count, bitCount, workgroupSize, checkOrder, avoidBankConflicts}
+   * (RadixSortTextureKernel.ts:15-35; README-style snake_case also accepted).  The texture is an
+   * rg32uint (key, value) texture from device.createTexture; it is sorted in place by key and
+   * always carries values (RadixSortTextureKernel.ts:27-29).
+   */
+  constructor(options) {
+    const opts = options || {};
+    const data = opts.data || {};
+    this.device = opts.device || null;
+    const texture = opts.texture !== undefined ? opts.texture : data.texture;
+    if (!(texture instanceof DeviceTexture) && !(texture && typeof texture.ptr === 'bigint')) {
+      throw new TypeError('texture is required');
+    }
+    if (texture.format !== undefined && texture.format !== 'rg32uint') {
+      throw new TypeError('texture format must be rg32uint');
+    }
+    this.count = opts.count !== undefined ? opts.count
+      : (texture.width !== undefined ? texture.width * texture.height : undefined);
+    if (!(this.count >= 0)) throw new TypeError('count is required');
+    if (texture.size !== undefined && texture.size < this.count * 8) {
+      throw new RangeError(`texture (${texture.size} bytes) smaller than count * 8`);
+    }
+    this.bitCount = pick(opts, ['bit_count', 'bitCount'], 32);
+    this.workgroupSize = pick(opts, ['workgroup_size', 'workgroupSize'], { x: 16, y: 16 });
+    this.checkOrder = !!pick(opts, ['check_order', 'checkOrder'], false);
+    this.avoidBankConflicts = !!pick(opts, ['avoid_bank_conflicts', 'avoidBankConflicts'], false);
+    this.radixBits = pick(opts, ['radix_bits', 'radixBits'], 0);
+    this.textures = { read: texture };
+    this._ptr = texture.ptr;
+    this._plan = addon.planCreate({
+      device: this.device ? this.device.ordinal : 0,
+      count: this.count,
+      bitCount: this.bitCount,
+      workgroupX: this.workgroupSize.x,
+      workgroupY: this.workgroupSize.y === undefined ? 1 : this.workgroupSize.y,
+      flags: addon.FLAG_INTERLEAVED | (this.checkOrder ? addon.FLAG_CHECK_ORDER : 0)
+        | (this.avoidBankConflicts ? addon.FLAG_AVOID_BANK_CONFLICTS : 0),
+      radixBits: this.radixBits,
+    });
+  }
+
+  get hasValues() { return true; }
+
+  get info() { return addon.planInfo(this._plan); }
+
+  dispatch(pass) {
+    const stream = this.device ? this.device.stream : null;
+    recordOrRun(pass, () => addon.planSort(this._plan, this._ptr, null, stream));
+  }
+
+  destroy() {
+    if (this._plan) addon.planDestroy(this._plan);
+    this._plan = null;
+  }
+}
+
 class PrefixSumKernel {
   /** {device, data, count, workgroupSize, avoidBankConflicts} (PrefixSumKernel.ts:24-43). */
   constructor(options) {
@@ -264,9 +369,11 @@ class PrefixSumKernel {
 module.exports = {
   RadixSortKernel,
   RadixSortBufferKernel,
+  RadixSortTextureKernel,
   PrefixSumKernel,
   Device,
   DeviceBuffer,
+  DeviceTexture,
   GPUBufferUsage,
   GPUMapMode,
   gpu,

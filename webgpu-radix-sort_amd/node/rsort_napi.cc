@@ -406,6 +406,7 @@ napi_value Init(napi_env env, napi_value exports) {
     napi_create_uint32(env, RS_FLAG_CHECK_ORDER, &v); napi_set_named_property(env, exports, "FLAG_CHECK_ORDER", v);
     napi_create_uint32(env, RS_FLAG_LOCAL_SHUFFLE, &v); napi_set_named_property(env, exports, "FLAG_LOCAL_SHUFFLE", v);
     napi_create_uint32(env, RS_FLAG_AVOID_BANK_CONFLICTS, &v); napi_set_named_property(env, exports, "FLAG_AVOID_BANK_CONFLICTS", v);
+    napi_create_uint32(env, RS_FLAG_INTERLEAVED, &v); napi_set_named_property(env, exports, "FLAG_INTERLEAVED", v);
     return exports;
 }
 

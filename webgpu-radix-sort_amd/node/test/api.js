@@ -5,11 +5,12 @@
 const assert = require('assert');
 const rs = require('..');
 
-for (const name of ['RadixSortKernel', 'RadixSortBufferKernel', 'PrefixSumKernel', 'gpu',
+for (const name of ['RadixSortKernel', 'RadixSortBufferKernel', 'RadixSortTextureKernel', 'PrefixSumKernel', 'gpu',
   'GPUBufferUsage', 'GPUMapMode']) {
   assert.ok(rs[name], `missing export ${name}`);
 }
 assert.strictEqual(typeof rs.addon.planCreate, 'function');
+assert.strictEqual(rs.addon.FLAG_INTERLEAVED, 0x10);
 assert.strictEqual(rs.addon.version(), 1);
 
 const fakeKeys = { ptr: 4096n };
@@ -25,4 +26,7 @@ assert.throws(() => new rs.RadixSortKernel({ keys: fakeKeys, count: 10, bit_coun
 assert.throws(() => new rs.RadixSortKernel({ data: { keys: fakeKeys }, count: 10, bitCount: 36 }), /bit_count/);
 assert.throws(() => new rs.RadixSortKernel({ count: 10 }), /keys buffer is required/);
 assert.throws(() => new rs.RadixSortKernel({ keys: fakeKeys }), /count is required/);
+assert.throws(() => new rs.RadixSortTextureKernel({ count: 10 }), /texture is required/);
+assert.throws(() => new rs.RadixSortTextureKernel({ data: { texture: { ptr: 4096n, format: 'r32uint' } }, count: 10 }),
+  /rg32uint/);
 console.log('node api checks ok');

@@ -5,7 +5,7 @@
 // additionally checks stability (values = iota stay increasing within equal keys) and the
 // prefix sum against prefixSumCpu (example/tests.ts:288-296).
 const assert = require('assert');
-const { gpu, RadixSortKernel, RadixSortBufferKernel, PrefixSumKernel, GPUBufferUsage, GPUMapMode } = require('..');
+const { gpu, RadixSortKernel, RadixSortBufferKernel, RadixSortTextureKernel, PrefixSumKernel, GPUBufferUsage, GPUMapMode } = require('..');
 
 function mulberry32(a) {
   return function next() {
@@ -93,6 +93,45 @@ async function testPrefixSum(device, rand) {
   }
 }
 
+// RadixSortTextureKernel (RadixSortTextureKernel.ts:15-35): an rg32uint (key, value) texture,
+// written with queue.writeTexture, sorted in place, read back with copyTextureToBuffer.
+async function testTextureSort(device, rand) {
+  let cases = 0;
+  for (const [w, h] of [[16, 4], [256, 40], [1000, 123], [2048, 512]]) {
+    const n = w * h;
+    const count = rand() > 0.5 ? n : Math.floor(n * rand()) + 1;
+    const texels = new Uint32Array(2 * n);
+    for (let i = 0; i < n; i += 1) {
+      texels[2 * i] = Math.floor(rand() * 2 ** 32) % (cases === 1 ? 61 : 2 ** 32);
+      texels[2 * i + 1] = i;
+    }
+    const texture = device.createTexture({ size: { width: w, height: h }, format: 'rg32uint' });
+    device.queue.writeTexture({ texture }, texels, { bytesPerRow: w * 8 }, { width: w, height: h });
+    const kernel = new RadixSortTextureKernel({ device, data: { texture }, count, bitCount: 32,
+      checkOrder: rand() > 0.5 });
+    const out = device.createBuffer({ size: n * 8, usage: GPUBufferUsage.MAP_READ | GPUBufferUsage.COPY_DST });
+    const encoder = device.createCommandEncoder();
+    const pass = encoder.beginComputePass();
+    kernel.dispatch(pass);
+    pass.end();
+    encoder.copyTextureToBuffer({ texture }, { buffer: out, bytesPerRow: w * 8 }, { width: w, height: h });
+    device.queue.submit([encoder.finish()]);
+    await out.mapAsync(GPUMapMode.READ);
+    const r = new Uint32Array(out.getMappedRange().slice());
+    const idx = Array.from({ length: count }, (_, i) => i)
+      .sort((a, b) => (texels[2 * a] - texels[2 * b]) || (a - b));   // stable by key
+    for (let i = 0; i < count; i += 1) {
+      assert.strictEqual(r[2 * i], texels[2 * idx[i]], `texture key ${w}x${h} @${i}`);
+      assert.strictEqual(r[2 * i + 1], idx[i], `texture value ${w}x${h} @${i}`);
+    }
+    for (let i = 2 * count; i < 2 * n; i += 1) assert.strictEqual(r[i], texels[i]);
+    kernel.destroy();
+    texture.destroy();
+    cases += 1;
+  }
+  return cases;
+}
+
 (async () => {
   const adapter = await gpu.requestAdapter();
   assert.ok(adapter, 'no HIP device');
@@ -100,6 +139,7 @@ async function testPrefixSum(device, rand) {
   const rand = mulberry32(20250404);
   const a = await testRadixSort(device, false, rand);
   const b = await testRadixSort(device, true, rand);
+  const c = await testTextureSort(device, rand);
   await testPrefixSum(device, rand);
-  console.log(`node sort checks ok (${a + b} sort cases, prefix sum)`);
+  console.log(`node sort checks ok (${a + b} sort cases, ${c} texture cases, prefix sum)`);
 })().catch((e) => { console.error(e); process.exit(1); });

@@ -8,8 +8,10 @@ All compute runs in librsort.so (hand-written gfx950 HIP kernels); this package 
 arguments across the C ABI (include/rsort.h).
 """
 from ._lib import RadixSortError, load as load_library  # noqa: F401
-from .kernel import DeviceBuffer, PrefixSumKernel, RadixSortBufferKernel, RadixSortKernel  # noqa: F401
+from .kernel import (DeviceBuffer, PrefixSumKernel, RadixSortBufferKernel,  # noqa: F401
+                     RadixSortKernel, RadixSortTextureKernel)
 from . import ops  # noqa: F401
 
-__all__ = ["RadixSortKernel", "RadixSortBufferKernel", "PrefixSumKernel", "DeviceBuffer",
+__all__ = ["RadixSortKernel", "RadixSortBufferKernel", "RadixSortTextureKernel", "PrefixSumKernel",
+           "DeviceBuffer",
            "RadixSortError", "load_library", "ops"]

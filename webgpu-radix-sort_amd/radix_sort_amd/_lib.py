@@ -26,6 +26,7 @@ RS_FLAG_HAS_VALUES = 0x1
 RS_FLAG_CHECK_ORDER = 0x2
 RS_FLAG_LOCAL_SHUFFLE = 0x4
 RS_FLAG_AVOID_BANK_CONFLICTS = 0x8
+RS_FLAG_INTERLEAVED = 0x10
 
 RS_KERNEL_HISTOGRAM, RS_KERNEL_SCAN, RS_KERNEL_SCATTER, RS_KERNEL_CHECK = range(4)
 RS_KERNEL_KINDS = 4

@@ -247,6 +247,63 @@ class RadixSortKernel:
 RadixSortBufferKernel = RadixSortKernel
 
 
+class RadixSortTextureKernel(RadixSortKernel):
+    """Drop-in for ``RadixSortTextureKernel`` (src/kernels/radix-sort/RadixSortTextureKernel.ts:
+    15-35): the data is ONE array of (key, value) u32 pairs - the rg32uint texels, texel i =
+    (x, y) with i = y * width + x (RadixSortReorder.ts:42-63) - sorted in place by key, values
+    always carried (``hasValues`` is true, :27-29).
+
+    ``data={"texture": t}`` (or ``texture=t``): a contiguous device tensor whose last dimension
+    is 2 (``[height, width, 2]`` or ``[n, 2]``, 4-byte elements), a :class:`DeviceBuffer`, or a
+    raw device pointer (then ``count`` is required).  ``count`` defaults to all texels.
+    """
+
+    def __init__(self, options: dict | None = None, **kw: Any):
+        opts = dict(options or {})
+        opts.update(kw)
+        data = opts.get("data") or {}
+        tex = _pick(opts, "texture") if "texture" in opts else data.get("texture")
+        if tex is None:
+            raise RadixSortError(_lib.RS_ERR_INVALID_ARG, "texture is required")
+        if _is_torch(tex) and (tex.dim() < 2 or tex.shape[-1] != 2):
+            raise RadixSortError(_lib.RS_ERR_INVALID_ARG,
+                                 "texture tensor must have a last dimension of 2 (rg32uint texels)")
+        tptr, tcap, tdev = _buffer_info(tex, "texture")
+        texels = None if tcap is None else tcap // 2
+        count = _pick(opts, "count")
+        if count is None:
+            if texels is None:
+                raise RadixSortError(_lib.RS_ERR_INVALID_ARG, "count is required with raw pointers")
+            count = texels
+        count = int(count)
+        if texels is not None and texels < count:
+            raise RadixSortError(_lib.RS_ERR_INVALID_ARG,
+                                 f"texture holds {texels} texels < count {count}")
+        self.device = _device_ordinal(opts.get("device", _SENTINEL), tdev)
+        self.count = count
+        self.bit_count = int(_pick(opts, "bit_count", "bitCount", default=32))
+        wx, wy = _workgroup(_pick(opts, "workgroup_size", "workgroupSize"))
+        self.workgroup_size = {"x": wx, "y": wy}
+        self.check_order = bool(_pick(opts, "check_order", "checkOrder", default=False))
+        self.local_shuffle = False
+        self.avoid_bank_conflicts = bool(_pick(opts, "avoid_bank_conflicts", "avoidBankConflicts",
+                                               default=False))
+        self.radix_bits = int(_pick(opts, "radix_bits", "radixBits", default=0))
+        self.has_values = True
+        self.textures = {"read": tex}
+        self.buffers = {}
+        self._uses_torch = _is_torch(tex)
+        self._ptrs = (tptr, None)
+        flags = (_lib.RS_FLAG_INTERLEAVED
+                 | (_lib.RS_FLAG_CHECK_ORDER if self.check_order else 0)
+                 | (_lib.RS_FLAG_AVOID_BANK_CONFLICTS if self.avoid_bank_conflicts else 0))
+        desc = _lib.PlanDesc(self.device, count, self.bit_count, wx, wy, flags, self.radix_bits, 0)
+        plan = ctypes.c_void_p()
+        check(_lib.load().rs_plan_create(ctypes.byref(desc), ctypes.byref(plan)),
+              "RadixSortTextureKernel")
+        self._plan = plan
+
+
 class PrefixSumKernel:
     """Drop-in for ``PrefixSumKernel``: in-place exclusive scan (mod 2^32) of data[:count]."""
 

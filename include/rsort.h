@@ -136,6 +136,14 @@ rs_status rs_stream_create(int32_t device, void** stream);
 rs_status rs_stream_destroy(void* stream);
 rs_status rs_stream_synchronize(void* stream);
 
+/* ---- timestamps (the reference's timestamp QuerySet, example/tests.ts:247-285; the demo
+ * times kernel.dispatch between beginningOfPass / endOfPass writes, example/index.ts:124-146) */
+rs_status rs_event_create(void** event);
+rs_status rs_event_destroy(void* event);
+rs_status rs_event_record(void* event, void* stream);
+/* Milliseconds between two recorded events; waits for `end` to complete. */
+rs_status rs_event_elapsed_ms(void* start, void* end, float* ms);
+
 /* ---- synthetic inputs (bench / tests) --------------------------------------------------- */
 /* dst[i] = low32(splitmix64_finaliser(seed * 0xD1B54A32D192ED03 + start + i)), i < n. */
 rs_status rs_fill_random_u32(void* dst, uint64_t n, uint64_t seed, uint64_t start, void* stream);

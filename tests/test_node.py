@@ -32,3 +32,38 @@ def test_node_api_and_validation():
 @pytest.mark.gpu
 def test_node_reference_flow_on_gpu():
     assert "node sort checks ok" in _run("sort.js", 300)
+
+
+def _demo(*args, timeout=300):
+    r = subprocess.run(["node", os.path.join(NODE_DIR, "demo.js"), *args], capture_output=True,
+                       text=True, timeout=timeout, cwd=NODE_DIR)
+    assert r.returncode == 0, r.stdout + r.stderr
+    return r.stdout
+
+
+def test_node_demo_rejects_unknown_setting():
+    r = subprocess.run(["node", os.path.join(NODE_DIR, "demo.js"), "--noSuchSetting=1"],
+                       capture_output=True, text=True, timeout=60, cwd=NODE_DIR)
+    assert r.returncode != 0 and "unknown setting" in r.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("args", [
+    (),                                                                  # the demo's defaults
+    ("--sortMode=Keys & Values", "--checkOrder", "--consecutiveSorts=3"),
+    ("--dataType=texture", "--elementCount=300000", "--bitCount=16", "--workgroupSize=8"),
+    ("--initialSort=Sorted", "--localShuffle", "--avoidBankConflicts"),
+])
+def test_node_demo_cli_report(args):
+    """example/index.ts's flow and report; --verify compares the GPU result with the CPU sort."""
+    out = _demo(*args, "--verify")
+    assert "> CPU Reference:" in out and "GPU Average" in out and "Speedup: x" in out, out
+    assert "GPU result matches CPU" in out, out
+
+
+@pytest.mark.gpu
+def test_node_demo_json_line():
+    import json
+    line = _demo("--elementCount=65536", "--json", "--verify").strip().splitlines()[-1]
+    rec = json.loads(line)
+    assert rec["verified"] is True and rec["gpu_avg_ms"] > 0 and rec["settings"]["elementCount"] == 65536

@@ -621,6 +621,32 @@ RS_EXPORT rs_status rs_stream_synchronize(void* stream) {
     return RS_OK;
 }
 
+RS_EXPORT rs_status rs_event_create(void** event) {
+    if (!event) return fail(RS_ERR_INVALID_ARG, "rs_event_create: null");
+    hipEvent_t e;
+    HIP_TRY(hipEventCreate(&e));
+    *event = (void*)e;
+    return RS_OK;
+}
+
+RS_EXPORT rs_status rs_event_destroy(void* event) {
+    if (event) HIP_TRY(hipEventDestroy((hipEvent_t)event));
+    return RS_OK;
+}
+
+RS_EXPORT rs_status rs_event_record(void* event, void* stream) {
+    if (!event) return fail(RS_ERR_INVALID_ARG, "rs_event_record: null event");
+    HIP_TRY(hipEventRecord((hipEvent_t)event, (hipStream_t)stream));
+    return RS_OK;
+}
+
+RS_EXPORT rs_status rs_event_elapsed_ms(void* start, void* end, float* ms) {
+    if (!start || !end || !ms) return fail(RS_ERR_INVALID_ARG, "rs_event_elapsed_ms: null");
+    HIP_TRY(hipEventSynchronize((hipEvent_t)end));
+    HIP_TRY(hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)end));
+    return RS_OK;
+}
+
 RS_EXPORT rs_status rs_fill_random_u32(void* dst, uint64_t n, uint64_t seed, uint64_t start,
                                        void* stream) {
     if (n == 0) return RS_OK;

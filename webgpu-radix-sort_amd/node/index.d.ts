@@ -31,10 +31,20 @@ export declare class DeviceTexture extends DeviceBuffer {
 }
 export interface Extent { width: number; height?: number; }
 
+export declare class QuerySet {
+  readonly type: 'timestamp';
+  readonly count: number;
+  destroy(): void;
+}
+export interface ComputePassDescriptor {
+  timestampWrites?: { querySet: QuerySet; beginningOfPassWriteIndex?: number; endOfPassWriteIndex?: number };
+}
+
 export interface ComputePass { end(): void; }
 export interface CommandBuffer { readonly commands: ReadonlyArray<() => void>; }
 export declare class CommandEncoder {
-  beginComputePass(descriptor?: unknown): ComputePass;
+  beginComputePass(descriptor?: ComputePassDescriptor): ComputePass;
+  resolveQuerySet(querySet: QuerySet, firstQuery: number, queryCount: number, destination: DeviceBuffer, destinationOffset?: number): void;
   copyBufferToBuffer(src: DeviceBuffer, srcOffset: number, dst: DeviceBuffer, dstOffset: number, size: number): void;
   copyTextureToBuffer(src: { texture: DeviceTexture }, dst: { buffer: DeviceBuffer; offset?: number; bytesPerRow?: number }, extent: Extent): void;
   finish(): CommandBuffer;
@@ -51,6 +61,7 @@ export declare class Device {
     onSubmittedWorkDone(): Promise<void>;
   };
   createBuffer(desc: { size: number; usage?: number; mappedAtCreation?: boolean; label?: string }): DeviceBuffer;
+  createQuerySet(desc: { type: 'timestamp'; count: number }): QuerySet;
   createTexture(desc: { size: Extent | [number, number?]; format?: 'rg32uint' | 'r32uint'; usage?: number; label?: string }): DeviceTexture;
   createCommandEncoder(): CommandEncoder;
   synchronize(): void;

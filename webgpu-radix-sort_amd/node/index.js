@@ -90,15 +90,64 @@ class DeviceTexture extends DeviceBuffer {
   }
 }
 
+// Timestamp QuerySet (createTimestampQuery, example/tests.ts:247-285): one HIP event per query;
+// resolveQuerySet writes nanoseconds relative to the first resolved query, so differences are
+// GPU time between the recorded points (timestamps[1] - timestamps[0] in example/index.ts:141).
+class QuerySet {
+  constructor(device, { type = 'timestamp', count }) {
+    if (type !== 'timestamp') throw new TypeError(`createQuerySet: unsupported type ${type}`);
+    this.device = device;
+    this.type = type;
+    this.count = count;
+    this.events = Array.from({ length: count }, () => addon.eventCreate());
+    this.written = new Array(count).fill(false);
+  }
+  write(index) {
+    addon.eventRecord(this.events[index], this.device.stream);
+    this.written[index] = true;
+  }
+  destroy() {
+    for (const e of this.events) if (e) addon.eventDestroy(e);
+    this.events = [];
+  }
+}
+
 class ComputePass {
-  constructor(encoder) { this.encoder = encoder; }
+  constructor(encoder, descriptor) {
+    this.encoder = encoder;
+    this.timestampWrites = descriptor && descriptor.timestampWrites;
+    const tw = this.timestampWrites;
+    if (tw && tw.beginningOfPassWriteIndex !== undefined) {
+      encoder.commands.push(() => tw.querySet.write(tw.beginningOfPassWriteIndex));
+    }
+  }
   record(fn) { this.encoder.commands.push(fn); }
-  end() {}
+  end() {
+    const tw = this.timestampWrites;
+    if (tw && tw.endOfPassWriteIndex !== undefined) {
+      this.encoder.commands.push(() => tw.querySet.write(tw.endOfPassWriteIndex));
+    }
+  }
 }
 
 class CommandEncoder {
   constructor(device) { this.device = device; this.commands = []; }
-  beginComputePass() { return new ComputePass(this); }
+  beginComputePass(descriptor) { return new ComputePass(this, descriptor); }
+  resolveQuerySet(querySet, first, count, dst, dstOffset = 0) {
+    const dev = this.device;
+    this.commands.push(() => {
+      const ts = new BigUint64Array(count);
+      const origin = querySet.events[first];
+      for (let i = 0; i < count; i += 1) {
+        const q = first + i;
+        if (!querySet.written[q] || !querySet.written[first]) continue;
+        ts[i] = BigInt(Math.round(addon.eventElapsed(origin, querySet.events[q]) * 1e6));
+      }
+      const bytes = new Uint8Array(ts.buffer);
+      if (dst.host) new Uint8Array(dst.hostData, dstOffset, bytes.length).set(bytes);
+      else addon.h2d(dst.ptr + BigInt(dstOffset), bytes, dev.stream);
+    });
+  }
   copyBufferToBuffer(src, srcOffset, dst, dstOffset, size) {
     const dev = this.device;
     this.commands.push(() => {
@@ -174,6 +223,7 @@ class Device {
   }
   createBuffer(desc) { return new DeviceBuffer(this, desc); }
   createTexture(desc) { return new DeviceTexture(this, desc); }
+  createQuerySet(desc) { return new QuerySet(this, desc); }
   createCommandEncoder() { return new CommandEncoder(this); }
   synchronize() { addon.streamSynchronize(this.stream); }
   destroy() {}
@@ -374,6 +424,7 @@ module.exports = {
   Device,
   DeviceBuffer,
   DeviceTexture,
+  QuerySet,
   GPUBufferUsage,
   GPUMapMode,
   gpu,

@@ -244,6 +244,47 @@ napi_value StreamSynchronize(napi_env env, napi_callback_info info) {
     return nullptr;
 }
 
+// Timestamp events: eventCreate() -> bigint, eventRecord(ev, stream), eventElapsed(a, b) -> ms,
+// eventDestroy(ev).  Back the WebGPU-shaped timestamp QuerySet of index.js.
+napi_value EventCreate(napi_env env, napi_callback_info info) {
+    (void)info;
+    void* e = nullptr;
+    RS_CALL(env, rs_event_create(&e), "eventCreate");
+    return bigint(env, (uint64_t)(uintptr_t)e);
+}
+
+napi_value EventRecord(napi_env env, napi_callback_info info) {
+    napi_value a[2];
+    if (!args(env, info, a)) return nullptr;
+    bool ok;
+    void* e = ptr_of(env, a[0], &ok);
+    void* s = ptr_of(env, a[1], &ok);
+    RS_CALL(env, rs_event_record(e, s), "eventRecord");
+    return nullptr;
+}
+
+napi_value EventElapsed(napi_env env, napi_callback_info info) {
+    napi_value a[2];
+    if (!args(env, info, a)) return nullptr;
+    bool ok;
+    void* e0 = ptr_of(env, a[0], &ok);
+    void* e1 = ptr_of(env, a[1], &ok);
+    float ms = 0.f;
+    RS_CALL(env, rs_event_elapsed_ms(e0, e1, &ms), "eventElapsed");
+    napi_value r;
+    napi_create_double(env, (double)ms, &r);
+    return r;
+}
+
+napi_value EventDestroy(napi_env env, napi_callback_info info) {
+    napi_value a[1];
+    if (!args(env, info, a)) return nullptr;
+    bool ok;
+    void* e = ptr_of(env, a[0], &ok);
+    RS_CALL(env, rs_event_destroy(e), "eventDestroy");
+    return nullptr;
+}
+
 // planCreate({device, count, bitCount, workgroupX, workgroupY, flags, radixBits}) -> external
 napi_value PlanCreate(napi_env env, napi_callback_info info) {
     napi_value a[1];
@@ -394,6 +435,10 @@ napi_value Init(napi_env env, napi_value exports) {
     Define(env, exports, "streamCreate", StreamCreate);
     Define(env, exports, "streamDestroy", StreamDestroy);
     Define(env, exports, "streamSynchronize", StreamSynchronize);
+    Define(env, exports, "eventCreate", EventCreate);
+    Define(env, exports, "eventRecord", EventRecord);
+    Define(env, exports, "eventElapsed", EventElapsed);
+    Define(env, exports, "eventDestroy", EventDestroy);
     Define(env, exports, "planCreate", PlanCreate);
     Define(env, exports, "planSort", PlanSort);
     Define(env, exports, "planDestroy", PlanDestroy);

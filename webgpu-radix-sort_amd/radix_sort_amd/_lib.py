@@ -86,6 +86,10 @@ _SIGS = {
     "rs_stream_create": (ctypes.c_int, [ctypes.c_int32, ctypes.POINTER(_VP)]),
     "rs_stream_destroy": (ctypes.c_int, [_VP]),
     "rs_stream_synchronize": (ctypes.c_int, [_VP]),
+    "rs_event_create": (ctypes.c_int, [ctypes.POINTER(_VP)]),
+    "rs_event_destroy": (ctypes.c_int, [_VP]),
+    "rs_event_record": (ctypes.c_int, [_VP, _VP]),
+    "rs_event_elapsed_ms": (ctypes.c_int, [_VP, _VP, ctypes.POINTER(ctypes.c_float)]),
     "rs_fill_random_u32": (ctypes.c_int, [_VP, ctypes.c_uint64, ctypes.c_uint64,
                                           ctypes.c_uint64, _VP]),
     "rs_fill_iota_u32": (ctypes.c_int, [_VP, ctypes.c_uint64, ctypes.c_uint32, _VP]),

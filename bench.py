@@ -42,6 +42,10 @@ WORKLOADS = {
     "config4": dict(n=1 << 28, values=True, local_shuffle=False, check_order=True,
                     kind="f32_nearly", seed=4,
                     desc="256M Float32 keys (nearly sorted) + Uint32 values, check_order=true"),
+    # config3's data as one rg32uint texture of (key, value) texels (RadixSortTextureKernel)
+    "config3_texture": dict(n=1 << 28, values=True, local_shuffle=False, check_order=False,
+                            kind="u32", seed=3, layout="aos",
+                            desc="256M (Uint32 key, Uint32 value) texels, RadixSortTextureKernel"),
 }
 
 
@@ -96,7 +100,19 @@ def make_input(torch, ops, wl, n, seed, start, dev):
     if wl["values"]:
         vals = torch.empty(n, dtype=torch.int32, device=dev)
         ops.fill_iota_u32(vals, start)
+    if wl.get("layout") == "aos":
+        rec = torch.stack([keys, vals], dim=1).contiguous()   # [n, 2] texels
+        return rec, None
     return keys, vals
+
+
+def make_kernel(RadixSortKernel, RadixSortTextureKernel, wl, local, k, v, n, radix_bits):
+    if wl.get("layout") == "aos":
+        return RadixSortTextureKernel(device=local, texture=k, count=n, bit_count=32,
+                                      check_order=wl["check_order"], radix_bits=radix_bits)
+    return RadixSortKernel(device=local, keys=k, values=v, count=n, bit_count=32,
+                           local_shuffle=wl["local_shuffle"], check_order=wl["check_order"],
+                           radix_bits=radix_bits)
 
 
 def main() -> None:
@@ -117,7 +133,7 @@ def main() -> None:
 
     import torch
     import torch.distributed as dist
-    from radix_sort_amd import RadixSortKernel, ops
+    from radix_sort_amd import RadixSortKernel, RadixSortTextureKernel, ops
     from radix_sort_amd.distributed import HipLocalOps, distributed_sort
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -128,9 +144,12 @@ def main() -> None:
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     use_dist = world > 1 or args.distributed
+    wl = dict(WORKLOADS[args.workload])
+    if use_dist and wl.get("layout") == "aos":
+        raise SystemExit("bench: the multi-GPU path sorts separate key/value arrays; "
+                         "use config3 for --gpus > 1")
     if use_dist:
         dist.init_process_group("nccl", device_id=dev)
-    wl = dict(WORKLOADS[args.workload])
     n = args.n or wl["n"]
     K, W = args.steps, args.warmup
 
@@ -150,13 +169,10 @@ def main() -> None:
             log(f"note: {K} steps but room for {nb} batches; later steps re-sort batches")
         batches = [make_input(torch, ops, wl, n, wl["seed"] + 7919 * i, 0, dev) for i in range(nb)]
         wk, wv = make_input(torch, ops, wl, n, wl["seed"] + 999331, 0, dev)
-        kern = RadixSortKernel(device=local, keys=wk, values=wv, count=n, bit_count=32,
-                               local_shuffle=wl["local_shuffle"], check_order=wl["check_order"],
-                               radix_bits=args.radix_bits)
-        kernels = [RadixSortKernel(device=local, keys=b[0], values=b[1], count=n, bit_count=32,
-                                   local_shuffle=wl["local_shuffle"],
-                                   check_order=wl["check_order"], radix_bits=args.radix_bits)
-                   for b in batches]
+        kern = make_kernel(RadixSortKernel, RadixSortTextureKernel, wl, local, wk, wv, n,
+                           args.radix_bits)
+        kernels = [make_kernel(RadixSortKernel, RadixSortTextureKernel, wl, local, b[0], b[1], n,
+                               args.radix_bits) for b in batches]
         for w in range(W):
             if w:
                 wk2, wv2 = make_input(torch, ops, wl, n, wl["seed"] + 999331 + w, 0, dev)
@@ -181,6 +197,8 @@ def main() -> None:
                 acc["launches"] += v["launches"]
         # sanity: the last sorted batch really is sorted (outside the timed region)
         lk = batches[(K - 1) % nb][0]
+        if wl.get("layout") == "aos":
+            lk = lk[:, 0].contiguous()
         if not ops.is_sorted(lk):
             raise SystemExit("bench: output not sorted")
         info = kernels[0].info
@@ -243,7 +261,14 @@ def main() -> None:
                 "avg_launch_ms": round(avg_ms, 4),
                 "algorithmic_bytes_per_launch": scatter_keys * bytes_per_key}
     passes = info["passes"]
-    sort_bytes = keys_per_step / max(world, 1) * passes * (12 + 8 * (1 if wl["values"] else 0))
+    # algorithmic HBM bytes of one sort per GPU: every pass reads and writes keys (+values);
+    # the digit counts cost one key read per pass (histogram path) or one per sort (one-sweep
+    # path: k_pass_totals reads the keys once, later totals come from the scatter itself)
+    hist = kernel_ms.get("histogram", {"launches": 0})["launches"]
+    hist_reads = max(1, round(hist / max(K, 1))) if hist else passes
+    sort_bytes = keys_per_step / max(world, 1) * (passes * (8 + 8 * (1 if wl["values"] else 0))
+                                                  + 4 * hist_reads)
+    extra["digit_count_reads_per_sort"] = hist_reads
     extra["whole_sort_hbm_GBs_per_gpu"] = round(sort_bytes / (elapsed / K) / 1e9, 1)
     extra["kernel_ms_per_step"] = {k: round(v["ms"] / max(K, 1), 4) for k, v in kernel_ms.items()}
     extra["passes"] = passes

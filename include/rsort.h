@@ -114,6 +114,9 @@ rs_status rs_plan_set_profiling(rs_plan* plan, int enable);
 rs_status rs_plan_kernel_times(rs_plan* plan, double ms[RS_KERNEL_KINDS],
                                uint64_t launches[RS_KERNEL_KINDS]);
 rs_status rs_plan_reset_kernel_times(rs_plan* plan);
+/* Device-side error word of the plan (synchronises the device): 0 = ok; bit 0 = a bounded
+ * inter-workgroup wait of the one-sweep scatter timed out (that sort's result is invalid). */
+rs_status rs_plan_device_errors(rs_plan* plan, uint32_t* errors);
 void      rs_plan_destroy(rs_plan* plan);     /* frees the workspace (reference quirk Q9) */
 
 /* ---- prefix sum (PrefixSumKernel) ------------------------------------------------------- */

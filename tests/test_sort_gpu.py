@@ -282,3 +282,41 @@ def test_rank_modes_and_tile_configs(monkeypatch, golden, rank, tile):
         if vals is not None:
             assert (v == exp_v).all(), case
 
+
+
+@pytest.mark.parametrize("onesweep", ["1", "0"])
+@pytest.mark.parametrize("tile", ["small", "large"])
+def test_onesweep_and_three_kernel_paths(monkeypatch, onesweep, tile):
+    """The one-sweep pass (whole-array totals + decoupled look-back) and the histogram / scan /
+    scatter pass give the oracle's result for every layout; no bounded wait times out."""
+    from radix_sort_amd import RadixSortKernel, RadixSortTextureKernel
+    monkeypatch.setenv("RSORT_ONESWEEP", onesweep)
+    monkeypatch.setenv("RSORT_TILE", tile)
+    for n, bits, kind in ((16_385, 32, "u32"), (100_003, 32, "few"), (2_500_000, 32, "u32"),
+                          (5_000_001, 20, "u32"), (40_000, 8, "sorted"), (300_000, 12, "u32")):
+        keys = O.gen_u32(n * 3 + bits, n)
+        if kind == "few":
+            keys = keys % np.uint32(5)
+        elif kind == "sorted":
+            keys = np.sort(keys)
+        vals = O.gen_u32(n * 5 + bits, n)
+        ek, ev = O.stable_sort_masked(keys, vals, bits)
+        kt, vt = _t(keys), _t(vals)
+        k = RadixSortKernel(keys=kt, values=vt, count=n, bit_count=bits, check_order=(n % 2 == 1))
+        k.dispatch()
+        assert k.device_errors() == 0
+        assert (_np(kt) == ek).all() and (_np(vt) == ev).all(), (n, bits, kind)
+        k.destroy()
+        kt = _t(keys)
+        k = RadixSortKernel(keys=kt, count=n, bit_count=bits)
+        k.dispatch()
+        assert k.device_errors() == 0
+        assert (_np(kt) == ek).all(), (n, bits, kind, "keys only")
+        k.destroy()
+        rt = _t(np.stack([keys, vals], axis=-1).reshape(-1)).view(-1, 2)
+        k = RadixSortTextureKernel(texture=rt, count=n, bit_count=bits)
+        k.dispatch()
+        assert k.device_errors() == 0
+        out = _np(rt).reshape(-1, 2)
+        assert (out[:, 0] == ek).all() and (out[:, 1] == ev).all(), (n, bits, kind, "aos")
+        k.destroy()

@@ -448,6 +448,248 @@ struct PassList {
     uint32_t width[16];
 };
 
+// ---- whole-array digit totals of every pass, from one read of the keys --------------------
+// The digit histogram of pass p over the whole array does not depend on the order earlier
+// passes left the keys in, so the unsorted input gives every pass's totals at once.
+// out[off(p) + d], off(p) = sum of 2^width[<p] (<= kTotalsMax entries), zeroed by the caller.
+// Wave-private LDS counters; one global atomic per non-zero counter per workgroup.  KS = words
+// per key (2 for AOS records).
+constexpr int kTotalsMax = 1024;
+template <int KS>
+__global__ __launch_bounds__(kBlock) void k_pass_totals(const uint32_t* __restrict__ keys,
+                                                        uint32_t n, PassList pl,
+                                                        uint32_t* __restrict__ out) {
+    __shared__ uint32_t hist[kWaves][kTotalsMax];
+    const uint32_t tid = threadIdx.x, w = tid >> 6;
+    uint32_t total = 0;
+    for (uint32_t p = 0; p < pl.count; ++p) total += 1u << pl.width[p];
+    for (uint32_t i = tid; i < (uint32_t)(kWaves * kTotalsMax); i += kBlock) (&hist[0][0])[i] = 0u;
+    __syncthreads();
+    uint32_t* h = hist[w];
+    auto count_key = [&](uint32_t key) {
+        uint32_t off = 0, shift = 0;
+        for (uint32_t p = 0; p < pl.count; ++p) {
+            const uint32_t wd = pl.width[p];
+            atomicAdd(&h[off + ((key >> shift) & ((1u << wd) - 1u))], 1u);
+            off += 1u << wd;
+            shift += wd;
+        }
+    };
+    constexpr uint32_t KPV = 4 / KS;               // keys per 16-byte load
+    const uint32_t nv = n / KPV;
+    const uint4* k4 = reinterpret_cast<const uint4*>(keys);
+    const bool vec = (((uintptr_t)keys) & 15u) == 0;
+    const uint32_t stride = gridDim.x * kBlock;
+    uint32_t i0 = 0;
+    if (vec) {
+        for (uint32_t i = blockIdx.x * kBlock + tid; i < nv; i += stride) {
+            const uint4 q = k4[i];
+            count_key(q.x);
+            if (KS == 1) count_key(q.y);
+            count_key(q.z);
+            if (KS == 1) count_key(q.w);
+        }
+        i0 = KPV * nv;
+    }
+    for (uint32_t i = i0 + blockIdx.x * kBlock + tid; i < n; i += stride)
+        count_key(keys[(size_t)i * KS]);
+    __syncthreads();
+    for (uint32_t i = tid; i < total; i += kBlock) {
+        uint32_t c = 0;
+#pragma unroll
+        for (int q = 0; q < kWaves; ++q) c += hist[q][i];
+        if (c) atomicAdd(&out[i], c);
+    }
+}
+
+// ---- one launch per pass: rank + scatter with decoupled look-back ----------------------
+// Tiles are taken in order from a ticket counter (so every tile's predecessors are finished or
+// held by running workgroups: no residency assumption, no deadlock).  Per tile and digit d the
+// tile publishes status[T][d] = (AGGREGATE, its count of d) right after ranking, walks back
+// over its predecessors summing aggregates until it meets an INCLUSIVE prefix, and publishes
+// (INCLUSIVE, digit base + count of d in tiles <= T).  The digit bases (exclusive scan of the
+// whole-array totals from k_pass_totals) replace the per-pass histogram + row scan: one read
+// and one write of the keys (+values) per pass instead of two reads and one write.
+// A status word is one 64-bit value ((epoch << 2 | flag) << 32 | count), stored and loaded as
+// agent-scope relaxed atomics: flag and payload travel together, so no fence or counter is
+// needed.  `epoch` is new for every launch, so words left by earlier launches read as "not
+// published" and the region never needs clearing (the host clears it when the epoch wraps).
+// Waits are bounded: a timeout sets err[0] (never a hang).
+constexpr uint32_t kStAggregate = 1u, kStInclusive = 2u;
+constexpr int kLookback = 4;   // predecessors read per look-back step
+
+__device__ __forceinline__ unsigned long long st_load(const unsigned long long* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_store(unsigned long long* p, uint32_t tag, uint32_t v) {
+    __hip_atomic_store(p, ((unsigned long long)tag << 32) | v, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int R, int BLOCK, int KPT, int L, int RANK>
+__global__ __launch_bounds__(BLOCK) void k_onesweep(
+    const uint32_t* __restrict__ in_k, const uint32_t* __restrict__ in_v,
+    uint32_t* __restrict__ out_k, uint32_t* __restrict__ out_v, uint32_t n, uint32_t shift,
+    uint32_t mask, uint32_t ntiles, const uint32_t* __restrict__ dtot,
+    unsigned long long* status, uint32_t* ticket, uint32_t* err, uint32_t* __restrict__ ntot,
+    uint32_t nshift, uint32_t nmask, uint32_t epoch, const uint32_t* gate, int pass) {
+    // ntot (may be null): whole-array totals of the NEXT pass's digit (key >> nshift) & nmask,
+    // counted here from the keys this workgroup stages, so only pass 0 needs k_pass_totals.
+    constexpr bool HAS_VALUES = L != LAYOUT_KEYS;
+    constexpr int RADIX = 1 << R;
+    constexpr int NW = BLOCK / 64;
+    constexpr int TILE = BLOCK * KPT;
+    constexpr int WAVE_KEYS = 64 * KPT;
+    static_assert(RADIX <= BLOCK, "one digit per thread");
+    __shared__ uint32_t s_whist[NW][RADIX];
+    __shared__ uint32_t s_gdelta[RADIX];
+    __shared__ uint32_t s_dbase[RADIX];
+    __shared__ uint32_t s_scratch[NW];
+    __shared__ uint32_t s_next;
+    __shared__ uint32_t s_ntot[256];
+    __shared__ uint32_t s_keys[HAS_VALUES ? 1 : TILE];
+    __shared__ uint2 s_kv[HAS_VALUES ? TILE : 1];
+
+    if (gated_off(gate, pass)) return;
+    const uint32_t tid = threadIdx.x, w = tid >> 6, lane = lane_id();
+    for (uint32_t d = tid; d < 256u; d += BLOCK) s_ntot[d] = 0u;
+    {   // first output position of every digit
+        const uint32_t c = (tid < (uint32_t)RADIX && tid <= mask) ? dtot[tid] : 0u;
+        uint32_t all;
+        const uint32_t ex = block_excl_scan_n<NW>(c, s_scratch, all);
+        if (tid < (uint32_t)RADIX) s_dbase[tid] = ex;
+        if (tid == 0) s_next = atomicAdd(ticket, 1u);
+        __syncthreads();
+    }
+    uint32_t T = s_next;
+    uint32_t k[KPT];
+    uint32_t v[HAS_VALUES ? KPT : 1];
+    if (T < ntiles) {
+        const uint32_t tile0 = T * (uint32_t)TILE;
+        load_tile<KPT, L>(in_k, in_v, tile0 + w * WAVE_KEYS, n, (uint64_t)tile0 + TILE <= n, k, v);
+    }
+    while (T < ntiles) {
+        const uint32_t tile0 = T * (uint32_t)TILE;
+        const uint32_t wbase = tile0 + w * WAVE_KEYS;
+        const bool full = (uint64_t)tile0 + TILE <= n;
+        for (uint32_t d = lane; d < (uint32_t)RADIX; d += 64) s_whist[w][d] = 0u;
+        uint32_t rank[KPT];
+        rank_slots<R, KPT, RANK>(k, rank, s_whist[w], shift, mask, wbase, n, full);
+        __syncthreads();
+        uint32_t c = 0, wc[NW];
+        if (tid < (uint32_t)RADIX) {
+#pragma unroll
+            for (int q = 0; q < NW; ++q) { wc[q] = s_whist[q][tid]; c += wc[q]; }
+        }
+        uint32_t ttot;
+        const uint32_t tstart = block_excl_scan_n<NW>(c, s_scratch, ttot);
+        // Publish this tile's counts first, then do everything that needs only tile-local
+        // offsets (staging, next ticket, next-tile prefetch) before walking back: the
+        // predecessors get that long to publish their inclusive prefixes, and the prefetch is
+        // in flight while we wait.
+        unsigned long long* st = status + (size_t)T * RADIX + tid;
+        if (tid < (uint32_t)RADIX) {
+            if (T == 0) st_store(st, (epoch << 2) | kStInclusive, s_dbase[tid] + c);
+            else st_store(st, (epoch << 2) | kStAggregate, c);
+            uint32_t o = tstart;
+#pragma unroll
+            for (int q = 0; q < NW; ++q) { s_whist[q][tid] = o; o += wc[q]; }
+        }
+        __syncthreads();
+        // Local shuffle: the tile, stably sorted by digit, in LDS.
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) {
+            if (full || wbase + j * 64 + lane < n) {
+                const uint32_t d = (k[j] >> shift) & mask;
+                const uint32_t s = s_whist[w][d] + rank[j];
+                if (s < (uint32_t)TILE) {
+                    if (HAS_VALUES) s_kv[s] = make_uint2(k[j], v[j]);
+                    else s_keys[s] = k[j];
+                }
+                if (ntot) atomicAdd(&s_ntot[(k[j] >> nshift) & nmask], 1u);
+            }
+        }
+        if (tid == 0) s_next = atomicAdd(ticket, 1u);
+        __syncthreads();
+        const uint32_t Tn = s_next;
+        if (Tn < ntiles) {   // prefetch the next tile; its latency hides under this scatter
+            const uint32_t nt0 = Tn * (uint32_t)TILE;
+            load_tile<KPT, L>(in_k, in_v, nt0 + w * WAVE_KEYS, n, (uint64_t)nt0 + TILE <= n, k, v);
+        }
+        if (tid < (uint32_t)RADIX) {
+            uint32_t excl = s_dbase[tid];
+            if (T != 0) {
+                // windowed look-back: kLookback predecessors loaded at once, consumed in order
+                // (aggregates summed) up to the first inclusive prefix; a not-yet-published
+                // word stops the window and is re-read next round
+                excl = 0;
+                uint32_t j = T - 1;                  // next predecessor to consume
+                uint32_t spins = 0;
+                for (;;) {
+                    unsigned long long sv[kLookback];
+#pragma unroll
+                    for (int i = 0; i < kLookback; ++i)
+                        sv[i] = (j >= (uint32_t)i) ? st_load(status + (size_t)(j - i) * RADIX + tid) : 0ull;
+                    uint32_t used = 0;
+                    bool done = false;
+#pragma unroll
+                    for (int i = 0; i < kLookback; ++i) {
+                        if (done || used != (uint32_t)i) break;
+                        const uint32_t f = (uint32_t)(sv[i] >> 32);
+                        if ((f >> 2) != epoch || j < (uint32_t)i) break;   // not yet published
+                        excl += (uint32_t)sv[i];
+                        ++used;
+                        done = (f & 3u) == kStInclusive;
+                    }
+                    if (done) break;
+                    j -= used;
+                    if (used == 0u) {
+                        // bounded: ~ms per wait, and once any wait timed out every other wait
+                        // gives up at its next check, so a bug can never hang the device
+                        if ((++spins & 255u) == 0u &&
+                            (spins > (1u << 20) ||
+                             __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+                            atomicOr(err, 1u);
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(1);
+                    }
+                }
+                st_store(st, (epoch << 2) | kStInclusive, excl + c);
+            }
+            s_gdelta[tid] = excl - tstart;
+        }
+        __syncthreads();
+        const uint32_t nvalid = full ? (uint32_t)TILE : n - tile0;
+#pragma unroll 4
+        for (uint32_t i = tid; i < nvalid; i += BLOCK) {
+            uint32_t key, val = 0;
+            if (HAS_VALUES) {
+                const uint2 kv = s_kv[i];
+                key = kv.x;
+                val = kv.y;
+            } else {
+                key = s_keys[i];
+            }
+            const uint32_t pos = s_gdelta[(key >> shift) & mask] + i;
+            if (pos < n) {
+                if (L == LAYOUT_AOS) {
+                    reinterpret_cast<uint2*>(out_k)[pos] = make_uint2(key, val);
+                } else {
+                    out_k[pos] = key;
+                    if (HAS_VALUES) out_v[pos] = val;
+                }
+            }
+        }
+        __syncthreads();
+        T = Tn;
+    }
+    if (ntot) {
+        for (uint32_t d = tid; d <= nmask; d += BLOCK)
+            if (s_ntot[d]) atomicAdd(&ntot[d], s_ntot[d]);
+    }
+}
+
 // ---- whole sort of a small array in one workgroup ------------------------------------------
 // n <= BLOCK*KPT: keys (+values) stay in registers between passes; every pass ranks, stages the
 // tile sorted by its digit in LDS, and reloads the registers from LDS.  One launch, one HBM read

@@ -134,6 +134,15 @@ struct rs_plan {
     uint32_t* counts = nullptr;    // [256][ntiles] digit-major tile counts
     uint32_t* totals = nullptr;    // [256]
     uint32_t* flags = nullptr;     // [16] check_order results
+    // one-sweep path (k_pass_totals + k_onesweep)
+    int onesweep_mode = -1;                // -1 auto (use_onesweep), 0 off, 1 on (RSORT_ONESWEEP)
+    unsigned long long* status = nullptr;  // [max_tiles][256] look-back status words
+    uint64_t status_words = 0;
+    uint32_t* ptot = nullptr;      // [kTotalsMax] whole-array digit totals of every pass
+    uint32_t ptot_off[16] = {};    // offset of pass i's totals in ptot
+    uint32_t* tickets = nullptr;   // = ptot + kTotalsMax: [16] per-pass tile tickets, [16] error
+    uint32_t epoch = 0;            // tag of the last k_onesweep launch's status words
+    uint32_t cus = 256;
     uint64_t workspace = 0;
     KernelTimer timer;
 };
@@ -199,15 +208,66 @@ void launch_scatter(int L, int rank_mode, const uint32_t* ik, const uint32_t* iv
         launch_scatter_l<R, BLOCK, KPT, rs::LAYOUT_KEYS>(rank_mode, ik, iv, ok, ov, n, shift, mask, ntiles, grid, counts, totals, gate, pass, s);
 }
 
+template <class F>
+uint32_t resident_per_cu(F kernel, int block) {
+    int api = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&api, kernel, block, 0) != hipSuccess || api < 1)
+        api = 1;
+    return (uint32_t)api;
+}
+
+template <int R, int BLOCK, int KPT, int L, int RANK>
+void launch_onesweep_t(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint32_t* ok,
+                       uint32_t* ov, uint32_t n, uint32_t shift, uint32_t mask, uint32_t ntiles,
+                       const uint32_t* gate, int pass, hipStream_t s) {
+    auto kern = rs::k_onesweep<R, BLOCK, KPT, L, RANK>;
+    static const uint32_t per_cu = resident_per_cu(kern, BLOCK);   // per instantiation
+    const uint32_t grid = std::min<uint32_t>(ntiles, p->cus * per_cu);
+    const bool last = (uint32_t)pass + 1 >= p->passes;
+    uint32_t* ntot = last ? nullptr : p->ptot + p->ptot_off[pass + 1];
+    const uint32_t nshift = last ? 0u : shift + p->widths[pass];
+    const uint32_t nmask = last ? 0u : (1u << p->widths[pass + 1]) - 1u;
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(BLOCK), 0, s, ik, iv, ok, ov, n, shift, mask, ntiles,
+                       p->ptot + p->ptot_off[pass], p->status, p->tickets + pass,
+                       p->tickets + 16, ntot, nshift, nmask, p->epoch, gate, pass);
+}
+
+template <int R, int BLOCK, int KPT, int L>
+void launch_onesweep_l(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint32_t* ok,
+                       uint32_t* ov, uint32_t n, uint32_t shift, uint32_t mask, uint32_t ntiles,
+                       const uint32_t* gate, int pass, hipStream_t s) {
+    if (p->rank_mode == rs::RANK_BALLOT)
+        launch_onesweep_t<R, BLOCK, KPT, L, rs::RANK_BALLOT>(p, ik, iv, ok, ov, n, shift, mask, ntiles, gate, pass, s);
+    else
+        launch_onesweep_t<R, BLOCK, KPT, L, rs::RANK_LDS_ATOMIC>(p, ik, iv, ok, ov, n, shift, mask, ntiles, gate, pass, s);
+}
+
 // One stable digit pass in -> out (histogram, scan, scatter) with tile configuration C.
 template <int R, int BLOCK, int KPT>
 rs_status run_pass_cfg(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint32_t* ok,
                        uint32_t* ov, uint32_t n, uint32_t shift, uint32_t w, int L,
-                       const uint32_t* gate, int pass, uint32_t max_grid, hipStream_t s) {
+                       const uint32_t* gate, int pass, uint32_t max_grid, bool onesweep,
+                       hipStream_t s) {
     constexpr int TILE = BLOCK * KPT;
     const uint32_t mask = (1u << w) - 1u;
     const uint32_t ntiles = (uint32_t)(((uint64_t)n + TILE - 1) / TILE);
     const uint32_t grid = std::min<uint32_t>(ntiles, max_grid);
+    if (onesweep) {
+        if (++p->epoch >= (1u << 30)) {   // tag space exhausted: clear the words, restart tags
+            HIP_TRY(hipMemsetAsync(p->status, 0, 8ull * p->status_words, s));
+            p->epoch = 1;
+        }
+        p->timer.run(RS_KERNEL_SCATTER, s, [&] {
+            if (L == rs::LAYOUT_AOS)
+                launch_onesweep_l<R, BLOCK, KPT, rs::LAYOUT_AOS>(p, ik, iv, ok, ov, n, shift, mask, ntiles, gate, pass, s);
+            else if (L == rs::LAYOUT_SOA)
+                launch_onesweep_l<R, BLOCK, KPT, rs::LAYOUT_SOA>(p, ik, iv, ok, ov, n, shift, mask, ntiles, gate, pass, s);
+            else
+                launch_onesweep_l<R, BLOCK, KPT, rs::LAYOUT_KEYS>(p, ik, iv, ok, ov, n, shift, mask, ntiles, gate, pass, s);
+        });
+        HIP_TRY(hipGetLastError());
+        return RS_OK;
+    }
     p->timer.run(RS_KERNEL_HISTOGRAM, s, [&] {
         launch_histogram<R, TILE>(L, ik, n, shift, mask, ntiles, p->counts, gate, pass, s);
     });
@@ -229,16 +289,16 @@ rs_status run_pass_cfg(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint3
 
 rs_status run_pass(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint32_t* ok,
                    uint32_t* ov, uint32_t n, uint32_t shift, uint32_t w, int L,
-                   const uint32_t* gate, int pass, hipStream_t s) {
+                   const uint32_t* gate, int pass, hipStream_t s, bool onesweep = false) {
     const uint32_t R = pick_R(w);
     if (use_small_tiles(n)) {
-        if (R == 2) return run_pass_cfg<2, kSmall.block, kSmall.kpt>(p, ik, iv, ok, ov, n, shift, w, L, gate, pass, kSmall.max_grid, s);
-        if (R == 4) return run_pass_cfg<4, kSmall.block, kSmall.kpt>(p, ik, iv, ok, ov, n, shift, w, L, gate, pass, kSmall.max_grid, s);
-        return run_pass_cfg<8, kSmall.block, kSmall.kpt>(p, ik, iv, ok, ov, n, shift, w, L, gate, pass, kSmall.max_grid, s);
+        if (R == 2) return run_pass_cfg<2, kSmall.block, kSmall.kpt>(p, ik, iv, ok, ov, n, shift, w, L, gate, pass, kSmall.max_grid, onesweep, s);
+        if (R == 4) return run_pass_cfg<4, kSmall.block, kSmall.kpt>(p, ik, iv, ok, ov, n, shift, w, L, gate, pass, kSmall.max_grid, onesweep, s);
+        return run_pass_cfg<8, kSmall.block, kSmall.kpt>(p, ik, iv, ok, ov, n, shift, w, L, gate, pass, kSmall.max_grid, onesweep, s);
     }
-    if (R == 2) return run_pass_cfg<2, kLarge.block, kLarge.kpt>(p, ik, iv, ok, ov, n, shift, w, L, gate, pass, kLarge.max_grid, s);
-    if (R == 4) return run_pass_cfg<4, kLarge.block, kLarge.kpt>(p, ik, iv, ok, ov, n, shift, w, L, gate, pass, kLarge.max_grid, s);
-    return run_pass_cfg<8, kLarge.block, kLarge.kpt>(p, ik, iv, ok, ov, n, shift, w, L, gate, pass, kLarge.max_grid, s);
+    if (R == 2) return run_pass_cfg<2, kLarge.block, kLarge.kpt>(p, ik, iv, ok, ov, n, shift, w, L, gate, pass, kLarge.max_grid, onesweep, s);
+    if (R == 4) return run_pass_cfg<4, kLarge.block, kLarge.kpt>(p, ik, iv, ok, ov, n, shift, w, L, gate, pass, kLarge.max_grid, onesweep, s);
+    return run_pass_cfg<8, kLarge.block, kLarge.kpt>(p, ik, iv, ok, ov, n, shift, w, L, gate, pass, kLarge.max_grid, onesweep, s);
 }
 
 // Whole sort of n <= kTinyMax in one workgroup (k_sort_small).
@@ -266,6 +326,15 @@ rs_status run_tiny(rs_plan* p, uint32_t* k, uint32_t* v, uint32_t n, hipStream_t
 }
 
 uint32_t full_mask(uint32_t bits) { return bits >= 32 ? 0xFFFFFFFFu : ((1u << bits) - 1u); }
+
+// One-sweep (k_pass_totals + k_onesweep) or histogram/scan/scatter for this sort.  Measured on
+// MI355X: one-sweep wins with values on large-tile sizes (256M KV: -14 %), loses
+// keys-only (a keys-only tile is processed so fast that the look-back wait shows: +10 % at 64M)
+// and on small tiles (thousands of tiles in flight at once make long look-back chains).
+bool use_onesweep(const rs_plan* p, uint64_t n) {
+    if (p->onesweep_mode >= 0) return p->onesweep_mode == 1;
+    return p->layout != rs::LAYOUT_KEYS && !use_small_tiles(n);
+}
 
 }  // namespace
 
@@ -320,6 +389,7 @@ RS_EXPORT rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out) {
               : (p->has_values ? rs::LAYOUT_SOA : rs::LAYOUT_KEYS);
     p->check_order = d.flags & RS_FLAG_CHECK_ORDER;
     p->local_shuffle = d.flags & RS_FLAG_LOCAL_SHUFFLE;
+    if (const char* os = getenv("RSORT_ONESWEEP")) p->onesweep_mode = strcmp(os, "0") != 0 ? 1 : 0;
     if (const char* rk = getenv("RSORT_RANK"))
         p->rank_mode = (strcmp(rk, "ballot") == 0) ? rs::RANK_BALLOT : rs::RANK_LDS_ATOMIC;
     // Even number of passes so the result lands in the caller's buffers, like the reference's
@@ -327,7 +397,11 @@ RS_EXPORT rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out) {
     uint32_t P = (d.bit_count + rb - 1) / rb;
     P += P & 1u;
     p->passes = P;
-    for (uint32_t i = 0; i < P; ++i) p->widths[i] = d.bit_count / P + (i < d.bit_count % P ? 1 : 0);
+    for (uint32_t i = 0, off = 0; i < P; ++i) {
+        p->widths[i] = d.bit_count / P + (i < d.bit_count % P ? 1 : 0);
+        p->ptot_off[i] = off;
+        off += 1u << p->widths[i];
+    }
     p->capacity = d.count;
 
     DeviceGuard guard(d.device);
@@ -337,15 +411,31 @@ RS_EXPORT rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out) {
         p->workspace += bytes;
         return hipMalloc((void**)ptr, bytes);
     };
+    {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, d.device) == hipSuccess && prop.multiProcessorCount > 0)
+            p->cus = (uint32_t)prop.multiProcessorCount;
+    }
+    // look-back status words: one per (tile, digit) of the finest tile configuration in use
+    const uint64_t max_tiles = std::max<uint64_t>(
+        1, std::max<uint64_t>((d.count + kLarge.tile - 1) / kLarge.tile,
+                              (std::min<uint64_t>(d.count, RS_SMALL_MAX) + kSmall.tile - 1) / kSmall.tile));
+    p->status_words = p->onesweep_mode != 0 ? max_tiles * 256 : 1;
     hipError_t e;
     if ((p->layout != rs::LAYOUT_AOS && (e = alloc(&p->tmp_k, 4 * d.count)) != hipSuccess) ||
         (p->layout == rs::LAYOUT_AOS && (e = alloc(&p->tmp_k, 8 * d.count)) != hipSuccess) ||
         (p->layout == rs::LAYOUT_SOA && (e = alloc(&p->tmp_v, 4 * d.count)) != hipSuccess) ||
         (e = alloc(&p->counts, 4ull * 256 * std::max<uint64_t>(1, (d.count + kSmall.tile - 1) / kSmall.tile))) != hipSuccess ||
         (e = alloc(&p->totals, 4ull * 256)) != hipSuccess ||
-        (e = alloc(&p->flags, 4ull * 16)) != hipSuccess)
+        (e = alloc(&p->flags, 4ull * 16)) != hipSuccess ||
+        (e = alloc(&p->ptot, 4ull * (rs::kTotalsMax + 32))) != hipSuccess ||
+        (e = alloc((uint32_t**)&p->status, 8ull * p->status_words)) != hipSuccess)
         return cleanup(fail(e == hipErrorOutOfMemory ? RS_ERR_OUT_OF_MEMORY : RS_ERR_HIP,
                             "rs_plan_create: hipMalloc failed: %s", hipGetErrorString(e)));
+    p->tickets = p->ptot + rs::kTotalsMax;   // [16] tickets, [16] error word
+    if ((e = hipMemset(p->ptot, 0, 4ull * (rs::kTotalsMax + 32))) != hipSuccess ||
+        (e = hipMemset(p->status, 0, 8ull * p->status_words)) != hipSuccess)
+        return cleanup(fail(RS_ERR_HIP, "rs_plan_create: hipMemset failed: %s", hipGetErrorString(e)));
     *out = p;
     return RS_OK;
 }
@@ -359,6 +449,8 @@ RS_EXPORT void rs_plan_destroy(rs_plan* p) {
     (void)hipFree(p->counts);
     (void)hipFree(p->totals);
     (void)hipFree(p->flags);
+    (void)hipFree(p->ptot);
+    (void)hipFree(p->status);
     delete p;
 }
 
@@ -387,6 +479,23 @@ RS_EXPORT rs_status rs_plan_sort_n(rs_plan* p, void* keys, void* values, uint64_
     if (n <= kTinyMax) return run_tiny(p, uk, uv, n32, s);   // one launch; check_order moot
     const uint32_t* gate = p->check_order ? p->flags : nullptr;
     if (p->check_order) HIP_TRY(hipMemsetAsync(p->flags, 0, 16 * 4, s));
+    const bool onesweep = use_onesweep(p, n);
+    if (onesweep) {
+        HIP_TRY(hipMemsetAsync(p->ptot, 0, 4ull * (rs::kTotalsMax + 16), s));   // totals + tickets
+        // pass 0's digit totals from one read of the input; every later pass's totals are
+        // counted by the pass before it (k_onesweep's ntot)
+        rs::PassList pl{};
+        pl.count = 1;
+        pl.width[0] = p->widths[0];
+        const uint32_t grid = (uint32_t)std::min<uint64_t>(8ull * p->cus, (n + 4ull * rs::kBlock - 1) / (4ull * rs::kBlock));
+        p->timer.run(RS_KERNEL_HISTOGRAM, s, [&] {
+            if (L == rs::LAYOUT_AOS)
+                hipLaunchKernelGGL(rs::k_pass_totals<2>, dim3(grid), dim3(rs::kBlock), 0, s, uk, n32, pl, p->ptot);
+            else
+                hipLaunchKernelGGL(rs::k_pass_totals<1>, dim3(grid), dim3(rs::kBlock), 0, s, uk, n32, pl, p->ptot);
+        });
+        HIP_TRY(hipGetLastError());
+    }
     const uint32_t fmask = full_mask(p->bit_count);
     uint32_t shift = 0;
     for (uint32_t i = 0; i < p->passes; ++i) {
@@ -405,7 +514,8 @@ RS_EXPORT rs_status rs_plan_sort_n(rs_plan* p, void* keys, void* values, uint64_
             });
             HIP_TRY(hipGetLastError());
         }
-        rs_status st = run_pass(p, ik, iv, ok, ov, n32, shift, p->widths[i], L, gate, (int)i, s);
+        rs_status st = run_pass(p, ik, iv, ok, ov, n32, shift, p->widths[i], L, gate, (int)i, s,
+                                onesweep);
         if (st != RS_OK) return st;
         shift += p->widths[i];
     }
@@ -451,6 +561,14 @@ RS_EXPORT rs_status rs_plan_partition(rs_plan* p, const void* in_keys, const voi
                             L, nullptr, 0, s);
     if (st != RS_OK) return st;
     if (d_hist) HIP_TRY(hipMemcpyAsync(d_hist, p->totals, 4u << bits, hipMemcpyDeviceToDevice, s));
+    return RS_OK;
+}
+
+RS_EXPORT rs_status rs_plan_device_errors(rs_plan* p, uint32_t* errors) {
+    if (!p || !errors) return fail(RS_ERR_INVALID_ARG, "rs_plan_device_errors: null argument");
+    DeviceGuard guard(p->desc.device);
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(errors, p->tickets + 16, 4, hipMemcpyDeviceToHost));
     return RS_OK;
 }
 

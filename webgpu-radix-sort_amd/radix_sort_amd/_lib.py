@@ -71,6 +71,7 @@ _SIGS = {
     "rs_plan_kernel_times": (ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_double),
                                             ctypes.POINTER(ctypes.c_uint64)]),
     "rs_plan_reset_kernel_times": (ctypes.c_int, [_VP]),
+    "rs_plan_device_errors": (ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_uint32)]),
     "rs_plan_destroy": (None, [_VP]),
     "rs_scan_plan_create": (ctypes.c_int, [ctypes.c_int32, ctypes.c_uint64, ctypes.c_uint32,
                                            ctypes.c_uint32, ctypes.c_uint32,

@@ -231,6 +231,12 @@ class RadixSortKernel:
                 "tile_keys": inf.tile_keys, "grid_blocks": inf.grid_blocks,
                 "workspace_bytes": inf.workspace_bytes}
 
+    def device_errors(self) -> int:
+        """Device error word (synchronises): 0 = ok; non-zero = a bounded wait timed out."""
+        e = ctypes.c_uint32(0)
+        check(_lib.load().rs_plan_device_errors(self._plan, ctypes.byref(e)), "device_errors")
+        return e.value
+
     def set_profiling(self, enable: bool) -> None:
         check(_lib.load().rs_plan_set_profiling(self._plan, 1 if enable else 0), "profiling")
 

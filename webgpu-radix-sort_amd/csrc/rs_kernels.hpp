@@ -526,7 +526,7 @@ __device__ __forceinline__ void st_store(unsigned long long* p, uint32_t tag, ui
                        __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <int R, int BLOCK, int KPT, int L, int RANK>
+template <int R, int BLOCK, int KPT, int L, int RANK, int LO = L>
 __global__ __launch_bounds__(BLOCK) void k_onesweep(
     const uint32_t* __restrict__ in_k, const uint32_t* __restrict__ in_v,
     uint32_t* __restrict__ out_k, uint32_t* __restrict__ out_v, uint32_t n, uint32_t shift,
@@ -535,7 +535,9 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(
     uint32_t nshift, uint32_t nmask, uint32_t epoch, const uint32_t* gate, int pass) {
     // ntot (may be null): whole-array totals of the NEXT pass's digit (key >> nshift) & nmask,
     // counted here from the keys this workgroup stages, so only pass 0 needs k_pass_totals.
+    // L / LO: input / output layout (SOA <-> AOS alternate on the separate-values path).
     constexpr bool HAS_VALUES = L != LAYOUT_KEYS;
+    static_assert((L == LAYOUT_KEYS) == (LO == LAYOUT_KEYS), "values in and out");
     constexpr int RADIX = 1 << R;
     constexpr int NW = BLOCK / 64;
     constexpr int TILE = BLOCK * KPT;
@@ -673,7 +675,7 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(
             }
             const uint32_t pos = s_gdelta[(key >> shift) & mask] + i;
             if (pos < n) {
-                if (L == LAYOUT_AOS) {
+                if (LO == LAYOUT_AOS) {
                     reinterpret_cast<uint2*>(out_k)[pos] = make_uint2(key, val);
                 } else {
                     out_k[pos] = key;
@@ -789,7 +791,7 @@ __global__ __launch_bounds__(kBlock) void k_check(const uint32_t* __restrict__ k
 
 // After an early exit at an odd pass the sorted data sits in the tmp buffers: copy it back so
 // the result is always in the caller's buffers (AbstractRadixSortKernel.ts:94-98).
-template <int L>
+template <int L, int LT = L>
 __global__ __launch_bounds__(kBlock) void k_finalize(const uint32_t* __restrict__ tk,
                                                      const uint32_t* __restrict__ tv,
                                                      uint32_t* __restrict__ uk,
@@ -803,6 +805,10 @@ __global__ __launch_bounds__(kBlock) void k_finalize(const uint32_t* __restrict_
     for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
         if (L == LAYOUT_AOS) {
             reinterpret_cast<uint2*>(uk)[i] = reinterpret_cast<const uint2*>(tk)[i];
+        } else if (LT == LAYOUT_AOS) {       // records in tmp -> the caller's two arrays
+            const uint2 r = reinterpret_cast<const uint2*>(tk)[i];
+            uk[i] = r.x;
+            uv[i] = r.y;
         } else {
             uk[i] = tk[i];
             if (L == LAYOUT_SOA) uv[i] = tv[i];

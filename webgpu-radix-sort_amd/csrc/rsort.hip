@@ -136,6 +136,7 @@ struct rs_plan {
     uint32_t* flags = nullptr;     // [16] check_order results
     // one-sweep path (k_pass_totals + k_onesweep)
     int onesweep_mode = -1;                // -1 auto (use_onesweep), 0 off, 1 on (RSORT_ONESWEEP)
+    bool aos_tmp = true;                   // one-sweep KV: records as the ping-pong copy (RSORT_AOS_TMP)
     unsigned long long* status = nullptr;  // [max_tiles][256] look-back status words
     uint64_t status_words = 0;
     uint32_t* ptot = nullptr;      // [kTotalsMax] whole-array digit totals of every pass
@@ -216,11 +217,11 @@ uint32_t resident_per_cu(F kernel, int block) {
     return (uint32_t)api;
 }
 
-template <int R, int BLOCK, int KPT, int L, int RANK>
+template <int R, int BLOCK, int KPT, int L, int RANK, int LO>
 void launch_onesweep_t(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint32_t* ok,
                        uint32_t* ov, uint32_t n, uint32_t shift, uint32_t mask, uint32_t ntiles,
                        const uint32_t* gate, int pass, hipStream_t s) {
-    auto kern = rs::k_onesweep<R, BLOCK, KPT, L, RANK>;
+    auto kern = rs::k_onesweep<R, BLOCK, KPT, L, RANK, LO>;
     static const uint32_t per_cu = resident_per_cu(kern, BLOCK);   // per instantiation
     const uint32_t grid = std::min<uint32_t>(ntiles, p->cus * per_cu);
     const bool last = (uint32_t)pass + 1 >= p->passes;
@@ -232,38 +233,45 @@ void launch_onesweep_t(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint3
                        p->tickets + 16, ntot, nshift, nmask, p->epoch, gate, pass);
 }
 
-template <int R, int BLOCK, int KPT, int L>
+template <int R, int BLOCK, int KPT, int L, int LO>
 void launch_onesweep_l(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint32_t* ok,
                        uint32_t* ov, uint32_t n, uint32_t shift, uint32_t mask, uint32_t ntiles,
                        const uint32_t* gate, int pass, hipStream_t s) {
     if (p->rank_mode == rs::RANK_BALLOT)
-        launch_onesweep_t<R, BLOCK, KPT, L, rs::RANK_BALLOT>(p, ik, iv, ok, ov, n, shift, mask, ntiles, gate, pass, s);
+        launch_onesweep_t<R, BLOCK, KPT, L, rs::RANK_BALLOT, LO>(p, ik, iv, ok, ov, n, shift, mask, ntiles, gate, pass, s);
     else
-        launch_onesweep_t<R, BLOCK, KPT, L, rs::RANK_LDS_ATOMIC>(p, ik, iv, ok, ov, n, shift, mask, ntiles, gate, pass, s);
+        launch_onesweep_t<R, BLOCK, KPT, L, rs::RANK_LDS_ATOMIC, LO>(p, ik, iv, ok, ov, n, shift, mask, ntiles, gate, pass, s);
 }
+
+// Layout pair of one pass: input layout | output layout << 4 (they differ only on the one-sweep
+// separate-values path, which stages its ping-pong copy as (key, value) records).
+constexpr int layout_pair(int in, int out) { return in | (out << 4); }
 
 // One stable digit pass in -> out (histogram, scan, scatter) with tile configuration C.
 template <int R, int BLOCK, int KPT>
 rs_status run_pass_cfg(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint32_t* ok,
-                       uint32_t* ov, uint32_t n, uint32_t shift, uint32_t w, int L,
+                       uint32_t* ov, uint32_t n, uint32_t shift, uint32_t w, int LL,
                        const uint32_t* gate, int pass, uint32_t max_grid, bool onesweep,
                        hipStream_t s) {
     constexpr int TILE = BLOCK * KPT;
     const uint32_t mask = (1u << w) - 1u;
     const uint32_t ntiles = (uint32_t)(((uint64_t)n + TILE - 1) / TILE);
     const uint32_t grid = std::min<uint32_t>(ntiles, max_grid);
+    const int L = LL & 15;
     if (onesweep) {
         if (++p->epoch >= (1u << 30)) {   // tag space exhausted: clear the words, restart tags
             HIP_TRY(hipMemsetAsync(p->status, 0, 8ull * p->status_words, s));
             p->epoch = 1;
         }
+        constexpr int K = rs::LAYOUT_KEYS, S = rs::LAYOUT_SOA, A = rs::LAYOUT_AOS;
         p->timer.run(RS_KERNEL_SCATTER, s, [&] {
-            if (L == rs::LAYOUT_AOS)
-                launch_onesweep_l<R, BLOCK, KPT, rs::LAYOUT_AOS>(p, ik, iv, ok, ov, n, shift, mask, ntiles, gate, pass, s);
-            else if (L == rs::LAYOUT_SOA)
-                launch_onesweep_l<R, BLOCK, KPT, rs::LAYOUT_SOA>(p, ik, iv, ok, ov, n, shift, mask, ntiles, gate, pass, s);
-            else
-                launch_onesweep_l<R, BLOCK, KPT, rs::LAYOUT_KEYS>(p, ik, iv, ok, ov, n, shift, mask, ntiles, gate, pass, s);
+            switch (LL) {
+                case layout_pair(A, A): launch_onesweep_l<R, BLOCK, KPT, A, A>(p, ik, iv, ok, ov, n, shift, mask, ntiles, gate, pass, s); break;
+                case layout_pair(S, S): launch_onesweep_l<R, BLOCK, KPT, S, S>(p, ik, iv, ok, ov, n, shift, mask, ntiles, gate, pass, s); break;
+                case layout_pair(S, A): launch_onesweep_l<R, BLOCK, KPT, S, A>(p, ik, iv, ok, ov, n, shift, mask, ntiles, gate, pass, s); break;
+                case layout_pair(A, S): launch_onesweep_l<R, BLOCK, KPT, A, S>(p, ik, iv, ok, ov, n, shift, mask, ntiles, gate, pass, s); break;
+                default: launch_onesweep_l<R, BLOCK, KPT, K, K>(p, ik, iv, ok, ov, n, shift, mask, ntiles, gate, pass, s);
+            }
         });
         HIP_TRY(hipGetLastError());
         return RS_OK;
@@ -288,17 +296,17 @@ rs_status run_pass_cfg(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint3
 }
 
 rs_status run_pass(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint32_t* ok,
-                   uint32_t* ov, uint32_t n, uint32_t shift, uint32_t w, int L,
+                   uint32_t* ov, uint32_t n, uint32_t shift, uint32_t w, int LL,
                    const uint32_t* gate, int pass, hipStream_t s, bool onesweep = false) {
     const uint32_t R = pick_R(w);
     if (use_small_tiles(n)) {
-        if (R == 2) return run_pass_cfg<2, kSmall.block, kSmall.kpt>(p, ik, iv, ok, ov, n, shift, w, L, gate, pass, kSmall.max_grid, onesweep, s);
-        if (R == 4) return run_pass_cfg<4, kSmall.block, kSmall.kpt>(p, ik, iv, ok, ov, n, shift, w, L, gate, pass, kSmall.max_grid, onesweep, s);
-        return run_pass_cfg<8, kSmall.block, kSmall.kpt>(p, ik, iv, ok, ov, n, shift, w, L, gate, pass, kSmall.max_grid, onesweep, s);
+        if (R == 2) return run_pass_cfg<2, kSmall.block, kSmall.kpt>(p, ik, iv, ok, ov, n, shift, w, LL, gate, pass, kSmall.max_grid, onesweep, s);
+        if (R == 4) return run_pass_cfg<4, kSmall.block, kSmall.kpt>(p, ik, iv, ok, ov, n, shift, w, LL, gate, pass, kSmall.max_grid, onesweep, s);
+        return run_pass_cfg<8, kSmall.block, kSmall.kpt>(p, ik, iv, ok, ov, n, shift, w, LL, gate, pass, kSmall.max_grid, onesweep, s);
     }
-    if (R == 2) return run_pass_cfg<2, kLarge.block, kLarge.kpt>(p, ik, iv, ok, ov, n, shift, w, L, gate, pass, kLarge.max_grid, onesweep, s);
-    if (R == 4) return run_pass_cfg<4, kLarge.block, kLarge.kpt>(p, ik, iv, ok, ov, n, shift, w, L, gate, pass, kLarge.max_grid, onesweep, s);
-    return run_pass_cfg<8, kLarge.block, kLarge.kpt>(p, ik, iv, ok, ov, n, shift, w, L, gate, pass, kLarge.max_grid, onesweep, s);
+    if (R == 2) return run_pass_cfg<2, kLarge.block, kLarge.kpt>(p, ik, iv, ok, ov, n, shift, w, LL, gate, pass, kLarge.max_grid, onesweep, s);
+    if (R == 4) return run_pass_cfg<4, kLarge.block, kLarge.kpt>(p, ik, iv, ok, ov, n, shift, w, LL, gate, pass, kLarge.max_grid, onesweep, s);
+    return run_pass_cfg<8, kLarge.block, kLarge.kpt>(p, ik, iv, ok, ov, n, shift, w, LL, gate, pass, kLarge.max_grid, onesweep, s);
 }
 
 // Whole sort of n <= kTinyMax in one workgroup (k_sort_small).
@@ -390,6 +398,7 @@ RS_EXPORT rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out) {
     p->check_order = d.flags & RS_FLAG_CHECK_ORDER;
     p->local_shuffle = d.flags & RS_FLAG_LOCAL_SHUFFLE;
     if (const char* os = getenv("RSORT_ONESWEEP")) p->onesweep_mode = strcmp(os, "0") != 0 ? 1 : 0;
+    if (const char* at = getenv("RSORT_AOS_TMP")) p->aos_tmp = strcmp(at, "0") != 0;
     if (const char* rk = getenv("RSORT_RANK"))
         p->rank_mode = (strcmp(rk, "ballot") == 0) ? rs::RANK_BALLOT : rs::RANK_LDS_ATOMIC;
     // Even number of passes so the result lands in the caller's buffers, like the reference's
@@ -422,9 +431,10 @@ RS_EXPORT rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out) {
                               (std::min<uint64_t>(d.count, RS_SMALL_MAX) + kSmall.tile - 1) / kSmall.tile));
     p->status_words = p->onesweep_mode != 0 ? max_tiles * 256 : 1;
     hipError_t e;
-    if ((p->layout != rs::LAYOUT_AOS && (e = alloc(&p->tmp_k, 4 * d.count)) != hipSuccess) ||
-        (p->layout == rs::LAYOUT_AOS && (e = alloc(&p->tmp_k, 8 * d.count)) != hipSuccess) ||
-        (p->layout == rs::LAYOUT_SOA && (e = alloc(&p->tmp_v, 4 * d.count)) != hipSuccess) ||
+    // with values the tmp copy is ONE 8n-byte buffer: (key, value) records for the one-sweep
+    // path, or tmp_k / tmp_v halves (tmp_v = tmp_k + count) for the histogram path
+    if ((p->layout == rs::LAYOUT_KEYS && (e = alloc(&p->tmp_k, 4 * d.count)) != hipSuccess) ||
+        (p->layout != rs::LAYOUT_KEYS && (e = alloc(&p->tmp_k, 8 * d.count)) != hipSuccess) ||
         (e = alloc(&p->counts, 4ull * 256 * std::max<uint64_t>(1, (d.count + kSmall.tile - 1) / kSmall.tile))) != hipSuccess ||
         (e = alloc(&p->totals, 4ull * 256)) != hipSuccess ||
         (e = alloc(&p->flags, 4ull * 16)) != hipSuccess ||
@@ -433,6 +443,7 @@ RS_EXPORT rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out) {
         return cleanup(fail(e == hipErrorOutOfMemory ? RS_ERR_OUT_OF_MEMORY : RS_ERR_HIP,
                             "rs_plan_create: hipMalloc failed: %s", hipGetErrorString(e)));
     p->tickets = p->ptot + rs::kTotalsMax;   // [16] tickets, [16] error word
+    if (p->layout == rs::LAYOUT_SOA) p->tmp_v = p->tmp_k + d.count;
     if ((e = hipMemset(p->ptot, 0, 4ull * (rs::kTotalsMax + 32))) != hipSuccess ||
         (e = hipMemset(p->status, 0, 8ull * p->status_words)) != hipSuccess)
         return cleanup(fail(RS_ERR_HIP, "rs_plan_create: hipMemset failed: %s", hipGetErrorString(e)));
@@ -445,7 +456,6 @@ RS_EXPORT void rs_plan_destroy(rs_plan* p) {
     DeviceGuard guard(p->desc.device);
     p->timer.drain();
     (void)hipFree(p->tmp_k);
-    (void)hipFree(p->tmp_v);
     (void)hipFree(p->counts);
     (void)hipFree(p->totals);
     (void)hipFree(p->flags);
@@ -497,24 +507,31 @@ RS_EXPORT rs_status rs_plan_sort_n(rs_plan* p, void* keys, void* values, uint64_
         HIP_TRY(hipGetLastError());
     }
     const uint32_t fmask = full_mask(p->bit_count);
+    // one-sweep with separate values: the ping-pong copy is (key, value) records - every
+    // even pass writes 8-byte records (twice the bytes per digit run of two 4-byte arrays,
+    // measured faster) and every odd pass reads them back into the caller's arrays
+    const bool recs = onesweep && L == rs::LAYOUT_SOA && p->aos_tmp;
+    constexpr int A = rs::LAYOUT_AOS;
     uint32_t shift = 0;
     for (uint32_t i = 0; i < p->passes; ++i) {
         const bool even = (i % 2) == 0;
         const uint32_t* ik = even ? uk : p->tmp_k;
-        const uint32_t* iv = even ? uv : p->tmp_v;
+        const uint32_t* iv = even ? uv : (recs ? nullptr : p->tmp_v);
         uint32_t* ok = even ? p->tmp_k : uk;
-        uint32_t* ov = even ? p->tmp_v : uv;
+        uint32_t* ov = even ? (recs ? nullptr : p->tmp_v) : uv;
+        const int in_layout = (recs && !even) ? A : L;
+        const int LL = recs ? (even ? layout_pair(L, A) : layout_pair(A, L)) : layout_pair(L, L);
         if (p->check_order) {
             // Order check before every pass (the reference checks every second 2-bit pass,
             // AbstractRadixSortKernel.ts:257-261); all pairs, masked keys (Q1/Q2 fixed).
             const uint32_t grid = (uint32_t)std::min<uint64_t>(kCheckGrid, (n + rs::kBlock - 1) / rs::kBlock);
             p->timer.run(RS_KERNEL_CHECK, s, [&] {
                 hipLaunchKernelGGL(rs::k_check, dim3(grid), dim3(rs::kBlock), 0, s, ik, n32,
-                                   L == rs::LAYOUT_AOS ? 2u : 1u, fmask, p->flags, (int)i, (int)i - 1);
+                                   in_layout == A ? 2u : 1u, fmask, p->flags, (int)i, (int)i - 1);
             });
             HIP_TRY(hipGetLastError());
         }
-        rs_status st = run_pass(p, ik, iv, ok, ov, n32, shift, p->widths[i], L, gate, (int)i, s,
+        rs_status st = run_pass(p, ik, iv, ok, ov, n32, shift, p->widths[i], LL, gate, (int)i, s,
                                 onesweep);
         if (st != RS_OK) return st;
         shift += p->widths[i];
@@ -526,6 +543,7 @@ RS_EXPORT rs_status rs_plan_sort_n(rs_plan* p, void* keys, void* values, uint64_
                                n32, p->flags, (int)p->passes);
         };
         if (L == rs::LAYOUT_AOS) fin(rs::k_finalize<rs::LAYOUT_AOS>);
+        else if (recs) fin(rs::k_finalize<rs::LAYOUT_SOA, rs::LAYOUT_AOS>);
         else if (L == rs::LAYOUT_SOA) fin(rs::k_finalize<rs::LAYOUT_SOA>);
         else fin(rs::k_finalize<rs::LAYOUT_KEYS>);
         HIP_TRY(hipGetLastError());
@@ -558,7 +576,7 @@ RS_EXPORT rs_status rs_plan_partition(rs_plan* p, const void* in_keys, const voi
     }
     rs_status st = run_pass(p, (const uint32_t*)in_keys, (const uint32_t*)in_values,
                             (uint32_t*)out_keys, (uint32_t*)out_values, (uint32_t)n, shift, bits,
-                            L, nullptr, 0, s);
+                            layout_pair(L, L), nullptr, 0, s);
     if (st != RS_OK) return st;
     if (d_hist) HIP_TRY(hipMemcpyAsync(d_hist, p->totals, 4u << bits, hipMemcpyDeviceToDevice, s));
     return RS_OK;

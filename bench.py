@@ -242,6 +242,9 @@ def main() -> None:
 
     value = keys_per_step * K / elapsed / 1e9
     sc = kernel_ms.get("scatter", {"ms": 0.0, "launches": 0})
+    hist_launches = kernel_ms.get("histogram", {"launches": 0})["launches"]
+    # one-sweep path: one digit-count launch per sort instead of one per pass
+    onesweep = 0 < hist_launches < sc["launches"]
     bytes_per_key = 16 if wl["values"] else 8
     roof = None
     if sc["launches"]:
@@ -257,7 +260,8 @@ def main() -> None:
             pass
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "kernel": "k_scatter (rank + local shuffle + scatter)",
+                "kernel": ("k_onesweep (rank + look-back + local shuffle + scatter)"
+                           if onesweep else "k_scatter (rank + local shuffle + scatter)"),
                 "avg_launch_ms": round(avg_ms, 4),
                 "algorithmic_bytes_per_launch": scatter_keys * bytes_per_key}
     passes = info["passes"]

@@ -257,12 +257,14 @@ def test_config4_256M_nearly_sorted_f32_check_order():
 
 
 @pytest.mark.parametrize("rank", ["atomic", "ballot"])
-@pytest.mark.parametrize("tile", ["small", "large"])
+@pytest.mark.parametrize("tile", ["small", "large", "large_keys1024"])
 def test_rank_modes_and_tile_configs(monkeypatch, golden, rank, tile):
     """Both in-wave ranking implementations and both tile configurations give the oracle's
     result (RSORT_RANK / RSORT_TILE are read at plan creation)."""
     monkeypatch.setenv("RSORT_RANK", rank)
-    monkeypatch.setenv("RSORT_TILE", tile)
+    monkeypatch.setenv("RSORT_TILE", tile.split("_")[0])
+    # keys-only large tiles: 512 x 32 by default, 1024 x 16 with RSORT_KEYS_CFG=0
+    monkeypatch.setenv("RSORT_KEYS_CFG", "0" if tile.endswith("1024") else "1")
     for n, bits, kind in ((20_000, 32, "u32"), (300_001, 32, "few"), (1_000_003, 24, "u32"),
                           (70_001, 12, "u32")):
         keys = O.gen_u32(n + bits, n)

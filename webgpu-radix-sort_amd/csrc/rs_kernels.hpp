@@ -32,6 +32,9 @@ namespace rs {
 
 constexpr int kBlock = 256;              // threads of the small kernels: 4 waves of 64
 constexpr int kWaves = kBlock / 64;
+// Pass kernels keep >= 4 waves per SIMD resident (<= 128 VGPRs) at every block size: implied
+// for 1024-thread blocks, and it lets 256 / 512-thread blocks share a CU 4 / 2 ways.
+constexpr int kMinWavesPerSimd = 4;
 
 // Key/value layouts in HBM.  KEYS: keys only.  SOA: separate key and value arrays (the
 // reference's RadixSortBufferKernel buffers).  AOS: one array of 8-byte (key, value) records,
@@ -310,7 +313,7 @@ __device__ __forceinline__ void rank_slots(const uint32_t (&k)[KPT], uint32_t (&
 // (8r + x) * (G/8) + slot: the workgroups of one XCD scatter ADJACENT tiles at the same time,
 // so each digit's writes from one XCD form one contiguous stream.
 template <int R, int BLOCK, int KPT, int L, int RANK>
-__global__ __launch_bounds__(BLOCK) void k_scatter(
+__global__ __launch_bounds__(BLOCK, kMinWavesPerSimd) void k_scatter(
     const uint32_t* __restrict__ in_k, const uint32_t* __restrict__ in_v,
     uint32_t* __restrict__ out_k, uint32_t* __restrict__ out_v, uint32_t n, uint32_t shift,
     uint32_t mask, uint32_t ntiles, const uint32_t* __restrict__ counts,
@@ -527,7 +530,7 @@ __device__ __forceinline__ void st_store(unsigned long long* p, uint32_t tag, ui
 }
 
 template <int R, int BLOCK, int KPT, int L, int RANK, int LO = L>
-__global__ __launch_bounds__(BLOCK) void k_onesweep(
+__global__ __launch_bounds__(BLOCK, kMinWavesPerSimd) void k_onesweep(
     const uint32_t* __restrict__ in_k, const uint32_t* __restrict__ in_v,
     uint32_t* __restrict__ out_k, uint32_t* __restrict__ out_v, uint32_t n, uint32_t shift,
     uint32_t mask, uint32_t ntiles, const uint32_t* __restrict__ dtot,

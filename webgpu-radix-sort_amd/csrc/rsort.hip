@@ -61,6 +61,9 @@ struct TileCfg {
 };
 constexpr TileCfg kLarge{1024, 16, 16384, 512};
 constexpr TileCfg kSmall{256, 16, 4096, 1024};
+// keys-only at >= 12M keys: the same 16K-key tile from 512 threads x 32 keys (75 KiB LDS), so
+// two workgroups share a CU and one's waits (look-back, barriers) overlap the other's work
+constexpr TileCfg kLargeKeys{512, 32, 16384, 512};
 constexpr uint32_t kTinyMax = 1024 * 16;
 constexpr uint32_t kHistGrid = 2048;
 constexpr int kCheckGrid = 2048;
@@ -137,6 +140,7 @@ struct rs_plan {
     // one-sweep path (k_pass_totals + k_onesweep)
     int onesweep_mode = -1;                // -1 auto (use_onesweep), 0 off, 1 on (RSORT_ONESWEEP)
     bool aos_tmp = true;                   // one-sweep KV: records as the ping-pong copy (RSORT_AOS_TMP)
+    bool keys_cfg = true;                  // keys-only 512x32 tiles (RSORT_KEYS_CFG=0: 1024x16)
     unsigned long long* status = nullptr;  // [max_tiles][256] look-back status words
     uint64_t status_words = 0;
     uint32_t* ptot = nullptr;      // [kTotalsMax] whole-array digit totals of every pass
@@ -248,7 +252,8 @@ void launch_onesweep_l(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint3
 constexpr int layout_pair(int in, int out) { return in | (out << 4); }
 
 // One stable digit pass in -> out (histogram, scan, scatter) with tile configuration C.
-template <int R, int BLOCK, int KPT>
+// KEYS_ONLY instantiates the keys-only kernels alone (configurations used only without values).
+template <int R, int BLOCK, int KPT, bool KEYS_ONLY = false>
 rs_status run_pass_cfg(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint32_t* ok,
                        uint32_t* ov, uint32_t n, uint32_t shift, uint32_t w, int LL,
                        const uint32_t* gate, int pass, uint32_t max_grid, bool onesweep,
@@ -265,12 +270,16 @@ rs_status run_pass_cfg(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint3
         }
         constexpr int K = rs::LAYOUT_KEYS, S = rs::LAYOUT_SOA, A = rs::LAYOUT_AOS;
         p->timer.run(RS_KERNEL_SCATTER, s, [&] {
-            switch (LL) {
-                case layout_pair(A, A): launch_onesweep_l<R, BLOCK, KPT, A, A>(p, ik, iv, ok, ov, n, shift, mask, ntiles, gate, pass, s); break;
-                case layout_pair(S, S): launch_onesweep_l<R, BLOCK, KPT, S, S>(p, ik, iv, ok, ov, n, shift, mask, ntiles, gate, pass, s); break;
-                case layout_pair(S, A): launch_onesweep_l<R, BLOCK, KPT, S, A>(p, ik, iv, ok, ov, n, shift, mask, ntiles, gate, pass, s); break;
-                case layout_pair(A, S): launch_onesweep_l<R, BLOCK, KPT, A, S>(p, ik, iv, ok, ov, n, shift, mask, ntiles, gate, pass, s); break;
-                default: launch_onesweep_l<R, BLOCK, KPT, K, K>(p, ik, iv, ok, ov, n, shift, mask, ntiles, gate, pass, s);
+            if constexpr (KEYS_ONLY) {
+                launch_onesweep_l<R, BLOCK, KPT, K, K>(p, ik, iv, ok, ov, n, shift, mask, ntiles, gate, pass, s);
+            } else {
+                switch (LL) {
+                    case layout_pair(A, A): launch_onesweep_l<R, BLOCK, KPT, A, A>(p, ik, iv, ok, ov, n, shift, mask, ntiles, gate, pass, s); break;
+                    case layout_pair(S, S): launch_onesweep_l<R, BLOCK, KPT, S, S>(p, ik, iv, ok, ov, n, shift, mask, ntiles, gate, pass, s); break;
+                    case layout_pair(S, A): launch_onesweep_l<R, BLOCK, KPT, S, A>(p, ik, iv, ok, ov, n, shift, mask, ntiles, gate, pass, s); break;
+                    case layout_pair(A, S): launch_onesweep_l<R, BLOCK, KPT, A, S>(p, ik, iv, ok, ov, n, shift, mask, ntiles, gate, pass, s); break;
+                    default: launch_onesweep_l<R, BLOCK, KPT, K, K>(p, ik, iv, ok, ov, n, shift, mask, ntiles, gate, pass, s);
+                }
             }
         });
         HIP_TRY(hipGetLastError());
@@ -288,8 +297,12 @@ rs_status run_pass_cfg(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint3
     // The scatter always stages the tile through LDS (the local shuffle,
     // RadixSortLocalShuffle.ts:94-116): it is what makes the writes coalesced.
     p->timer.run(RS_KERNEL_SCATTER, s, [&] {
-        launch_scatter<R, BLOCK, KPT>(L, p->rank_mode, ik, iv, ok, ov, n, shift, mask, ntiles,
-                                      grid, p->counts, p->totals, gate, pass, s);
+        if constexpr (KEYS_ONLY)
+            launch_scatter_l<R, BLOCK, KPT, rs::LAYOUT_KEYS>(p->rank_mode, ik, iv, ok, ov, n, shift, mask,
+                                                             ntiles, grid, p->counts, p->totals, gate, pass, s);
+        else
+            launch_scatter<R, BLOCK, KPT>(L, p->rank_mode, ik, iv, ok, ov, n, shift, mask, ntiles,
+                                          grid, p->counts, p->totals, gate, pass, s);
     });
     HIP_TRY(hipGetLastError());
     return RS_OK;
@@ -304,6 +317,8 @@ rs_status run_pass(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint32_t*
         if (R == 4) return run_pass_cfg<4, kSmall.block, kSmall.kpt>(p, ik, iv, ok, ov, n, shift, w, LL, gate, pass, kSmall.max_grid, onesweep, s);
         return run_pass_cfg<8, kSmall.block, kSmall.kpt>(p, ik, iv, ok, ov, n, shift, w, LL, gate, pass, kSmall.max_grid, onesweep, s);
     }
+    if (R == 8 && LL == layout_pair(rs::LAYOUT_KEYS, rs::LAYOUT_KEYS) && p->keys_cfg)
+        return run_pass_cfg<8, kLargeKeys.block, kLargeKeys.kpt, true>(p, ik, iv, ok, ov, n, shift, w, LL, gate, pass, kLargeKeys.max_grid, onesweep, s);
     if (R == 2) return run_pass_cfg<2, kLarge.block, kLarge.kpt>(p, ik, iv, ok, ov, n, shift, w, LL, gate, pass, kLarge.max_grid, onesweep, s);
     if (R == 4) return run_pass_cfg<4, kLarge.block, kLarge.kpt>(p, ik, iv, ok, ov, n, shift, w, LL, gate, pass, kLarge.max_grid, onesweep, s);
     return run_pass_cfg<8, kLarge.block, kLarge.kpt>(p, ik, iv, ok, ov, n, shift, w, LL, gate, pass, kLarge.max_grid, onesweep, s);
@@ -399,6 +414,7 @@ RS_EXPORT rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out) {
     p->local_shuffle = d.flags & RS_FLAG_LOCAL_SHUFFLE;
     if (const char* os = getenv("RSORT_ONESWEEP")) p->onesweep_mode = strcmp(os, "0") != 0 ? 1 : 0;
     if (const char* at = getenv("RSORT_AOS_TMP")) p->aos_tmp = strcmp(at, "0") != 0;
+    if (const char* kc = getenv("RSORT_KEYS_CFG")) p->keys_cfg = strcmp(kc, "0") != 0;
     if (const char* rk = getenv("RSORT_RANK"))
         p->rank_mode = (strcmp(rk, "ballot") == 0) ? rs::RANK_BALLOT : rs::RANK_LDS_ATOMIC;
     // Even number of passes so the result lands in the caller's buffers, like the reference's

@@ -24,6 +24,9 @@
 #ifndef RS_XCD_GROUP
 #define RS_XCD_GROUP 1       // consecutive tiles run on one XCD in the same round (speed only)
 #endif
+#ifndef RS_ONESWEEP_TRACE
+#define RS_ONESWEEP_TRACE 0  // 1: printf the stuck tile when a look-back wait times out
+#endif
 #ifndef RS_SCATTER_DEBUG
 #define RS_SCATTER_DEBUG 0   // ablations (tools/sweep.py): 1 linear writes, 3 no stores,
 #endif                       //   4 drop partially covered 32-B sectors
@@ -654,6 +657,11 @@ __global__ __launch_bounds__(BLOCK, kMinWavesPerSimd) void k_onesweep(
                         if ((++spins & 255u) == 0u &&
                             (spins > (1u << 20) ||
                              __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+#if RS_ONESWEEP_TRACE
+                            if (spins > (1u << 20))
+                                printf("lookback timeout: pass %d tile %u/%u digit %u waiting on %u word %llx epoch %u\n",
+                                       pass, T, ntiles, tid, j, sv[0], epoch);
+#endif
                             atomicOr(err, 1u);
                             break;
                         }

@@ -148,6 +148,13 @@ def main() -> None:
     if use_dist and wl.get("layout") == "aos":
         raise SystemExit("bench: the multi-GPU path sorts separate key/value arrays; "
                          "use config3 for --gpus > 1")
+    if use_dist and "RANK" not in os.environ:     # --distributed without a launcher: world 1
+        import socket
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            port = sk.getsockname()[1]
+        os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                          MASTER_PORT=str(port))
     if use_dist:
         dist.init_process_group("nccl", device_id=dev)
     n = args.n or wl["n"]
@@ -206,13 +213,13 @@ def main() -> None:
         scatter_keys = n
     else:
         keys, vals = make_input(torch, ops, wl, n, wl["seed"], rank * n, dev)
+        # plans and receive buffers are created during the warmup steps (the local sort plan
+        # grows once if a rank receives more than 1.25 n), so the timed steps allocate nothing
         lo = HipLocalOps(local, int(n * 1.25), wl["values"], args.radix_bits)
         r = None
         for _ in range(W):
             r = distributed_sort(keys, vals, lo)
         torch.cuda.synchronize()
-        lo.plan.destroy()
-        lo = HipLocalOps(local, max(int(n * 1.25), r.n if r else 0), wl["values"], args.radix_bits)
         from radix_sort_amd import _lib
         import ctypes
         _lib.load().rs_plan_set_profiling(lo.plan._plan, 1)
@@ -238,7 +245,8 @@ def main() -> None:
         keys_per_step = n * world
         scatter_keys = r.n
         extra["recv_keys_rank0"] = r.n
-        extra["partition"] = "top 8 bits, whole-bucket split"
+        extra["partition"] = "top 8 bits, whole-bucket split, 4 chunks pipelined with the exchange"
+        extra["roofline_scope"] = "local sort of the received keys (rank 0)"
 
     value = keys_per_step * K / elapsed / 1e9
     sc = kernel_ms.get("scatter", {"ms": 0.0, "launches": 0})

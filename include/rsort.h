@@ -152,6 +152,10 @@ rs_status rs_event_elapsed_ms(void* start, void* end, float* ms);
 rs_status rs_fill_random_u32(void* dst, uint64_t n, uint64_t seed, uint64_t start, void* stream);
 /* dst[i] = first + i (u32 wrap), i < n. */
 rs_status rs_fill_iota_u32(void* dst, uint64_t n, uint32_t first, void* stream);
+/* d_hist[d] = #{i < n : ((keys[i] >> shift) & (2^bits - 1)) == d}, 1 <= bits <= 8 (device u32,
+ * 2^bits words, overwritten).  The multi-GPU sort's bucket counts before the exchange. */
+rs_status rs_histogram(const void* keys, uint64_t n, uint32_t shift, uint32_t bits, void* d_hist,
+                       void* stream);
 /* Device-side order check of keys[0..n) by (key & mask): writes 1 (sorted) or 0 to *d_flag
  * (device u32).  Checks every adjacent pair. */
 rs_status rs_is_sorted(const void* keys, uint64_t n, uint32_t bit_count, void* d_flag,

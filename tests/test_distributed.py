@@ -14,7 +14,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 import oracle as O
-from radix_sort_amd.distributed import bucket_owners, distributed_sort, split_sizes
+from radix_sort_amd.distributed import bucket_owners, distributed_sort, exchange_plan, split_sizes
 
 
 class OracleLocalOps:
@@ -23,14 +23,24 @@ class OracleLocalOps:
     def empty(self, n, like):
         return torch.empty(n, dtype=like.dtype)
 
-    def partition(self, keys, values, shift, bits):
+    def histogram(self, keys, shift, bits):
+        k = keys.numpy().view(np.uint32)
+        top = (k >> np.uint32(shift)) & np.uint32((1 << bits) - 1)
+        return torch.from_numpy(np.bincount(top, minlength=1 << bits).astype(np.int32))
+
+    def partition(self, keys, values, shift, bits, out_keys=None, out_values=None):
         k = keys.numpy().view(np.uint32)
         top = (k >> np.uint32(shift)) & np.uint32((1 << bits) - 1)
         perm = np.argsort(top, kind="stable")
-        hist = np.bincount(top, minlength=1 << bits).astype(np.int32)
         sk = torch.from_numpy(k[perm].view(np.int32).copy())
         sv = None if values is None else torch.from_numpy(values.numpy()[perm].copy())
-        return sk, sv, torch.from_numpy(hist)
+        if out_keys is not None:
+            out_keys.copy_(sk)
+            sk = out_keys
+        if sv is not None and out_values is not None:
+            out_values.copy_(sv)
+            sv = out_values
+        return sk, sv
 
     def sort(self, keys, values, n):
         k = keys.numpy().view(np.uint32)
@@ -49,7 +59,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, n_per_rank, kind, q):
+def _worker(rank, world, port, n_per_rank, kind, q, chunks):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -62,20 +72,23 @@ def _worker(rank, world, port, n_per_rank, kind, q):
             k = O.gen_u32(9, n_per_rank, start=rank * n_per_rank) & np.uint32(0x03FFFFFF)
         v = np.arange(rank * n_per_rank, (rank + 1) * n_per_rank, dtype=np.uint32)
         r = distributed_sort(torch.from_numpy(k.view(np.int32).copy()),
-                             torch.from_numpy(v.view(np.int32).copy()), OracleLocalOps())
+                             torch.from_numpy(v.view(np.int32).copy()), OracleLocalOps(),
+                             chunks=chunks)
         q.put((rank, r.keys[: r.n].numpy().view(np.uint32).copy(),
                r.values[: r.n].numpy().view(np.uint32).copy(), r.send_sizes, r.recv_sizes))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("kind", ["uniform", "few", "skewed"])
-def test_gloo_world2_bucket_exchange_is_global_stable_sort(kind):
-    world, n = 2, 20_000
+@pytest.mark.parametrize("kind,world,chunks", [("uniform", 2, 4), ("few", 2, 3), ("skewed", 2, 1),
+                                               ("uniform", 3, 4), ("few", 3, 2)])
+def test_gloo_bucket_exchange_is_global_stable_sort(kind, world, chunks):
+    n = 20_000
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n, kind, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, kind, q, chunks))
+             for r in range(world)]
     for p in procs:
         p.start()
     outs = sorted([q.get(timeout=120) for _ in range(world)], key=lambda x: x[0])
@@ -91,8 +104,10 @@ def test_gloo_world2_bucket_exchange_is_global_stable_sort(kind):
     ek, ev = O.stable_sort_masked(all_k, np.arange(world * n, dtype=np.uint32), 32)
     assert (keys == ek).all() and (vals == ev).all()
     # every rank sent exactly its input, received what others sent it
-    assert sum(outs[0][3]) == n and sum(outs[1][3]) == n
-    assert outs[0][4][1] == outs[1][3][0] and outs[1][4][0] == outs[0][3][1]
+    for r in range(world):
+        assert sum(outs[r][3]) == n
+        for s in range(world):
+            assert outs[r][4][s] == outs[s][3][r]
 
 
 def test_bucket_owners_balanced_and_whole():
@@ -113,8 +128,21 @@ def test_bucket_owners_balanced_and_whole():
     assert sum(r0) + sum(r1) == 150 and (sum(r0) == 0 or sum(r1) == 0)
 
 
+def test_exchange_plan_places_segments_in_global_input_order():
+    # world 2, 3 chunks, 4 buckets; rank 1 owns buckets [2, 4)
+    h = [[[1, 2, 3, 4], [0, 0, 5, 0], [2, 2, 2, 2]],
+         [[4, 3, 2, 1], [1, 1, 1, 1], [0, 0, 0, 7]]]
+    bounds = [0, 2, 4]
+    send, recv, off = exchange_plan(h, bounds, 1, 2)
+    assert send == [[7, 3], [2, 2], [0, 7]]                 # rank 1's chunks to ranks 0 / 1
+    assert recv == [[7, 3], [5, 2], [4, 7]]                 # from ranks 0 / 1, per chunk
+    # source-major, then chunk: src0 c0, src0 c1, src0 c2, src1 c0, src1 c1, src1 c2
+    assert off == [[0, 16], [7, 19], [12, 21]]
+
+
 @pytest.mark.gpu
-def test_rccl_world1_hip_local_ops_round_trip():
+@pytest.mark.parametrize("chunks", [1, 4])
+def test_rccl_world1_hip_local_ops_round_trip(chunks):
     """The product path (HipLocalOps + RCCL calls) on one GPU: world size 1 over nccl."""
     from radix_sort_amd.distributed import HipLocalOps
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -127,7 +155,7 @@ def test_rccl_world1_hip_local_ops_round_trip():
         kt = torch.from_numpy(k.view(np.int32)).cuda()
         vt = torch.from_numpy(v.view(np.int32)).cuda()
         ops = HipLocalOps(0, n, True)
-        r = distributed_sort(kt, vt, ops)
+        r = distributed_sort(kt, vt, ops, chunks=chunks)
         torch.cuda.synchronize()
         ek, ev = O.stable_sort_masked(k, v, 32)
         assert r.n == n
@@ -135,3 +163,16 @@ def test_rccl_world1_hip_local_ops_round_trip():
         assert (r.values.cpu().numpy().view(np.uint32) == ev).all()
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_rs_histogram_matches_bincount():
+    from radix_sort_amd import ops
+    n = 1_000_003
+    k = O.gen_u32(33, n)
+    kt = torch.from_numpy(k.view(np.int32)).cuda()
+    for shift, bits in ((24, 8), (0, 8), (13, 5), (30, 2)):
+        h = torch.empty(1 << bits, dtype=torch.int32, device="cuda")
+        ops.histogram(kt[1:], n - 1, shift, bits, h)
+        exp = np.bincount((k[1:] >> np.uint32(shift)) & np.uint32((1 << bits) - 1), minlength=1 << bits)
+        assert (h.cpu().numpy() == exp).all(), (shift, bits)

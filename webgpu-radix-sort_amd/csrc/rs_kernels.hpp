@@ -463,8 +463,9 @@ struct PassList {
 constexpr int kTotalsMax = 1024;
 template <int KS>
 __global__ __launch_bounds__(kBlock) void k_pass_totals(const uint32_t* __restrict__ keys,
-                                                        uint32_t n, PassList pl,
+                                                        uint32_t n, PassList pl, uint32_t shift0,
                                                         uint32_t* __restrict__ out) {
+    // pass p's digit starts at bit shift0 + sum(width[<p]) (shift0 = 0 for a sort)
     __shared__ uint32_t hist[kWaves][kTotalsMax];
     const uint32_t tid = threadIdx.x, w = tid >> 6;
     uint32_t total = 0;
@@ -473,7 +474,7 @@ __global__ __launch_bounds__(kBlock) void k_pass_totals(const uint32_t* __restri
     __syncthreads();
     uint32_t* h = hist[w];
     auto count_key = [&](uint32_t key) {
-        uint32_t off = 0, shift = 0;
+        uint32_t off = 0, shift = shift0;
         for (uint32_t p = 0; p < pl.count; ++p) {
             const uint32_t wd = pl.width[p];
             atomicAdd(&h[off + ((key >> shift) & ((1u << wd) - 1u))], 1u);

@@ -516,9 +516,9 @@ RS_EXPORT rs_status rs_plan_sort_n(rs_plan* p, void* keys, void* values, uint64_
         const uint32_t grid = (uint32_t)std::min<uint64_t>(8ull * p->cus, (n + 4ull * rs::kBlock - 1) / (4ull * rs::kBlock));
         p->timer.run(RS_KERNEL_HISTOGRAM, s, [&] {
             if (L == rs::LAYOUT_AOS)
-                hipLaunchKernelGGL(rs::k_pass_totals<2>, dim3(grid), dim3(rs::kBlock), 0, s, uk, n32, pl, p->ptot);
+                hipLaunchKernelGGL(rs::k_pass_totals<2>, dim3(grid), dim3(rs::kBlock), 0, s, uk, n32, pl, 0u, p->ptot);
             else
-                hipLaunchKernelGGL(rs::k_pass_totals<1>, dim3(grid), dim3(rs::kBlock), 0, s, uk, n32, pl, p->ptot);
+                hipLaunchKernelGGL(rs::k_pass_totals<1>, dim3(grid), dim3(rs::kBlock), 0, s, uk, n32, pl, 0u, p->ptot);
         });
         HIP_TRY(hipGetLastError());
     }
@@ -816,6 +816,25 @@ RS_EXPORT rs_status rs_fill_iota_u32(void* dst, uint64_t n, uint32_t first, void
     const uint32_t grid = (uint32_t)std::min<uint64_t>(8192, (n + rs::kBlock - 1) / rs::kBlock);
     hipLaunchKernelGGL(rs::k_fill_iota, dim3(grid), dim3(rs::kBlock), 0, (hipStream_t)stream,
                        (uint32_t*)dst, n, first);
+    HIP_TRY(hipGetLastError());
+    return RS_OK;
+}
+
+RS_EXPORT rs_status rs_histogram(const void* keys, uint64_t n, uint32_t shift, uint32_t bits,
+                                 void* d_hist, void* stream) {
+    if (bits == 0 || bits > 8 || shift + bits > 32)
+        return fail(RS_ERR_INVALID_ARG, "rs_histogram: need 1 <= bits <= 8 and shift + bits <= 32");
+    if (!d_hist || (n && !keys)) return fail(RS_ERR_INVALID_ARG, "rs_histogram: null pointer");
+    if (n > 0xFFFFFFFFull) return fail(RS_ERR_INVALID_ARG, "rs_histogram: n must be < 2^32");
+    hipStream_t s = (hipStream_t)stream;
+    HIP_TRY(hipMemsetAsync(d_hist, 0, 4u << bits, s));
+    if (n == 0) return RS_OK;
+    rs::PassList pl{};
+    pl.count = 1;
+    pl.width[0] = bits;
+    const uint32_t grid = (uint32_t)std::min<uint64_t>(2048, (n + 4ull * rs::kBlock - 1) / (4ull * rs::kBlock));
+    hipLaunchKernelGGL(rs::k_pass_totals<1>, dim3(grid), dim3(rs::kBlock), 0, s, (const uint32_t*)keys,
+                       (uint32_t)n, pl, shift, (uint32_t*)d_hist);
     HIP_TRY(hipGetLastError());
     return RS_OK;
 }

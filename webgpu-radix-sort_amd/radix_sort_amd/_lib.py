@@ -94,6 +94,8 @@ _SIGS = {
     "rs_fill_random_u32": (ctypes.c_int, [_VP, ctypes.c_uint64, ctypes.c_uint64,
                                           ctypes.c_uint64, _VP]),
     "rs_fill_iota_u32": (ctypes.c_int, [_VP, ctypes.c_uint64, ctypes.c_uint32, _VP]),
+    "rs_histogram": (ctypes.c_int, [_VP, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                                    _VP, _VP]),
     "rs_is_sorted": (ctypes.c_int, [_VP, ctypes.c_uint64, ctypes.c_uint32, _VP, _VP]),
 }
 

@@ -36,6 +36,13 @@ def is_sorted(t, n: int | None = None, bit_count: int = 32, stream=None) -> bool
     return bool(flag.item())
 
 
+def histogram(t, n: int, shift: int, bits: int, out, stream=None) -> None:
+    """out[d] = number of t[:n] whose digit (key >> shift) & (2^bits - 1) is d (out: 2^bits
+    int32 words on t's device, overwritten)."""
+    check(_lib.load().rs_histogram(t.data_ptr(), n, shift, bits, out.data_ptr(),
+                                   _stream(t, stream)), "rs_histogram")
+
+
 class SortPlan:
     """A sort plan with a capacity; sorts any n <= capacity (multi-GPU receive buffers)."""
 

@@ -322,3 +322,34 @@ def test_onesweep_and_three_kernel_paths(monkeypatch, onesweep, tile):
         out = _np(rt).reshape(-1, 2)
         assert (out[:, 0] == ek).all() and (out[:, 1] == ev).all(), (n, bits, kind, "aos")
         k.destroy()
+
+
+@pytest.mark.parametrize("tile", ["small", "large"])
+def test_onesweep_check_order_exits_and_narrow_digits(monkeypatch, tile):
+    """One-sweep path: check_order early exits (the exit after pass 0 leaves the data as
+    (key, value) records in the ping-pong copy: k_finalize<SOA, AOS>), and 2-/4-bit digits."""
+    from radix_sort_amd import RadixSortKernel
+    monkeypatch.setenv("RSORT_ONESWEEP", "1")
+    monkeypatch.setenv("RSORT_TILE", tile)
+    n = 1_500_001
+    u = O.gen_u32(77, n)
+    vals = O.gen_u32(78, n)
+    for kind in ("sorted", "sorted_after_first_pass", "random"):
+        keys = {"sorted": np.sort(u), "sorted_after_first_pass": u & np.uint32(0x3F),
+                "random": u}[kind]
+        ek, ev = O.stable_sort_masked(keys, vals, 32)
+        kt, vt = _t(keys), _t(vals)
+        k = RadixSortKernel(keys=kt, values=vt, count=n, check_order=True)
+        k.dispatch()
+        assert k.device_errors() == 0
+        assert (_np(kt) == ek).all() and (_np(vt) == ev).all(), kind
+        k.destroy()
+    for radix_bits, bits in ((2, 12), (4, 16), (4, 32)):
+        keys = u & np.uint32((1 << bits) - 1 if bits < 32 else 0xFFFFFFFF)
+        ek, ev = O.stable_sort_masked(keys, vals, bits)
+        kt, vt = _t(keys), _t(vals)
+        k = RadixSortKernel(keys=kt, values=vt, count=n, bit_count=bits, radix_bits=radix_bits)
+        k.dispatch()
+        assert k.device_errors() == 0
+        assert (_np(kt) == ek).all() and (_np(vt) == ev).all(), (radix_bits, bits)
+        k.destroy()

@@ -685,7 +685,11 @@ __global__ __launch_bounds__(BLOCK, kMinWavesPerSimd) void k_onesweep(
             } else {
                 key = s_keys[i];
             }
+#if RS_SCATTER_DEBUG == 1
+            const uint32_t pos = tile0 + i + (s_gdelta[(key >> shift) & mask] & 0);  // ablation
+#else
             const uint32_t pos = s_gdelta[(key >> shift) & mask] + i;
+#endif
             if (pos < n) {
                 if (LO == LAYOUT_AOS) {
                     reinterpret_cast<uint2*>(out_k)[pos] = make_uint2(key, val);

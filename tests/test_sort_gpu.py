@@ -326,17 +326,19 @@ def test_onesweep_and_three_kernel_paths(monkeypatch, onesweep, tile):
 
 @pytest.mark.parametrize("tile", ["small", "large"])
 def test_onesweep_check_order_exits_and_narrow_digits(monkeypatch, tile):
-    """One-sweep path: check_order early exits (the exit after pass 0 leaves the data as
-    (key, value) records in the ping-pong copy: k_finalize<SOA, AOS>), and 2-/4-bit digits."""
+    """One-sweep path: check_order early exits (an exit after pass 0 or 1 leaves the data as
+    (key, value) records in one of the two records buffers: k_finalize<SOA, AOS>), and 2-/4-bit
+    digits."""
     from radix_sort_amd import RadixSortKernel
     monkeypatch.setenv("RSORT_ONESWEEP", "1")
     monkeypatch.setenv("RSORT_TILE", tile)
     n = 1_500_001
     u = O.gen_u32(77, n)
     vals = O.gen_u32(78, n)
-    for kind in ("sorted", "sorted_after_first_pass", "random"):
+    # exits before pass 0, 1 (data in the first records buffer) and 2 (in the second one)
+    for kind in ("sorted", "sorted_after_first_pass", "sorted_after_two_passes", "random"):
         keys = {"sorted": np.sort(u), "sorted_after_first_pass": u & np.uint32(0x3F),
-                "random": u}[kind]
+                "sorted_after_two_passes": u & np.uint32(0xFFFF), "random": u}[kind]
         ek, ev = O.stable_sort_masked(keys, vals, 32)
         kt, vt = _t(keys), _t(vals)
         k = RadixSortKernel(keys=kt, values=vt, count=n, check_order=True)

@@ -807,16 +807,23 @@ __global__ __launch_bounds__(kBlock) void k_check(const uint32_t* __restrict__ k
 
 // After an early exit at an odd pass the sorted data sits in the tmp buffers: copy it back so
 // the result is always in the caller's buffers (AbstractRadixSortKernel.ts:94-98).
+// With a second records buffer (tk_even, one-sweep separate-values path) the data found sorted
+// before an even pass > 0 sits there; otherwise even exits are already in the caller's buffers.
 template <int L, int LT = L>
 __global__ __launch_bounds__(kBlock) void k_finalize(const uint32_t* __restrict__ tk,
                                                      const uint32_t* __restrict__ tv,
                                                      uint32_t* __restrict__ uk,
                                                      uint32_t* __restrict__ uv, uint32_t n,
-                                                     const uint32_t* inv, int passes) {
+                                                     const uint32_t* inv, int passes,
+                                                     const uint32_t* __restrict__ tk_even) {
     int first = -1;
     for (int c = 0; c < passes; ++c)
         if (inv[c] == 0u) { first = c; break; }
-    if (first < 0 || (first & 1) == 0) return;
+    if (first <= 0) return;
+    if ((first & 1) == 0) {
+        if (!tk_even) return;
+        tk = tk_even;
+    }
     const uint32_t stride = gridDim.x * kBlock;
     for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
         if (L == LAYOUT_AOS) {

@@ -140,6 +140,7 @@ struct rs_plan {
     // one-sweep path (k_pass_totals + k_onesweep)
     int onesweep_mode = -1;                // -1 auto (use_onesweep), 0 off, 1 on (RSORT_ONESWEEP)
     bool aos_tmp = true;                   // one-sweep KV: records as the ping-pong copy (RSORT_AOS_TMP)
+    uint32_t* tmp2 = nullptr;              // one-sweep KV: second records buffer (RSORT_RECS2=0: none)
     bool keys_cfg = true;                  // keys-only 512x32 tiles (RSORT_KEYS_CFG=0: 1024x16)
     unsigned long long* status = nullptr;  // [max_tiles][256] look-back status words
     uint64_t status_words = 0;
@@ -414,6 +415,8 @@ RS_EXPORT rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out) {
     p->local_shuffle = d.flags & RS_FLAG_LOCAL_SHUFFLE;
     if (const char* os = getenv("RSORT_ONESWEEP")) p->onesweep_mode = strcmp(os, "0") != 0 ? 1 : 0;
     if (const char* at = getenv("RSORT_AOS_TMP")) p->aos_tmp = strcmp(at, "0") != 0;
+    bool recs2 = true;
+    if (const char* r2 = getenv("RSORT_RECS2")) recs2 = strcmp(r2, "0") != 0;
     if (const char* kc = getenv("RSORT_KEYS_CFG")) p->keys_cfg = strcmp(kc, "0") != 0;
     if (const char* rk = getenv("RSORT_RANK"))
         p->rank_mode = (strcmp(rk, "ballot") == 0) ? rs::RANK_BALLOT : rs::RANK_LDS_ATOMIC;
@@ -451,6 +454,8 @@ RS_EXPORT rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out) {
     // path, or tmp_k / tmp_v halves (tmp_v = tmp_k + count) for the histogram path
     if ((p->layout == rs::LAYOUT_KEYS && (e = alloc(&p->tmp_k, 4 * d.count)) != hipSuccess) ||
         (p->layout != rs::LAYOUT_KEYS && (e = alloc(&p->tmp_k, 8 * d.count)) != hipSuccess) ||
+        (p->layout == rs::LAYOUT_SOA && p->onesweep_mode != 0 && p->aos_tmp && recs2 &&
+         d.count > kTinyMax && (e = alloc(&p->tmp2, 8 * d.count)) != hipSuccess) ||
         (e = alloc(&p->counts, 4ull * 256 * std::max<uint64_t>(1, (d.count + kSmall.tile - 1) / kSmall.tile))) != hipSuccess ||
         (e = alloc(&p->totals, 4ull * 256)) != hipSuccess ||
         (e = alloc(&p->flags, 4ull * 16)) != hipSuccess ||
@@ -472,6 +477,7 @@ RS_EXPORT void rs_plan_destroy(rs_plan* p) {
     DeviceGuard guard(p->desc.device);
     p->timer.drain();
     (void)hipFree(p->tmp_k);
+    (void)hipFree(p->tmp2);
     (void)hipFree(p->counts);
     (void)hipFree(p->totals);
     (void)hipFree(p->flags);
@@ -527,6 +533,9 @@ RS_EXPORT rs_status rs_plan_sort_n(rs_plan* p, void* keys, void* values, uint64_
     // even pass writes 8-byte records (twice the bytes per digit run of two 4-byte arrays,
     // measured faster) and every odd pass reads them back into the caller's arrays
     const bool recs = onesweep && L == rs::LAYOUT_SOA && p->aos_tmp;
+    // with a second records buffer only the last pass writes the caller's two arrays:
+    // U -> R1, R1 -> R2, R2 -> R1, ..., R1 -> U (every other pass writes 8-byte records)
+    uint32_t* r2 = recs ? p->tmp2 : nullptr;
     constexpr int A = rs::LAYOUT_AOS;
     uint32_t shift = 0;
     for (uint32_t i = 0; i < p->passes; ++i) {
@@ -535,8 +544,16 @@ RS_EXPORT rs_status rs_plan_sort_n(rs_plan* p, void* keys, void* values, uint64_
         const uint32_t* iv = even ? uv : (recs ? nullptr : p->tmp_v);
         uint32_t* ok = even ? p->tmp_k : uk;
         uint32_t* ov = even ? (recs ? nullptr : p->tmp_v) : uv;
-        const int in_layout = (recs && !even) ? A : L;
-        const int LL = recs ? (even ? layout_pair(L, A) : layout_pair(A, L)) : layout_pair(L, L);
+        int in_layout = (recs && !even) ? A : L;
+        int LL = recs ? (even ? layout_pair(L, A) : layout_pair(A, L)) : layout_pair(L, L);
+        if (r2 && i > 0 && i + 1 < p->passes) {
+            ik = even ? r2 : p->tmp_k;
+            ok = even ? p->tmp_k : r2;
+            iv = nullptr;
+            ov = nullptr;
+            in_layout = A;
+            LL = layout_pair(A, A);
+        }
         if (p->check_order) {
             // Order check before every pass (the reference checks every second 2-bit pass,
             // AbstractRadixSortKernel.ts:257-261); all pairs, masked keys (Q1/Q2 fixed).
@@ -556,7 +573,7 @@ RS_EXPORT rs_status rs_plan_sort_n(rs_plan* p, void* keys, void* values, uint64_
         const uint32_t grid = (uint32_t)std::min<uint64_t>(kCheckGrid, (n + rs::kBlock - 1) / rs::kBlock);
         auto fin = [&](auto kern) {
             hipLaunchKernelGGL(kern, dim3(grid), dim3(rs::kBlock), 0, s, p->tmp_k, p->tmp_v, uk, uv,
-                               n32, p->flags, (int)p->passes);
+                               n32, p->flags, (int)p->passes, (const uint32_t*)r2);
         };
         if (L == rs::LAYOUT_AOS) fin(rs::k_finalize<rs::LAYOUT_AOS>);
         else if (recs) fin(rs::k_finalize<rs::LAYOUT_SOA, rs::LAYOUT_AOS>);

@@ -486,29 +486,10 @@ RS_EXPORT void rs_plan_destroy(rs_plan* p) {
     delete p;
 }
 
-RS_EXPORT rs_status rs_plan_sort_n(rs_plan* p, void* keys, void* values, uint64_t n,
-                                   void* stream) {
-    if (!p) return fail(RS_ERR_INVALID_ARG, "rs_plan_sort: null plan");
-    if (n > p->capacity)
-        return fail(RS_ERR_CAPACITY, "count %llu exceeds plan capacity %llu",
-                    (unsigned long long)n, (unsigned long long)p->capacity);
-    if (n <= 1) return RS_OK;
-    if (!keys) return fail(RS_ERR_INVALID_ARG, "rs_plan_sort: keys is null");
+// Enqueue every launch of one sort (n > kTinyMax) on stream s.
+static rs_status enqueue_sort(rs_plan* p, uint32_t* uk, uint32_t* uv, uint64_t n, hipStream_t s) {
     const int L = p->layout;
-    if (L == rs::LAYOUT_SOA && !values)
-        return fail(RS_ERR_INVALID_ARG, "rs_plan_sort: plan has values but values is null");
-    if (L == rs::LAYOUT_AOS && values)
-        return fail(RS_ERR_INVALID_ARG, "rs_plan_sort: interleaved plan takes (key, value) records in keys; values must be null");
-    if (((uintptr_t)keys & 3) || (values && ((uintptr_t)values & 3)))
-        return fail(RS_ERR_INVALID_ARG, "keys/values must be 4-byte aligned (README.md limitations)");
-    if (L == rs::LAYOUT_AOS && ((uintptr_t)keys & 7))
-        return fail(RS_ERR_INVALID_ARG, "interleaved records must be 8-byte aligned");
-    DeviceGuard guard(p->desc.device);
-    hipStream_t s = (hipStream_t)stream;
     const uint32_t n32 = (uint32_t)n;
-    uint32_t* uk = (uint32_t*)keys;
-    uint32_t* uv = L == rs::LAYOUT_SOA ? (uint32_t*)values : nullptr;
-    if (n <= kTinyMax) return run_tiny(p, uk, uv, n32, s);   // one launch; check_order moot
     const uint32_t* gate = p->check_order ? p->flags : nullptr;
     if (p->check_order) HIP_TRY(hipMemsetAsync(p->flags, 0, 16 * 4, s));
     const bool onesweep = use_onesweep(p, n);
@@ -582,6 +563,32 @@ RS_EXPORT rs_status rs_plan_sort_n(rs_plan* p, void* keys, void* values, uint64_
         HIP_TRY(hipGetLastError());
     }
     return RS_OK;
+}
+
+RS_EXPORT rs_status rs_plan_sort_n(rs_plan* p, void* keys, void* values, uint64_t n,
+                                   void* stream) {
+    if (!p) return fail(RS_ERR_INVALID_ARG, "rs_plan_sort: null plan");
+    if (n > p->capacity)
+        return fail(RS_ERR_CAPACITY, "count %llu exceeds plan capacity %llu",
+                    (unsigned long long)n, (unsigned long long)p->capacity);
+    if (n <= 1) return RS_OK;
+    if (!keys) return fail(RS_ERR_INVALID_ARG, "rs_plan_sort: keys is null");
+    const int L = p->layout;
+    if (L == rs::LAYOUT_SOA && !values)
+        return fail(RS_ERR_INVALID_ARG, "rs_plan_sort: plan has values but values is null");
+    if (L == rs::LAYOUT_AOS && values)
+        return fail(RS_ERR_INVALID_ARG, "rs_plan_sort: interleaved plan takes (key, value) records in keys; values must be null");
+    if (((uintptr_t)keys & 3) || (values && ((uintptr_t)values & 3)))
+        return fail(RS_ERR_INVALID_ARG, "keys/values must be 4-byte aligned (README.md limitations)");
+    if (L == rs::LAYOUT_AOS && ((uintptr_t)keys & 7))
+        return fail(RS_ERR_INVALID_ARG, "interleaved records must be 8-byte aligned");
+    DeviceGuard guard(p->desc.device);
+    hipStream_t s = (hipStream_t)stream;
+    const uint32_t n32 = (uint32_t)n;
+    uint32_t* uk = (uint32_t*)keys;
+    uint32_t* uv = L == rs::LAYOUT_SOA ? (uint32_t*)values : nullptr;
+    if (n <= kTinyMax) return run_tiny(p, uk, uv, n32, s);   // one launch; check_order moot
+    return enqueue_sort(p, uk, uv, n, s);
 }
 
 RS_EXPORT rs_status rs_plan_sort(rs_plan* p, void* keys, void* values, void* stream) {

@@ -126,7 +126,7 @@ def main() -> None:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--distributed", action="store_true",
                     help="use the bucket-exchange path even at world size 1 (testing)")
-    ap.add_argument("--cpu-log2", type=int, default=23)
+    ap.add_argument("--cpu-log2", type=int, default=24)
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per scatter launch (tools/pmc_traffic.py)")
     args = ap.parse_args()

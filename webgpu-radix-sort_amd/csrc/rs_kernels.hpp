@@ -28,8 +28,8 @@
 #define RS_ONESWEEP_TRACE 0  // 1: printf the stuck tile when a look-back wait times out
 #endif
 #ifndef RS_SCATTER_DEBUG
-#define RS_SCATTER_DEBUG 0   // ablations (tools/sweep.py): 1 linear writes, 3 no stores,
-#endif                       //   4 drop partially covered 32-B sectors
+#define RS_SCATTER_DEBUG 0   // ablation (tools/sweep.py): 1 = linear writes (output pos = input pos)
+#endif
 
 namespace rs {
 
@@ -310,6 +310,101 @@ __device__ __forceinline__ void rank_slots(const uint32_t (&k)[KPT], uint32_t (&
     }
 }
 
+// ---- one tile: rank, digit offsets, local shuffle, scatter (shared by the pass kernels) -------
+// Tile = BLOCK threads x KPT keys in registers (slot j of lane l of wave w = position
+// w*64*KPT + j*64 + l).  `s_whist` holds per-wave digit counts, then per-wave tile offsets.
+
+// Rank the tile's keys (stable, per wave) and return, for thread d < RADIX, the count of digit d
+// in the tile (c), its per-wave counts (wc) and its start in the tile (the return value).  The
+// caller turns wc into per-wave offsets (set_wave_offsets) before staging.  Two barriers.
+template <int R, int NW, int KPT, int RANK>
+__device__ __forceinline__ uint32_t rank_tile(const uint32_t (&k)[KPT], uint32_t (&rank)[KPT],
+                                              uint32_t (*s_whist)[1 << R], uint32_t* s_scratch,
+                                              uint32_t shift, uint32_t mask, uint32_t wbase,
+                                              uint32_t n, bool full, uint32_t& c,
+                                              uint32_t (&wc)[NW]) {
+    constexpr int RADIX = 1 << R;
+    const uint32_t tid = threadIdx.x, w = tid >> 6;
+    // zero this wave's counters (the previous tile's readers finished at the last barrier)
+    for (uint32_t d = lane_id(); d < (uint32_t)RADIX; d += 64) s_whist[w][d] = 0u;
+    rank_slots<R, KPT, RANK>(k, rank, s_whist[w], shift, mask, wbase, n, full);
+    __syncthreads();
+    c = 0;
+    if (tid < (uint32_t)RADIX) {
+#pragma unroll
+        for (int q = 0; q < NW; ++q) { wc[q] = s_whist[q][tid]; c += wc[q]; }
+    }
+    uint32_t ttot;
+    return block_excl_scan_n<NW>(c, s_scratch, ttot);
+}
+
+// Thread d < RADIX: per-wave offsets of digit d inside the tile.
+template <int R, int NW>
+__device__ __forceinline__ void set_wave_offsets(uint32_t (*s_whist)[1 << R], uint32_t tstart,
+                                                 const uint32_t (&wc)[NW]) {
+    uint32_t o = tstart;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) { s_whist[q][threadIdx.x] = o; o += wc[q]; }
+}
+
+// Local shuffle: the tile, stably sorted by digit, into LDS (s_kv with values, else s_keys).
+// With s_ntot, also counts the next pass's digit of every key (whole-array totals).
+template <int KPT, bool HAS_VALUES, int TILE>
+__device__ __forceinline__ void stage_tile(const uint32_t (&k)[KPT], const uint32_t (&v)[HAS_VALUES ? KPT : 1],
+                                           const uint32_t (&rank)[KPT], const uint32_t* whist_w,
+                                           uint32_t* s_keys, uint2* s_kv, uint32_t shift,
+                                           uint32_t mask, uint32_t wbase, uint32_t n, bool full,
+                                           uint32_t* s_ntot, uint32_t nshift, uint32_t nmask) {
+    const uint32_t lane = lane_id();
+#pragma unroll
+    for (int j = 0; j < KPT; ++j) {
+        if (full || wbase + j * 64 + lane < n) {
+            const uint32_t d = (k[j] >> shift) & mask;
+            const uint32_t s = whist_w[d] + rank[j];
+            if (s < (uint32_t)TILE) {
+                if (HAS_VALUES) s_kv[s] = make_uint2(k[j], v[j]);
+                else s_keys[s] = k[j];
+            }
+            if (s_ntot) atomicAdd(&s_ntot[(k[j] >> nshift) & nmask], 1u);
+        }
+    }
+}
+
+// Coalesced scatter of the staged tile: consecutive lanes write consecutive positions of a digit
+// run (global position = s_gdelta[digit] + position in the tile).  LO: output layout.
+template <int BLOCK, bool HAS_VALUES, int LO>
+__device__ __forceinline__ void scatter_tile(const uint32_t* s_keys, const uint2* s_kv,
+                                             const uint32_t* s_gdelta, uint32_t* __restrict__ out_k,
+                                             uint32_t* __restrict__ out_v, uint32_t n,
+                                             uint32_t nvalid, uint32_t tile0, uint32_t shift,
+                                             uint32_t mask) {
+#pragma unroll 4
+    for (uint32_t i = threadIdx.x; i < nvalid; i += BLOCK) {
+        uint32_t key, val = 0;
+        if (HAS_VALUES) {
+            const uint2 kv = s_kv[i];
+            key = kv.x;
+            val = kv.y;
+        } else {
+            key = s_keys[i];
+        }
+#if RS_SCATTER_DEBUG == 1
+        const uint32_t pos = tile0 + i + (s_gdelta[(key >> shift) & mask] & 0);  // ablation
+#else
+        const uint32_t pos = s_gdelta[(key >> shift) & mask] + i;
+        (void)tile0;
+#endif
+        if (pos < n) {  // never false for consistent offsets; keeps a bug from faulting
+            if (LO == LAYOUT_AOS) {
+                reinterpret_cast<uint2*>(out_k)[pos] = make_uint2(key, val);
+            } else {
+                out_k[pos] = key;
+                if (HAS_VALUES) out_v[pos] = val;
+            }
+        }
+    }
+}
+
 // Workgroup g owns tiles g, g+G, g+2G, ... (per-tile counts, so any ownership works).
 // XCD grouping (speed only, never correctness): workgroups are dealt round-robin over the 8
 // XCDs, so workgroup g sits on XCD g % 8 as slot g / 8.  Round r gives XCD x the tiles
@@ -329,16 +424,13 @@ __global__ __launch_bounds__(BLOCK, kMinWavesPerSimd) void k_scatter(
     static_assert(RADIX <= BLOCK, "one digit per thread");
     __shared__ uint32_t s_whist[NW][RADIX];          // per-wave counts -> per-wave tile offsets
     __shared__ uint32_t s_gdelta[RADIX];             // global pos - tile pos, per digit
-#if RS_SCATTER_DEBUG >= 4
-    __shared__ uint2 s_run[RADIX];                   // [lo, hi) of the digit's run in this tile
-#endif
     __shared__ uint32_t s_scratch[NW];
     __shared__ uint32_t s_keys[HAS_VALUES ? 1 : TILE];
     __shared__ uint2 s_kv[HAS_VALUES ? TILE : 1];    // (key, value) staged as one 64-bit word
 
     if (gated_off(gate, pass)) return;
     const uint32_t G = gridDim.x, g = blockIdx.x, tid = threadIdx.x;
-    const uint32_t w = tid >> 6, lane = lane_id();
+    const uint32_t w = tid >> 6;
 
     // Global base of digit `tid`: sum of the totals of smaller digits; the tile's row prefix
     // is added per tile.
@@ -362,88 +454,25 @@ __global__ __launch_bounds__(BLOCK, kMinWavesPerSimd) void k_scatter(
         const bool full = (uint64_t)tile0 + TILE <= n;
         uint32_t run = 0;
         if (tid < (uint32_t)RADIX) run = dbase + counts[(size_t)tid * ntiles + tidx];
-        // zero this wave's counters (the previous tile's readers finished at the last barrier)
-        for (uint32_t d = lane; d < (uint32_t)RADIX; d += 64) s_whist[w][d] = 0u;
-
-        uint32_t rank[KPT];
-        rank_slots<R, KPT, RANK>(k, rank, s_whist[w], shift, mask, wbase, n, full);
-        __syncthreads();
-
-        // Per digit: offsets of each wave inside the tile, tile digit start, global delta.
-        uint32_t c = 0, wc[NW];
+        uint32_t rank[KPT], c, wc[NW];
+        const uint32_t tstart = rank_tile<R, NW, KPT, RANK>(k, rank, s_whist, s_scratch, shift,
+                                                            mask, wbase, n, full, c, wc);
         if (tid < (uint32_t)RADIX) {
-#pragma unroll
-            for (int q = 0; q < NW; ++q) { wc[q] = s_whist[q][tid]; c += wc[q]; }
-        }
-        uint32_t ttot;
-        const uint32_t tstart = block_excl_scan_n<NW>(c, s_scratch, ttot);
-        if (tid < (uint32_t)RADIX) {
-            uint32_t o = tstart;
-#pragma unroll
-            for (int q = 0; q < NW; ++q) { s_whist[q][tid] = o; o += wc[q]; }
+            set_wave_offsets<R, NW>(s_whist, tstart, wc);
             s_gdelta[tid] = run - tstart;
-#if RS_SCATTER_DEBUG >= 4
-            s_run[tid] = make_uint2(run, run + c);
-#endif
         }
         __syncthreads();
-
-        // Local shuffle: the tile, stably sorted by digit, in LDS.
-#pragma unroll
-        for (int j = 0; j < KPT; ++j) {
-            if (full || wbase + j * 64 + lane < n) {
-                const uint32_t d = (k[j] >> shift) & mask;
-                const uint32_t s = s_whist[w][d] + rank[j];
-                if (s < (uint32_t)TILE) {
-                    if (HAS_VALUES) s_kv[s] = make_uint2(k[j], v[j]);
-                    else s_keys[s] = k[j];
-                }
-            }
-        }
+        stage_tile<KPT, HAS_VALUES, TILE>(k, v, rank, s_whist[w], s_keys, s_kv, shift, mask, wbase,
+                                          n, full, nullptr, 0u, 0u);
         __syncthreads();
         // Prefetch the next tile into the (now free) key/value registers; its latency hides
         // under this tile's scatter.
         if (t + 1 < count) {
             const uint32_t nt0 = tile0 + G * TILE;
-            load_tile<KPT, L>(in_k, in_v, nt0 + w * WAVE_KEYS, n,
-                                       (uint64_t)nt0 + TILE <= n, k, v);
+            load_tile<KPT, L>(in_k, in_v, nt0 + w * WAVE_KEYS, n, (uint64_t)nt0 + TILE <= n, k, v);
         }
-        // Coalesced scatter: consecutive lanes write consecutive positions of a digit run.
-        const uint32_t nvalid = full ? (uint32_t)TILE : n - tile0;
-#pragma unroll 4
-        for (uint32_t i = tid; i < nvalid; i += BLOCK) {
-            uint32_t key, val = 0;
-            if (HAS_VALUES) {
-                const uint2 kv = s_kv[i];
-                key = kv.x;
-                val = kv.y;
-            } else {
-                key = s_keys[i];
-            }
-#if RS_SCATTER_DEBUG == 1
-            const uint32_t pos = tile0 + i + (s_gdelta[(key >> shift) & mask] & 0);
-#else
-            const uint32_t pos = s_gdelta[(key >> shift) & mask] + i;
-#endif
-#if RS_SCATTER_DEBUG == 3
-            asm volatile("" ::"v"(key), "v"(pos), "v"(val));
-#elif RS_SCATTER_DEBUG == 4
-            const uint2 rr = s_run[(key >> shift) & mask];
-            if ((pos & ~7u) >= rr.x && (pos | 7u) < rr.y) {
-                out_k[pos] = key;
-                if (HAS_VALUES) out_v[pos] = val;
-            }
-#else
-            if (pos < n) {  // never false for a consistent histogram; keeps a bug from faulting
-                if (L == LAYOUT_AOS) {
-                    reinterpret_cast<uint2*>(out_k)[pos] = make_uint2(key, val);
-                } else {
-                    out_k[pos] = key;
-                    if (HAS_VALUES) out_v[pos] = val;
-                }
-            }
-#endif
-        }
+        scatter_tile<BLOCK, HAS_VALUES, L>(s_keys, s_kv, s_gdelta, out_k, out_v, n,
+                                           full ? (uint32_t)TILE : n - tile0, tile0, shift, mask);
         __syncthreads();
     }
 }
@@ -560,7 +589,7 @@ __global__ __launch_bounds__(BLOCK, kMinWavesPerSimd) void k_onesweep(
     __shared__ uint2 s_kv[HAS_VALUES ? TILE : 1];
 
     if (gated_off(gate, pass)) return;
-    const uint32_t tid = threadIdx.x, w = tid >> 6, lane = lane_id();
+    const uint32_t tid = threadIdx.x, w = tid >> 6;
     for (uint32_t d = tid; d < 256u; d += BLOCK) s_ntot[d] = 0u;
     {   // first output position of every digit
         const uint32_t c = (tid < (uint32_t)RADIX && tid <= mask) ? dtot[tid] : 0u;
@@ -581,17 +610,9 @@ __global__ __launch_bounds__(BLOCK, kMinWavesPerSimd) void k_onesweep(
         const uint32_t tile0 = T * (uint32_t)TILE;
         const uint32_t wbase = tile0 + w * WAVE_KEYS;
         const bool full = (uint64_t)tile0 + TILE <= n;
-        for (uint32_t d = lane; d < (uint32_t)RADIX; d += 64) s_whist[w][d] = 0u;
-        uint32_t rank[KPT];
-        rank_slots<R, KPT, RANK>(k, rank, s_whist[w], shift, mask, wbase, n, full);
-        __syncthreads();
-        uint32_t c = 0, wc[NW];
-        if (tid < (uint32_t)RADIX) {
-#pragma unroll
-            for (int q = 0; q < NW; ++q) { wc[q] = s_whist[q][tid]; c += wc[q]; }
-        }
-        uint32_t ttot;
-        const uint32_t tstart = block_excl_scan_n<NW>(c, s_scratch, ttot);
+        uint32_t rank[KPT], c, wc[NW];
+        const uint32_t tstart = rank_tile<R, NW, KPT, RANK>(k, rank, s_whist, s_scratch, shift,
+                                                            mask, wbase, n, full, c, wc);
         // Publish this tile's counts first, then do everything that needs only tile-local
         // offsets (staging, next ticket, next-tile prefetch) before walking back: the
         // predecessors get that long to publish their inclusive prefixes, and the prefetch is
@@ -600,24 +621,11 @@ __global__ __launch_bounds__(BLOCK, kMinWavesPerSimd) void k_onesweep(
         if (tid < (uint32_t)RADIX) {
             if (T == 0) st_store(st, (epoch << 2) | kStInclusive, s_dbase[tid] + c);
             else st_store(st, (epoch << 2) | kStAggregate, c);
-            uint32_t o = tstart;
-#pragma unroll
-            for (int q = 0; q < NW; ++q) { s_whist[q][tid] = o; o += wc[q]; }
+            set_wave_offsets<R, NW>(s_whist, tstart, wc);
         }
         __syncthreads();
-        // Local shuffle: the tile, stably sorted by digit, in LDS.
-#pragma unroll
-        for (int j = 0; j < KPT; ++j) {
-            if (full || wbase + j * 64 + lane < n) {
-                const uint32_t d = (k[j] >> shift) & mask;
-                const uint32_t s = s_whist[w][d] + rank[j];
-                if (s < (uint32_t)TILE) {
-                    if (HAS_VALUES) s_kv[s] = make_uint2(k[j], v[j]);
-                    else s_keys[s] = k[j];
-                }
-                if (ntot) atomicAdd(&s_ntot[(k[j] >> nshift) & nmask], 1u);
-            }
-        }
+        stage_tile<KPT, HAS_VALUES, TILE>(k, v, rank, s_whist[w], s_keys, s_kv, shift, mask, wbase,
+                                          n, full, ntot ? s_ntot : nullptr, nshift, nmask);
         if (tid == 0) s_next = atomicAdd(ticket, 1u);
         __syncthreads();
         const uint32_t Tn = s_next;
@@ -674,31 +682,8 @@ __global__ __launch_bounds__(BLOCK, kMinWavesPerSimd) void k_onesweep(
             s_gdelta[tid] = excl - tstart;
         }
         __syncthreads();
-        const uint32_t nvalid = full ? (uint32_t)TILE : n - tile0;
-#pragma unroll 4
-        for (uint32_t i = tid; i < nvalid; i += BLOCK) {
-            uint32_t key, val = 0;
-            if (HAS_VALUES) {
-                const uint2 kv = s_kv[i];
-                key = kv.x;
-                val = kv.y;
-            } else {
-                key = s_keys[i];
-            }
-#if RS_SCATTER_DEBUG == 1
-            const uint32_t pos = tile0 + i + (s_gdelta[(key >> shift) & mask] & 0);  // ablation
-#else
-            const uint32_t pos = s_gdelta[(key >> shift) & mask] + i;
-#endif
-            if (pos < n) {
-                if (LO == LAYOUT_AOS) {
-                    reinterpret_cast<uint2*>(out_k)[pos] = make_uint2(key, val);
-                } else {
-                    out_k[pos] = key;
-                    if (HAS_VALUES) out_v[pos] = val;
-                }
-            }
-        }
+        scatter_tile<BLOCK, HAS_VALUES, LO>(s_keys, s_kv, s_gdelta, out_k, out_v, n,
+                                            full ? (uint32_t)TILE : n - tile0, tile0, shift, mask);
         __syncthreads();
         T = Tn;
     }

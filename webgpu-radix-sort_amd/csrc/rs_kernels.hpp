@@ -27,6 +27,12 @@
 #ifndef RS_ONESWEEP_TRACE
 #define RS_ONESWEEP_TRACE 0  // 1: printf the stuck tile when a look-back wait times out
 #endif
+#ifndef RS_RANK_GROUP
+#define RS_RANK_GROUP 16     // slots ranked between scheduling fences (see rank_slots)
+#endif
+#ifndef RS_PACK_POS
+#define RS_PACK_POS 1        // 1: staging-round kernels keep tile positions as 16-bit pairs
+#endif
 #ifndef RS_SCATTER_DEBUG
 #define RS_SCATTER_DEBUG 0   // ablation (tools/sweep.py): 1 = linear writes (output pos = input pos)
 #endif
@@ -51,6 +57,14 @@ __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
 // Popcount of the bits of m below this lane (v_mbcnt_lo/hi).
 __device__ __forceinline__ uint32_t mbcnt(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// A uniform value the compiler cannot see through: digit arithmetic recomputed from it is not
+// merged with the same arithmetic of an earlier phase (keeping a slot's digit or LDS address
+// alive across phases costs one register per key slot).
+__device__ __forceinline__ uint32_t opaque_u(uint32_t x) {
+    asm volatile("" : "+s"(x));
+    return x;
 }
 
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
@@ -227,35 +241,82 @@ __global__ __launch_bounds__(kBlock) void k_scan_rows(uint32_t* __restrict__ cou
 //    (ds_bpermute).  Architecture-guaranteed; ~60 VALU per 64 keys.  RSORT_RANK=ballot.
 enum RankMode { RANK_LDS_ATOMIC = 0, RANK_BALLOT = 1 };
 
-template <int KPT, int L>
+// Per-slot 32-bit values (ranks, then tile positions) of a thread's KPT keys.  PACK keeps two
+// 16-bit values per register (a position in a <= 64K-key tile), which is what lets a 32-key-per-
+// thread tile hold keys, values and positions in 128 VGPRs.
+template <int KPT, bool PACK>
+struct Slots {
+    uint32_t r[KPT];
+    __device__ __forceinline__ uint32_t get(int j) const { return r[j]; }
+    __device__ __forceinline__ void set(int j, uint32_t x) { r[j] = x; }
+    __device__ __forceinline__ void set2(int j, uint32_t a, uint32_t b) { r[j] = a; r[j + 1] = b; }
+};
+template <int KPT>
+struct Slots<KPT, true> {
+    uint32_t r[(KPT + 1) / 2];
+    __device__ __forceinline__ uint32_t get(int j) const {
+        return (j & 1) ? (r[j >> 1] >> 16) : (r[j >> 1] & 0xFFFFu);
+    }
+    __device__ __forceinline__ void set(int j, uint32_t x) {   // x < 2^16
+        r[j >> 1] = (j & 1) ? (r[j >> 1] & 0xFFFFu) | (x << 16) : (r[j >> 1] & 0xFFFF0000u) | x;
+    }
+    __device__ __forceinline__ void set2(int j, uint32_t a, uint32_t b) {   // j even
+        r[j >> 1] = a | (b << 16);
+    }
+};
+
+// Keys past n (the last tile only) load as kPadKey: every pass's digit of it is the largest, and
+// it comes after every real key in input order, so the stable rank puts the pads at tile
+// positions [nvalid, TILE) - after every real key - and no per-slot validity test is needed
+// while ranking and staging (such tests cost a lane mask per slot, which spilled).  Only the
+// published digit count (rank_tile's npad), the next-pass totals and the scatter exclude them.
+constexpr uint32_t kPadKey = 0xFFFFFFFFu;
+
+template <int KPT, int L, bool CLAMP = false>
 __device__ __forceinline__ void load_tile(const uint32_t* __restrict__ in_k,
                                           const uint32_t* __restrict__ in_v, uint32_t wbase,
                                           uint32_t n, bool full, uint32_t (&k)[KPT],
                                           uint32_t (&v)[L != LAYOUT_KEYS ? KPT : 1]) {
     constexpr bool HAS_VALUES = L != LAYOUT_KEYS;
     const uint32_t lane = lane_id();
+    // one base address per array and constant per-slot offsets (a 32-bit index per slot would
+    // have to be recomputed and widened for every slot: it may wrap)
+    const size_t b = (size_t)wbase + lane;
     if (L == LAYOUT_AOS) {
-        const uint2* rec = reinterpret_cast<const uint2*>(in_k);
+        const uint2* rec = reinterpret_cast<const uint2*>(in_k) + b;
 #pragma unroll
         for (int j = 0; j < KPT; ++j) {
-            const uint32_t p = wbase + j * 64 + lane;
-            const uint2 r = (full || p < n) ? rec[p] : make_uint2(0u, 0u);
+            const uint2 r = (full || b + j * 64 < n) ? rec[j * 64] : make_uint2(kPadKey, 0u);
             k[j] = r.x;
             v[j] = r.y;
         }
     } else if (full) {
+        const uint32_t* pk = in_k + b;
 #pragma unroll
-        for (int j = 0; j < KPT; ++j) k[j] = in_k[wbase + j * 64 + lane];
+        for (int j = 0; j < KPT; ++j) k[j] = pk[j * 64];
         if (HAS_VALUES) {
+            const uint32_t* pv = in_v + b;
 #pragma unroll
-            for (int j = 0; j < KPT; ++j) v[j] = in_v[wbase + j * 64 + lane];
+            for (int j = 0; j < KPT; ++j) v[j] = pv[j * 64];
         }
-    } else {
+    } else if (CLAMP) {
+        // branch-free: every slot loads (index clamped to n - 1, n >= 1), pads selected after
 #pragma unroll
         for (int j = 0; j < KPT; ++j) {
-            const uint32_t p = wbase + j * 64 + lane;
-            k[j] = (p < n) ? in_k[p] : 0u;
-            if (HAS_VALUES) v[j] = (p < n) ? in_v[p] : 0u;
+            const size_t p = b + j * 64;
+            const size_t q = p < n ? p : (size_t)n - 1;
+            const uint32_t kk = in_k[q];
+            k[j] = p < n ? kk : kPadKey;
+            if (HAS_VALUES) v[j] = in_v[q];
+        }
+    } else {
+        const uint32_t* pk = in_k + b;
+        const uint32_t* pv = in_v + b;
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) {
+            const bool ok = b + j * 64 < n;
+            k[j] = ok ? pk[j * 64] : kPadKey;
+            if (HAS_VALUES) v[j] = ok ? pv[j * 64] : 0u;
         }
     }
 }
@@ -276,37 +337,36 @@ __device__ __forceinline__ uint64_t match_mask(uint32_t d, uint64_t valid) {
 }
 
 // Stable in-wave ranks of the KPT slots (see RankMode); counters in `whist` (this wave's row).
-template <int R, int KPT, int RANK>
-__device__ __forceinline__ void rank_slots(const uint32_t (&k)[KPT], uint32_t (&rank)[KPT],
-                                           uint32_t* whist, uint32_t shift, uint32_t mask,
-                                           uint32_t wbase, uint32_t n, bool full) {
+// Every slot is ranked (pads included, see kPadKey).
+template <int R, int KPT, int RANK, class RK>
+__device__ __forceinline__ void rank_slots(const uint32_t (&k)[KPT], RK& rank,
+                                           uint32_t* whist, uint32_t shift, uint32_t mask) {
     const uint32_t lane = lane_id();
     if (RANK == RANK_LDS_ATOMIC) {
 #pragma unroll
         for (int j = 0; j < KPT; ++j) {
-            const uint32_t d = (k[j] >> shift) & mask;
-            if (full || wbase + j * 64 + lane < n) rank[j] = atomicAdd(&whist[d], 1u);
+            if (j & 1) rank.set2(j - 1, rank.get(j - 1), atomicAdd(&whist[(k[j] >> shift) & mask], 1u));
+            else rank.set(j, atomicAdd(&whist[(k[j] >> shift) & mask], 1u));
+            // groups of RS_RANK_GROUP slots: the scheduler would otherwise hoist every slot's
+            // LDS address and keep every returned rank live at once (spills at 64 keys/thread)
+            if ((j + 1) % RS_RANK_GROUP == 0) asm volatile("" ::: "memory");
         }
     } else {
         uint32_t info[KPT];
 #pragma unroll
         for (int j = 0; j < KPT; ++j) {
             const uint32_t d = (k[j] >> shift) & mask;
-            const uint64_t valid = full ? ~0ull : __ballot(wbase + j * 64 + lane < n);
-            const uint64_t m = match_mask<R>(d, valid);
+            const uint64_t m = match_mask<R>(d, ~0ull);
             const uint32_t lt = mbcnt(m);
             const uint32_t lo = (uint32_t)m, hi = (uint32_t)(m >> 32);
-            const uint32_t leader = lo ? (uint32_t)__builtin_ctz(lo)
-                                       : (hi ? 32u + (uint32_t)__builtin_ctz(hi) : 0u);
+            const uint32_t leader = lo ? (uint32_t)__builtin_ctz(lo) : 32u + (uint32_t)__builtin_ctz(hi);
             uint32_t old = 0;
-            if (lt == 0 && ((valid >> lane) & 1ull)) old = atomicAdd(&whist[d], (uint32_t)__popcll(m));
-            rank[j] = old;
-            info[j] = (leader << 16) | lt;
+            if (lt == 0) old = atomicAdd(&whist[d], (uint32_t)__popcll(m));
+            info[j] = __builtin_amdgcn_ds_bpermute((int)(leader << 2), (int)old) + lt;
         }
+        (void)lane;
 #pragma unroll
-        for (int j = 0; j < KPT; ++j)
-            rank[j] = __builtin_amdgcn_ds_bpermute((int)((info[j] >> 16) << 2), (int)rank[j]) +
-                      (info[j] & 0xFFFFu);
+        for (int j = 0; j < KPT; ++j) rank.set(j, info[j]);
     }
 }
 
@@ -315,69 +375,106 @@ __device__ __forceinline__ void rank_slots(const uint32_t (&k)[KPT], uint32_t (&
 // w*64*KPT + j*64 + l).  `s_whist` holds per-wave digit counts, then per-wave tile offsets.
 
 // Rank the tile's keys (stable, per wave) and return, for thread d < RADIX, the count of digit d
-// in the tile (c), its per-wave counts (wc) and its start in the tile (the return value).  The
-// caller turns wc into per-wave offsets (set_wave_offsets) before staging.  Two barriers.
-template <int R, int NW, int KPT, int RANK>
-__device__ __forceinline__ uint32_t rank_tile(const uint32_t (&k)[KPT], uint32_t (&rank)[KPT],
+// in the tile without the npad pads (c) and its start in the tile (the return value).  The
+// caller turns the per-wave counts into per-wave offsets (set_wave_offsets) before staging.
+// Two barriers.
+template <int R, int NW, int KPT, int RANK, class RK>
+__device__ __forceinline__ uint32_t rank_tile(const uint32_t (&k)[KPT], RK& rank,
                                               uint32_t (*s_whist)[1 << R], uint32_t* s_scratch,
-                                              uint32_t shift, uint32_t mask, uint32_t wbase,
-                                              uint32_t n, bool full, uint32_t& c,
-                                              uint32_t (&wc)[NW]) {
+                                              uint32_t shift, uint32_t mask, uint32_t npad,
+                                              uint32_t& c) {
     constexpr int RADIX = 1 << R;
     const uint32_t tid = threadIdx.x, w = tid >> 6;
     // zero this wave's counters (the previous tile's readers finished at the last barrier)
     for (uint32_t d = lane_id(); d < (uint32_t)RADIX; d += 64) s_whist[w][d] = 0u;
-    rank_slots<R, KPT, RANK>(k, rank, s_whist[w], shift, mask, wbase, n, full);
+    rank_slots<R, KPT, RANK>(k, rank, s_whist[w], shift, mask);
     __syncthreads();
     c = 0;
     if (tid < (uint32_t)RADIX) {
 #pragma unroll
-        for (int q = 0; q < NW; ++q) { wc[q] = s_whist[q][tid]; c += wc[q]; }
+        for (int q = 0; q < NW; ++q) c += s_whist[q][tid];
+        if (tid == mask) c -= npad;   // the pads' digit; they sort after every real key
     }
     uint32_t ttot;
     return block_excl_scan_n<NW>(c, s_scratch, ttot);
 }
 
-// Thread d < RADIX: per-wave offsets of digit d inside the tile.
+// Thread d < RADIX: per-wave counts of digit d -> per-wave offsets inside the tile.
 template <int R, int NW>
-__device__ __forceinline__ void set_wave_offsets(uint32_t (*s_whist)[1 << R], uint32_t tstart,
-                                                 const uint32_t (&wc)[NW]) {
+__device__ __forceinline__ void set_wave_offsets(uint32_t (*s_whist)[1 << R], uint32_t tstart) {
     uint32_t o = tstart;
 #pragma unroll
-    for (int q = 0; q < NW; ++q) { s_whist[q][threadIdx.x] = o; o += wc[q]; }
+    for (int q = 0; q < NW; ++q) {
+        const uint32_t x = s_whist[q][threadIdx.x];
+        s_whist[q][threadIdx.x] = o;
+        o += x;
+    }
 }
 
 // Local shuffle: the tile, stably sorted by digit, into LDS (s_kv with values, else s_keys).
-// With s_ntot, also counts the next pass's digit of every key (whole-array totals).
-template <int KPT, bool HAS_VALUES, int TILE>
+// With s_ntot, also counts the next pass's digit of every key (whole-array totals; the caller
+// removes the pads' count).
+template <int KPT, bool HAS_VALUES, int TILE, class RK>
 __device__ __forceinline__ void stage_tile(const uint32_t (&k)[KPT], const uint32_t (&v)[HAS_VALUES ? KPT : 1],
-                                           const uint32_t (&rank)[KPT], const uint32_t* whist_w,
+                                           const RK& rank, const uint32_t* whist_w,
                                            uint32_t* s_keys, uint2* s_kv, uint32_t shift,
-                                           uint32_t mask, uint32_t wbase, uint32_t n, bool full,
-                                           uint32_t* s_ntot, uint32_t nshift, uint32_t nmask) {
-    const uint32_t lane = lane_id();
+                                           uint32_t mask, uint32_t* s_ntot, uint32_t nshift,
+                                           uint32_t nmask) {
+    shift = opaque_u(shift);
 #pragma unroll
     for (int j = 0; j < KPT; ++j) {
-        if (full || wbase + j * 64 + lane < n) {
-            const uint32_t d = (k[j] >> shift) & mask;
-            const uint32_t s = whist_w[d] + rank[j];
-            if (s < (uint32_t)TILE) {
-                if (HAS_VALUES) s_kv[s] = make_uint2(k[j], v[j]);
-                else s_keys[s] = k[j];
-            }
-            if (s_ntot) atomicAdd(&s_ntot[(k[j] >> nshift) & nmask], 1u);
+        const uint32_t s = whist_w[(k[j] >> shift) & mask] + rank.get(j);
+        if (s < (uint32_t)TILE) {   // always; keeps a bug from writing past the staging area
+            if (HAS_VALUES) s_kv[s] = make_uint2(k[j], v[j]);
+            else s_keys[s] = k[j];
         }
+        if (s_ntot) atomicAdd(&s_ntot[(k[j] >> nshift) & nmask], 1u);
+    }
+}
+
+// Staging round of a tile larger than the LDS staging area: the keys whose tile position
+// (pos, from set_positions) lies in [lo, lo + STAGE) go to LDS slot pos - lo.
+template <int KPT, bool HAS_VALUES, int STAGE, class RK>
+__device__ __forceinline__ void stage_round(const uint32_t (&k)[KPT], const uint32_t (&v)[HAS_VALUES ? KPT : 1],
+                                            const RK& pos, uint32_t* s_keys, uint2* s_kv,
+                                            uint32_t lo) {
+#pragma unroll
+    for (int j = 0; j < KPT; ++j) {
+        const uint32_t s = pos.get(j) - lo;
+        if (s < (uint32_t)STAGE) {
+            if (HAS_VALUES) s_kv[s] = make_uint2(k[j], v[j]);
+            else s_keys[s] = k[j];
+        }
+    }
+}
+
+// Ranks -> tile positions in place (per-wave offsets in whist_w); with s_ntot, also counts the
+// next pass's digit of every key (the caller removes the pads' count).
+template <int KPT, class RK>
+__device__ __forceinline__ void set_positions(const uint32_t (&k)[KPT], RK& rank,
+                                              const uint32_t* whist_w, uint32_t shift, uint32_t mask,
+                                              uint32_t* s_ntot, uint32_t nshift, uint32_t nmask) {
+    static_assert(KPT % 2 == 0, "slot pairs");
+    shift = opaque_u(shift);
+#pragma unroll
+    for (int j = 0; j < KPT; j += 2)
+        rank.set2(j, whist_w[(k[j] >> shift) & mask] + rank.get(j),
+                  whist_w[(k[j + 1] >> shift) & mask] + rank.get(j + 1));
+    if (s_ntot) {
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) atomicAdd(&s_ntot[(k[j] >> nshift) & nmask], 1u);
     }
 }
 
 // Coalesced scatter of the staged tile: consecutive lanes write consecutive positions of a digit
 // run (global position = s_gdelta[digit] + position in the tile).  LO: output layout.
+// The staged keys are tile positions [pbase, pbase + nvalid).
 template <int BLOCK, bool HAS_VALUES, int LO>
 __device__ __forceinline__ void scatter_tile(const uint32_t* s_keys, const uint2* s_kv,
                                              const uint32_t* s_gdelta, uint32_t* __restrict__ out_k,
                                              uint32_t* __restrict__ out_v, uint32_t n,
                                              uint32_t nvalid, uint32_t tile0, uint32_t shift,
-                                             uint32_t mask) {
+                                             uint32_t mask, uint32_t pbase = 0) {
 #pragma unroll 4
     for (uint32_t i = threadIdx.x; i < nvalid; i += BLOCK) {
         uint32_t key, val = 0;
@@ -389,9 +486,9 @@ __device__ __forceinline__ void scatter_tile(const uint32_t* s_keys, const uint2
             key = s_keys[i];
         }
 #if RS_SCATTER_DEBUG == 1
-        const uint32_t pos = tile0 + i + (s_gdelta[(key >> shift) & mask] & 0);  // ablation
+        const uint32_t pos = tile0 + pbase + i + (s_gdelta[(key >> shift) & mask] & 0);  // ablation
 #else
-        const uint32_t pos = s_gdelta[(key >> shift) & mask] + i;
+        const uint32_t pos = s_gdelta[(key >> shift) & mask] + pbase + i;
         (void)tile0;
 #endif
         if (pos < n) {  // never false for consistent offsets; keeps a bug from faulting
@@ -450,20 +547,20 @@ __global__ __launch_bounds__(BLOCK, kMinWavesPerSimd) void k_scatter(
     for (uint32_t t = 0; t < count; ++t) {
         const uint32_t tidx = first + t * G;
         const uint32_t tile0 = tidx * (uint32_t)TILE;
-        const uint32_t wbase = tile0 + w * WAVE_KEYS;
         const bool full = (uint64_t)tile0 + TILE <= n;
         uint32_t run = 0;
         if (tid < (uint32_t)RADIX) run = dbase + counts[(size_t)tid * ntiles + tidx];
-        uint32_t rank[KPT], c, wc[NW];
+        Slots<KPT, false> rank;
+        uint32_t c;
         const uint32_t tstart = rank_tile<R, NW, KPT, RANK>(k, rank, s_whist, s_scratch, shift,
-                                                            mask, wbase, n, full, c, wc);
+                                                            mask, full ? 0u : tile0 + TILE - n, c);
         if (tid < (uint32_t)RADIX) {
-            set_wave_offsets<R, NW>(s_whist, tstart, wc);
+            set_wave_offsets<R, NW>(s_whist, tstart);
             s_gdelta[tid] = run - tstart;
         }
         __syncthreads();
-        stage_tile<KPT, HAS_VALUES, TILE>(k, v, rank, s_whist[w], s_keys, s_kv, shift, mask, wbase,
-                                          n, full, nullptr, 0u, 0u);
+        stage_tile<KPT, HAS_VALUES, TILE>(k, v, rank, s_whist[w], s_keys, s_kv, shift, mask,
+                                          nullptr, 0u, 0u);
         __syncthreads();
         // Prefetch the next tile into the (now free) key/value registers; its latency hides
         // under this tile's scatter.
@@ -562,8 +659,12 @@ __device__ __forceinline__ void st_store(unsigned long long* p, uint32_t tag, ui
                        __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <int R, int BLOCK, int KPT, int L, int RANK, int LO = L>
-__global__ __launch_bounds__(BLOCK, kMinWavesPerSimd) void k_onesweep(
+// SR > 1: the tile is SR times the LDS staging area (32K-key tiles from 1024 threads x 32 keys
+// with values, staged and scattered in two rounds of 16K positions).  Longer digit runs per tile
+// mean fewer 128-B lines shared by two tiles' runs; such a line reaches memory as two partial
+// writes, and those cost as much as a third more than whole lines (tools/line_probe.hip).
+template <int R, int BLOCK, int KPT, int L, int RANK, int LO = L, int SR = 1>
+__global__ __launch_bounds__(BLOCK, SR > 1 ? BLOCK / 256 : kMinWavesPerSimd) void k_onesweep(
     const uint32_t* __restrict__ in_k, const uint32_t* __restrict__ in_v,
     uint32_t* __restrict__ out_k, uint32_t* __restrict__ out_v, uint32_t n, uint32_t shift,
     uint32_t mask, uint32_t ntiles, const uint32_t* __restrict__ dtot,
@@ -577,16 +678,18 @@ __global__ __launch_bounds__(BLOCK, kMinWavesPerSimd) void k_onesweep(
     constexpr int RADIX = 1 << R;
     constexpr int NW = BLOCK / 64;
     constexpr int TILE = BLOCK * KPT;
+    constexpr int STAGE = TILE / SR;
     constexpr int WAVE_KEYS = 64 * KPT;
     static_assert(RADIX <= BLOCK, "one digit per thread");
+    static_assert(SR == 1 || TILE <= 65536, "packed 16-bit tile positions");
     __shared__ uint32_t s_whist[NW][RADIX];
     __shared__ uint32_t s_gdelta[RADIX];
     __shared__ uint32_t s_dbase[RADIX];
     __shared__ uint32_t s_scratch[NW];
     __shared__ uint32_t s_next;
     __shared__ uint32_t s_ntot[256];
-    __shared__ uint32_t s_keys[HAS_VALUES ? 1 : TILE];
-    __shared__ uint2 s_kv[HAS_VALUES ? TILE : 1];
+    __shared__ uint32_t s_keys[HAS_VALUES ? 1 : STAGE];
+    __shared__ uint2 s_kv[HAS_VALUES ? STAGE : 1];
 
     if (gated_off(gate, pass)) return;
     const uint32_t tid = threadIdx.x, w = tid >> 6;
@@ -602,17 +705,31 @@ __global__ __launch_bounds__(BLOCK, kMinWavesPerSimd) void k_onesweep(
     uint32_t T = s_next;
     uint32_t k[KPT];
     uint32_t v[HAS_VALUES ? KPT : 1];
-    if (T < ntiles) {
-        const uint32_t tile0 = T * (uint32_t)TILE;
-        load_tile<KPT, L>(in_k, in_v, tile0 + w * WAVE_KEYS, n, (uint64_t)tile0 + TILE <= n, k, v);
-    }
+    // SR > 1: no per-slot load branches (they spilled).  Records come from a plan-owned buffer
+    // padded to whole tiles: whole-tile loads, and the slots past n are set to kPadKey once the
+    // tile has arrived.  Arrays (the caller's) load with clamped indices.
+    auto load = [&](uint32_t t0) {
+        if (SR > 1 && L == LAYOUT_AOS)
+            load_tile<KPT, L>(in_k, in_v, t0 + w * WAVE_KEYS, n, true, k, v);
+        else
+            load_tile<KPT, L, (SR > 1)>(in_k, in_v, t0 + w * WAVE_KEYS, n, (uint64_t)t0 + TILE <= n, k, v);
+    };
+    if (T < ntiles) load(T * (uint32_t)TILE);
     while (T < ntiles) {
         const uint32_t tile0 = T * (uint32_t)TILE;
-        const uint32_t wbase = tile0 + w * WAVE_KEYS;
         const bool full = (uint64_t)tile0 + TILE <= n;
-        uint32_t rank[KPT], c, wc[NW];
+        const uint32_t nvalid = full ? (uint32_t)TILE : n - tile0;
+        if (SR > 1 && L == LAYOUT_AOS && !full) {
+            const uint32_t wb = tile0 + w * WAVE_KEYS + lane_id();
+#pragma unroll
+            for (int j = 0; j < KPT; ++j)
+                if (wb + j * 64 >= n) k[j] = kPadKey;
+        }
+        const uint32_t npad = (uint32_t)TILE - nvalid;
+        Slots<KPT, RS_PACK_POS && (SR > 1)> rank;
+        uint32_t c;
         const uint32_t tstart = rank_tile<R, NW, KPT, RANK>(k, rank, s_whist, s_scratch, shift,
-                                                            mask, wbase, n, full, c, wc);
+                                                            mask, npad, c);
         // Publish this tile's counts first, then do everything that needs only tile-local
         // offsets (staging, next ticket, next-tile prefetch) before walking back: the
         // predecessors get that long to publish their inclusive prefixes, and the prefetch is
@@ -621,18 +738,24 @@ __global__ __launch_bounds__(BLOCK, kMinWavesPerSimd) void k_onesweep(
         if (tid < (uint32_t)RADIX) {
             if (T == 0) st_store(st, (epoch << 2) | kStInclusive, s_dbase[tid] + c);
             else st_store(st, (epoch << 2) | kStAggregate, c);
-            set_wave_offsets<R, NW>(s_whist, tstart, wc);
+            set_wave_offsets<R, NW>(s_whist, tstart);
         }
         __syncthreads();
-        stage_tile<KPT, HAS_VALUES, TILE>(k, v, rank, s_whist[w], s_keys, s_kv, shift, mask, wbase,
-                                          n, full, ntot ? s_ntot : nullptr, nshift, nmask);
-        if (tid == 0) s_next = atomicAdd(ticket, 1u);
+        if (SR == 1) {
+            stage_tile<KPT, HAS_VALUES, TILE>(k, v, rank, s_whist[w], s_keys, s_kv, shift, mask,
+                                              ntot ? s_ntot : nullptr, nshift, nmask);
+        } else {
+            set_positions<KPT>(k, rank, s_whist[w], shift, mask, ntot ? s_ntot : nullptr, nshift,
+                               nmask);
+            stage_round<KPT, HAS_VALUES, STAGE>(k, v, rank, s_keys, s_kv, 0u);
+        }
+        if (tid == 0) {
+            s_next = atomicAdd(ticket, 1u);
+            if (ntot && npad) atomicSub(&s_ntot[nmask], npad);   // the pads' next digit
+        }
         __syncthreads();
         const uint32_t Tn = s_next;
-        if (Tn < ntiles) {   // prefetch the next tile; its latency hides under this scatter
-            const uint32_t nt0 = Tn * (uint32_t)TILE;
-            load_tile<KPT, L>(in_k, in_v, nt0 + w * WAVE_KEYS, n, (uint64_t)nt0 + TILE <= n, k, v);
-        }
+        if (SR == 1 && Tn < ntiles) load(Tn * (uint32_t)TILE);   // prefetch: hides under this scatter
         if (tid < (uint32_t)RADIX) {
             uint32_t excl = s_dbase[tid];
             if (T != 0) {
@@ -680,11 +803,38 @@ __global__ __launch_bounds__(BLOCK, kMinWavesPerSimd) void k_onesweep(
                 st_store(st, (epoch << 2) | kStInclusive, excl + c);
             }
             s_gdelta[tid] = excl - tstart;
+#if RS_SCATTER_DEBUG >= 2
+            // ablation (write-pattern study, n a power of 2): every (tile, digit) run starts on
+            // its own 512-B-aligned slot; mode 2 also fills the run's last line with padding
+            s_gdelta[tid] = ((((uint32_t)tid * ntiles + T) * 64u) & (n - 1u)) - tstart;
+#endif
         }
         __syncthreads();
-        scatter_tile<BLOCK, HAS_VALUES, LO>(s_keys, s_kv, s_gdelta, out_k, out_v, n,
-                                            full ? (uint32_t)TILE : n - tile0, tile0, shift, mask);
+#pragma unroll
+        for (int h = 0; h < SR; ++h) {
+            if (h > 0) {   // the previous round's scatter has read the staging area
+                stage_round<KPT, HAS_VALUES, STAGE>(k, v, rank, s_keys, s_kv, h * (uint32_t)STAGE);
+                __syncthreads();
+                if (h == SR - 1 && Tn < ntiles) load(Tn * (uint32_t)TILE);   // registers free: prefetch
+            }
+            const uint32_t lo = h * (uint32_t)STAGE;
+            if (lo < nvalid)
+                scatter_tile<BLOCK, HAS_VALUES, LO>(s_keys, s_kv, s_gdelta, out_k, out_v, n,
+                                                    nvalid - lo < (uint32_t)STAGE ? nvalid - lo : (uint32_t)STAGE,
+                                                    tile0, shift, mask, lo);
+            __syncthreads();
+        }
+#if RS_SCATTER_DEBUG == 2
+        if (tid < (uint32_t)RADIX) {
+            constexpr uint32_t LINE = LO == LAYOUT_AOS ? 16u : 32u;
+            const uint32_t e = s_gdelta[tid] + tstart + c;
+            for (uint32_t q = e; q < ((e + LINE - 1u) & ~(LINE - 1u)) && q < n; ++q) {
+                if (LO == LAYOUT_AOS) reinterpret_cast<uint2*>(out_k)[q] = make_uint2(q, 0u);
+                else { out_k[q] = q; if (HAS_VALUES) out_v[q] = 0u; }
+            }
+        }
         __syncthreads();
+#endif
         T = Tn;
     }
     if (ntot) {
@@ -719,8 +869,8 @@ __global__ __launch_bounds__(BLOCK) void k_sort_small(uint32_t* __restrict__ key
     for (uint32_t p = 0; p < passes.count; ++p) {
         const uint32_t mask = (1u << passes.width[p]) - 1u;
         for (uint32_t d = lane; d < (uint32_t)RADIX; d += 64) s_whist[w][d] = 0u;
-        uint32_t rank[KPT];
-        rank_slots<R, KPT, RANK>(k, rank, s_whist[w], shift, mask, wbase, n, false);
+        Slots<KPT, false> rank;
+        rank_slots<R, KPT, RANK>(k, rank, s_whist[w], shift, mask);   // pads included (kPadKey)
         __syncthreads();
         uint32_t c = 0, wc[NW];
         if (tid < (uint32_t)RADIX) {
@@ -735,26 +885,23 @@ __global__ __launch_bounds__(BLOCK) void k_sort_small(uint32_t* __restrict__ key
             for (int q = 0; q < NW; ++q) { s_whist[q][tid] = o; o += wc[q]; }
         }
         __syncthreads();
+        // every key, pads too: they stay at positions [n, TILE) in every pass
 #pragma unroll
         for (int j = 0; j < KPT; ++j) {
-            if (wbase + j * 64 + lane < n) {
-                const uint32_t s = s_whist[w][(k[j] >> shift) & mask] + rank[j];
-                if (HAS_VALUES) s_kv[s] = make_uint2(k[j], v[j]);
-                else s_keys[s] = k[j];
-            }
+            const uint32_t s = s_whist[w][(k[j] >> shift) & mask] + rank.get(j);
+            if (HAS_VALUES) s_kv[s] = make_uint2(k[j], v[j]);
+            else s_keys[s] = k[j];
         }
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < KPT; ++j) {
             const uint32_t p2 = wbase + j * 64 + lane;
-            if (p2 < n) {
-                if (HAS_VALUES) {
-                    const uint2 kv = s_kv[p2];
-                    k[j] = kv.x;
-                    v[j] = kv.y;
-                } else {
-                    k[j] = s_keys[p2];
-                }
+            if (HAS_VALUES) {
+                const uint2 kv = s_kv[p2];
+                k[j] = kv.x;
+                v[j] = kv.y;
+            } else {
+                k[j] = s_keys[p2];
             }
         }
         shift += passes.width[p];

@@ -64,6 +64,10 @@ constexpr TileCfg kSmall{256, 16, 4096, 1024};
 // keys-only at >= 12M keys: the same 16K-key tile from 512 threads x 32 keys (75 KiB LDS), so
 // two workgroups share a CU and one's waits (look-back, barriers) overlap the other's work
 constexpr TileCfg kLargeKeys{512, 32, 16384, 512};
+// one-sweep passes that read a plan-owned records buffer (padded to whole tiles): 24K-record
+// tiles (1024 threads x 24 records, positions packed 16-bit) staged through LDS in two rounds of
+// 12K; longer digit runs per tile than 16K tiles (fewer lines shared by two tiles' runs)
+constexpr TileCfg kHuge{1024, 24, 24576, 512};
 constexpr uint32_t kTinyMax = 1024 * 16;
 constexpr uint32_t kHistGrid = 2048;
 constexpr int kCheckGrid = 2048;
@@ -142,6 +146,7 @@ struct rs_plan {
     bool aos_tmp = true;                   // one-sweep KV: records as the ping-pong copy (RSORT_AOS_TMP)
     uint32_t* tmp2 = nullptr;              // one-sweep KV: second records buffer (RSORT_RECS2=0: none)
     bool keys_cfg = true;                  // keys-only 512x32 tiles (RSORT_KEYS_CFG=0: 1024x16)
+    bool huge_tiles = true;                // one-sweep KV: 32K-key tiles (RSORT_HUGE=0: 16K)
     unsigned long long* status = nullptr;  // [max_tiles][256] look-back status words
     uint64_t status_words = 0;
     uint32_t* ptot = nullptr;      // [kTotalsMax] whole-array digit totals of every pass
@@ -222,11 +227,11 @@ uint32_t resident_per_cu(F kernel, int block) {
     return (uint32_t)api;
 }
 
-template <int R, int BLOCK, int KPT, int L, int RANK, int LO>
+template <int R, int BLOCK, int KPT, int L, int RANK, int LO, int SR>
 void launch_onesweep_t(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint32_t* ok,
                        uint32_t* ov, uint32_t n, uint32_t shift, uint32_t mask, uint32_t ntiles,
                        const uint32_t* gate, int pass, hipStream_t s) {
-    auto kern = rs::k_onesweep<R, BLOCK, KPT, L, RANK, LO>;
+    auto kern = rs::k_onesweep<R, BLOCK, KPT, L, RANK, LO, SR>;
     static const uint32_t per_cu = resident_per_cu(kern, BLOCK);   // per instantiation
     const uint32_t grid = std::min<uint32_t>(ntiles, p->cus * per_cu);
     const bool last = (uint32_t)pass + 1 >= p->passes;
@@ -238,14 +243,14 @@ void launch_onesweep_t(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint3
                        p->tickets + 16, ntot, nshift, nmask, p->epoch, gate, pass);
 }
 
-template <int R, int BLOCK, int KPT, int L, int LO>
+template <int R, int BLOCK, int KPT, int L, int LO, int SR>
 void launch_onesweep_l(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint32_t* ok,
                        uint32_t* ov, uint32_t n, uint32_t shift, uint32_t mask, uint32_t ntiles,
                        const uint32_t* gate, int pass, hipStream_t s) {
     if (p->rank_mode == rs::RANK_BALLOT)
-        launch_onesweep_t<R, BLOCK, KPT, L, rs::RANK_BALLOT, LO>(p, ik, iv, ok, ov, n, shift, mask, ntiles, gate, pass, s);
+        launch_onesweep_t<R, BLOCK, KPT, L, rs::RANK_BALLOT, LO, SR>(p, ik, iv, ok, ov, n, shift, mask, ntiles, gate, pass, s);
     else
-        launch_onesweep_t<R, BLOCK, KPT, L, rs::RANK_LDS_ATOMIC, LO>(p, ik, iv, ok, ov, n, shift, mask, ntiles, gate, pass, s);
+        launch_onesweep_t<R, BLOCK, KPT, L, rs::RANK_LDS_ATOMIC, LO, SR>(p, ik, iv, ok, ov, n, shift, mask, ntiles, gate, pass, s);
 }
 
 // Layout pair of one pass: input layout | output layout << 4 (they differ only on the one-sweep
@@ -254,7 +259,7 @@ constexpr int layout_pair(int in, int out) { return in | (out << 4); }
 
 // One stable digit pass in -> out (histogram, scan, scatter) with tile configuration C.
 // KEYS_ONLY instantiates the keys-only kernels alone (configurations used only without values).
-template <int R, int BLOCK, int KPT, bool KEYS_ONLY = false>
+template <int R, int BLOCK, int KPT, bool KEYS_ONLY = false, int SR = 1>
 rs_status run_pass_cfg(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint32_t* ok,
                        uint32_t* ov, uint32_t n, uint32_t shift, uint32_t w, int LL,
                        const uint32_t* gate, int pass, uint32_t max_grid, bool onesweep,
@@ -272,41 +277,45 @@ rs_status run_pass_cfg(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint3
         constexpr int K = rs::LAYOUT_KEYS, S = rs::LAYOUT_SOA, A = rs::LAYOUT_AOS;
         p->timer.run(RS_KERNEL_SCATTER, s, [&] {
             if constexpr (KEYS_ONLY) {
-                launch_onesweep_l<R, BLOCK, KPT, K, K>(p, ik, iv, ok, ov, n, shift, mask, ntiles, gate, pass, s);
+                launch_onesweep_l<R, BLOCK, KPT, K, K, SR>(p, ik, iv, ok, ov, n, shift, mask, ntiles, gate, pass, s);
             } else {
                 switch (LL) {
-                    case layout_pair(A, A): launch_onesweep_l<R, BLOCK, KPT, A, A>(p, ik, iv, ok, ov, n, shift, mask, ntiles, gate, pass, s); break;
-                    case layout_pair(S, S): launch_onesweep_l<R, BLOCK, KPT, S, S>(p, ik, iv, ok, ov, n, shift, mask, ntiles, gate, pass, s); break;
-                    case layout_pair(S, A): launch_onesweep_l<R, BLOCK, KPT, S, A>(p, ik, iv, ok, ov, n, shift, mask, ntiles, gate, pass, s); break;
-                    case layout_pair(A, S): launch_onesweep_l<R, BLOCK, KPT, A, S>(p, ik, iv, ok, ov, n, shift, mask, ntiles, gate, pass, s); break;
-                    default: launch_onesweep_l<R, BLOCK, KPT, K, K>(p, ik, iv, ok, ov, n, shift, mask, ntiles, gate, pass, s);
+                    case layout_pair(A, A): launch_onesweep_l<R, BLOCK, KPT, A, A, SR>(p, ik, iv, ok, ov, n, shift, mask, ntiles, gate, pass, s); break;
+                    case layout_pair(S, S): launch_onesweep_l<R, BLOCK, KPT, S, S, SR>(p, ik, iv, ok, ov, n, shift, mask, ntiles, gate, pass, s); break;
+                    case layout_pair(S, A): launch_onesweep_l<R, BLOCK, KPT, S, A, SR>(p, ik, iv, ok, ov, n, shift, mask, ntiles, gate, pass, s); break;
+                    case layout_pair(A, S): launch_onesweep_l<R, BLOCK, KPT, A, S, SR>(p, ik, iv, ok, ov, n, shift, mask, ntiles, gate, pass, s); break;
+                    default: launch_onesweep_l<R, BLOCK, KPT, K, K, SR>(p, ik, iv, ok, ov, n, shift, mask, ntiles, gate, pass, s);
                 }
             }
         });
         HIP_TRY(hipGetLastError());
         return RS_OK;
     }
-    p->timer.run(RS_KERNEL_HISTOGRAM, s, [&] {
-        launch_histogram<R, TILE>(L, ik, n, shift, mask, ntiles, p->counts, gate, pass, s);
-    });
-    HIP_TRY(hipGetLastError());
-    p->timer.run(RS_KERNEL_SCAN, s, [&] {
-        hipLaunchKernelGGL(rs::k_scan_rows, dim3(1u << R), dim3(rs::kBlock), 0, s, p->counts,
-                           ntiles, p->totals, gate, pass);
-    });
-    HIP_TRY(hipGetLastError());
-    // The scatter always stages the tile through LDS (the local shuffle,
-    // RadixSortLocalShuffle.ts:94-116): it is what makes the writes coalesced.
-    p->timer.run(RS_KERNEL_SCATTER, s, [&] {
-        if constexpr (KEYS_ONLY)
-            launch_scatter_l<R, BLOCK, KPT, rs::LAYOUT_KEYS>(p->rank_mode, ik, iv, ok, ov, n, shift, mask,
-                                                             ntiles, grid, p->counts, p->totals, gate, pass, s);
-        else
-            launch_scatter<R, BLOCK, KPT>(L, p->rank_mode, ik, iv, ok, ov, n, shift, mask, ntiles,
-                                          grid, p->counts, p->totals, gate, pass, s);
-    });
-    HIP_TRY(hipGetLastError());
-    return RS_OK;
+    if constexpr (SR != 1) {
+        return fail(RS_ERR_INVALID_ARG, "staging rounds are one-sweep only");
+    } else {
+        p->timer.run(RS_KERNEL_HISTOGRAM, s, [&] {
+            launch_histogram<R, TILE>(L, ik, n, shift, mask, ntiles, p->counts, gate, pass, s);
+        });
+        HIP_TRY(hipGetLastError());
+        p->timer.run(RS_KERNEL_SCAN, s, [&] {
+            hipLaunchKernelGGL(rs::k_scan_rows, dim3(1u << R), dim3(rs::kBlock), 0, s, p->counts,
+                               ntiles, p->totals, gate, pass);
+        });
+        HIP_TRY(hipGetLastError());
+        // The scatter always stages the tile through LDS (the local shuffle,
+        // RadixSortLocalShuffle.ts:94-116): it is what makes the writes coalesced.
+        p->timer.run(RS_KERNEL_SCATTER, s, [&] {
+            if constexpr (KEYS_ONLY)
+                launch_scatter_l<R, BLOCK, KPT, rs::LAYOUT_KEYS>(p->rank_mode, ik, iv, ok, ov, n, shift, mask,
+                                                                 ntiles, grid, p->counts, p->totals, gate, pass, s);
+            else
+                launch_scatter<R, BLOCK, KPT>(L, p->rank_mode, ik, iv, ok, ov, n, shift, mask, ntiles,
+                                              grid, p->counts, p->totals, gate, pass, s);
+        });
+        HIP_TRY(hipGetLastError());
+        return RS_OK;
+    }
 }
 
 rs_status run_pass(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint32_t* ok,
@@ -318,6 +327,13 @@ rs_status run_pass(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint32_t*
         if (R == 4) return run_pass_cfg<4, kSmall.block, kSmall.kpt>(p, ik, iv, ok, ov, n, shift, w, LL, gate, pass, kSmall.max_grid, onesweep, s);
         return run_pass_cfg<8, kSmall.block, kSmall.kpt>(p, ik, iv, ok, ov, n, shift, w, LL, gate, pass, kSmall.max_grid, onesweep, s);
     }
+    // with values; records only from a plan-owned buffer padded to whole kHuge tiles (the
+    // kernel loads whole record tiles without per-slot bounds, see k_onesweep's SR > 1)
+    const int Lin = LL & 15;
+    if (R == 8 && onesweep && p->huge_tiles &&
+        (Lin == rs::LAYOUT_SOA ||
+         (Lin == rs::LAYOUT_AOS && (ik == p->tmp_k || (p->tmp2 && ik == p->tmp2)))))
+        return run_pass_cfg<8, kHuge.block, kHuge.kpt, false, 2>(p, ik, iv, ok, ov, n, shift, w, LL, gate, pass, kHuge.max_grid, onesweep, s);
     if (R == 8 && LL == layout_pair(rs::LAYOUT_KEYS, rs::LAYOUT_KEYS) && p->keys_cfg)
         return run_pass_cfg<8, kLargeKeys.block, kLargeKeys.kpt, true>(p, ik, iv, ok, ov, n, shift, w, LL, gate, pass, kLargeKeys.max_grid, onesweep, s);
     if (R == 2) return run_pass_cfg<2, kLarge.block, kLarge.kpt>(p, ik, iv, ok, ov, n, shift, w, LL, gate, pass, kLarge.max_grid, onesweep, s);
@@ -418,6 +434,7 @@ RS_EXPORT rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out) {
     bool recs2 = true;
     if (const char* r2 = getenv("RSORT_RECS2")) recs2 = strcmp(r2, "0") != 0;
     if (const char* kc = getenv("RSORT_KEYS_CFG")) p->keys_cfg = strcmp(kc, "0") != 0;
+    if (const char* hg = getenv("RSORT_HUGE")) p->huge_tiles = strcmp(hg, "0") != 0;
     if (const char* rk = getenv("RSORT_RANK"))
         p->rank_mode = (strcmp(rk, "ballot") == 0) ? rs::RANK_BALLOT : rs::RANK_LDS_ATOMIC;
     // Even number of passes so the result lands in the caller's buffers, like the reference's
@@ -452,10 +469,13 @@ RS_EXPORT rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out) {
     hipError_t e;
     // with values the tmp copy is ONE 8n-byte buffer: (key, value) records for the one-sweep
     // path, or tmp_k / tmp_v halves (tmp_v = tmp_k + count) for the histogram path
+    // records buffers are padded to whole kHuge tiles (k_onesweep with staging rounds reads
+    // whole tiles)
+    const uint64_t padded = (d.count + kHuge.tile - 1) / kHuge.tile * kHuge.tile;
     if ((p->layout == rs::LAYOUT_KEYS && (e = alloc(&p->tmp_k, 4 * d.count)) != hipSuccess) ||
-        (p->layout != rs::LAYOUT_KEYS && (e = alloc(&p->tmp_k, 8 * d.count)) != hipSuccess) ||
+        (p->layout != rs::LAYOUT_KEYS && (e = alloc(&p->tmp_k, 8 * padded)) != hipSuccess) ||
         (p->layout == rs::LAYOUT_SOA && p->onesweep_mode != 0 && p->aos_tmp && recs2 &&
-         d.count > kTinyMax && (e = alloc(&p->tmp2, 8 * d.count)) != hipSuccess) ||
+         d.count > kTinyMax && (e = alloc(&p->tmp2, 8 * padded)) != hipSuccess) ||
         (e = alloc(&p->counts, 4ull * 256 * std::max<uint64_t>(1, (d.count + kSmall.tile - 1) / kSmall.tile))) != hipSuccess ||
         (e = alloc(&p->totals, 4ull * 256)) != hipSuccess ||
         (e = alloc(&p->flags, 4ull * 16)) != hipSuccess ||

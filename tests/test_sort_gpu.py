@@ -355,3 +355,55 @@ def test_onesweep_check_order_exits_and_narrow_digits(monkeypatch, tile):
         assert k.device_errors() == 0
         assert (_np(kt) == ek).all() and (_np(vt) == ev).all(), (radix_bits, bits)
         k.destroy()
+
+
+def _dup_pattern(kind: str, n: int, seed: int) -> np.ndarray:
+    """Duplicate-heavy key layouts that drive the run-counting ranks (rs_kernels.hpp, LDS
+    counters under duplicate-heavy keys): runs of equal keys, the same digit recurring in
+    separate runs of one 64-lane slot, sorted keys with repeats, few distinct keys."""
+    u = O.gen_u32(seed, n)
+    idx = np.arange(n, dtype=np.int64)
+    if kind.startswith("runs"):
+        r = int(kind[4:])
+        return u[idx // r]
+    if kind == "recurring":     # runs of 5 drawn from 6 values: one digit in several runs per slot
+        pool = O.gen_u32(seed + 1, 6)
+        return pool[(u[idx // 5] % np.uint32(6)).astype(np.int64)]
+    if kind == "sorted_repeats":
+        return np.sort(u[idx // 16])
+    if kind == "two_values":
+        return np.where(u & np.uint32(1), np.uint32(0xDEADBEEF), np.uint32(0x0000BEEF)).astype(np.uint32)
+    raise ValueError(kind)
+
+
+@pytest.mark.parametrize("huge", ["0", "1"])
+@pytest.mark.parametrize("kind", ["runs2", "runs7", "runs16", "runs64", "runs100", "recurring",
+                                  "sorted_repeats", "two_values"])
+def test_duplicate_heavy_keys_every_layout(monkeypatch, kind, huge):
+    """Run-counting ranks and counts give the oracle's stable order for duplicate-heavy inputs,
+    on both tile sizes of the one-sweep path (RSORT_HUGE), the histogram path (keys only) and
+    the small-tile path; values are a permutation so stability is checked word for word."""
+    from radix_sort_amd import RadixSortKernel, RadixSortTextureKernel
+    monkeypatch.setenv("RSORT_HUGE", huge)
+    for n in (3_000_017, 13_000_001):
+        keys = _dup_pattern(kind, n, n + len(kind))
+        vals = np.arange(n, dtype=np.uint32)
+        ek, ev = O.stable_sort_masked(keys, vals, 32)
+        kt, vt = _t(keys), _t(vals)
+        k = RadixSortKernel(keys=kt, values=vt, count=n)
+        k.dispatch()
+        assert k.device_errors() == 0
+        assert (_np(kt) == ek).all() and (_np(vt) == ev).all(), (kind, n)
+        k.destroy()
+        kt = _t(keys)
+        k = RadixSortKernel(keys=kt, count=n)
+        k.dispatch()
+        assert (_np(kt) == ek).all(), (kind, n, "keys only")
+        k.destroy()
+        rt = _t(np.stack([keys, vals], axis=-1).reshape(-1)).view(-1, 2)
+        k = RadixSortTextureKernel(texture=rt, count=n)
+        k.dispatch()
+        assert k.device_errors() == 0
+        out = _np(rt).reshape(-1, 2)
+        assert (out[:, 0] == ek).all() and (out[:, 1] == ev).all(), (kind, n, "aos")
+        k.destroy()

@@ -27,9 +27,6 @@
 #ifndef RS_ONESWEEP_TRACE
 #define RS_ONESWEEP_TRACE 0  // 1: printf the stuck tile when a look-back wait times out
 #endif
-#ifndef RS_RANK_GROUP
-#define RS_RANK_GROUP 16     // slots ranked between scheduling fences (see rank_slots)
-#endif
 #ifndef RS_PACK_POS
 #define RS_PACK_POS 1        // 1: staging-round kernels keep tile positions as 16-bit pairs
 #endif
@@ -44,6 +41,9 @@ constexpr int kWaves = kBlock / 64;
 // Pass kernels keep >= 4 waves per SIMD resident (<= 128 VGPRs) at every block size: implied
 // for 1024-thread blocks, and it lets 256 / 512-thread blocks share a CU 4 / 2 ways.
 constexpr int kMinWavesPerSimd = 4;
+// ... except tiles of more than 32 keys per thread, which get the whole register file of one
+// workgroup per CU (BLOCK / 256 waves per SIMD)
+constexpr int pass_min_waves(int block, int kpt) { return kpt > 32 ? block / 256 : kMinWavesPerSimd; }
 
 // Key/value layouts in HBM.  KEYS: keys only.  SOA: separate key and value arrays (the
 // reference's RadixSortBufferKernel buffers).  AOS: one array of 8-byte (key, value) records,
@@ -123,6 +123,18 @@ __device__ __forceinline__ Chunk chunk_of(uint32_t g, uint32_t base, uint32_t ex
     return c;
 }
 
+// Count d in counter row h: one atomic for the wave when every active lane has the same digit
+// (a 64-way same-address conflict otherwise: sorted or few-valued keys), else one per lane.
+__device__ __forceinline__ void count_uniform_or_each(uint32_t* h, uint32_t d) {
+    const uint32_t d0 = __builtin_amdgcn_readfirstlane(d);
+    if (__ballot(d != d0) == 0ull) {
+        const uint64_t act = __ballot(true);
+        if (mbcnt(act) == 0) atomicAdd(&h[d0], (uint32_t)__popcll(act));
+    } else {
+        atomicAdd(&h[d], 1u);
+    }
+}
+
 // ---- histogram (upsweep) -----------------------------------------------------------------
 // counts[d * ntiles + t] = number of keys of tile t whose digit is d.  Every wave histograms
 // whole tiles on its own (wave-private LDS counters: one wave's LDS operations execute in
@@ -145,10 +157,10 @@ __global__ __launch_bounds__(kBlock) void k_histogram(
     uint32_t* h = hist[w];
     const bool vec = (((uintptr_t)keys) & 15u) == 0;
     auto count4 = [&](const uint4& q) {
-        atomicAdd(&h[(q.x >> shift) & mask], 1u);
-        if (KS == 1) atomicAdd(&h[(q.y >> shift) & mask], 1u);
-        atomicAdd(&h[(q.z >> shift) & mask], 1u);
-        if (KS == 1) atomicAdd(&h[(q.w >> shift) & mask], 1u);
+        count_uniform_or_each(h, (q.x >> shift) & mask);
+        if (KS == 1) count_uniform_or_each(h, (q.y >> shift) & mask);
+        count_uniform_or_each(h, (q.z >> shift) & mask);
+        if (KS == 1) count_uniform_or_each(h, (q.w >> shift) & mask);
     };
     for (uint32_t t = blockIdx.x * kWaves + w; t < ntiles; t += nwaves) {
         for (uint32_t d = lane; d < (uint32_t)RADIX; d += 64) h[d] = 0u;
@@ -336,6 +348,80 @@ __device__ __forceinline__ uint64_t match_mask(uint32_t d, uint64_t valid) {
     return ((uint64_t)mhi << 32) | mlo;
 }
 
+// ---- LDS counters under duplicate-heavy keys -------------------------------------------------
+// Lanes of one wave instruction that add to the SAME LDS address are serialised
+// (SQ_LDS_ADDR_CONFLICT): sorted input or runs of equal keys (e.g. 2^28 keys drawn from 2^24
+// values, 16 equal keys in a row) put 16-64 lanes of a slot on one counter, and a pass ran up to
+// 2x slower.  Equal digits of such inputs sit in neighbouring lanes.  Each wave therefore first
+// counts, over its KPT slots, the lanes that start a run of equal digits (neighbour compare by
+// DPP wave_shr:1), and picks for the whole tile: few runs -> one atomic per run, by its first
+// lane, adding the run length (ranks = old + position in the run); otherwise one atomic per lane
+// (the uniform-key path, unchanged).  Both rank a digit's lanes in lane order (stable): the LDS
+// resolves one instruction's same-address atomics in lane order, so runs of one digit get their
+// bases in lane order too.
+#ifndef RS_RUN_HEADS_MAX
+#define RS_RUN_HEADS_MAX 32   // average run heads per slot at or below which a wave counts runs
+#endif
+
+// Lanes that start a run of equal d (lane 0 always does).
+__device__ __forceinline__ uint64_t run_heads(uint32_t d) {
+    const uint32_t dp = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)d, 0x138 /* wave_shr:1 */,
+                                                              0xf, 0xf, false);
+    return __ballot(lane_id() == 0 || d != dp);
+}
+
+// Does this wave's tile have at most RS_RUN_HEADS_MAX run heads per slot on average?  Sampled
+// on every RS_RUN_SAMPLE-th slot (the test runs on every tile of uniform keys too).
+#ifndef RS_RUN_SAMPLE
+#define RS_RUN_SAMPLE 4
+#endif
+template <int KPT>
+__device__ __forceinline__ bool few_runs(const uint32_t (&k)[KPT], uint32_t shift, uint32_t mask) {
+    shift = opaque_u(shift);   // these digits are not kept for the counting loop (registers)
+    uint32_t heads = 0, slots = 0;
+#pragma unroll
+    for (int j = 0; j < KPT; j += RS_RUN_SAMPLE) {
+        heads += (uint32_t)__popcll(run_heads((k[j] >> shift) & mask));
+        ++slots;
+    }
+    return heads <= slots * (uint32_t)RS_RUN_HEADS_MAX;
+}
+
+// Length of the run that head lane `lane` starts.
+__device__ __forceinline__ uint32_t run_length(uint64_t hm, uint32_t lane) {
+    const uint64_t above = lane == 63 ? 0ull : hm & (~0ull << (lane + 1));
+    return (above ? (uint32_t)__builtin_ctzll(above) : 64u) - lane;
+}
+
+// Runs path, one slot: stable rank of this lane's digit d in counter row h.
+__device__ __forceinline__ uint32_t rank_add_runs(uint32_t* h, uint32_t d) {
+    const uint32_t lane = lane_id();
+    const uint64_t hm = run_heads(d);
+    uint32_t old = 0;
+    if ((hm >> lane) & 1ull) old = atomicAdd(&h[d], run_length(hm, lane));
+    const uint64_t le = hm & (lane == 63 ? ~0ull : ((2ull << lane) - 1ull));
+    const uint32_t hl = 63u - (uint32_t)__builtin_clzll(le);     // my run's first lane
+    return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(hl << 2), (int)old) + (lane - hl);
+}
+
+// Counts every slot's digit (k >> shift) & mask in counter row h (whole-array totals).
+template <int KPT>
+__device__ __forceinline__ void count_slots(const uint32_t (&k)[KPT], uint32_t* h, uint32_t shift,
+                                            uint32_t mask) {
+    const uint32_t lane = lane_id();
+    if (few_runs<KPT>(k, shift, mask)) {
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) {
+            const uint32_t d = (k[j] >> shift) & mask;
+            const uint64_t hm = run_heads(d);
+            if ((hm >> lane) & 1ull) atomicAdd(&h[d], run_length(hm, lane));
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) atomicAdd(&h[(k[j] >> shift) & mask], 1u);
+    }
+}
+
 // Stable in-wave ranks of the KPT slots (see RankMode); counters in `whist` (this wave's row).
 // Every slot is ranked (pads included, see kPadKey).
 template <int R, int KPT, int RANK, class RK>
@@ -343,13 +429,20 @@ __device__ __forceinline__ void rank_slots(const uint32_t (&k)[KPT], RK& rank,
                                            uint32_t* whist, uint32_t shift, uint32_t mask) {
     const uint32_t lane = lane_id();
     if (RANK == RANK_LDS_ATOMIC) {
+        if (few_runs<KPT>(k, shift, mask)) {
 #pragma unroll
-        for (int j = 0; j < KPT; ++j) {
-            if (j & 1) rank.set2(j - 1, rank.get(j - 1), atomicAdd(&whist[(k[j] >> shift) & mask], 1u));
-            else rank.set(j, atomicAdd(&whist[(k[j] >> shift) & mask], 1u));
-            // groups of RS_RANK_GROUP slots: the scheduler would otherwise hoist every slot's
-            // LDS address and keep every returned rank live at once (spills at 64 keys/thread)
-            if ((j + 1) % RS_RANK_GROUP == 0) asm volatile("" ::: "memory");
+            for (int j = 0; j < KPT; ++j) {
+                const uint32_t r = rank_add_runs(whist, (k[j] >> shift) & mask);
+                if (j & 1) rank.set2(j - 1, rank.get(j - 1), r);
+                else rank.set(j, r);
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) {
+                const uint32_t r = atomicAdd(&whist[(k[j] >> shift) & mask], 1u);
+                if (j & 1) rank.set2(j - 1, rank.get(j - 1), r);
+                else rank.set(j, r);
+            }
         }
     } else {
         uint32_t info[KPT];
@@ -428,8 +521,8 @@ __device__ __forceinline__ void stage_tile(const uint32_t (&k)[KPT], const uint3
             if (HAS_VALUES) s_kv[s] = make_uint2(k[j], v[j]);
             else s_keys[s] = k[j];
         }
-        if (s_ntot) atomicAdd(&s_ntot[(k[j] >> nshift) & nmask], 1u);
     }
+    if (s_ntot) count_slots<KPT>(k, s_ntot, nshift, nmask);
 }
 
 // Staging round of a tile larger than the LDS staging area: the keys whose tile position
@@ -460,10 +553,7 @@ __device__ __forceinline__ void set_positions(const uint32_t (&k)[KPT], RK& rank
     for (int j = 0; j < KPT; j += 2)
         rank.set2(j, whist_w[(k[j] >> shift) & mask] + rank.get(j),
                   whist_w[(k[j + 1] >> shift) & mask] + rank.get(j + 1));
-    if (s_ntot) {
-#pragma unroll
-        for (int j = 0; j < KPT; ++j) atomicAdd(&s_ntot[(k[j] >> nshift) & nmask], 1u);
-    }
+    if (s_ntot) count_slots<KPT>(k, s_ntot, nshift, nmask);
 }
 
 // Coalesced scatter of the staged tile: consecutive lanes write consecutive positions of a digit
@@ -508,7 +598,7 @@ __device__ __forceinline__ void scatter_tile(const uint32_t* s_keys, const uint2
 // (8r + x) * (G/8) + slot: the workgroups of one XCD scatter ADJACENT tiles at the same time,
 // so each digit's writes from one XCD form one contiguous stream.
 template <int R, int BLOCK, int KPT, int L, int RANK>
-__global__ __launch_bounds__(BLOCK, kMinWavesPerSimd) void k_scatter(
+__global__ __launch_bounds__(BLOCK, pass_min_waves(BLOCK, KPT)) void k_scatter(
     const uint32_t* __restrict__ in_k, const uint32_t* __restrict__ in_v,
     uint32_t* __restrict__ out_k, uint32_t* __restrict__ out_v, uint32_t n, uint32_t shift,
     uint32_t mask, uint32_t ntiles, const uint32_t* __restrict__ counts,
@@ -664,7 +754,7 @@ __device__ __forceinline__ void st_store(unsigned long long* p, uint32_t tag, ui
 // mean fewer 128-B lines shared by two tiles' runs; such a line reaches memory as two partial
 // writes, and those cost as much as a third more than whole lines (tools/line_probe.hip).
 template <int R, int BLOCK, int KPT, int L, int RANK, int LO = L, int SR = 1>
-__global__ __launch_bounds__(BLOCK, SR > 1 ? BLOCK / 256 : kMinWavesPerSimd) void k_onesweep(
+__global__ __launch_bounds__(BLOCK, pass_min_waves(BLOCK, KPT)) void k_onesweep(
     const uint32_t* __restrict__ in_k, const uint32_t* __restrict__ in_v,
     uint32_t* __restrict__ out_k, uint32_t* __restrict__ out_v, uint32_t n, uint32_t shift,
     uint32_t mask, uint32_t ntiles, const uint32_t* __restrict__ dtot,

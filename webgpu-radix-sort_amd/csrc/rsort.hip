@@ -63,7 +63,13 @@ constexpr TileCfg kLarge{1024, 16, 16384, 512};
 constexpr TileCfg kSmall{256, 16, 4096, 1024};
 // keys-only at >= 12M keys: the same 16K-key tile from 512 threads x 32 keys (75 KiB LDS), so
 // two workgroups share a CU and one's waits (look-back, barriers) overlap the other's work
-constexpr TileCfg kLargeKeys{512, 32, 16384, 512};
+#ifndef RS_KEYS_BLOCK
+#define RS_KEYS_BLOCK 512
+#endif
+#ifndef RS_KEYS_KPT
+#define RS_KEYS_KPT 32
+#endif
+constexpr TileCfg kLargeKeys{RS_KEYS_BLOCK, RS_KEYS_KPT, RS_KEYS_BLOCK * RS_KEYS_KPT, 512};
 // one-sweep passes that read a plan-owned records buffer (padded to whole tiles): 24K-record
 // tiles (1024 threads x 24 records, positions packed 16-bit) staged through LDS in two rounds of
 // 12K; longer digit runs per tile than 16K tiles (fewer lines shared by two tiles' runs)
@@ -146,7 +152,7 @@ struct rs_plan {
     bool aos_tmp = true;                   // one-sweep KV: records as the ping-pong copy (RSORT_AOS_TMP)
     uint32_t* tmp2 = nullptr;              // one-sweep KV: second records buffer (RSORT_RECS2=0: none)
     bool keys_cfg = true;                  // keys-only 512x32 tiles (RSORT_KEYS_CFG=0: 1024x16)
-    bool huge_tiles = true;                // one-sweep KV: 32K-key tiles (RSORT_HUGE=0: 16K)
+    bool huge_tiles = false;               // one-sweep KV: 24K-record tiles (RSORT_HUGE=1)
     unsigned long long* status = nullptr;  // [max_tiles][256] look-back status words
     uint64_t status_words = 0;
     uint32_t* ptot = nullptr;      // [kTotalsMax] whole-array digit totals of every pass

@@ -33,6 +33,12 @@
 #ifndef RS_SCATTER_DEBUG
 #define RS_SCATTER_DEBUG 0   // ablation (tools/sweep.py): 1 = linear writes (output pos = input pos)
 #endif
+#ifndef RS_NT_STORE
+#define RS_NT_STORE 0        // 1: pass outputs stored non-temporal (streamed, read back next pass)
+#endif
+#ifndef RS_NT_LOAD
+#define RS_NT_LOAD 0         // 1: pass inputs (full tiles) loaded non-temporal (read once per pass)
+#endif
 
 namespace rs {
 
@@ -53,6 +59,24 @@ enum Layout { LAYOUT_KEYS = 0, LAYOUT_SOA = 1, LAYOUT_AOS = 2 };
 // ---- small helpers ---------------------------------------------------------------------
 
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
+
+// Stream accesses of the pass kernels (cache policy per RS_NT_STORE / RS_NT_LOAD).
+template <class T>
+__device__ __forceinline__ void st_out(T* p, T v) {
+#if RS_NT_STORE
+    __builtin_nontemporal_store(v, p);
+#else
+    *p = v;
+#endif
+}
+template <class T>
+__device__ __forceinline__ T ld_in(const T* p) {
+#if RS_NT_LOAD
+    return __builtin_nontemporal_load(p);
+#else
+    return *p;
+#endif
+}
 
 // Popcount of the bits of m below this lane (v_mbcnt_lo/hi).
 __device__ __forceinline__ uint32_t mbcnt(uint64_t m) {
@@ -295,21 +319,22 @@ __device__ __forceinline__ void load_tile(const uint32_t* __restrict__ in_k,
     // have to be recomputed and widened for every slot: it may wrap)
     const size_t b = (size_t)wbase + lane;
     if (L == LAYOUT_AOS) {
-        const uint2* rec = reinterpret_cast<const uint2*>(in_k) + b;
+        const unsigned long long* rec = reinterpret_cast<const unsigned long long*>(in_k) + b;
 #pragma unroll
         for (int j = 0; j < KPT; ++j) {
-            const uint2 r = (full || b + j * 64 < n) ? rec[j * 64] : make_uint2(kPadKey, 0u);
-            k[j] = r.x;
-            v[j] = r.y;
+            const unsigned long long r = (full || b + j * 64 < n) ? ld_in(rec + j * 64)
+                                                                  : (unsigned long long)kPadKey;
+            k[j] = (uint32_t)r;
+            v[j] = (uint32_t)(r >> 32);
         }
     } else if (full) {
         const uint32_t* pk = in_k + b;
 #pragma unroll
-        for (int j = 0; j < KPT; ++j) k[j] = pk[j * 64];
+        for (int j = 0; j < KPT; ++j) k[j] = ld_in(pk + j * 64);
         if (HAS_VALUES) {
             const uint32_t* pv = in_v + b;
 #pragma unroll
-            for (int j = 0; j < KPT; ++j) v[j] = pv[j * 64];
+            for (int j = 0; j < KPT; ++j) v[j] = ld_in(pv + j * 64);
         }
     } else if (CLAMP) {
         // branch-free: every slot loads (index clamped to n - 1, n >= 1), pads selected after
@@ -583,10 +608,11 @@ __device__ __forceinline__ void scatter_tile(const uint32_t* s_keys, const uint2
 #endif
         if (pos < n) {  // never false for consistent offsets; keeps a bug from faulting
             if (LO == LAYOUT_AOS) {
-                reinterpret_cast<uint2*>(out_k)[pos] = make_uint2(key, val);
+                st_out(reinterpret_cast<unsigned long long*>(out_k) + pos,
+                       (unsigned long long)key | ((unsigned long long)val << 32));
             } else {
-                out_k[pos] = key;
-                if (HAS_VALUES) out_v[pos] = val;
+                st_out(out_k + pos, key);
+                if (HAS_VALUES) st_out(out_v + pos, val);
             }
         }
     }
@@ -676,11 +702,15 @@ struct PassList {
 // out[off(p) + d], off(p) = sum of 2^width[<p] (<= kTotalsMax entries), zeroed by the caller.
 // Wave-private LDS counters; one global atomic per non-zero counter per workgroup.  KS = words
 // per key (2 for AOS records).
+// chk (may be null, check_order): the order check of pass 0's input fused into this read of it,
+// *chk |= 1 if any adjacent pair is out of order under fmask (k_check's job, one read fewer).
 constexpr int kTotalsMax = 1024;
 template <int KS>
 __global__ __launch_bounds__(kBlock) void k_pass_totals(const uint32_t* __restrict__ keys,
                                                         uint32_t n, PassList pl, uint32_t shift0,
-                                                        uint32_t* __restrict__ out) {
+                                                        uint32_t* __restrict__ out,
+                                                        uint32_t* chk = nullptr,
+                                                        uint32_t fmask = 0xFFFFFFFFu) {
     // pass p's digit starts at bit shift0 + sum(width[<p]) (shift0 = 0 for a sort)
     __shared__ uint32_t hist[kWaves][kTotalsMax];
     const uint32_t tid = threadIdx.x, w = tid >> 6;
@@ -704,6 +734,8 @@ __global__ __launch_bounds__(kBlock) void k_pass_totals(const uint32_t* __restri
     const bool vec = (((uintptr_t)keys) & 15u) == 0;
     const uint32_t stride = gridDim.x * kBlock;
     uint32_t i0 = 0;
+    bool bad = false;
+    auto inv = [&](uint32_t a, uint32_t b) { bad |= (a & fmask) > (b & fmask); };
     if (vec) {
         for (uint32_t i = blockIdx.x * kBlock + tid; i < nv; i += stride) {
             const uint4 q = k4[i];
@@ -711,11 +743,30 @@ __global__ __launch_bounds__(kBlock) void k_pass_totals(const uint32_t* __restri
             if (KS == 1) count_key(q.y);
             count_key(q.z);
             if (KS == 1) count_key(q.w);
+            if (chk) {
+                // the vector's last key against its successor: the next lane's first key (a
+                // cache hit), none after key n - 1
+                const uint32_t j = KPV * (i + 1);
+                const uint32_t nx = j < n ? keys[(size_t)j * KS] : 0xFFFFFFFFu;
+                if (KS == 1) {
+                    inv(q.x, q.y);
+                    inv(q.y, q.z);
+                    inv(q.z, q.w);
+                    inv(q.w, nx);
+                } else {
+                    inv(q.x, q.z);
+                    inv(q.z, nx);
+                }
+            }
         }
         i0 = KPV * nv;
     }
-    for (uint32_t i = i0 + blockIdx.x * kBlock + tid; i < n; i += stride)
-        count_key(keys[(size_t)i * KS]);
+    for (uint32_t i = i0 + blockIdx.x * kBlock + tid; i < n; i += stride) {
+        const uint32_t key = keys[(size_t)i * KS];
+        count_key(key);
+        if (chk && i + 1 < n) inv(key, keys[(size_t)(i + 1) * KS]);
+    }
+    if (chk && __ballot(bad) != 0ull && lane_id() == 0) atomicOr(chk, 1u);
     __syncthreads();
     for (uint32_t i = tid; i < total; i += kBlock) {
         uint32_t c = 0;
@@ -749,6 +800,25 @@ __device__ __forceinline__ void st_store(unsigned long long* p, uint32_t tag, ui
                        __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Any adjacent pair of this wave's slot-ordered keys out of order under fmask?  Slot j lane l is
+// position j*64 + l: its successor is lane l+1 (DPP wave_shl:1), or lane 0 of slot j+1, or, after
+// the last slot, `after`.  Pads (kPadKey) mask to the maximum and never form an inversion.
+template <int KPT>
+__device__ __forceinline__ bool wave_inversion(const uint32_t (&k)[KPT], uint32_t after,
+                                               uint32_t fmask) {
+    const bool last = lane_id() == 63;
+    bool bad = false;
+#pragma unroll
+    for (int j = 0; j < KPT; ++j) {
+        const uint32_t nx = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)k[j], 0x130 /* wave_shl:1 */,
+                                                                  0xf, 0xf, false);
+        const uint32_t s0 = (j + 1 < KPT) ? (uint32_t)__builtin_amdgcn_readfirstlane(k[j + 1 < KPT ? j + 1 : j])
+                                          : after;
+        bad |= (k[j] & fmask) > ((last ? s0 : nx) & fmask);
+    }
+    return __ballot(bad) != 0ull;
+}
+
 // SR > 1: the tile is SR times the LDS staging area (32K-key tiles from 1024 threads x 32 keys
 // with values, staged and scattered in two rounds of 16K positions).  Longer digit runs per tile
 // mean fewer 128-B lines shared by two tiles' runs; such a line reaches memory as two partial
@@ -759,9 +829,13 @@ __global__ __launch_bounds__(BLOCK, pass_min_waves(BLOCK, KPT)) void k_onesweep(
     uint32_t* __restrict__ out_k, uint32_t* __restrict__ out_v, uint32_t n, uint32_t shift,
     uint32_t mask, uint32_t ntiles, const uint32_t* __restrict__ dtot,
     unsigned long long* status, uint32_t* ticket, uint32_t* err, uint32_t* __restrict__ ntot,
-    uint32_t nshift, uint32_t nmask, uint32_t epoch, const uint32_t* gate, int pass) {
+    uint32_t nshift, uint32_t nmask, uint32_t epoch, const uint32_t* gate, int pass,
+    uint32_t* chk, uint32_t fmask) {
     // ntot (may be null): whole-array totals of the NEXT pass's digit (key >> nshift) & nmask,
     // counted here from the keys this workgroup stages, so only pass 0 needs k_pass_totals.
+    // chk (may be null, check_order, pass > 0): the order check of this pass's input, fused:
+    // chk[pass] |= 1 if any adjacent pair is out of order under fmask (k_check's job, without
+    // reading the keys again); this pass then gates on the checks of the passes before it only.
     // L / LO: input / output layout (SOA <-> AOS alternate on the separate-values path).
     constexpr bool HAS_VALUES = L != LAYOUT_KEYS;
     static_assert((L == LAYOUT_KEYS) == (LO == LAYOUT_KEYS), "values in and out");
@@ -780,10 +854,12 @@ __global__ __launch_bounds__(BLOCK, pass_min_waves(BLOCK, KPT)) void k_onesweep(
     __shared__ uint32_t s_ntot[256];
     __shared__ uint32_t s_keys[HAS_VALUES ? 1 : STAGE];
     __shared__ uint2 s_kv[HAS_VALUES ? STAGE : 1];
+    __shared__ uint32_t s_inv;
 
-    if (gated_off(gate, pass)) return;
+    if (gated_off(gate, chk ? pass - 1 : pass)) return;
     const uint32_t tid = threadIdx.x, w = tid >> 6;
     for (uint32_t d = tid; d < 256u; d += BLOCK) s_ntot[d] = 0u;
+    if (tid == 0) s_inv = 0u;
     {   // first output position of every digit
         const uint32_t c = (tid < (uint32_t)RADIX && tid <= mask) ? dtot[tid] : 0u;
         uint32_t all;
@@ -816,10 +892,16 @@ __global__ __launch_bounds__(BLOCK, pass_min_waves(BLOCK, KPT)) void k_onesweep(
                 if (wb + j * 64 >= n) k[j] = kPadKey;
         }
         const uint32_t npad = (uint32_t)TILE - nvalid;
+        uint32_t bkey = kPadKey;   // the key after this wave's slots (next wave or next tile)
+        if (chk) {
+            const uint32_t q = tile0 + (w + 1) * (uint32_t)WAVE_KEYS;
+            if (q < n) bkey = in_k[(size_t)q * (L == LAYOUT_AOS ? 2u : 1u)];
+        }
         Slots<KPT, RS_PACK_POS && (SR > 1)> rank;
         uint32_t c;
         const uint32_t tstart = rank_tile<R, NW, KPT, RANK>(k, rank, s_whist, s_scratch, shift,
                                                             mask, npad, c);
+        if (chk && wave_inversion<KPT>(k, bkey, fmask) && lane_id() == 0) s_inv = 1u;
         // Publish this tile's counts first, then do everything that needs only tile-local
         // offsets (staging, next ticket, next-tile prefetch) before walking back: the
         // predecessors get that long to publish their inclusive prefixes, and the prefetch is
@@ -931,6 +1013,7 @@ __global__ __launch_bounds__(BLOCK, pass_min_waves(BLOCK, KPT)) void k_onesweep(
         for (uint32_t d = tid; d <= nmask; d += BLOCK)
             if (s_ntot[d]) atomicAdd(&ntot[d], s_ntot[d]);
     }
+    if (chk && tid == 0 && s_inv) atomicOr(chk + pass, 1u);
 }
 
 // ---- whole sort of a small array in one workgroup ------------------------------------------

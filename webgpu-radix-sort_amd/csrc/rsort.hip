@@ -153,6 +153,8 @@ struct rs_plan {
     uint32_t* tmp2 = nullptr;              // one-sweep KV: second records buffer (RSORT_RECS2=0: none)
     bool keys_cfg = true;                  // keys-only 512x32 tiles (RSORT_KEYS_CFG=0: 1024x16)
     bool huge_tiles = false;               // one-sweep KV: 24K-record tiles (RSORT_HUGE=1)
+    bool fused_check = true;               // one-sweep check_order: passes > 0 check their input
+                                           // in k_onesweep (RSORT_FUSED_CHECK=0: k_check)
     unsigned long long* status = nullptr;  // [max_tiles][256] look-back status words
     uint64_t status_words = 0;
     uint32_t* ptot = nullptr;      // [kTotalsMax] whole-array digit totals of every pass
@@ -173,6 +175,8 @@ struct rs_scan_plan {
 namespace {
 
 uint32_t pick_R(uint32_t w) { return w <= 2 ? 2 : (w <= 4 ? 4 : 8); }
+
+uint32_t full_mask(uint32_t bits) { return bits >= 32 ? 0xFFFFFFFFu : ((1u << bits) - 1u); }
 
 bool use_small_tiles(uint64_t n) {
     if (const char* e = getenv("RSORT_TILE")) return strcmp(e, "small") == 0;
@@ -244,9 +248,12 @@ void launch_onesweep_t(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint3
     uint32_t* ntot = last ? nullptr : p->ptot + p->ptot_off[pass + 1];
     const uint32_t nshift = last ? 0u : shift + p->widths[pass];
     const uint32_t nmask = last ? 0u : (1u << p->widths[pass + 1]) - 1u;
+    // check_order: passes > 0 check their own input (k_check runs before pass 0 only)
+    uint32_t* chk = (gate && pass > 0 && p->fused_check) ? p->flags : nullptr;
     hipLaunchKernelGGL(kern, dim3(grid), dim3(BLOCK), 0, s, ik, iv, ok, ov, n, shift, mask, ntiles,
                        p->ptot + p->ptot_off[pass], p->status, p->tickets + pass,
-                       p->tickets + 16, ntot, nshift, nmask, p->epoch, gate, pass);
+                       p->tickets + 16, ntot, nshift, nmask, p->epoch, gate, pass, chk,
+                       full_mask(p->bit_count));
 }
 
 template <int R, int BLOCK, int KPT, int L, int LO, int SR>
@@ -371,8 +378,6 @@ rs_status run_tiny(rs_plan* p, uint32_t* k, uint32_t* v, uint32_t n, hipStream_t
     return RS_OK;
 }
 
-uint32_t full_mask(uint32_t bits) { return bits >= 32 ? 0xFFFFFFFFu : ((1u << bits) - 1u); }
-
 // One-sweep (k_pass_totals + k_onesweep) or histogram/scan/scatter for this sort.  Measured on
 // MI355X: one-sweep wins with values on large-tile sizes (256M KV: -14 %), loses
 // keys-only (a keys-only tile is processed so fast that the look-back wait shows: +10 % at 64M)
@@ -441,6 +446,7 @@ RS_EXPORT rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out) {
     if (const char* r2 = getenv("RSORT_RECS2")) recs2 = strcmp(r2, "0") != 0;
     if (const char* kc = getenv("RSORT_KEYS_CFG")) p->keys_cfg = strcmp(kc, "0") != 0;
     if (const char* hg = getenv("RSORT_HUGE")) p->huge_tiles = strcmp(hg, "0") != 0;
+    if (const char* fc = getenv("RSORT_FUSED_CHECK")) p->fused_check = strcmp(fc, "0") != 0;
     if (const char* rk = getenv("RSORT_RANK"))
         p->rank_mode = (strcmp(rk, "ballot") == 0) ? rs::RANK_BALLOT : rs::RANK_LDS_ATOMIC;
     // Even number of passes so the result lands in the caller's buffers, like the reference's
@@ -527,11 +533,15 @@ static rs_status enqueue_sort(rs_plan* p, uint32_t* uk, uint32_t* uv, uint64_t n
         pl.count = 1;
         pl.width[0] = p->widths[0];
         const uint32_t grid = (uint32_t)std::min<uint64_t>(8ull * p->cus, (n + 4ull * rs::kBlock - 1) / (4ull * rs::kBlock));
+        // check_order: the check of pass 0's input rides on this read (every later pass's check
+        // on that pass's k_onesweep), so no k_check launch at all
+        uint32_t* chk0 = (p->check_order && p->fused_check) ? p->flags : nullptr;
+        const uint32_t fm = full_mask(p->bit_count);
         p->timer.run(RS_KERNEL_HISTOGRAM, s, [&] {
             if (L == rs::LAYOUT_AOS)
-                hipLaunchKernelGGL(rs::k_pass_totals<2>, dim3(grid), dim3(rs::kBlock), 0, s, uk, n32, pl, 0u, p->ptot);
+                hipLaunchKernelGGL(rs::k_pass_totals<2>, dim3(grid), dim3(rs::kBlock), 0, s, uk, n32, pl, 0u, p->ptot, chk0, fm);
             else
-                hipLaunchKernelGGL(rs::k_pass_totals<1>, dim3(grid), dim3(rs::kBlock), 0, s, uk, n32, pl, 0u, p->ptot);
+                hipLaunchKernelGGL(rs::k_pass_totals<1>, dim3(grid), dim3(rs::kBlock), 0, s, uk, n32, pl, 0u, p->ptot, chk0, fm);
         });
         HIP_TRY(hipGetLastError());
     }
@@ -561,7 +571,7 @@ static rs_status enqueue_sort(rs_plan* p, uint32_t* uk, uint32_t* uv, uint64_t n
             in_layout = A;
             LL = layout_pair(A, A);
         }
-        if (p->check_order) {
+        if (p->check_order && !(onesweep && p->fused_check)) {
             // Order check before every pass (the reference checks every second 2-bit pass,
             // AbstractRadixSortKernel.ts:257-261); all pairs, masked keys (Q1/Q2 fixed).
             const uint32_t grid = (uint32_t)std::min<uint64_t>(kCheckGrid, (n + rs::kBlock - 1) / rs::kBlock);

@@ -9,8 +9,9 @@ A step = one full sort of one batch of synthetic input resident in HBM:
   local_shuffle=true, bit_count 32, one RadixSortKernel.dispatch() per step.  Every step sorts a
   different pre-generated batch (sorting already-sorted data would be a different workload).
 * N > 1 (torch.distributed.run, one process per GPU, RCCL): BASELINE configs[4] shape with
-  2^28 keys+values per rank (2^31 at 8 GPUs): stable top-byte partition -> histogram all_gather
-  -> RCCL all_to_all of keys and values over xGMI -> local LSD sort.  Weak scaling.
+  2^28 keys+values per rank (2^31 at 8 GPUs): histogram all_gather -> stable top-byte partition
+  -> 4 rounds of RCCL all_to_all over xGMI (bucket groups), each group sorted locally (LSD)
+  while the later rounds are in flight.  Weak scaling.
 
 Rank 0 prints ONE JSON line.  `value` = keys sorted by all ranks / max-over-ranks wall time.
 `roofline` is for the dominant kernel (the scatter pass): algorithmic bytes per launch
@@ -254,7 +255,8 @@ def main() -> None:
         keys_per_step = n * world
         scatter_keys = r.n
         extra["recv_keys_rank0"] = r.n
-        extra["partition"] = "top 8 bits, whole-bucket split, 4 chunks pipelined with the exchange"
+        extra["partition"] = ("top 8 bits, whole-bucket split; 4 exchange rounds of bucket groups, "
+                              "each group sorted while the later rounds are on the wire")
         extra["roofline_scope"] = "local sort of the received keys (rank 0)"
 
     value = keys_per_step * K / elapsed / 1e9

@@ -14,7 +14,8 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 import oracle as O
-from radix_sort_amd.distributed import bucket_owners, distributed_sort, exchange_plan, split_sizes
+from radix_sort_amd.distributed import (bucket_groups, bucket_owners, distributed_sort, group_plan,
+                                        split_sizes)
 
 
 class OracleLocalOps:
@@ -128,16 +129,22 @@ def test_bucket_owners_balanced_and_whole():
     assert sum(r0) + sum(r1) == 150 and (sum(r0) == 0 or sum(r1) == 0)
 
 
-def test_exchange_plan_places_segments_in_global_input_order():
-    # world 2, 3 chunks, 4 buckets; rank 1 owns buckets [2, 4)
-    h = [[[1, 2, 3, 4], [0, 0, 5, 0], [2, 2, 2, 2]],
-         [[4, 3, 2, 1], [1, 1, 1, 1], [0, 0, 0, 7]]]
-    bounds = [0, 2, 4]
-    send, recv, off = exchange_plan(h, bounds, 1, 2)
-    assert send == [[7, 3], [2, 2], [0, 7]]                 # rank 1's chunks to ranks 0 / 1
-    assert recv == [[7, 3], [5, 2], [4, 7]]                 # from ranks 0 / 1, per chunk
-    # source-major, then chunk: src0 c0, src0 c1, src0 c2, src1 c0, src1 c1, src1 c2
-    assert off == [[0, 16], [7, 19], [12, 21]]
+def test_group_plan_rounds_are_contiguous_and_source_ordered():
+    # world 2, 4 buckets, 2 rounds: rank 0 owns buckets [0, 2), rank 1 [2, 4)
+    h = [[1, 2, 3, 4], [4, 3, 2, 1]]
+    bounds = bucket_owners(h, 2)
+    assert bounds == [0, 2, 4]
+    cuts = bucket_groups(h, bounds, 2)
+    assert cuts == [[0, 1, 2], [2, 3, 4]]
+    p = group_plan(h, cuts, 1, 2)
+    # rank 1's partitioned slice: bucket 0 at [0, 4), 1 at [4, 7), 2 at [7, 9), 3 at [9, 10)
+    assert p.send == [[(0, 4), (7, 9)], [(4, 7), (9, 10)]]
+    assert p.recv == [[3, 2], [4, 1]]                       # bucket 2, then bucket 3, per source
+    assert p.off == [[0, 3], [5, 9]] and p.base == [0, 5, 10]
+    # more rounds than buckets: empty rounds, still whole buckets in order
+    c3 = bucket_groups(h, bounds, 4)
+    assert all(len(c) == 5 and c == sorted(c) for c in c3)
+    assert c3[0][0] == 0 and c3[0][-1] == 2 and c3[1][0] == 2 and c3[1][-1] == 4
 
 
 @pytest.mark.gpu

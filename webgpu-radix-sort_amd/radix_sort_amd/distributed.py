@@ -3,26 +3,32 @@
 The reference has no multi-device path; this is the build's sharding of the
 same sort for inputs spread over the GPUs of one node (BASELINE config 5):
 
-1. rank r holds a contiguous slice of the global input, cut into C chunks;
-2. the top-``bits`` digit histogram of every chunk (``rs_histogram``, one read of the keys);
-3. ``all_gather`` of the [C][2^bits] histograms (RCCL over xGMI; a few KB) and one copy to the
-   host, where every rank computes the same bucket -> rank assignment on whole-bucket
-   boundaries (equal keys never split) and every send / receive segment's size and place;
-4. per chunk: a stable partition of the chunk by the top digit (one scatter pass of the radix
-   sort, ``rs_plan_partition``) on the compute stream, then an asynchronous all-to-all of its
-   keys and values (RCCL: every rank sends to all peers at once, using all 7 xGMI links of a
-   rank) that runs while the next chunk is partitioned.  Each received segment lands directly
-   at its final place: the receive buffer is ordered by (source rank, chunk), i.e. by global
-   input position;
-5. a local stable LSD sort of the receive buffer is rank r's part of the global stable order.
+1. rank r holds a contiguous slice of the global input;
+2. the top-``bits`` digit histogram of the slice (``rs_histogram``, one read of the keys);
+3. ``all_gather`` of the histograms (RCCL over xGMI; a few KB) and one copy to the host, where
+   every rank computes the same bucket -> rank assignment on whole-bucket boundaries (equal
+   keys never split), and splits every rank's buckets into G consecutive groups of about equal
+   key counts (again whole buckets);
+4. a stable partition of the slice by the top digit (one scatter pass of the radix sort,
+   ``rs_plan_partition``), overlapped with the host's wait for the counts: every (peer, group)
+   send segment is now one contiguous range of buckets;
+5. G exchange rounds, round g an asynchronous all-to-all (RCCL: each rank sends to all peers at
+   once, over all 7 xGMI links of a rank) of every rank's group-g buckets, keys and values.  The
+   receiver lays round g out as [source 0's segment, source 1's, ...] in its group-g region,
+   which is therefore complete once round g lands: it holds every key of those buckets,
+   equal keys in (source rank, input position) order = global input order;
+6. as soon as round g has landed, the group-g region is sorted locally (stable LSD, the same
+   plan), while rounds g+1.. are still on the wire: the local sort hides under the exchange,
+   and only the last group's sort is exposed.  Groups hold increasing buckets, so the regions
+   concatenated are rank r's part of the global stable order.
 
-Stability: ties keep input order because each chunk's partition is stable and segments are
-placed in (source rank, chunk) order, which is global input order; the local sort is stable.
+Stability: the partition is stable, segments are placed in source-rank order, the local sort
+is stable, and a bucket never spans two groups or two ranks.
 
 The local compute is injected (`LocalOps`): the product uses :class:`HipLocalOps` (librsort);
 the CPU gloo tests inject an oracle-backed implementation to exercise the orchestration.  gloo
-has no list all-to-all, so there (and only there) each chunk is exchanged with
-``all_to_all_single`` into a staging buffer and copied into place.
+has no list all-to-all, so there (and only there) a round's send segments are gathered into one
+staging buffer for ``all_to_all_single``.
 """
 from __future__ import annotations
 
@@ -45,6 +51,25 @@ class LocalOps(Protocol):
         """Uninitialised buffer of n 32-bit words on like's device."""
 
 
+def _split_whole(counts, lo: int, hi: int, parts: int):
+    """Cut buckets [lo, hi) into `parts` consecutive runs of whole buckets of ~equal total count.
+    Returns parts + 1 bucket indices (first lo, last hi); part p = [cut[p], cut[p + 1])."""
+    total = sum(int(counts[b]) for b in range(lo, hi))
+    cuts = [lo]
+    cum = 0
+    p = 1
+    for b in range(lo, hi):
+        while p < parts and cum >= (total * p + parts - 1) // parts:
+            cuts.append(b)
+            p += 1
+        cum += int(counts[b])
+    while p < parts:
+        cuts.append(hi)
+        p += 1
+    cuts.append(hi)
+    return cuts
+
+
 def bucket_owners(hist_all, world: int):
     """Whole-bucket split of the global histogram (host, identical on every rank).
 
@@ -53,20 +78,16 @@ def bucket_owners(hist_all, world: int):
     running total reaches q/world of the keys, so each rank gets ~1/world of them."""
     B = len(hist_all[0])
     totals = [sum(int(h[b]) for h in hist_all) for b in range(B)]
-    grand = sum(totals)
-    bounds = [0] * (world + 1)
-    bounds[world] = B
-    cum = 0
-    q = 1
-    for b in range(B):
-        while q < world and cum >= (grand * q + world - 1) // world:
-            bounds[q] = b
-            q += 1
-        cum += totals[b]
-    while q < world:
-        bounds[q] = B
-        q += 1
-    return bounds
+    return _split_whole(totals, 0, B, world)
+
+
+def bucket_groups(hist_all, bounds, groups: int):
+    """Every rank's buckets cut into `groups` exchange rounds: cuts[q] = groups + 1 bucket
+    indices, round g of rank q = buckets [cuts[q][g], cuts[q][g + 1]) (whole buckets, ~equal
+    key counts; empty rounds are allowed)."""
+    B = len(hist_all[0])
+    totals = [sum(int(h[b]) for h in hist_all) for b in range(B)]
+    return [_split_whole(totals, bounds[q], bounds[q + 1], groups) for q in range(len(bounds) - 1)]
 
 
 def split_sizes(hist_all, bounds, rank: int, world: int):
@@ -78,24 +99,39 @@ def split_sizes(hist_all, bounds, rank: int, world: int):
     return send, recv
 
 
-def exchange_plan(hist_chunks, bounds, rank: int, world: int):
-    """Segment sizes and receive offsets for a chunked exchange.
+@dataclass
+class GroupPlan:
+    send: list   # send[g][q] = (begin, end) of the partitioned slice going to peer q in round g
+    recv: list   # recv[g][s] = keys arriving from source s in round g
+    off: list    # off[g][s] = where they land in the receive buffer
+    base: list   # base[g] = start of round g's region; base[G] = total received
 
-    hist_chunks: [world][C][B] top-digit counts.  Returns (send[c][q], recv[c][s], off[c][s])
-    where off[c][s] is where source s's chunk-c segment starts in this rank's receive buffer,
-    ordered by (source, chunk) = global input order."""
-    C = len(hist_chunks[0])
-    lo, hi = bounds[rank], bounds[rank + 1]
-    send = [[sum(int(x) for x in hist_chunks[rank][c][bounds[q]:bounds[q + 1]]) for q in range(world)]
-            for c in range(C)]
-    recv = [[sum(int(x) for x in hist_chunks[s][c][lo:hi]) for s in range(world)] for c in range(C)]
-    off = [[0] * world for _ in range(C)]
-    pos = 0
-    for s in range(world):
-        for c in range(C):
-            off[c][s] = pos
-            pos += recv[c][s]
-    return send, recv, off
+
+def group_plan(hist_all, cuts, rank: int, world: int) -> GroupPlan:
+    """Send ranges, receive sizes and receive offsets of every exchange round.
+
+    hist_all: [world][B] top-digit counts; cuts: bucket_groups().  The partitioned slice holds
+    bucket b at [start[b], start[b + 1]) (start = exclusive scan of this rank's counts), so a
+    round's segment to one peer is one contiguous range.  The receive buffer is round-major,
+    then source-major: round g's region is complete when round g has landed."""
+    mine = [int(x) for x in hist_all[rank]]
+    start = [0]
+    for c in mine:
+        start.append(start[-1] + c)
+    G = len(cuts[0]) - 1
+    send = [[(start[cuts[q][g]], start[cuts[q][g + 1]]) for q in range(world)] for g in range(G)]
+    recv = [[sum(int(x) for x in hist_all[s][cuts[rank][g]:cuts[rank][g + 1]]) for s in range(world)]
+            for g in range(G)]
+    off, base, pos = [], [], 0
+    for g in range(G):
+        base.append(pos)
+        row = []
+        for s in range(world):
+            row.append(pos)
+            pos += recv[g][s]
+        off.append(row)
+    base.append(pos)
+    return GroupPlan(send, recv, off, base)
 
 
 @dataclass
@@ -107,18 +143,14 @@ class ExchangeResult:
     recv_sizes: list
 
 
-def _chunk_bounds(n: int, chunks: int):
-    step = -(-n // chunks) if n else 0
-    return [(min(n, c * step), min(n, (c + 1) * step)) for c in range(chunks)]
-
-
 def distributed_sort(keys, values, ops: LocalOps, group=None, bits: int = 8,
                      chunks: int = 4) -> ExchangeResult:
     """Sort the global array whose slice on this rank is (keys, values); returns this rank's
-    slice of the global stable sorted order (rank-ordered concatenation).
+    slice of the global stable sorted order (rank-ordered concatenation).  `chunks` = exchange
+    rounds (bucket groups per rank), each sorted while the next ones are on the wire.
 
     On the GPU the work runs on a side stream (ordered after the caller's current stream, and
-    the caller's stream after it): the legacy default stream would serialise every partition
+    the caller's stream after it): the legacy default stream would serialise every local sort
     with the in-flight all-to-alls and undo the overlap."""
     import torch
 
@@ -153,62 +185,70 @@ def _distributed_sort(keys, values, ops, group, bits, chunks) -> ExchangeResult:
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     n_local = keys.numel()
-    chunks = max(1, min(chunks, n_local)) if n_local else 1
+    G = max(1, int(chunks))
     shift = 32 - bits
-    cb = _chunk_bounds(n_local, chunks)
-    hist = torch.stack([ops.histogram(keys[a:b], shift, bits) for a, b in cb])   # [C][2^bits]
+    hist = ops.histogram(keys, shift, bits)                     # [2^bits]
     gathered = [torch.empty_like(hist) for _ in range(world)]
     dist.all_gather(gathered, hist, group=group)
     sk = ops.empty(n_local, keys)
     sv = None if values is None else ops.empty(n_local, values)
 
-    def partition(c):
-        a, b = cb[c]
-        ops.partition(keys[a:b], None if values is None else values[a:b], shift, bits,
-                      sk[a:b], None if sv is None else sv[a:b])
+    def partition():
+        if n_local:
+            ops.partition(keys, values, shift, bits, sk, sv)
 
     if keys.is_cuda:
-        # the counts travel to the host while chunk 0 is partitioned (the partition needs no
+        # the counts travel to the host while the slice is partitioned (the partition needs no
         # bucket ownership): copy, mark, enqueue the partition, then wait for the mark only
         hcpu = torch.empty((world,) + tuple(hist.shape), dtype=hist.dtype, pin_memory=True)
         hcpu.copy_(torch.stack(gathered), non_blocking=True)
         ready = torch.cuda.Event()
         ready.record()
-        partition(0)
+        partition()
         ready.synchronize()
         hist_all = hcpu.tolist()
     else:
         hist_all = torch.stack(gathered).tolist()
-        partition(0)
-    bounds = bucket_owners([[sum(h[c][b] for c in range(chunks)) for b in range(1 << bits)]
-                            for h in hist_all], world)
-    send, recv, off = exchange_plan(hist_all, bounds, rank, world)
-    n_recv = sum(sum(r) for r in recv)
+        partition()
+    bounds = bucket_owners(hist_all, world)
+    cuts = bucket_groups(hist_all, bounds, G)
+    plan = group_plan(hist_all, cuts, rank, world)
+    n_recv = plan.base[G]
     rk = ops.empty(n_recv, keys)
     rv = None if values is None else ops.empty(n_recv, values)
     list_a2a = dist.get_backend(group) != "gloo"
-    works = []
-    for c, (a, b) in enumerate(cb):
-        if c:
-            partition(c)
+    rounds = []
+    for g in range(G):
+        works = []
         for src, dst in ((sk, rk), (sv, rv)):
             if src is None:
                 continue
-            ins = list(src[a:b].split(send[c]))
-            outs = [dst[off[c][s]:off[c][s] + recv[c][s]] for s in range(world)]
+            ins = [src[a:b] for a, b in plan.send[g]]
+            region = dst[plan.base[g]:plan.base[g + 1]]
             if list_a2a:
-                works.append(dist.all_to_all(outs, ins, group=group, async_op=True))
+                outs = [dst[plan.off[g][s]:plan.off[g][s] + plan.recv[g][s]] for s in range(world)]
+                # this rank's own segment is a local device copy (RCCL moves a self segment
+                # through a few channels at ~0.3 TB/s: 0.8 ms per 256 MiB, measured)
+                outs[rank].copy_(ins[rank])
+                if world > 1:
+                    ins[rank], outs[rank] = ins[rank][:0], outs[rank][:0]
+                    works.append(dist.all_to_all(outs, ins, group=group, async_op=True))
             else:
-                stage = ops.empty(sum(recv[c]), dst)
-                dist.all_to_all_single(stage, src[a:b], output_split_sizes=recv[c],
-                                       input_split_sizes=send[c], group=group)
-                for s, o in enumerate(outs):
-                    o.copy_(stage[sum(recv[c][:s]):sum(recv[c][:s + 1])])
-    for w in works:
-        w.wait()
-    ops.sort(rk, rv, n_recv)
-    return ExchangeResult(rk, rv, n_recv, [sum(send[c][q] for c in range(chunks)) for q in range(world)],
-                          [sum(recv[c][s] for c in range(chunks)) for s in range(world)])
+                dist.all_to_all_single(region, torch.cat(ins), output_split_sizes=plan.recv[g],
+                                       input_split_sizes=[b - a for a, b in plan.send[g]],
+                                       group=group)
+        rounds.append(works)
+    # round g's local sort waits for round g only (the stream waits, not the host); later rounds
+    # keep moving on RCCL's stream meanwhile
+    for g in range(G):
+        for w in rounds[g]:
+            w.wait()
+        a, b = plan.base[g], plan.base[g + 1]
+        if b > a:
+            ops.sort(rk[a:b], None if rv is None else rv[a:b], b - a)
+    return ExchangeResult(rk, rv, n_recv,
+                          [sum(b - a for a, b in (plan.send[g][q] for g in range(G))) for q in range(world)],
+                          [sum(plan.recv[g][s] for g in range(G)) for s in range(world)])
 
 
 class HipLocalOps:

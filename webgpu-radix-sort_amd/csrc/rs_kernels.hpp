@@ -705,18 +705,28 @@ struct PassList {
 // chk (may be null, check_order): the order check of pass 0's input fused into this read of it,
 // *chk |= 1 if any adjacent pair is out of order under fmask (k_check's job, one read fewer).
 constexpr int kTotalsMax = 1024;
-template <int KS>
-__global__ __launch_bounds__(kBlock) void k_pass_totals(const uint32_t* __restrict__ keys,
-                                                        uint32_t n, PassList pl, uint32_t shift0,
-                                                        uint32_t* __restrict__ out,
-                                                        uint32_t* chk = nullptr,
-                                                        uint32_t fmask = 0xFFFFFFFFu) {
+#ifndef RS_TOT_BLOCK
+#define RS_TOT_BLOCK 256     // k_pass_totals threads per workgroup
+#endif
+#ifndef RS_TOT_PER_CU
+#define RS_TOT_PER_CU 8      // k_pass_totals workgroups per CU
+#endif
+#ifndef RS_TOT_U
+#define RS_TOT_U 1           // k_pass_totals 16-byte loads per lane issued together
+#endif
+template <int KS, int BLOCK = RS_TOT_BLOCK>
+__global__ __launch_bounds__(BLOCK) void k_pass_totals(const uint32_t* __restrict__ keys,
+                                                       uint32_t n, PassList pl, uint32_t shift0,
+                                                       uint32_t* __restrict__ out,
+                                                       uint32_t* chk = nullptr,
+                                                       uint32_t fmask = 0xFFFFFFFFu) {
     // pass p's digit starts at bit shift0 + sum(width[<p]) (shift0 = 0 for a sort)
-    __shared__ uint32_t hist[kWaves][kTotalsMax];
+    constexpr int NWT = BLOCK / 64;
+    __shared__ uint32_t hist[NWT][kTotalsMax];
     const uint32_t tid = threadIdx.x, w = tid >> 6;
     uint32_t total = 0;
     for (uint32_t p = 0; p < pl.count; ++p) total += 1u << pl.width[p];
-    for (uint32_t i = tid; i < (uint32_t)(kWaves * kTotalsMax); i += kBlock) (&hist[0][0])[i] = 0u;
+    for (uint32_t i = tid; i < (uint32_t)(NWT * kTotalsMax); i += BLOCK) (&hist[0][0])[i] = 0u;
     __syncthreads();
     uint32_t* h = hist[w];
     auto count_key = [&](uint32_t key) {
@@ -732,46 +742,62 @@ __global__ __launch_bounds__(kBlock) void k_pass_totals(const uint32_t* __restri
     const uint32_t nv = n / KPV;
     const uint4* k4 = reinterpret_cast<const uint4*>(keys);
     const bool vec = (((uintptr_t)keys) & 15u) == 0;
-    const uint32_t stride = gridDim.x * kBlock;
+    const uint32_t stride = gridDim.x * BLOCK;
     uint32_t i0 = 0;
     bool bad = false;
     auto inv = [&](uint32_t a, uint32_t b) { bad |= (a & fmask) > (b & fmask); };
-    if (vec) {
-        for (uint32_t i = blockIdx.x * kBlock + tid; i < nv; i += stride) {
-            const uint4 q = k4[i];
-            count_key(q.x);
-            if (KS == 1) count_key(q.y);
-            count_key(q.z);
-            if (KS == 1) count_key(q.w);
-            if (chk) {
-                // the vector's last key against its successor: the next lane's first key (a
-                // cache hit), none after key n - 1
+    // vector i's keys, and (check) its last key against its successor: the first key of vector
+    // i + 1, held by the next lane when the whole wave runs this iteration (DPP wave_shl:1),
+    // else loaded; none after key n - 1
+    auto vec4 = [&](uint32_t i, const uint4& q) {
+        count_key(q.x);
+        if (KS == 1) count_key(q.y);
+        count_key(q.z);
+        if (KS == 1) count_key(q.w);
+        if (chk) {
+            const uint32_t nl = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)q.x, 0x130 /* wave_shl:1 */,
+                                                                      0xf, 0xf, false);
+            uint32_t nx = nl;
+            if (!(__ballot(true) == ~0ull && lane_id() != 63)) {
                 const uint32_t j = KPV * (i + 1);
-                const uint32_t nx = j < n ? keys[(size_t)j * KS] : 0xFFFFFFFFu;
-                if (KS == 1) {
-                    inv(q.x, q.y);
-                    inv(q.y, q.z);
-                    inv(q.z, q.w);
-                    inv(q.w, nx);
-                } else {
-                    inv(q.x, q.z);
-                    inv(q.z, nx);
-                }
+                nx = j < n ? keys[(size_t)j * KS] : 0xFFFFFFFFu;
+            }
+            if (KS == 1) {
+                inv(q.x, q.y);
+                inv(q.y, q.z);
+                inv(q.z, q.w);
+                inv(q.w, nx);
+            } else {
+                inv(q.x, q.z);
+                inv(q.z, nx);
             }
         }
+    };
+    if (vec) {
+        // kTotU 16-byte loads per lane in flight, then their counts
+        constexpr int kTotU = RS_TOT_U;
+        uint32_t i = blockIdx.x * BLOCK + tid;
+        for (; (uint64_t)i + (kTotU - 1) * (uint64_t)stride < nv; i += kTotU * stride) {
+            uint4 q[kTotU];
+#pragma unroll
+            for (int u = 0; u < kTotU; ++u) q[u] = k4[i + u * stride];
+#pragma unroll
+            for (int u = 0; u < kTotU; ++u) vec4(i + u * stride, q[u]);
+        }
+        for (; i < nv; i += stride) vec4(i, k4[i]);
         i0 = KPV * nv;
     }
-    for (uint32_t i = i0 + blockIdx.x * kBlock + tid; i < n; i += stride) {
+    for (uint32_t i = i0 + blockIdx.x * BLOCK + tid; i < n; i += stride) {
         const uint32_t key = keys[(size_t)i * KS];
         count_key(key);
         if (chk && i + 1 < n) inv(key, keys[(size_t)(i + 1) * KS]);
     }
     if (chk && __ballot(bad) != 0ull && lane_id() == 0) atomicOr(chk, 1u);
     __syncthreads();
-    for (uint32_t i = tid; i < total; i += kBlock) {
+    for (uint32_t i = tid; i < total; i += BLOCK) {
         uint32_t c = 0;
 #pragma unroll
-        for (int q = 0; q < kWaves; ++q) c += hist[q][i];
+        for (int q = 0; q < NWT; ++q) c += hist[q][i];
         if (c) atomicAdd(&out[i], c);
     }
 }

@@ -532,16 +532,17 @@ static rs_status enqueue_sort(rs_plan* p, uint32_t* uk, uint32_t* uv, uint64_t n
         rs::PassList pl{};
         pl.count = 1;
         pl.width[0] = p->widths[0];
-        const uint32_t grid = (uint32_t)std::min<uint64_t>(8ull * p->cus, (n + 4ull * rs::kBlock - 1) / (4ull * rs::kBlock));
+        const uint32_t grid = (uint32_t)std::min<uint64_t>((uint64_t)RS_TOT_PER_CU * p->cus,
+                                                           (n + 4ull * RS_TOT_BLOCK - 1) / (4ull * RS_TOT_BLOCK));
         // check_order: the check of pass 0's input rides on this read (every later pass's check
         // on that pass's k_onesweep), so no k_check launch at all
         uint32_t* chk0 = (p->check_order && p->fused_check) ? p->flags : nullptr;
         const uint32_t fm = full_mask(p->bit_count);
         p->timer.run(RS_KERNEL_HISTOGRAM, s, [&] {
             if (L == rs::LAYOUT_AOS)
-                hipLaunchKernelGGL(rs::k_pass_totals<2>, dim3(grid), dim3(rs::kBlock), 0, s, uk, n32, pl, 0u, p->ptot, chk0, fm);
+                hipLaunchKernelGGL(rs::k_pass_totals<2>, dim3(grid), dim3(RS_TOT_BLOCK), 0, s, uk, n32, pl, 0u, p->ptot, chk0, fm);
             else
-                hipLaunchKernelGGL(rs::k_pass_totals<1>, dim3(grid), dim3(rs::kBlock), 0, s, uk, n32, pl, 0u, p->ptot, chk0, fm);
+                hipLaunchKernelGGL(rs::k_pass_totals<1>, dim3(grid), dim3(RS_TOT_BLOCK), 0, s, uk, n32, pl, 0u, p->ptot, chk0, fm);
         });
         HIP_TRY(hipGetLastError());
     }
@@ -893,7 +894,7 @@ RS_EXPORT rs_status rs_histogram(const void* keys, uint64_t n, uint32_t shift, u
     pl.count = 1;
     pl.width[0] = bits;
     const uint32_t grid = (uint32_t)std::min<uint64_t>(2048, (n + 4ull * rs::kBlock - 1) / (4ull * rs::kBlock));
-    hipLaunchKernelGGL(rs::k_pass_totals<1>, dim3(grid), dim3(rs::kBlock), 0, s, (const uint32_t*)keys,
+    hipLaunchKernelGGL((rs::k_pass_totals<1, rs::kBlock>), dim3(grid), dim3(rs::kBlock), 0, s, (const uint32_t*)keys,
                        (uint32_t)n, pl, shift, (uint32_t*)d_hist);
     HIP_TRY(hipGetLastError());
     return RS_OK;

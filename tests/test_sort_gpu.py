@@ -328,8 +328,9 @@ def test_onesweep_and_three_kernel_paths(monkeypatch, onesweep, tile):
 def test_onesweep_check_order_exits_and_narrow_digits(monkeypatch, tile):
     """One-sweep path: check_order early exits (an exit after pass 0 or 1 leaves the data as
     (key, value) records in one of the two records buffers: k_finalize<SOA, AOS>), and 2-/4-bit
-    digits."""
-    from radix_sort_amd import RadixSortKernel
+    digits.  The order checks are fused into k_pass_totals / k_onesweep here, on all three
+    layouts."""
+    from radix_sort_amd import RadixSortKernel, RadixSortTextureKernel
     monkeypatch.setenv("RSORT_ONESWEEP", "1")
     monkeypatch.setenv("RSORT_TILE", tile)
     n = 1_500_001
@@ -345,6 +346,33 @@ def test_onesweep_check_order_exits_and_narrow_digits(monkeypatch, tile):
         k.dispatch()
         assert k.device_errors() == 0
         assert (_np(kt) == ek).all() and (_np(vt) == ev).all(), kind
+        k.destroy()
+        # the fused checks on the other two layouts (keys only; (key, value) records, where the
+        # key after a wave's last slot is word 2q of the records)
+        kt = _t(keys)
+        k = RadixSortKernel(keys=kt, count=n, check_order=True)
+        k.dispatch()
+        assert k.device_errors() == 0
+        assert (_np(kt) == ek).all(), (kind, "keys only")
+        k.destroy()
+        rt = _t(np.stack([keys, vals], axis=-1).reshape(-1)).view(-1, 2)
+        k = RadixSortTextureKernel(texture=rt, count=n, check_order=True)
+        k.dispatch()
+        assert k.device_errors() == 0
+        out = _np(rt).reshape(-1, 2)
+        assert (out[:, 0] == ek).all() and (out[:, 1] == ev).all(), (kind, "records")
+        k.destroy()
+    # an inversion only at the very last pair (the reference's unchecked pair, Q1), only across
+    # a wave boundary inside a tile, only across a tile boundary: all must still be sorted
+    for pos in (n - 2, 16384 * 3 + 1023, 16384 * 2 - 1):
+        keys = np.sort(u)
+        keys[pos], keys[pos + 1] = keys[pos + 1], keys[pos]
+        ek, ev = O.stable_sort_masked(keys, vals, 32)
+        kt, vt = _t(keys), _t(vals)
+        k = RadixSortKernel(keys=kt, values=vt, count=n, check_order=True)
+        k.dispatch()
+        assert k.device_errors() == 0
+        assert (_np(kt) == ek).all() and (_np(vt) == ev).all(), pos
         k.destroy()
     for radix_bits, bits in ((2, 12), (4, 16), (4, 32)):
         keys = u & np.uint32((1 << bits) - 1 if bits < 32 else 0xFFFFFFFF)

@@ -24,6 +24,9 @@
 #ifndef RS_XCD_GROUP
 #define RS_XCD_GROUP 1       // consecutive tiles run on one XCD in the same round (speed only)
 #endif
+#ifndef RS_HIST_XCD
+#define RS_HIST_XCD 1        // k_histogram: adjacent tiles' counts written from one XCD (speed only)
+#endif
 #ifndef RS_ONESWEEP_TRACE
 #define RS_ONESWEEP_TRACE 0  // 1: printf the stuck tile when a look-back wait times out
 #endif
@@ -186,7 +189,12 @@ __global__ __launch_bounds__(kBlock) void k_histogram(
         count_uniform_or_each(h, (q.z >> shift) & mask);
         if (KS == 1) count_uniform_or_each(h, (q.w >> shift) & mask);
     };
-    for (uint32_t t = blockIdx.x * kWaves + w; t < ntiles; t += nwaves) {
+    // XCD grouping (speed only): workgroups are dealt round-robin over the 8 XCDs, so the
+    // workgroups of one XCD take adjacent tile groups and a 128-B line of a digit's counts row
+    // (32 tiles) is written from one L2 (from 8 XCDs it reaches memory as 8 partial writes)
+    const uint32_t G = gridDim.x, g = blockIdx.x;
+    const uint32_t gx = (RS_HIST_XCD && (G % 8u) == 0u) ? (g & 7u) * (G >> 3) + (g >> 3) : g;
+    for (uint32_t t = gx * kWaves + w; t < ntiles; t += nwaves) {
         for (uint32_t d = lane; d < (uint32_t)RADIX; d += 64) h[d] = 0u;
         const uint32_t lo = t * (uint32_t)TILE;
         if (vec && (uint64_t)lo + TILE <= n) {

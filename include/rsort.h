@@ -107,6 +107,13 @@ rs_status rs_plan_sort_n(rs_plan* plan, void* keys, void* values, uint64_t n, vo
 rs_status rs_plan_partition(rs_plan* plan, const void* in_keys, const void* in_values,
                             void* out_keys, void* out_values, uint64_t n, uint32_t shift,
                             uint32_t bits, void* d_hist, void* stream);
+/* rs_plan_partition given the digit totals of in[0..n) (device, 2^bits u32, e.g. from
+ * rs_histogram): where the one-sweep scatter wins (values, n >= 12M) the pass then reads the keys
+ * once instead of twice (no per-tile histogram, decoupled look-back); otherwise the same as
+ * rs_plan_partition.  Multi-GPU partition step (the histogram is exchanged anyway). */
+rs_status rs_plan_partition_totals(rs_plan* plan, const void* in_keys, const void* in_values,
+                                   void* out_keys, void* out_values, uint64_t n, uint32_t shift,
+                                   uint32_t bits, const void* d_totals, void* stream);
 rs_status rs_plan_info_get(const rs_plan* plan, rs_plan_info* info);
 /* Kernel timing: when enabled, every launch of the plan is bracketed by HIP events on the
  * launch stream and per-kind durations are accumulated (read after synchronising). */

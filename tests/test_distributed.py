@@ -29,7 +29,7 @@ class OracleLocalOps:
         top = (k >> np.uint32(shift)) & np.uint32((1 << bits) - 1)
         return torch.from_numpy(np.bincount(top, minlength=1 << bits).astype(np.int32))
 
-    def partition(self, keys, values, shift, bits, out_keys=None, out_values=None):
+    def partition(self, keys, values, shift, bits, out_keys=None, out_values=None, totals=None):
         k = keys.numpy().view(np.uint32)
         top = (k >> np.uint32(shift)) & np.uint32((1 << bits) - 1)
         perm = np.argsort(top, kind="stable")

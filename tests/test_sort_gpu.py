@@ -182,6 +182,25 @@ def test_partition_pass_and_histogram():
     assert (_np(hist) == np.bincount(top, minlength=256)).all()
 
 
+@pytest.mark.parametrize("n", [1_000_003, 13_000_001])
+def test_partition_given_totals(n):
+    """rs_plan_partition_totals: the one-sweep partition (values, n >= 12M) fed the digit totals
+    from rs_histogram, and its fallback below that size, give the stable partition."""
+    from radix_sort_amd import ops
+    keys = O.gen_u32(n + 5, n)
+    kt, vt = _t(keys), torch.arange(n, dtype=torch.int32, device=DEV)
+    ok, ov = torch.empty_like(kt), torch.empty_like(vt)
+    hist = torch.empty(256, dtype=torch.int32, device=DEV)
+    ops.histogram(kt, n, 24, 8, hist)
+    plan = ops.SortPlan(0, n, has_values=True)
+    plan.partition_totals(kt, vt, ok, ov, n, 24, 8, hist)
+    torch.cuda.synchronize()
+    top = keys >> np.uint32(24)
+    perm = np.argsort(top, kind="stable")
+    assert (_np(ok) == keys[perm]).all() and (_np(ov) == perm.astype(np.uint32)).all()
+    plan.destroy()
+
+
 def test_kernel_profiling_counts_launches():
     from radix_sort_amd import RadixSortKernel, ops
     n = 1 << 22

@@ -659,6 +659,33 @@ RS_EXPORT rs_status rs_plan_partition(rs_plan* p, const void* in_keys, const voi
     return RS_OK;
 }
 
+RS_EXPORT rs_status rs_plan_partition_totals(rs_plan* p, const void* in_keys, const void* in_values,
+                                             void* out_keys, void* out_values, uint64_t n,
+                                             uint32_t shift, uint32_t bits, const void* d_totals,
+                                             void* stream) {
+    if (!p) return fail(RS_ERR_INVALID_ARG, "rs_plan_partition_totals: null plan");
+    if (!d_totals) return fail(RS_ERR_INVALID_ARG, "rs_plan_partition_totals: null totals");
+    const bool soa = p->layout == rs::LAYOUT_SOA && in_values && out_values;
+    // the one-sweep pass where it wins (with values, large tiles); elsewhere the
+    // histogram / scan / scatter pass, which counts for itself
+    if (n > p->capacity || bits == 0 || bits > 8 || shift + bits > 32 || n == 0 ||
+        !(soa || p->layout == rs::LAYOUT_AOS) || !use_onesweep(p, n))
+        return rs_plan_partition(p, in_keys, in_values, out_keys, out_values, n, shift, bits,
+                                 nullptr, stream);
+    if (!in_keys || !out_keys) return fail(RS_ERR_INVALID_ARG, "rs_plan_partition_totals: null keys");
+    DeviceGuard guard(p->desc.device);
+    hipStream_t s = (hipStream_t)stream;
+    // run as the plan's last pass: no next-pass totals, its own ticket and totals slot
+    const int pass = (int)p->passes - 1;
+    HIP_TRY(hipMemsetAsync(p->tickets + pass, 0, 4, s));
+    HIP_TRY(hipMemcpyAsync(p->ptot + p->ptot_off[pass], d_totals, 4u << bits,
+                           hipMemcpyDeviceToDevice, s));
+    const int L = p->layout;
+    return run_pass(p, (const uint32_t*)in_keys, (const uint32_t*)in_values, (uint32_t*)out_keys,
+                    (uint32_t*)out_values, (uint32_t)n, shift, bits, layout_pair(L, L), nullptr,
+                    pass, s, /*onesweep=*/true);
+}
+
 RS_EXPORT rs_status rs_plan_device_errors(rs_plan* p, uint32_t* errors) {
     if (!p || !errors) return fail(RS_ERR_INVALID_ARG, "rs_plan_device_errors: null argument");
     DeviceGuard guard(p->desc.device);

@@ -10,8 +10,9 @@ same sort for inputs spread over the GPUs of one node (BASELINE config 5):
    keys never split), and splits every rank's buckets into G consecutive groups of about equal
    key counts (again whole buckets);
 4. a stable partition of the slice by the top digit (one scatter pass of the radix sort,
-   ``rs_plan_partition``), overlapped with the host's wait for the counts: every (peer, group)
-   send segment is now one contiguous range of buckets;
+   ``rs_plan_partition_totals``: given the step-2 counts it is the one-sweep pass, one key read),
+   overlapped with the host's wait for the counts: every (peer, group) send segment is now one
+   contiguous range of buckets;
 5. G exchange rounds, round g an asynchronous all-to-all (RCCL: each rank sends to all peers at
    once, over all 7 xGMI links of a rank) of every rank's group-g buckets, keys and values.  The
    receiver lays round g out as [source 0's segment, source 1's, ...] in its group-g region,
@@ -40,9 +41,11 @@ class LocalOps(Protocol):
     def histogram(self, keys, shift: int, bits: int):
         """-> hist[2^bits] int32 tensor on the keys' device (top-digit counts of keys)."""
 
-    def partition(self, keys, values, shift: int, bits: int, out_keys=None, out_values=None):
+    def partition(self, keys, values, shift: int, bits: int, out_keys=None, out_values=None,
+                  totals=None):
         """Stable partition by (key >> shift) & (2^bits - 1) -> (keys_out, values_out); written
-        into out_keys / out_values when given."""
+        into out_keys / out_values when given.  totals (optional): histogram() of the same keys,
+        which lets the pass skip its own digit count."""
 
     def sort(self, keys, values, n: int) -> None:
         """Stable in-place sort of keys[:n] (and values[:n]) by the full 32-bit key."""
@@ -195,7 +198,7 @@ def _distributed_sort(keys, values, ops, group, bits, chunks) -> ExchangeResult:
 
     def partition():
         if n_local:
-            ops.partition(keys, values, shift, bits, sk, sv)
+            ops.partition(keys, values, shift, bits, sk, sv, totals=hist)
 
     if keys.is_cuda:
         # the counts travel to the host while the slice is partitioned (the partition needs no
@@ -274,7 +277,8 @@ class HipLocalOps:
         histogram(keys, keys.numel(), shift, bits, h)
         return h
 
-    def partition(self, keys, values, shift: int, bits: int, out_keys=None, out_values=None):
+    def partition(self, keys, values, shift: int, bits: int, out_keys=None, out_values=None,
+                  totals=None):
         import torch
         n = keys.numel()
         sk = torch.empty_like(keys) if out_keys is None else out_keys
@@ -284,7 +288,10 @@ class HipLocalOps:
             if self.part_plan is not None:
                 self.part_plan.destroy()
             self.part_plan = SortPlan(self.device, max(n, 1), self.has_values, 32, self.radix_bits)
-        self.part_plan.partition(keys, values, sk, sv, n, shift, bits, None)
+        if totals is not None:
+            self.part_plan.partition_totals(keys, values, sk, sv, n, shift, bits, totals)
+        else:
+            self.part_plan.partition(keys, values, sk, sv, n, shift, bits, None)
         return sk, sv
 
     def destroy(self) -> None:

@@ -72,6 +72,15 @@ class SortPlan:
             bits, None if hist is None else hist.data_ptr(), _stream(in_keys, stream)),
             "rs_plan_partition")
 
+    def partition_totals(self, in_keys, in_values, out_keys, out_values, n: int, shift: int,
+                         bits: int, totals, stream=None) -> None:
+        """partition() given the digit totals of the input (device u32[2^bits], e.g. from
+        histogram()): one key read fewer where the one-sweep scatter applies."""
+        check(_lib.load().rs_plan_partition_totals(
+            self._plan, in_keys.data_ptr(), None if in_values is None else in_values.data_ptr(),
+            out_keys.data_ptr(), None if out_values is None else out_values.data_ptr(), n, shift,
+            bits, totals.data_ptr(), _stream(in_keys, stream)), "rs_plan_partition_totals")
+
     def destroy(self) -> None:
         if getattr(self, "_plan", None):
             _lib.load().rs_plan_destroy(self._plan)

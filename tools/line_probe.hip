@@ -17,6 +17,8 @@
 //           line completed with the previous tile's tail records (read from a side buffer of
 //           16-record slots) and its body lines, and leaves its own tail records in its side slot
 //           (the traffic of a tail-carrying scatter, without its synchronisation)
+//   mode 7: as 2, but the shift is a multiple of 4 records: runs start on 32-B sectors, not on
+//           128-B lines (is the cost per partial line or per partial 32-B sector?)
 // Build: hipcc -O3 --offload-arch=gfx950 -o tools/line_probe tools/line_probe.hip
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -66,7 +68,8 @@ __global__ __launch_bounds__(1024) void copy_runs(const uint2* __restrict__ src,
                 continue;
             }
             if (MODE == 0) pos = (size_t)t * 16384 + i;
-            else pos = ((size_t)d * ntiles + t) * RL + o + ((MODE == 2 || MODE == 3) ? ((d * 7u) & 15u) : 0u);
+            else pos = ((size_t)d * ntiles + t) * RL + o + ((MODE == 2 || MODE == 3) ? ((d * 7u) & 15u)
+                                                            : MODE == 7 ? ((d * 7u) & 12u) : 0u);
             dst[pos] = r[j];
         }
     }
@@ -104,11 +107,13 @@ int main() {
         const float t4 = run<4>(s, d, ntiles, grid);
         const float t5 = run<5>(s, d, ntiles, grid);
         const float t6 = run<6>(s, d, ntiles, grid);
-        const char* names[7] = {"linear", "runs_line_aligned", "runs_shifted",
+        const float t7 = run<7>(s, d, ntiles, grid);
+        const char* names[8] = {"linear", "runs_line_aligned", "runs_shifted",
                                 "runs_shifted_xcd_adjacent", "runs_line_aligned_xcd_adjacent",
-                                "runs_shifted_aligned_stores", "runs_shifted_tail_carry"};
-        const float ts[7] = {t0, t1, t2, t3, t4, t5, t6};
-        for (int m = 0; m < 7; ++m)
+                                "runs_shifted_aligned_stores", "runs_shifted_tail_carry",
+                                "runs_sector_aligned"};
+        const float ts[8] = {t0, t1, t2, t3, t4, t5, t6, t7};
+        for (int m = 0; m < 8; ++m)
             printf("{\"probe\": \"line_probe\", \"mode\": \"%s\", \"grid\": %d, \"ms\": %.4f, \"rw_GBs\": %.1f}\n",
                    names[m], grid, ts[m], 2.0 * n * 8 / (ts[m] * 1e-3) / 1e9);
     }

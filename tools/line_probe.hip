@@ -17,8 +17,12 @@
 //           line completed with the previous tile's tail records (read from a side buffer of
 //           16-record slots) and its body lines, and leaves its own tail records in its side slot
 //           (the traffic of a tail-carrying scatter, without its synchronisation)
-//   mode 7: as 2, but the shift is a multiple of 4 records: runs start on 32-B sectors, not on
+//   mode 7: as 3, but the shift is a multiple of 4 records: runs start on 32-B sectors, not on
 //           128-B lines (is the cost per partial line or per partial 32-B sector?)
+//   mode 8: as 1, but the last 4 records of every run are not written: each run's last line is
+//           partial and nobody else writes it (does a partial line cost without a second writer?)
+//   mode 9: as 0 shifted by 8 records: every 4th line is written half by one wave, half by the
+//           next wave of the same workgroup (does a line split inside a workgroup cost?)
 // Build: hipcc -O3 --offload-arch=gfx950 -o tools/line_probe tools/line_probe.hip
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -31,7 +35,7 @@ __global__ __launch_bounds__(1024) void copy_runs(const uint2* __restrict__ src,
                                                   uint2* __restrict__ dst, uint32_t ntiles,
                                                   uint2* __restrict__ side) {
     const uint32_t G = gridDim.x, b = blockIdx.x;
-    const uint32_t first = MODE >= 3 ? (b & 7u) * (G >> 3) + (b >> 3) : b;
+    const uint32_t first = (MODE >= 3 && MODE <= 7) ? (b & 7u) * (G >> 3) + (b >> 3) : b;
     for (uint32_t t = first; t < ntiles; t += G) {
         uint2 r[16];
 #pragma unroll
@@ -68,8 +72,10 @@ __global__ __launch_bounds__(1024) void copy_runs(const uint2* __restrict__ src,
                 continue;
             }
             if (MODE == 0) pos = (size_t)t * 16384 + i;
+            else if (MODE == 9) pos = (size_t)t * 16384 + i + 8;   // linear, lines split between waves
             else pos = ((size_t)d * ntiles + t) * RL + o + ((MODE == 2 || MODE == 3) ? ((d * 7u) & 15u)
                                                             : MODE == 7 ? ((d * 7u) & 12u) : 0u);
+            if (MODE == 8 && o >= (uint32_t)RL - 4u) continue;   // last line 12/16 written, by one writer
             dst[pos] = r[j];
         }
     }
@@ -108,12 +114,15 @@ int main() {
         const float t5 = run<5>(s, d, ntiles, grid);
         const float t6 = run<6>(s, d, ntiles, grid);
         const float t7 = run<7>(s, d, ntiles, grid);
-        const char* names[8] = {"linear", "runs_line_aligned", "runs_shifted",
-                                "runs_shifted_xcd_adjacent", "runs_line_aligned_xcd_adjacent",
-                                "runs_shifted_aligned_stores", "runs_shifted_tail_carry",
-                                "runs_sector_aligned"};
-        const float ts[8] = {t0, t1, t2, t3, t4, t5, t6, t7};
-        for (int m = 0; m < 8; ++m)
+        const float t8 = run<8>(s, d, ntiles, grid);
+        const float t9 = run<9>(s, d, ntiles, grid);
+        const char* names[10] = {"linear", "runs_line_aligned", "runs_shifted",
+                                 "runs_shifted_xcd_adjacent", "runs_line_aligned_xcd_adjacent",
+                                 "runs_shifted_aligned_stores", "runs_shifted_tail_carry",
+                                 "runs_sector_aligned", "runs_aligned_last_line_partial_one_writer",
+                                 "linear_shifted_lines_split_between_waves"};
+        const float ts[10] = {t0, t1, t2, t3, t4, t5, t6, t7, t8, t9};
+        for (int m = 0; m < 10; ++m)
             printf("{\"probe\": \"line_probe\", \"mode\": \"%s\", \"grid\": %d, \"ms\": %.4f, \"rw_GBs\": %.1f}\n",
                    names[m], grid, ts[m], 2.0 * n * 8 / (ts[m] * 1e-3) / 1e9);
     }

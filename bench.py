@@ -34,6 +34,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "webgpu-radix-sort_amd"))
 
 HBM_PEAK_GBS = 8000.0    # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+EXCHANGE_ROUNDS = 4      # multi-GPU: bucket groups per rank, each sorted while later rounds fly
 
 WORKLOADS = {
     "config3": dict(n=1 << 28, values=True, local_shuffle=True, check_order=False, kind="u32",
@@ -228,7 +229,7 @@ def main() -> None:
         lo = HipLocalOps(local, int(n * 1.25), wl["values"], args.radix_bits)
         r = None
         for _ in range(W):
-            r = distributed_sort(keys, vals, lo)
+            r = distributed_sort(keys, vals, lo, chunks=EXCHANGE_ROUNDS)
         torch.cuda.synchronize()
         from radix_sort_amd import _lib
         import ctypes
@@ -237,7 +238,7 @@ def main() -> None:
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(K):
-            r = distributed_sort(keys, vals, lo)
+            r = distributed_sort(keys, vals, lo, chunks=EXCHANGE_ROUNDS)
         torch.cuda.synchronize()
         barrier()
         elapsed = time.perf_counter() - t0
@@ -253,11 +254,14 @@ def main() -> None:
             raise SystemExit(f"bench: rank {rank} output not sorted")
         info = {"passes": 4}
         keys_per_step = n * world
-        scatter_keys = r.n
+        # the local sort runs as `chunks` group sorts per step: a pass launch handles one group
+        scatter_keys = r.n / EXCHANGE_ROUNDS
         extra["recv_keys_rank0"] = r.n
-        extra["partition"] = ("top 8 bits, whole-bucket split; 4 exchange rounds of bucket groups, "
-                              "each group sorted while the later rounds are on the wire")
-        extra["roofline_scope"] = "local sort of the received keys (rank 0)"
+        extra["partition"] = (f"top 8 bits, whole-bucket split; {EXCHANGE_ROUNDS} exchange rounds of "
+                              "bucket groups, each sorted while the later rounds are on the wire")
+        extra["roofline_scope"] = ("local group sorts of the received keys (rank 0; a pass launch "
+                                   f"handles one of the {EXCHANGE_ROUNDS} bucket groups)")
+        extra["group_sorts_per_step"] = EXCHANGE_ROUNDS
 
     value = keys_per_step * K / elapsed / 1e9
     sc = kernel_ms.get("scatter", {"ms": 0.0, "launches": 0})
@@ -273,7 +277,7 @@ def main() -> None:
         try:
             with open(args.traffic_json) as f:
                 tj = json.load(f).get(args.workload)
-            if tj:
+            if tj and not use_dist:   # measured for the single-GPU launch shape only
                 traffic = tj.get("scatter_bytes_per_launch")
         except (OSError, ValueError):
             pass
@@ -289,6 +293,8 @@ def main() -> None:
     # path: k_pass_totals reads the keys once, later totals come from the scatter itself)
     hist = kernel_ms.get("histogram", {"launches": 0})["launches"]
     hist_reads = max(1, round(hist / max(K, 1))) if hist else passes
+    if use_dist and hist:
+        hist_reads = 1   # one totals read per group sort: each key once per step
     sort_bytes = keys_per_step / max(world, 1) * (passes * (8 + 8 * (1 if wl["values"] else 0))
                                                   + 4 * hist_reads)
     extra["digit_count_reads_per_sort"] = hist_reads

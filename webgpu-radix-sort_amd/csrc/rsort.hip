@@ -152,7 +152,8 @@ struct rs_plan {
     bool aos_tmp = true;                   // one-sweep KV: records as the ping-pong copy (RSORT_AOS_TMP)
     uint32_t* tmp2 = nullptr;              // one-sweep KV: second records buffer (RSORT_RECS2=0: none)
     bool keys_cfg = true;                  // keys-only 512x32 tiles (RSORT_KEYS_CFG=0: 1024x16)
-    bool huge_tiles = false;               // one-sweep KV: 24K-record tiles (RSORT_HUGE=1)
+    int huge_tiles = 0;                    // one-sweep KV: 24K-record tiles (RSORT_HUGE=1: every
+                                           // pass; 2: the records -> arrays pass only)
     bool fused_check = true;               // one-sweep check_order: passes > 0 check their input
                                            // in k_onesweep (RSORT_FUSED_CHECK=0: k_check)
     unsigned long long* status = nullptr;  // [max_tiles][256] look-back status words
@@ -344,6 +345,7 @@ rs_status run_pass(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint32_t*
     // kernel loads whole record tiles without per-slot bounds, see k_onesweep's SR > 1)
     const int Lin = LL & 15;
     if (R == 8 && onesweep && p->huge_tiles &&
+        (p->huge_tiles == 1 || LL == layout_pair(rs::LAYOUT_AOS, rs::LAYOUT_SOA)) &&
         (Lin == rs::LAYOUT_SOA ||
          (Lin == rs::LAYOUT_AOS && (ik == p->tmp_k || (p->tmp2 && ik == p->tmp2)))))
         return run_pass_cfg<8, kHuge.block, kHuge.kpt, false, 2>(p, ik, iv, ok, ov, n, shift, w, LL, gate, pass, kHuge.max_grid, onesweep, s);
@@ -445,7 +447,7 @@ RS_EXPORT rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out) {
     bool recs2 = true;
     if (const char* r2 = getenv("RSORT_RECS2")) recs2 = strcmp(r2, "0") != 0;
     if (const char* kc = getenv("RSORT_KEYS_CFG")) p->keys_cfg = strcmp(kc, "0") != 0;
-    if (const char* hg = getenv("RSORT_HUGE")) p->huge_tiles = strcmp(hg, "0") != 0;
+    if (const char* hg = getenv("RSORT_HUGE")) p->huge_tiles = atoi(hg);
     if (const char* fc = getenv("RSORT_FUSED_CHECK")) p->fused_check = strcmp(fc, "0") != 0;
     if (const char* rk = getenv("RSORT_RANK"))
         p->rank_mode = (strcmp(rk, "ballot") == 0) ? rs::RANK_BALLOT : rs::RANK_LDS_ATOMIC;

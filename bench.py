@@ -93,6 +93,35 @@ def cpu_baseline(n_log2: int, seed: int) -> dict:
 _NEARLY = {}
 
 
+def _splitmix_u32(seed: int, n: int) -> "np.ndarray":
+    """key[i] = low32(splitmix64 finaliser(seed * 0xD1B54A32D192ED03 + i)): the same counter
+    generator as the device fill (rs_fill_random_u32), on the host."""
+    import numpy as np
+    with np.errstate(over="ignore"):
+        z = np.uint64((seed * 0xD1B54A32D192ED03) & 0xFFFFFFFFFFFFFFFF) + np.arange(n, dtype=np.uint64)
+        z = z + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    return (z & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+
+
+def nearly_sorted_f32_bits(n: int, seed: int) -> "np.ndarray":
+    """BASELINE config4 input: f32 keys (u >> 8) * 2^-24 in [0, 1) sorted
+    ascending, then n // 1000 seeded transpositions applied in sequence; raw u32 bits."""
+    import numpy as np
+    keys = ((_splitmix_u32(seed, n) >> np.uint32(8)).astype(np.float64) * 2.0 ** -24).astype(np.float32)
+    keys.sort(kind="stable")
+    bits = keys.view(np.uint32).copy()
+    swaps = max(1, n // 1000)
+    r = _splitmix_u32(seed ^ 0x5EED, 2 * swaps).astype(np.uint64)
+    a = (r[0::2] % np.uint64(n)).astype(np.int64)
+    b = (r[1::2] % np.uint64(n)).astype(np.int64)
+    for x, y in zip(a.tolist(), b.tolist()):
+        bits[x], bits[y] = bits[y], bits[x]
+    return bits
+
+
 def make_input(torch, ops, wl, n, seed, start, dev):
     keys = torch.empty(n, dtype=torch.int32, device=dev)
     if wl["kind"] == "f32_nearly":
@@ -100,10 +129,8 @@ def make_input(torch, ops, wl, n, seed, start, dev):
         # every batch is a fresh copy of the same input (a sorted batch would be a different
         # workload), so only the first seed is used
         if n not in _NEARLY:
-            sys.path.insert(0, os.path.join(ROOT, "oracle"))
-            import oracle as O
             log(f"generating the nearly-sorted f32 input (n={n}) on the host ...")
-            _NEARLY[n] = torch.from_numpy(O.nearly_sorted_f32_bits(n, seed).view("int32"))
+            _NEARLY[n] = torch.from_numpy(nearly_sorted_f32_bits(n, seed).view("int32"))
         keys.copy_(_NEARLY[n])
     else:
         ops.fill_random_u32(keys, seed, start)

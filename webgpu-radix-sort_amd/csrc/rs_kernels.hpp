@@ -824,7 +824,10 @@ __global__ __launch_bounds__(BLOCK) void k_pass_totals(const uint32_t* __restric
 // published" and the region never needs clearing (the host clears it when the epoch wraps).
 // Waits are bounded: a timeout sets err[0] (never a hang).
 constexpr uint32_t kStAggregate = 1u, kStInclusive = 2u;
-constexpr int kLookback = 4;   // predecessors read per look-back step
+#ifndef RS_LOOKBACK
+#define RS_LOOKBACK 4
+#endif
+constexpr int kLookback = RS_LOOKBACK;   // predecessors read per look-back step
 
 __device__ __forceinline__ unsigned long long st_load(const unsigned long long* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -244,7 +244,10 @@ void launch_onesweep_t(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint3
                        const uint32_t* gate, int pass, hipStream_t s) {
     auto kern = rs::k_onesweep<R, BLOCK, KPT, L, RANK, LO, SR>;
     static const uint32_t per_cu = resident_per_cu(kern, BLOCK);   // per instantiation
-    const uint32_t grid = std::min<uint32_t>(ntiles, p->cus * per_cu);
+    // RSORT_OS_GRID caps the persistent grid (tiles come from tickets, so any grid >= 1 is correct)
+    static const uint32_t cap = [] { const char* g = getenv("RSORT_OS_GRID"); return g ? (uint32_t)atoi(g) : 0u; }();
+    uint32_t grid = std::min<uint32_t>(ntiles, p->cus * per_cu);
+    if (cap > 0 && cap < grid) grid = cap;
     const bool last = (uint32_t)pass + 1 >= p->passes;
     uint32_t* ntot = last ? nullptr : p->ptot + p->ptot_off[pass + 1];
     const uint32_t nshift = last ? 0u : shift + p->widths[pass];

@@ -26,7 +26,7 @@ extern "C" {
 #endif
 
 #define RSORT_VERSION_MAJOR 0
-#define RSORT_VERSION_MINOR 1
+#define RSORT_VERSION_MINOR 2
 
 typedef enum rs_status {
     RS_OK = 0,
@@ -37,7 +37,13 @@ typedef enum rs_status {
                                  the reference leaves this unchecked) */
     RS_ERR_HIP = 4,           /* a HIP runtime call failed (message in rs_last_error) */
     RS_ERR_OUT_OF_MEMORY = 5,
-    RS_ERR_CAPACITY = 6       /* count exceeds the plan's capacity */
+    RS_ERR_CAPACITY = 6,      /* count exceeds the plan's capacity */
+    RS_ERR_DEVICE = 7         /* a device-side failure of an EARLIER sort on this plan: a bounded
+                                 inter-workgroup wait of the one-sweep pass timed out, so that
+                                 sort's output is invalid (reported once, by rs_plan_check or by
+                                 the next rs_plan_sort / rs_plan_sort_n on the plan, which then
+                                 enqueues nothing).  The reference's dispatch never produces
+                                 output silently wrong (AbstractRadixSortKernel.ts:221-247). */
 } rs_status;
 
 /* rs_plan_desc.flags — the reference's boolean options. */
@@ -74,6 +80,11 @@ typedef struct rs_plan_info {
     uint32_t tile_keys;         /* keys per tile of the rank/scatter kernel */
     uint32_t grid_blocks;       /* workgroups of the histogram / scatter kernels */
     uint64_t workspace_bytes;   /* device bytes owned by the plan */
+    uint32_t rank_mode;         /* in-wave stable ranking: 0 = lane-ordered LDS atomics (one
+                                   ds_add_rtn_u32 per key), 1 = ballot-match ranking */
+    int32_t  lane_order_selftest;  /* the device's LDS-atomic lane-order self-test (run once per
+                                   device at the first plan creation): 1 passed, 0 failed (plans
+                                   then use rank_mode 1), -1 could not run */
 } rs_plan_info;
 
 /* Kernel kinds reported by rs_plan_kernel_times(). */
@@ -124,6 +135,14 @@ rs_status rs_plan_reset_kernel_times(rs_plan* plan);
 /* Device-side error word of the plan (synchronises the device): 0 = ok; bit 0 = a bounded
  * inter-workgroup wait of the one-sweep scatter timed out (that sort's result is invalid). */
 rs_status rs_plan_device_errors(rs_plan* plan, uint32_t* errors);
+/* Wait for the plan's last enqueued sort and report any device-side failure since the last
+ * report: RS_OK, or RS_ERR_DEVICE (cleared by the report).  The façades call it at their
+ * synchronising points (mapAsync / Python check()). */
+rs_status rs_plan_check(rs_plan* plan);
+/* Bound of every inter-workgroup wait of the one-sweep pass, in s_sleep(1) periods (default
+ * 2^20, ~ms; env RSORT_SPIN_MAX at plan creation).  0 makes any wait on a not-yet-published
+ * predecessor time out at once: the failure path's test (rs_plan_check must then report it). */
+rs_status rs_plan_set_wait_limit(rs_plan* plan, uint32_t sleeps);
 void      rs_plan_destroy(rs_plan* plan);     /* frees the workspace (reference quirk Q9) */
 
 /* ---- prefix sum (PrefixSumKernel) ------------------------------------------------------- */
@@ -133,6 +152,18 @@ rs_status rs_scan_plan_create(int32_t device, uint64_t count, uint32_t workgroup
                               uint32_t workgroup_y, uint32_t flags, rs_scan_plan** out);
 /* In-place exclusive scan (mod 2^32) of data[0..count); data[count..] untouched. */
 rs_status rs_scan_plan_run(rs_scan_plan* plan, void* data, void* stream);
+/* PrefixSumKernel.dispatch(pass, dispatchSizeBuffer, offset) (PrefixSumKernel.ts:147-158): the
+ * scan as above, gated on the device: dispatch_size_buffer (device memory) holds u32 (x, y, z)
+ * workgroup triples from byte `offset`, one per pipeline of rs_scan_plan_dispatch_chain; the scan
+ * runs iff the first triple has no zero entry (the reference's check-sort zeroes the chain to
+ * skip work).  The HIP scan is one fused chain, so later triples are not read: it runs whole or
+ * not at all.  Nothing is read on the host. */
+rs_status rs_scan_plan_run_indirect(rs_scan_plan* plan, void* data, const void* dispatch_size_buffer,
+                                    uint64_t offset, void* stream);
+/* The reference's dispatch chain for this plan (PrefixSumKernel.getDispatchChain,
+ * PrefixSumKernel.ts:135-137): (x, y, 1) per pipeline, written to out[0..max_words); returns the
+ * number of words of the whole chain. */
+uint32_t  rs_scan_plan_dispatch_chain(const rs_scan_plan* plan, uint32_t* out, uint32_t max_words);
 void      rs_scan_plan_destroy(rs_scan_plan* plan);
 
 /* ---- device memory / streams (the reference's createBuffers / queue analogue) ---------- */

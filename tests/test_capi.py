@@ -20,8 +20,9 @@ def test_library_exports_every_header_symbol():
 
 def test_version_and_status_strings():
     L = _lib.load()
-    assert L.rs_version() == (0 << 16) | 1
+    assert L.rs_version() == (0 << 16) | 2
     assert L.rs_status_string(_lib.RS_ERR_NOT_POW2).decode().startswith("workgroup")
+    assert "device-side failure" in L.rs_status_string(_lib.RS_ERR_DEVICE).decode()
 
 
 def _create(**kw):
@@ -63,6 +64,9 @@ def test_null_arguments():
     L = _lib.load()
     assert L.rs_plan_create(None, None) == _lib.RS_ERR_INVALID_ARG
     assert L.rs_plan_sort(None, None, None, None) == _lib.RS_ERR_INVALID_ARG
+    assert L.rs_plan_check(None) == _lib.RS_ERR_INVALID_ARG
+    assert L.rs_scan_plan_run_indirect(None, None, None, 0, None) == _lib.RS_ERR_INVALID_ARG
+    assert L.rs_scan_plan_dispatch_chain(None, None, 0) == 0
     L.rs_plan_destroy(None)  # no-op
 
 

@@ -43,7 +43,24 @@
 #define RS_NT_LOAD 0         // 1: pass inputs (full tiles) loaded non-temporal (read once per pass)
 #endif
 
+#ifndef RS_STAMPS
+#define RS_STAMPS 0          // diagnostic build: per-tile phase timestamps of k_onesweep
+#endif
+
 namespace rs {
+
+#if RS_STAMPS
+// [pass][tile][8] s_memtime stamps (thread 0 of the workgroup); slot 7 = workgroup id.  Set by
+// rs_debug_set_stamps (diagnostic builds only, tools/stamp_probe.py).
+__device__ unsigned long long* g_rs_stamps;
+#define RS_STAMP(pass, ntiles, T, i, v)                                                        \
+    do {                                                                                       \
+        if (threadIdx.x == 0 && g_rs_stamps)                                                   \
+            g_rs_stamps[((size_t)(pass) * (ntiles) + (T)) * 8 + (i)] = (v);                    \
+    } while (0)
+#else
+#define RS_STAMP(pass, ntiles, T, i, v) do { } while (0)
+#endif
 
 constexpr int kBlock = 256;              // threads of the small kernels: 4 waves of 64
 constexpr int kWaves = kBlock / 64;
@@ -220,8 +237,8 @@ __global__ __launch_bounds__(kBlock) void k_histogram(
                 }
             }
         } else {
-            const uint32_t hi = (uint64_t)lo + TILE < n ? lo + (uint32_t)TILE : n;
-            for (uint32_t j = lo + lane; j < hi; j += 64)
+            const uint64_t hi = (uint64_t)lo + TILE < n ? (uint64_t)lo + TILE : n;
+            for (uint64_t j = (uint64_t)lo + lane; j < hi; j += 64)
                 atomicAdd(&h[(keys[(size_t)j * KS] >> shift) & mask], 1u);
         }
         for (uint32_t d = lane; d < (uint32_t)RADIX; d += 64) counts[(size_t)d * ntiles + t] = h[d];
@@ -318,14 +335,14 @@ constexpr uint32_t kPadKey = 0xFFFFFFFFu;
 
 template <int KPT, int L, bool CLAMP = false>
 __device__ __forceinline__ void load_tile(const uint32_t* __restrict__ in_k,
-                                          const uint32_t* __restrict__ in_v, uint32_t wbase,
+                                          const uint32_t* __restrict__ in_v, uint64_t wbase,
                                           uint32_t n, bool full, uint32_t (&k)[KPT],
                                           uint32_t (&v)[L != LAYOUT_KEYS ? KPT : 1]) {
     constexpr bool HAS_VALUES = L != LAYOUT_KEYS;
     const uint32_t lane = lane_id();
     // one base address per array and constant per-slot offsets (a 32-bit index per slot would
     // have to be recomputed and widened for every slot: it may wrap)
-    const size_t b = (size_t)wbase + lane;
+    const size_t b = wbase + lane;
     if (L == LAYOUT_AOS) {
         const unsigned long long* rec = reinterpret_cast<const unsigned long long*>(in_k) + b;
 #pragma unroll
@@ -665,7 +682,7 @@ __global__ __launch_bounds__(BLOCK, pass_min_waves(BLOCK, KPT)) void k_scatter(
     uint32_t v[HAS_VALUES ? KPT : 1];
     if (count) {
         const uint32_t tile0 = first * (uint32_t)TILE;
-        load_tile<KPT, L>(in_k, in_v, tile0 + w * WAVE_KEYS, n,
+        load_tile<KPT, L>(in_k, in_v, (uint64_t)tile0 + w * WAVE_KEYS, n,
                                    (uint64_t)tile0 + TILE <= n, k, v);
     }
     for (uint32_t t = 0; t < count; ++t) {
@@ -690,7 +707,7 @@ __global__ __launch_bounds__(BLOCK, pass_min_waves(BLOCK, KPT)) void k_scatter(
         // under this tile's scatter.
         if (t + 1 < count) {
             const uint32_t nt0 = tile0 + G * TILE;
-            load_tile<KPT, L>(in_k, in_v, nt0 + w * WAVE_KEYS, n, (uint64_t)nt0 + TILE <= n, k, v);
+            load_tile<KPT, L>(in_k, in_v, (uint64_t)nt0 + w * WAVE_KEYS, n, (uint64_t)nt0 + TILE <= n, k, v);
         }
         scatter_tile<BLOCK, HAS_VALUES, L>(s_keys, s_kv, s_gdelta, out_k, out_v, n,
                                            full ? (uint32_t)TILE : n - tile0, tile0, shift, mask);
@@ -795,10 +812,11 @@ __global__ __launch_bounds__(BLOCK) void k_pass_totals(const uint32_t* __restric
         for (; i < nv; i += stride) vec4(i, k4[i]);
         i0 = KPV * nv;
     }
-    for (uint32_t i = i0 + blockIdx.x * BLOCK + tid; i < n; i += stride) {
-        const uint32_t key = keys[(size_t)i * KS];
+    // 64-bit index: with n close to 2^32, i + stride would wrap (stride divides 2^32)
+    for (uint64_t i = (uint64_t)i0 + blockIdx.x * BLOCK + tid; i < n; i += stride) {
+        const uint32_t key = keys[i * KS];
         count_key(key);
-        if (chk && i + 1 < n) inv(key, keys[(size_t)(i + 1) * KS]);
+        if (chk && i + 1 < n) inv(key, keys[(i + 1) * KS]);
     }
     if (chk && __ballot(bad) != 0ull && lane_id() == 0) atomicOr(chk, 1u);
     __syncthreads();
@@ -826,6 +844,18 @@ __global__ __launch_bounds__(BLOCK) void k_pass_totals(const uint32_t* __restric
 constexpr uint32_t kStAggregate = 1u, kStInclusive = 2u;
 #ifndef RS_LOOKBACK
 #define RS_LOOKBACK 4
+#endif
+// Where k_onesweep issues the next tile's loads (speed only).  A wave's vector-memory operations
+// complete in issue order (one vmcnt), so look-back status loads issued behind the wave's prefetch
+// wait for the whole prefetch to land.  0: every wave before the look-back; 1: the look-back waves
+// after their look-back, the others before it; 2: every wave after the look-back barrier.
+#ifndef RS_PREFETCH
+#define RS_PREFETCH 0
+#endif
+// 1: thread 0 takes the next tile's ticket at the top of the current tile (the atomic's round
+// trip overlaps the rank phase instead of stalling the staging barrier).
+#ifndef RS_EARLY_TICKET
+#define RS_EARLY_TICKET 0
 #endif
 constexpr int kLookback = RS_LOOKBACK;   // predecessors read per look-back step
 
@@ -867,7 +897,7 @@ __global__ __launch_bounds__(BLOCK, pass_min_waves(BLOCK, KPT)) void k_onesweep(
     uint32_t mask, uint32_t ntiles, const uint32_t* __restrict__ dtot,
     unsigned long long* status, uint32_t* ticket, uint32_t* err, uint32_t* __restrict__ ntot,
     uint32_t nshift, uint32_t nmask, uint32_t epoch, const uint32_t* gate, int pass,
-    uint32_t* chk, uint32_t fmask) {
+    uint32_t* chk, uint32_t fmask, uint32_t spin_max, uint32_t* host_err) {
     // ntot (may be null): whole-array totals of the NEXT pass's digit (key >> nshift) & nmask,
     // counted here from the keys this workgroup stages, so only pass 0 needs k_pass_totals.
     // chk (may be null, check_order, pass > 0): the order check of this pass's input, fused:
@@ -913,17 +943,21 @@ __global__ __launch_bounds__(BLOCK, pass_min_waves(BLOCK, KPT)) void k_onesweep(
     // tile has arrived.  Arrays (the caller's) load with clamped indices.
     auto load = [&](uint32_t t0) {
         if (SR > 1 && L == LAYOUT_AOS)
-            load_tile<KPT, L>(in_k, in_v, t0 + w * WAVE_KEYS, n, true, k, v);
+            load_tile<KPT, L>(in_k, in_v, (uint64_t)t0 + w * WAVE_KEYS, n, true, k, v);
         else
-            load_tile<KPT, L, (SR > 1)>(in_k, in_v, t0 + w * WAVE_KEYS, n, (uint64_t)t0 + TILE <= n, k, v);
+            load_tile<KPT, L, (SR > 1)>(in_k, in_v, (uint64_t)t0 + w * WAVE_KEYS, n, (uint64_t)t0 + TILE <= n, k, v);
     };
     if (T < ntiles) load(T * (uint32_t)TILE);
     while (T < ntiles) {
+        RS_STAMP(pass, ntiles, T, 0, __builtin_amdgcn_s_memtime());
+        RS_STAMP(pass, ntiles, T, 7, blockIdx.x);
+        uint32_t early_ticket = 0;
+        if (RS_EARLY_TICKET && tid == 0) early_ticket = atomicAdd(ticket, 1u);
         const uint32_t tile0 = T * (uint32_t)TILE;
         const bool full = (uint64_t)tile0 + TILE <= n;
         const uint32_t nvalid = full ? (uint32_t)TILE : n - tile0;
         if (SR > 1 && L == LAYOUT_AOS && !full) {
-            const uint32_t wb = tile0 + w * WAVE_KEYS + lane_id();
+            const uint64_t wb = (uint64_t)tile0 + w * WAVE_KEYS + lane_id();
 #pragma unroll
             for (int j = 0; j < KPT; ++j)
                 if (wb + j * 64 >= n) k[j] = kPadKey;
@@ -931,13 +965,14 @@ __global__ __launch_bounds__(BLOCK, pass_min_waves(BLOCK, KPT)) void k_onesweep(
         const uint32_t npad = (uint32_t)TILE - nvalid;
         uint32_t bkey = kPadKey;   // the key after this wave's slots (next wave or next tile)
         if (chk) {
-            const uint32_t q = tile0 + (w + 1) * (uint32_t)WAVE_KEYS;
-            if (q < n) bkey = in_k[(size_t)q * (L == LAYOUT_AOS ? 2u : 1u)];
+            const uint64_t q = (uint64_t)tile0 + (w + 1) * (uint32_t)WAVE_KEYS;
+            if (q < n) bkey = in_k[q * (L == LAYOUT_AOS ? 2u : 1u)];
         }
         Slots<KPT, RS_PACK_POS && (SR > 1)> rank;
         uint32_t c;
         const uint32_t tstart = rank_tile<R, NW, KPT, RANK>(k, rank, s_whist, s_scratch, shift,
                                                             mask, npad, c);
+        RS_STAMP(pass, ntiles, T, 1, __builtin_amdgcn_s_memtime());
         if (chk && wave_inversion<KPT>(k, bkey, fmask) && lane_id() == 0) s_inv = 1u;
         // Publish this tile's counts first, then do everything that needs only tile-local
         // offsets (staging, next ticket, next-tile prefetch) before walking back: the
@@ -950,6 +985,7 @@ __global__ __launch_bounds__(BLOCK, pass_min_waves(BLOCK, KPT)) void k_onesweep(
             set_wave_offsets<R, NW>(s_whist, tstart);
         }
         __syncthreads();
+        RS_STAMP(pass, ntiles, T, 2, __builtin_amdgcn_s_memtime());
         if (SR == 1) {
             stage_tile<KPT, HAS_VALUES, TILE>(k, v, rank, s_whist[w], s_keys, s_kv, shift, mask,
                                               ntot ? s_ntot : nullptr, nshift, nmask);
@@ -959,12 +995,14 @@ __global__ __launch_bounds__(BLOCK, pass_min_waves(BLOCK, KPT)) void k_onesweep(
             stage_round<KPT, HAS_VALUES, STAGE>(k, v, rank, s_keys, s_kv, 0u);
         }
         if (tid == 0) {
-            s_next = atomicAdd(ticket, 1u);
+            s_next = RS_EARLY_TICKET ? early_ticket : atomicAdd(ticket, 1u);
             if (ntot && npad) atomicSub(&s_ntot[nmask], npad);   // the pads' next digit
         }
         __syncthreads();
         const uint32_t Tn = s_next;
-        if (SR == 1 && Tn < ntiles) load(Tn * (uint32_t)TILE);   // prefetch: hides under this scatter
+        RS_STAMP(pass, ntiles, T, 3, __builtin_amdgcn_s_memtime());
+        // prefetch (RS_PREFETCH): hides under the look-back and this scatter
+        if (RS_PREFETCH == 0 && SR == 1 && Tn < ntiles) load(Tn * (uint32_t)TILE);
         if (tid < (uint32_t)RADIX) {
             uint32_t excl = s_dbase[tid];
             if (T != 0) {
@@ -993,17 +1031,24 @@ __global__ __launch_bounds__(BLOCK, pass_min_waves(BLOCK, KPT)) void k_onesweep(
                     if (done) break;
                     j -= used;
                     if (used == 0u) {
-                        // bounded: ~ms per wait, and once any wait timed out every other wait
-                        // gives up at its next check, so a bug can never hang the device
-                        if ((++spins & 255u) == 0u &&
-                            (spins > (1u << 20) ||
+                        // bounded: spin_max sleeps (~ms by default) per wait, and once any wait
+                        // timed out every other wait gives up at its next check, so a bug can
+                        // never hang the device.  The error reaches the host through the
+                        // host-mapped word (rs_plan_check / the next rs_plan_sort report it);
+                        // the device word is cleared at every sort.
+                        ++spins;
+                        if (spins > spin_max ||
+                            ((spins & 255u) == 0u &&
                              __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
 #if RS_ONESWEEP_TRACE
-                            if (spins > (1u << 20))
+                            if (spins > spin_max)
                                 printf("lookback timeout: pass %d tile %u/%u digit %u waiting on %u word %llx epoch %u\n",
                                        pass, T, ntiles, tid, j, sv[0], epoch);
 #endif
                             atomicOr(err, 1u);
+                            if (host_err)
+                                __hip_atomic_fetch_or(host_err, 1u, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_SYSTEM);
                             break;
                         }
                         __builtin_amdgcn_s_sleep(1);
@@ -1018,7 +1063,10 @@ __global__ __launch_bounds__(BLOCK, pass_min_waves(BLOCK, KPT)) void k_onesweep(
             s_gdelta[tid] = ((((uint32_t)tid * ntiles + T) * 64u) & (n - 1u)) - tstart;
 #endif
         }
+        if (RS_PREFETCH == 1 && SR == 1 && Tn < ntiles) load(Tn * (uint32_t)TILE);
         __syncthreads();
+        if (RS_PREFETCH == 2 && SR == 1 && Tn < ntiles) load(Tn * (uint32_t)TILE);
+        RS_STAMP(pass, ntiles, T, 4, __builtin_amdgcn_s_memtime());
 #pragma unroll
         for (int h = 0; h < SR; ++h) {
             if (h > 0) {   // the previous round's scatter has read the staging area
@@ -1044,6 +1092,7 @@ __global__ __launch_bounds__(BLOCK, pass_min_waves(BLOCK, KPT)) void k_onesweep(
         }
         __syncthreads();
 #endif
+        RS_STAMP(pass, ntiles, T, 5, __builtin_amdgcn_s_memtime());
         T = Tn;
     }
     if (ntot) {
@@ -1140,8 +1189,9 @@ __global__ __launch_bounds__(kBlock) void k_check(const uint32_t* __restrict__ k
     if (gate_upto >= 0 && gated_off(inv, gate_upto)) return;
     bool bad = false;
     const uint32_t stride = gridDim.x * kBlock;
-    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i + 1 < n; i += stride) {
-        const uint32_t a = keys[(size_t)i * kstride] & mask, b = keys[(size_t)(i + 1) * kstride] & mask;
+    // 64-bit index (n may be close to 2^32; the stride divides 2^32)
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i + 1 < n; i += stride) {
+        const uint32_t a = keys[i * kstride] & mask, b = keys[(i + 1) * kstride] & mask;
         bad |= a > b;
     }
     if (__ballot(bad) != 0 && lane_id() == 0) atomicOr(inv + pass, 1u);
@@ -1167,7 +1217,7 @@ __global__ __launch_bounds__(kBlock) void k_finalize(const uint32_t* __restrict_
         tk = tk_even;
     }
     const uint32_t stride = gridDim.x * kBlock;
-    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
         if (L == LAYOUT_AOS) {
             reinterpret_cast<uint2*>(uk)[i] = reinterpret_cast<const uint2*>(tk)[i];
         } else if (LT == LAYOUT_AOS) {       // records in tmp -> the caller's two arrays
@@ -1183,17 +1233,25 @@ __global__ __launch_bounds__(kBlock) void k_finalize(const uint32_t* __restrict_
 
 // ---- prefix sum (PrefixSumKernel) ---------------------------------------------------------
 // Three kernels, reduce-then-scan: chunk sums -> scan of chunk sums -> rescan with carry.
+// ind (may be null): the caller's indirect dispatch triple (x, y, z workgroups,
+// PrefixSumKernel.ts:147-158); a zero entry skips the scan, as a zeroed indirect dispatch does.
+__device__ __forceinline__ bool indirect_off(const uint32_t* ind) {
+    return ind && (ind[0] == 0u || ind[1] == 0u || ind[2] == 0u);
+}
+
 template <int TILE>
 __global__ __launch_bounds__(kBlock) void k_chunk_sums(const uint32_t* __restrict__ data,
                                                        uint32_t n, uint32_t base, uint32_t extra,
-                                                       uint32_t* __restrict__ sums) {
+                                                       uint32_t* __restrict__ sums,
+                                                       const uint32_t* ind) {
     __shared__ uint32_t scratch[kWaves];
+    if (indirect_off(ind)) return;
     const Chunk ch = chunk_of(blockIdx.x, base, extra);
     const uint64_t lo = (uint64_t)ch.first * TILE;
     const uint64_t hi64 = lo + (uint64_t)ch.count * TILE;
-    const uint32_t hi = (uint32_t)(hi64 < n ? hi64 : n);
+    const uint64_t hi = hi64 < n ? hi64 : n;
     uint32_t s = 0;
-    for (uint32_t i = (uint32_t)lo + threadIdx.x; i < hi; i += kBlock) s += data[i];
+    for (uint64_t i = lo + threadIdx.x; i < hi; i += kBlock) s += data[i];
     uint32_t tot;
     block_excl_scan(s, scratch, tot);
     if (threadIdx.x == 0) sums[blockIdx.x] = tot;
@@ -1202,9 +1260,11 @@ __global__ __launch_bounds__(kBlock) void k_chunk_sums(const uint32_t* __restric
 template <int TILE>
 __global__ __launch_bounds__(kBlock) void k_chunk_rescan(uint32_t* __restrict__ data, uint32_t n,
                                                          uint32_t base, uint32_t extra,
-                                                         const uint32_t* __restrict__ sums_scanned) {
+                                                         const uint32_t* __restrict__ sums_scanned,
+                                                         const uint32_t* ind) {
     constexpr int PER = TILE / kBlock;  // consecutive elements per thread
     __shared__ uint32_t scratch[kWaves];
+    if (indirect_off(ind)) return;
     const Chunk ch = chunk_of(blockIdx.x, base, extra);
     uint32_t carry = sums_scanned[blockIdx.x];
     for (uint32_t t = 0; t < ch.count; ++t) {
@@ -1228,8 +1288,10 @@ __global__ __launch_bounds__(kBlock) void k_chunk_rescan(uint32_t* __restrict__ 
 }
 
 // Single-block exclusive scan of a short array (<= a few thousand) in place.
-__global__ __launch_bounds__(kBlock) void k_scan_small(uint32_t* __restrict__ a, uint32_t m) {
+__global__ __launch_bounds__(kBlock) void k_scan_small(uint32_t* __restrict__ a, uint32_t m,
+                                                      const uint32_t* ind) {
     __shared__ uint32_t scratch[kWaves];
+    if (indirect_off(ind)) return;
     const uint32_t per = (m + kBlock - 1) / kBlock;
     const uint32_t b0 = threadIdx.x * per;
     uint32_t s = 0;
@@ -1243,6 +1305,53 @@ __global__ __launch_bounds__(kBlock) void k_scan_small(uint32_t* __restrict__ a,
             a[b0 + k] = run;
             run += c;
         }
+}
+
+// ---- self-test of the lane-ordered LDS atomics that RANK_LDS_ATOMIC relies on ----------------
+// gfx950 resolves one wave instruction's same-address ds_add_rtn_u32 in lane order (probed, not
+// an ISA guarantee).  Every wave here repeatedly adds per-lane amounts (1, as the per-key ranks
+// do, or 1-4, as the per-run ranks do) to 1-256 LDS addresses, some lanes inactive, with the same
+// atomicAdd the ranking uses, and checks that each lane got the sum of the amounts of the active
+// lower lanes with the same address.  *bad |= 1 on any mismatch.  Run once per device at the
+// first plan creation (rsort.hip); a failure switches plans to RANK_BALLOT.
+__device__ __forceinline__ uint32_t st_hash(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x7feb352du;
+    x ^= x >> 15;
+    x *= 0x846ca68bu;
+    x ^= x >> 16;
+    return x;
+}
+
+__global__ __launch_bounds__(kBlock) void k_lane_order_selftest(uint32_t iters, uint32_t* bad) {
+    __shared__ uint32_t cnt[kWaves][256];
+    const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+    uint32_t* c = cnt[w];
+    bool fail = false;
+    for (uint32_t it = 0; it < iters; ++it) {
+        const uint32_t seed = st_hash((blockIdx.x * kWaves + w) * 0x9E3779B9u + it * 0x85EBCA6Bu);
+        const uint32_t naddr = 1u << (st_hash(seed) % 9u);          // 1 .. 256 addresses
+        const bool some_off = (st_hash(seed ^ 0xABCDu) & 3u) != 0u;  // 3/4: ~1/8 lanes inactive
+        auto lane_info = [&](uint32_t l, uint32_t& addr, uint32_t& amt) -> bool {
+            const uint32_t h = st_hash(seed + l * 0x27D4EB2Fu);
+            addr = h % naddr;
+            amt = (it & 1u) ? 1u + ((h >> 12) & 3u) : 1u;
+            return !some_off || ((h >> 20) & 7u) != 0u;
+        };
+        for (uint32_t d = lane; d < 256u; d += 64) c[d] = 0u;
+        uint32_t my_addr, my_amt;
+        const bool act = lane_info(lane, my_addr, my_amt);
+        if (act) {
+            const uint32_t got = atomicAdd(&c[my_addr], my_amt);
+            uint32_t expect = 0;
+            for (uint32_t l = 0; l < lane; ++l) {
+                uint32_t a, m;
+                if (lane_info(l, a, m) && a == my_addr) expect += m;
+            }
+            fail |= got != expect;
+        }
+    }
+    if (__ballot(fail) != 0ull && lane == 0) atomicOr(bad, 1u);
 }
 
 // ---- synthetic inputs -----------------------------------------------------------------------
@@ -1273,7 +1382,7 @@ __global__ __launch_bounds__(kBlock) void k_is_sorted(const uint32_t* __restrict
                                                       uint32_t* flag) {
     bool bad = false;
     const uint32_t stride = gridDim.x * kBlock;
-    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i + 1 < n; i += stride)
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i + 1 < n; i += stride)
         bad |= (keys[i] & mask) > (keys[i + 1] & mask);
     if (__ballot(bad) != 0 && lane_id() == 0) atomicAnd(flag, 0u);
 }

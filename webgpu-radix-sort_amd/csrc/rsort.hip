@@ -9,10 +9,15 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
+#include <map>
+#include <mutex>
 #include <new>
 #include <string>
 #include <vector>
@@ -74,6 +79,18 @@ constexpr TileCfg kLargeKeys{RS_KEYS_BLOCK, RS_KEYS_KPT, RS_KEYS_BLOCK * RS_KEYS
 // tiles (1024 threads x 24 records, positions packed 16-bit) staged through LDS in two rounds of
 // 12K; longer digit runs per tile than 16K tiles (fewer lines shared by two tiles' runs)
 constexpr TileCfg kHuge{1024, 24, 24576, 512};
+// one-sweep KV tile configurations with two or more workgroups per CU (RSORT_KV_CFG): one
+// workgroup's rank / look-back / staging phases overlap another's loads and stores
+//   1: 512 threads x 16 = 8K-record tiles (~75 KiB LDS, 2 per CU)
+//   2: 512 threads x 32 = 16K-record tiles staged in two rounds of 8K (2 per CU)
+//   3: 256 threads x 32 = 8K-record tiles staged in two rounds of 4K (4 per CU)
+//   4: 512 threads x 24 = 12K-record tiles staged in two rounds of 6K (2 per CU)
+constexpr TileCfg kKv512x16{512, 16, 8192, 1024};
+constexpr TileCfg kKv512x32{512, 32, 16384, 1024};
+constexpr TileCfg kKv256x32{256, 32, 8192, 2048};
+constexpr TileCfg kKv512x24{512, 24, 12288, 1024};
+constexpr uint32_t kMinOnesweepTile = 8192;   // finest one-sweep tile (status words per plan)
+constexpr uint64_t kRecPad = 49152;           // records buffers: whole tiles of every config
 constexpr uint32_t kTinyMax = 1024 * 16;
 constexpr uint32_t kHistGrid = 2048;
 constexpr int kCheckGrid = 2048;
@@ -152,6 +169,7 @@ struct rs_plan {
     bool aos_tmp = true;                   // one-sweep KV: records as the ping-pong copy (RSORT_AOS_TMP)
     uint32_t* tmp2 = nullptr;              // one-sweep KV: second records buffer (RSORT_RECS2=0: none)
     bool keys_cfg = true;                  // keys-only 512x32 tiles (RSORT_KEYS_CFG=0: 1024x16)
+    int kv_cfg = 0;                        // one-sweep KV tile configuration (RSORT_KV_CFG)
     int huge_tiles = 0;                    // one-sweep KV: 24K-record tiles (RSORT_HUGE=1: every
                                            // pass; 2: the records -> arrays pass only)
     bool fused_check = true;               // one-sweep check_order: passes > 0 check their input
@@ -162,6 +180,12 @@ struct rs_plan {
     uint32_t ptot_off[16] = {};    // offset of pass i's totals in ptot
     uint32_t* tickets = nullptr;   // = ptot + kTotalsMax: [16] per-pass tile tickets, [16] error
     uint32_t epoch = 0;            // tag of the last k_onesweep launch's status words
+    uint32_t spin_max = 1u << 20;  // look-back wait bound in sleeps (RSORT_SPIN_MAX; tests force 0)
+    uint32_t* host_err = nullptr;  // host-mapped error word: set by a timed-out look-back wait,
+    uint32_t* host_err_dev = nullptr;   // read + cleared by rs_plan_check / the next rs_plan_sort
+    hipEvent_t done = nullptr;     // recorded after every sort (rs_plan_check waits for it)
+    bool done_recorded = false;
+    int selftest = -1;             // lane-order self-test of this device: 1 passed, 0 failed
     uint32_t cus = 256;
     uint64_t workspace = 0;
     KernelTimer timer;
@@ -170,6 +194,7 @@ struct rs_plan {
 struct rs_scan_plan {
     int device = 0;
     uint64_t count = 0;
+    uint32_t threads = 256;       // workgroup_x * workgroup_y (reference dispatch-chain shape)
     uint32_t* sums = nullptr;     // [kScanMaxGrid]
 };
 
@@ -257,7 +282,7 @@ void launch_onesweep_t(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint3
     hipLaunchKernelGGL(kern, dim3(grid), dim3(BLOCK), 0, s, ik, iv, ok, ov, n, shift, mask, ntiles,
                        p->ptot + p->ptot_off[pass], p->status, p->tickets + pass,
                        p->tickets + 16, ntot, nshift, nmask, p->epoch, gate, pass, chk,
-                       full_mask(p->bit_count));
+                       full_mask(p->bit_count), p->spin_max, p->host_err_dev);
 }
 
 template <int R, int BLOCK, int KPT, int L, int LO, int SR>
@@ -352,6 +377,20 @@ rs_status run_pass(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint32_t*
         (Lin == rs::LAYOUT_SOA ||
          (Lin == rs::LAYOUT_AOS && (ik == p->tmp_k || (p->tmp2 && ik == p->tmp2)))))
         return run_pass_cfg<8, kHuge.block, kHuge.kpt, false, 2>(p, ik, iv, ok, ov, n, shift, w, LL, gate, pass, kHuge.max_grid, onesweep, s);
+    // staging rounds (SR > 1) load whole record tiles: separate arrays (clamped loads) or
+    // records from a plan-owned buffer padded to whole tiles
+    const bool whole_ok = Lin == rs::LAYOUT_SOA ||
+        (Lin == rs::LAYOUT_AOS && (ik == p->tmp_k || (p->tmp2 && ik == p->tmp2)));
+    if (R == 8 && onesweep && Lin != rs::LAYOUT_KEYS && p->kv_cfg > 0) {
+        switch (p->kv_cfg) {
+            case 1: return run_pass_cfg<8, kKv512x16.block, kKv512x16.kpt>(p, ik, iv, ok, ov, n, shift, w, LL, gate, pass, kKv512x16.max_grid, onesweep, s);
+            case 2: if (whole_ok) return run_pass_cfg<8, kKv512x32.block, kKv512x32.kpt, false, 2>(p, ik, iv, ok, ov, n, shift, w, LL, gate, pass, kKv512x32.max_grid, onesweep, s); break;
+            case 3: if (whole_ok) return run_pass_cfg<8, kKv256x32.block, kKv256x32.kpt, false, 2>(p, ik, iv, ok, ov, n, shift, w, LL, gate, pass, kKv256x32.max_grid, onesweep, s); break;
+            case 4: if (whole_ok) return run_pass_cfg<8, kKv512x24.block, kKv512x24.kpt, false, 2>(p, ik, iv, ok, ov, n, shift, w, LL, gate, pass, kKv512x24.max_grid, onesweep, s); break;
+            default: break;
+        }
+        return run_pass_cfg<8, kKv512x16.block, kKv512x16.kpt>(p, ik, iv, ok, ov, n, shift, w, LL, gate, pass, kKv512x16.max_grid, onesweep, s);
+    }
     if (R == 8 && LL == layout_pair(rs::LAYOUT_KEYS, rs::LAYOUT_KEYS) && p->keys_cfg)
         return run_pass_cfg<8, kLargeKeys.block, kLargeKeys.kpt, true>(p, ik, iv, ok, ov, n, shift, w, LL, gate, pass, kLargeKeys.max_grid, onesweep, s);
     if (R == 2) return run_pass_cfg<2, kLarge.block, kLarge.kpt>(p, ik, iv, ok, ov, n, shift, w, LL, gate, pass, kLarge.max_grid, onesweep, s);
@@ -392,6 +431,49 @@ bool use_onesweep(const rs_plan* p, uint64_t n) {
     return p->layout != rs::LAYOUT_KEYS && !use_small_tiles(n);
 }
 
+// Lane-order self-test of the device's LDS atomics (k_lane_order_selftest), once per device
+// per process: 1 passed, 0 failed (plans then rank with RANK_BALLOT), -1 could not run.
+// RSORT_SELFTEST=fail simulates a failure (tests), RSORT_SELFTEST=0 skips it (counts as passed).
+int lane_order_selftest(int dev) {
+    static std::mutex mu;
+    static std::map<int, int> done;
+    const char* env = getenv("RSORT_SELFTEST");
+    if (env && strcmp(env, "fail") == 0) return 0;
+    if (env && strcmp(env, "0") == 0) return 1;
+    std::lock_guard<std::mutex> lock(mu);
+    auto it = done.find(dev);
+    if (it != done.end()) return it->second;
+    int result = -1;
+    uint32_t* bad = nullptr;
+    hipStream_t s = nullptr;
+    if (hipMalloc((void**)&bad, 4) == hipSuccess &&
+        hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess &&
+        hipMemsetAsync(bad, 0, 4, s) == hipSuccess) {
+        hipLaunchKernelGGL(rs::k_lane_order_selftest, dim3(256), dim3(rs::kBlock), 0, s, 256u, bad);
+        uint32_t h = 1;
+        if (hipGetLastError() == hipSuccess &&
+            hipMemcpyAsync(&h, bad, 4, hipMemcpyDeviceToHost, s) == hipSuccess &&
+            hipStreamSynchronize(s) == hipSuccess)
+            result = h == 0 ? 1 : 0;
+    }
+    if (s) (void)hipStreamDestroy(s);
+    if (bad) (void)hipFree(bad);
+    if (result >= 0) done[dev] = result;
+    return result;
+}
+
+// A previous sort on this plan hit a device-side failure (look-back wait timeout): report it
+// once and clear it.
+rs_status take_device_error(rs_plan* p, const char* what) {
+    if (!p->host_err) return RS_OK;
+    const uint32_t e = __atomic_exchange_n(p->host_err, 0u, __ATOMIC_ACQ_REL);
+    if (e == 0u) return RS_OK;
+    return fail(RS_ERR_DEVICE,
+                "%s: an earlier sort on this plan failed on the device (error word 0x%x: a "
+                "look-back wait of the one-sweep pass timed out); that sort's output is invalid",
+                what, e);
+}
+
 }  // namespace
 
 // ============================================================================================
@@ -406,6 +488,7 @@ RS_EXPORT const char* rs_status_string(rs_status s) {
         case RS_ERR_HIP: return "HIP runtime error";
         case RS_ERR_OUT_OF_MEMORY: return "out of device memory";
         case RS_ERR_CAPACITY: return "count exceeds plan capacity";
+        case RS_ERR_DEVICE: return "device-side failure (a sort's result is invalid)";
     }
     return "unknown status";
 }
@@ -451,9 +534,9 @@ RS_EXPORT rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out) {
     if (const char* r2 = getenv("RSORT_RECS2")) recs2 = strcmp(r2, "0") != 0;
     if (const char* kc = getenv("RSORT_KEYS_CFG")) p->keys_cfg = strcmp(kc, "0") != 0;
     if (const char* hg = getenv("RSORT_HUGE")) p->huge_tiles = atoi(hg);
+    if (const char* kc = getenv("RSORT_KV_CFG")) p->kv_cfg = atoi(kc);
     if (const char* fc = getenv("RSORT_FUSED_CHECK")) p->fused_check = strcmp(fc, "0") != 0;
-    if (const char* rk = getenv("RSORT_RANK"))
-        p->rank_mode = (strcmp(rk, "ballot") == 0) ? rs::RANK_BALLOT : rs::RANK_LDS_ATOMIC;
+    if (const char* sm = getenv("RSORT_SPIN_MAX")) p->spin_max = (uint32_t)strtoul(sm, nullptr, 10);
     // Even number of passes so the result lands in the caller's buffers, like the reference's
     // bit_count/2 passes with ping-pong on bit % 4 (AbstractRadixSortKernel.ts:93-107).
     uint32_t P = (d.bit_count + rb - 1) / rb;
@@ -468,6 +551,12 @@ RS_EXPORT rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out) {
 
     DeviceGuard guard(d.device);
     auto cleanup = [&](rs_status s) { rs_plan_destroy(p); return s; };
+    // stable ranking: lane-ordered LDS atomics where the device passes the self-test, else the
+    // architecture-guaranteed ballot ranking; RSORT_RANK=ballot|atomic overrides
+    p->selftest = lane_order_selftest(d.device);
+    p->rank_mode = p->selftest == 1 ? rs::RANK_LDS_ATOMIC : rs::RANK_BALLOT;
+    if (const char* rk = getenv("RSORT_RANK"))
+        p->rank_mode = (strcmp(rk, "ballot") == 0) ? rs::RANK_BALLOT : rs::RANK_LDS_ATOMIC;
     auto alloc = [&](uint32_t** ptr, uint64_t bytes) -> hipError_t {
         if (bytes == 0) bytes = 4;
         p->workspace += bytes;
@@ -480,7 +569,7 @@ RS_EXPORT rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out) {
     }
     // look-back status words: one per (tile, digit) of the finest tile configuration in use
     const uint64_t max_tiles = std::max<uint64_t>(
-        1, std::max<uint64_t>((d.count + kLarge.tile - 1) / kLarge.tile,
+        1, std::max<uint64_t>((d.count + kMinOnesweepTile - 1) / kMinOnesweepTile,
                               (std::min<uint64_t>(d.count, RS_SMALL_MAX) + kSmall.tile - 1) / kSmall.tile));
     p->status_words = p->onesweep_mode != 0 ? max_tiles * 256 : 1;
     hipError_t e;
@@ -488,7 +577,7 @@ RS_EXPORT rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out) {
     // path, or tmp_k / tmp_v halves (tmp_v = tmp_k + count) for the histogram path
     // records buffers are padded to whole kHuge tiles (k_onesweep with staging rounds reads
     // whole tiles)
-    const uint64_t padded = (d.count + kHuge.tile - 1) / kHuge.tile * kHuge.tile;
+    const uint64_t padded = (d.count + kRecPad - 1) / kRecPad * kRecPad;
     if ((p->layout == rs::LAYOUT_KEYS && (e = alloc(&p->tmp_k, 4 * d.count)) != hipSuccess) ||
         (p->layout != rs::LAYOUT_KEYS && (e = alloc(&p->tmp_k, 8 * padded)) != hipSuccess) ||
         (p->layout == rs::LAYOUT_SOA && p->onesweep_mode != 0 && p->aos_tmp && recs2 &&
@@ -501,6 +590,11 @@ RS_EXPORT rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out) {
         return cleanup(fail(e == hipErrorOutOfMemory ? RS_ERR_OUT_OF_MEMORY : RS_ERR_HIP,
                             "rs_plan_create: hipMalloc failed: %s", hipGetErrorString(e)));
     p->tickets = p->ptot + rs::kTotalsMax;   // [16] tickets, [16] error word
+    if ((e = hipHostMalloc((void**)&p->host_err, 4, hipHostMallocMapped)) != hipSuccess ||
+        (e = hipHostGetDevicePointer((void**)&p->host_err_dev, p->host_err, 0)) != hipSuccess ||
+        (e = hipEventCreateWithFlags(&p->done, hipEventDisableTiming)) != hipSuccess)
+        return cleanup(fail(RS_ERR_HIP, "rs_plan_create: host error word: %s", hipGetErrorString(e)));
+    *p->host_err = 0u;
     if (p->layout == rs::LAYOUT_SOA) p->tmp_v = p->tmp_k + d.count;
     if ((e = hipMemset(p->ptot, 0, 4ull * (rs::kTotalsMax + 32))) != hipSuccess ||
         (e = hipMemset(p->status, 0, 8ull * p->status_words)) != hipSuccess)
@@ -520,6 +614,8 @@ RS_EXPORT void rs_plan_destroy(rs_plan* p) {
     (void)hipFree(p->flags);
     (void)hipFree(p->ptot);
     (void)hipFree(p->status);
+    if (p->host_err) (void)hipHostFree(p->host_err);
+    if (p->done) (void)hipEventDestroy(p->done);
     delete p;
 }
 
@@ -531,7 +627,8 @@ static rs_status enqueue_sort(rs_plan* p, uint32_t* uk, uint32_t* uv, uint64_t n
     if (p->check_order) HIP_TRY(hipMemsetAsync(p->flags, 0, 16 * 4, s));
     const bool onesweep = use_onesweep(p, n);
     if (onesweep) {
-        HIP_TRY(hipMemsetAsync(p->ptot, 0, 4ull * (rs::kTotalsMax + 16), s));   // totals + tickets
+        // totals, tickets and the device error word (a timeout never outlives its sort)
+        HIP_TRY(hipMemsetAsync(p->ptot, 0, 4ull * (rs::kTotalsMax + 32), s));
         // pass 0's digit totals from one read of the input; every later pass's totals are
         // counted by the pass before it (k_onesweep's ntot)
         rs::PassList pl{};
@@ -629,8 +726,20 @@ RS_EXPORT rs_status rs_plan_sort_n(rs_plan* p, void* keys, void* values, uint64_
     const uint32_t n32 = (uint32_t)n;
     uint32_t* uk = (uint32_t*)keys;
     uint32_t* uv = L == rs::LAYOUT_SOA ? (uint32_t*)values : nullptr;
-    if (n <= kTinyMax) return run_tiny(p, uk, uv, n32, s);   // one launch; check_order moot
-    return enqueue_sort(p, uk, uv, n, s);
+    if (rs_status st = take_device_error(p, "rs_plan_sort")) return st;
+    const rs_status st = n <= kTinyMax ? run_tiny(p, uk, uv, n32, s)   // one launch; check_order moot
+                                       : enqueue_sort(p, uk, uv, n, s);
+    if (st != RS_OK) return st;
+    HIP_TRY(hipEventRecord(p->done, s));
+    p->done_recorded = true;
+    return RS_OK;
+}
+
+RS_EXPORT rs_status rs_plan_check(rs_plan* p) {
+    if (!p) return fail(RS_ERR_INVALID_ARG, "rs_plan_check: null plan");
+    DeviceGuard guard(p->desc.device);
+    if (p->done_recorded) HIP_TRY(hipEventSynchronize(p->done));
+    return take_device_error(p, "rs_plan_check");
 }
 
 RS_EXPORT rs_status rs_plan_sort(rs_plan* p, void* keys, void* values, void* stream) {
@@ -682,7 +791,9 @@ RS_EXPORT rs_status rs_plan_partition_totals(rs_plan* p, const void* in_keys, co
     hipStream_t s = (hipStream_t)stream;
     // run as the plan's last pass: no next-pass totals, its own ticket and totals slot
     const int pass = (int)p->passes - 1;
+    if (rs_status st = take_device_error(p, "rs_plan_partition_totals")) return st;
     HIP_TRY(hipMemsetAsync(p->tickets + pass, 0, 4, s));
+    HIP_TRY(hipMemsetAsync(p->tickets + 16, 0, 4, s));
     HIP_TRY(hipMemcpyAsync(p->ptot + p->ptot_off[pass], d_totals, 4u << bits,
                            hipMemcpyDeviceToDevice, s));
     const int L = p->layout;
@@ -696,8 +807,17 @@ RS_EXPORT rs_status rs_plan_device_errors(rs_plan* p, uint32_t* errors) {
     DeviceGuard guard(p->desc.device);
     HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipMemcpy(errors, p->tickets + 16, 4, hipMemcpyDeviceToHost));
+    *errors |= p->host_err ? __atomic_load_n(p->host_err, __ATOMIC_ACQUIRE) : 0u;
     return RS_OK;
 }
+
+#if RS_STAMPS
+// Diagnostic builds only (not in rsort.h): device buffer for k_onesweep's phase stamps.
+RS_EXPORT rs_status rs_debug_set_stamps(void* dev_ptr) {
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(rs::g_rs_stamps), &dev_ptr, sizeof(dev_ptr)));
+    return RS_OK;
+}
+#endif
 
 RS_EXPORT rs_status rs_plan_info_get(const rs_plan* p, rs_plan_info* info) {
     if (!p || !info) return fail(RS_ERR_INVALID_ARG, "rs_plan_info_get: null argument");
@@ -709,6 +829,14 @@ RS_EXPORT rs_status rs_plan_info_get(const rs_plan* p, rs_plan_info* info) {
     info->grid_blocks = p->capacity <= kTinyMax ? 1u
         : (uint32_t)std::min<uint64_t>((p->capacity + c.tile - 1) / c.tile, c.max_grid);
     info->workspace_bytes = p->workspace;
+    info->rank_mode = (uint32_t)p->rank_mode;
+    info->lane_order_selftest = p->selftest;
+    return RS_OK;
+}
+
+RS_EXPORT rs_status rs_plan_set_wait_limit(rs_plan* p, uint32_t sleeps) {
+    if (!p) return fail(RS_ERR_INVALID_ARG, "rs_plan_set_wait_limit: null plan");
+    p->spin_max = sleeps;
     return RS_OK;
 }
 
@@ -771,6 +899,7 @@ RS_EXPORT rs_status rs_scan_plan_create(int32_t device, uint64_t count, uint32_t
     if (!p) return fail(RS_ERR_OUT_OF_MEMORY, "host allocation failed");
     p->device = device;
     p->count = count;
+    p->threads = (uint32_t)T;
     DeviceGuard guard(device);
     hipError_t e = hipMalloc((void**)&p->sums, 4ull * kScanMaxGrid);
     if (e != hipSuccess) {
@@ -781,23 +910,70 @@ RS_EXPORT rs_status rs_scan_plan_create(int32_t device, uint64_t count, uint32_t
     return RS_OK;
 }
 
+static rs_status scan_run(rs_scan_plan* p, void* data, const uint32_t* ind, hipStream_t s) {
+    const uint64_t n = p->count;
+    const Geometry geo = geometry(n, kScanTile, kScanMaxGrid);
+    hipLaunchKernelGGL(rs::k_chunk_sums<kScanTile>, dim3(geo.grid), dim3(rs::kBlock), 0, s,
+                       (const uint32_t*)data, (uint32_t)n, geo.base, geo.extra, p->sums, ind);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(rs::k_scan_small, dim3(1), dim3(rs::kBlock), 0, s, p->sums, geo.grid, ind);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(rs::k_chunk_rescan<kScanTile>, dim3(geo.grid), dim3(rs::kBlock), 0, s,
+                       (uint32_t*)data, (uint32_t)n, geo.base, geo.extra, (const uint32_t*)p->sums,
+                       ind);
+    HIP_TRY(hipGetLastError());
+    return RS_OK;
+}
+
 RS_EXPORT rs_status rs_scan_plan_run(rs_scan_plan* p, void* data, void* stream) {
     if (!p) return fail(RS_ERR_INVALID_ARG, "rs_scan_plan_run: null plan");
     if (p->count == 0) return RS_OK;
     if (!data) return fail(RS_ERR_INVALID_ARG, "rs_scan_plan_run: null data");
     DeviceGuard guard(p->device);
-    hipStream_t s = (hipStream_t)stream;
-    const uint32_t n = (uint32_t)p->count;
-    const Geometry geo = geometry(n, kScanTile, kScanMaxGrid);
-    hipLaunchKernelGGL(rs::k_chunk_sums<kScanTile>, dim3(geo.grid), dim3(rs::kBlock), 0, s,
-                       (const uint32_t*)data, n, geo.base, geo.extra, p->sums);
-    HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(rs::k_scan_small, dim3(1), dim3(rs::kBlock), 0, s, p->sums, geo.grid);
-    HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(rs::k_chunk_rescan<kScanTile>, dim3(geo.grid), dim3(rs::kBlock), 0, s,
-                       (uint32_t*)data, n, geo.base, geo.extra, (const uint32_t*)p->sums);
-    HIP_TRY(hipGetLastError());
-    return RS_OK;
+    return scan_run(p, data, nullptr, (hipStream_t)stream);
+}
+
+RS_EXPORT rs_status rs_scan_plan_run_indirect(rs_scan_plan* p, void* data,
+                                              const void* dispatch_size_buffer, uint64_t offset,
+                                              void* stream) {
+    if (!p) return fail(RS_ERR_INVALID_ARG, "rs_scan_plan_run_indirect: null plan");
+    if (!dispatch_size_buffer)
+        return fail(RS_ERR_INVALID_ARG, "rs_scan_plan_run_indirect: null dispatch size buffer");
+    if (offset % 4)
+        return fail(RS_ERR_INVALID_ARG, "rs_scan_plan_run_indirect: offset %llu is not a multiple of 4",
+                    (unsigned long long)offset);
+    if (p->count == 0) return RS_OK;
+    if (!data) return fail(RS_ERR_INVALID_ARG, "rs_scan_plan_run_indirect: null data");
+    DeviceGuard guard(p->device);
+    return scan_run(p, data, (const uint32_t*)((const char*)dispatch_size_buffer + offset),
+                    (hipStream_t)stream);
+}
+
+RS_EXPORT uint32_t rs_scan_plan_dispatch_chain(const rs_scan_plan* p, uint32_t* out,
+                                               uint32_t max_words) {
+    // the reference's chain for T = workgroup_x * workgroup_y threads, 2T items per workgroup:
+    // scan(count) [+ chain(workgroups) + add_block_sums] (PrefixSumKernel.ts:45-137), one
+    // (x, y, 1) triple per pipeline; findOptimalDispatchSize folds x > 65535 (the default
+    // maxComputeWorkgroupsPerDimension) into x = floor(sqrt(wc)), y = ceil(wc / x) (utils.ts:8-23)
+    if (!p) return 0;
+    std::vector<uint32_t> chain;
+    const uint64_t T = p->threads;
+    std::function<void(uint64_t)> rec = [&](uint64_t count) {
+        const uint64_t wc = (count + 2 * T - 1) / (2 * T);
+        uint64_t x = wc, y = 1;
+        if (wc > 65535) {
+            x = (uint64_t)std::floor(std::sqrt((double)wc));
+            y = (wc + x - 1) / x;
+        }
+        chain.insert(chain.end(), {(uint32_t)x, (uint32_t)y, 1u});
+        if (wc > 1) {
+            rec(wc);
+            chain.insert(chain.end(), {(uint32_t)x, (uint32_t)y, 1u});
+        }
+    };
+    rec(std::max<uint64_t>(p->count, 1));
+    for (uint32_t i = 0; i < max_words && i < chain.size(); ++i) out[i] = chain[i];
+    return (uint32_t)chain.size();
 }
 
 RS_EXPORT void rs_scan_plan_destroy(rs_scan_plan* p) {

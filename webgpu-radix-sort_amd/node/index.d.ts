@@ -10,6 +10,13 @@ export declare const GPUBufferUsage: {
 export declare const GPUMapMode: { readonly READ: number; readonly WRITE: number };
 
 export interface WorkgroupSize { x: number; y: number; }
+export interface PlanInfo {
+  passes: number; digitBits: number[]; tileKeys: number; gridBlocks: number; workspaceBytes: number;
+  /** in-wave stable ranking: lane-ordered LDS atomics, or ballot-match (self-test fallback) */
+  rankMode: 'lds_atomic' | 'ballot';
+  /** the device's LDS-atomic lane-order self-test: 1 passed, 0 failed, -1 not run */
+  laneOrderSelftest: number;
+}
 
 export declare class DeviceBuffer {
   readonly device: Device;
@@ -102,9 +109,11 @@ export declare class RadixSortKernel {
   readonly workgroupSize: WorkgroupSize;
   readonly threadsPerWorkgroup: number;
   readonly workgroupCount: number;
-  readonly info: { passes: number; digitBits: number[]; tileKeys: number; gridBlocks: number; workspaceBytes: number };
+  readonly info: PlanInfo;
   /** Records the sort into `pass` (runs at queue.submit) or runs it immediately. */
   dispatch(pass?: ComputePass): void;
+  /** Waits for the last sort; throws if a sort failed on the device since the last check. */
+  check(): void;
   destroy(): void;
 }
 export declare class RadixSortBufferKernel extends RadixSortKernel {}
@@ -126,13 +135,16 @@ export declare class RadixSortTextureKernel {
   readonly textures: { read: DeviceTexture };
   readonly hasValues: true;
   readonly count: number;
-  readonly info: { passes: number; digitBits: number[]; tileKeys: number; gridBlocks: number; workspaceBytes: number };
+  readonly info: PlanInfo;
   dispatch(pass?: ComputePass): void;
+  check(): void;
   destroy(): void;
 }
 
 export declare class PrefixSumKernel {
   constructor(options: { device?: Device; data: DeviceBuffer; count: number; workgroupSize?: WorkgroupSize; avoidBankConflicts?: boolean });
-  dispatch(pass?: ComputePass): void;
+  /** Indirect when dispatchSizeBuffer is given (PrefixSumKernel.ts:147-158). */
+  dispatch(pass?: ComputePass, dispatchSizeBuffer?: DeviceBuffer, offset?: number): void;
+  getDispatchChain(): number[];
   destroy(): void;
 }

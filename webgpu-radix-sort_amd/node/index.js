@@ -59,7 +59,12 @@ class DeviceBuffer {
 
   mapAsync(mode) {
     if (!this.host) return Promise.reject(new Error('mapAsync needs a MAP_READ/MAP_WRITE buffer'));
-    addon.streamSynchronize(this.device.stream);   // results of submitted work are complete
+    try {
+      addon.streamSynchronize(this.device.stream);   // results of submitted work are complete
+      this.device.checkPlans();                      // and none of them failed on the device
+    } catch (e) {
+      return Promise.reject(e);
+    }
     this.mapped = this.hostData;
     return Promise.resolve(mode);
   }
@@ -203,7 +208,15 @@ class Queue {
       : new Uint8Array(data);
     addon.h2d(buffer.ptr + BigInt(offset), bytes, this.device.stream);
   }
-  onSubmittedWorkDone() { addon.streamSynchronize(this.device.stream); return Promise.resolve(); }
+  onSubmittedWorkDone() {
+    try {
+      addon.streamSynchronize(this.device.stream);
+      this.device.checkPlans();
+    } catch (e) {
+      return Promise.reject(e);
+    }
+    return Promise.resolve();
+  }
 }
 
 class Device {
@@ -221,6 +234,11 @@ class Device {
       maxBufferSize: 2 ** 34,
     });
   }
+  // Sort plans created on this device: their device-side failures (rs_plan_check) surface at the
+  // synchronising points (mapAsync, onSubmittedWorkDone), as a rejected promise.
+  registerPlan(kernel) { (this._plans || (this._plans = new Set())).add(kernel); }
+  unregisterPlan(kernel) { if (this._plans) this._plans.delete(kernel); }
+  checkPlans() { if (this._plans) for (const k of this._plans) k.check(); }
   createBuffer(desc) { return new DeviceBuffer(this, desc); }
   createTexture(desc) { return new DeviceTexture(this, desc); }
   createQuerySet(desc) { return new QuerySet(this, desc); }
@@ -308,9 +326,14 @@ class RadixSortKernel {
       flags,
       radixBits: this.radixBits,
     });
+    if (this.device && this.device.registerPlan) this.device.registerPlan(this);
   }
 
   get threadsPerWorkgroup() { return this.workgroupSize.x * (this.workgroupSize.y || 1); }
+
+  /** Wait for the last sort; throws if a sort of this kernel failed on the device since the
+   * last check (its output is invalid; rs_plan_check). */
+  check() { if (this._plan) addon.planCheck(this._plan); }
 
   get workgroupCount() { return Math.ceil(this.count / this.threadsPerWorkgroup); }
 
@@ -323,6 +346,7 @@ class RadixSortKernel {
   }
 
   destroy() {
+    if (this.device && this.device.unregisterPlan) this.device.unregisterPlan(this);
     if (this._plan) addon.planDestroy(this._plan);
     this._plan = null;
   }
@@ -371,9 +395,12 @@ class RadixSortTextureKernel {
         | (this.avoidBankConflicts ? addon.FLAG_AVOID_BANK_CONFLICTS : 0),
       radixBits: this.radixBits,
     });
+    if (this.device && this.device.registerPlan) this.device.registerPlan(this);
   }
 
   get hasValues() { return true; }
+
+  check() { if (this._plan) addon.planCheck(this._plan); }
 
   get info() { return addon.planInfo(this._plan); }
 
@@ -383,6 +410,7 @@ class RadixSortTextureKernel {
   }
 
   destroy() {
+    if (this.device && this.device.unregisterPlan) this.device.unregisterPlan(this);
     if (this._plan) addon.planDestroy(this._plan);
     this._plan = null;
   }
@@ -404,11 +432,23 @@ class PrefixSumKernel {
       this.avoidBankConflicts ? addon.FLAG_AVOID_BANK_CONFLICTS : 0);
   }
 
-  dispatch(pass, dispatchSizeBuffer) {
-    if (dispatchSizeBuffer) throw new Error('indirect dispatch buffers are not used by the HIP backend');
+  /**
+   * PrefixSumKernel.ts:147-158.  With dispatchSizeBuffer (a device buffer of u32 (x, y, z)
+   * triples, e.g. getDispatchChain() written to it) the dispatch is indirect: the scan runs iff
+   * the triple at byte `offset` has no zero entry, decided on the device.
+   */
+  dispatch(pass, dispatchSizeBuffer, offset = 0) {
     const stream = this.device ? this.device.stream : null;
-    recordOrRun(pass, () => addon.scanPlanRun(this._plan, this._data, stream));
+    if (!dispatchSizeBuffer) {
+      recordOrRun(pass, () => addon.scanPlanRun(this._plan, this._data, stream));
+      return;
+    }
+    const buf = bufferPtr(dispatchSizeBuffer, 'dispatchSizeBuffer');
+    recordOrRun(pass, () => addon.scanPlanRunIndirect(this._plan, this._data, buf, offset, stream));
   }
+
+  /** PrefixSumKernel.getDispatchChain (PrefixSumKernel.ts:135-137): [x, y, 1] per pipeline. */
+  getDispatchChain() { return addon.scanPlanDispatchChain(this._plan); }
 
   destroy() {
     if (this._plan) addon.scanPlanDestroy(this._plan);

@@ -35,17 +35,21 @@ napi_value throw_status(napi_env env, rs_status st, const char* what) {
         if (st_ != RS_OK) return throw_status((env), st_, what); \
     } while (0)
 
+// A non-negative integer: BigInt (must fit u64 exactly: negative or wider BigInts are rejected),
+// a Number (integral, >= 0, < 2^53), or null/undefined (0).
 bool get_u64(napi_env env, napi_value v, uint64_t* out) {
     napi_valuetype t;
     if (napi_typeof(env, v, &t) != napi_ok) return false;
     if (t == napi_null || t == napi_undefined) { *out = 0; return true; }
     if (t == napi_bigint) {
-        bool lossless = true;
-        return napi_get_value_bigint_uint64(env, v, out, &lossless) == napi_ok;
+        bool lossless = false;
+        return napi_get_value_bigint_uint64(env, v, out, &lossless) == napi_ok && lossless;
     }
     if (t == napi_number) {
         double d = 0;
-        if (napi_get_value_double(env, v, &d) != napi_ok || d < 0) return false;
+        if (napi_get_value_double(env, v, &d) != napi_ok || !(d >= 0) || d >= 9007199254740992.0 ||
+            d != (double)(uint64_t)d)
+            return false;
         *out = (uint64_t)d;
         return true;
     }
@@ -60,7 +64,7 @@ bool get_u32_prop(napi_env env, napi_value obj, const char* key, uint32_t* out, 
     napi_value v;
     if (napi_get_named_property(env, obj, key, &v) != napi_ok) return false;
     uint64_t x = 0;
-    if (!get_u64(env, v, &x)) return false;
+    if (!get_u64(env, v, &x) || x > 0xFFFFFFFFull) return false;   // no silent truncation
     *out = (uint32_t)x;
     return true;
 }
@@ -85,6 +89,19 @@ void* ptr_of(napi_env env, napi_value v, bool* ok) {
     *ok = get_u64(env, v, &x);
     return (void*)(uintptr_t)x;
 }
+
+// Pointer / stream arguments: every one must convert, else TypeError (a bad argument never
+// silently becomes NULL).
+#define PTR_ARG(env, var, value, what)                                   \
+    void* var;                                                           \
+    do {                                                                 \
+        bool ok_;                                                        \
+        var = ptr_of((env), (value), &ok_);                              \
+        if (!ok_) {                                                      \
+            napi_throw_type_error((env), nullptr, what);                 \
+            return nullptr;                                              \
+        }                                                                \
+    } while (0)
 
 // ---- plans as externals ------------------------------------------------------------------
 struct PlanBox { rs_plan* plan; };
@@ -141,9 +158,7 @@ napi_value Malloc(napi_env env, napi_callback_info info) {
 napi_value Free(napi_env env, napi_callback_info info) {
     napi_value a[1];
     if (!args(env, info, a)) return nullptr;
-    bool ok;
-    void* p = ptr_of(env, a[0], &ok);
-    if (!ok) return napi_throw_type_error(env, nullptr, "free(ptr)"), nullptr;
+    PTR_ARG(env, p, a[0], "free(ptr)");
     RS_CALL(env, rs_free(p), "free");
     return nullptr;
 }
@@ -175,13 +190,12 @@ bool host_span(napi_env env, napi_value v, void** data, size_t* bytes) {
 napi_value H2D(napi_env env, napi_callback_info info) {
     napi_value a[3];
     if (!args(env, info, a)) return nullptr;
-    bool ok;
-    void* dst = ptr_of(env, a[0], &ok);
+    PTR_ARG(env, dst, a[0], "h2d(ptr, typedArray, stream)");
     void* src = nullptr;
     size_t bytes = 0;
-    if (!ok || !host_span(env, a[1], &src, &bytes))
+    if (!host_span(env, a[1], &src, &bytes))
         return napi_throw_type_error(env, nullptr, "h2d(ptr, typedArray)"), nullptr;
-    void* stream = ptr_of(env, a[2], &ok);
+    PTR_ARG(env, stream, a[2], "h2d: bad stream");
     RS_CALL(env, rs_memcpy_h2d(dst, src, bytes, stream), "h2d");
     RS_CALL(env, rs_stream_synchronize(stream), "h2d");
     return nullptr;
@@ -192,11 +206,10 @@ napi_value D2H(napi_env env, napi_callback_info info) {
     if (!args(env, info, a)) return nullptr;
     void* dst = nullptr;
     size_t bytes = 0;
-    bool ok;
     if (!host_span(env, a[0], &dst, &bytes))
         return napi_throw_type_error(env, nullptr, "d2h(typedArray, ptr)"), nullptr;
-    void* src = ptr_of(env, a[1], &ok);
-    void* stream = ptr_of(env, a[2], &ok);
+    PTR_ARG(env, src, a[1], "d2h(typedArray, ptr, stream): bad ptr");
+    PTR_ARG(env, stream, a[2], "d2h: bad stream");
     RS_CALL(env, rs_memcpy_d2h(dst, src, bytes, stream), "d2h");
     return nullptr;
 }
@@ -204,14 +217,11 @@ napi_value D2H(napi_env env, napi_callback_info info) {
 napi_value D2D(napi_env env, napi_callback_info info) {
     napi_value a[4];
     if (!args(env, info, a)) return nullptr;
-    bool ok1, ok2, ok3;
-    void* dst = ptr_of(env, a[0], &ok1);
-    void* src = ptr_of(env, a[1], &ok2);
+    PTR_ARG(env, dst, a[0], "d2d(dst, src, bytes, stream): bad dst");
+    PTR_ARG(env, src, a[1], "d2d(dst, src, bytes, stream): bad src");
     uint64_t bytes = 0;
-    ok3 = get_u64(env, a[2], &bytes);
-    bool ok4;
-    void* stream = ptr_of(env, a[3], &ok4);
-    if (!ok1 || !ok2 || !ok3) return napi_throw_type_error(env, nullptr, "d2d(dst, src, bytes, stream)"), nullptr;
+    if (!get_u64(env, a[2], &bytes)) return napi_throw_type_error(env, nullptr, "d2d: bad bytes"), nullptr;
+    PTR_ARG(env, stream, a[3], "d2d: bad stream");
     RS_CALL(env, rs_memcpy_d2d(dst, src, bytes, stream), "d2d");
     return nullptr;
 }
@@ -220,7 +230,8 @@ napi_value StreamCreate(napi_env env, napi_callback_info info) {
     napi_value a[1];
     if (!args(env, info, a)) return nullptr;
     uint64_t dev = 0;
-    get_u64(env, a[0], &dev);
+    if (!get_u64(env, a[0], &dev) || dev > 0x7FFFFFFF)
+        return napi_throw_type_error(env, nullptr, "streamCreate(device)"), nullptr;
     void* s = nullptr;
     RS_CALL(env, rs_stream_create((int32_t)dev, &s), "streamCreate");
     return bigint(env, (uint64_t)(uintptr_t)s);
@@ -229,8 +240,7 @@ napi_value StreamCreate(napi_env env, napi_callback_info info) {
 napi_value StreamDestroy(napi_env env, napi_callback_info info) {
     napi_value a[1];
     if (!args(env, info, a)) return nullptr;
-    bool ok;
-    void* s = ptr_of(env, a[0], &ok);
+    PTR_ARG(env, s, a[0], "streamDestroy(stream)");
     RS_CALL(env, rs_stream_destroy(s), "streamDestroy");
     return nullptr;
 }
@@ -238,8 +248,7 @@ napi_value StreamDestroy(napi_env env, napi_callback_info info) {
 napi_value StreamSynchronize(napi_env env, napi_callback_info info) {
     napi_value a[1];
     if (!args(env, info, a)) return nullptr;
-    bool ok;
-    void* s = ptr_of(env, a[0], &ok);
+    PTR_ARG(env, s, a[0], "streamSynchronize(stream)");
     RS_CALL(env, rs_stream_synchronize(s), "streamSynchronize");
     return nullptr;
 }
@@ -256,9 +265,8 @@ napi_value EventCreate(napi_env env, napi_callback_info info) {
 napi_value EventRecord(napi_env env, napi_callback_info info) {
     napi_value a[2];
     if (!args(env, info, a)) return nullptr;
-    bool ok;
-    void* e = ptr_of(env, a[0], &ok);
-    void* s = ptr_of(env, a[1], &ok);
+    PTR_ARG(env, e, a[0], "eventRecord(event, stream): bad event");
+    PTR_ARG(env, s, a[1], "eventRecord: bad stream");
     RS_CALL(env, rs_event_record(e, s), "eventRecord");
     return nullptr;
 }
@@ -266,9 +274,8 @@ napi_value EventRecord(napi_env env, napi_callback_info info) {
 napi_value EventElapsed(napi_env env, napi_callback_info info) {
     napi_value a[2];
     if (!args(env, info, a)) return nullptr;
-    bool ok;
-    void* e0 = ptr_of(env, a[0], &ok);
-    void* e1 = ptr_of(env, a[1], &ok);
+    PTR_ARG(env, e0, a[0], "eventElapsed(a, b): bad event");
+    PTR_ARG(env, e1, a[1], "eventElapsed(a, b): bad event");
     float ms = 0.f;
     RS_CALL(env, rs_event_elapsed_ms(e0, e1, &ms), "eventElapsed");
     napi_value r;
@@ -279,8 +286,7 @@ napi_value EventElapsed(napi_env env, napi_callback_info info) {
 napi_value EventDestroy(napi_env env, napi_callback_info info) {
     napi_value a[1];
     if (!args(env, info, a)) return nullptr;
-    bool ok;
-    void* e = ptr_of(env, a[0], &ok);
+    PTR_ARG(env, e, a[0], "eventDestroy(event)");
     RS_CALL(env, rs_event_destroy(e), "eventDestroy");
     return nullptr;
 }
@@ -329,10 +335,9 @@ napi_value PlanSort(napi_env env, napi_callback_info info) {
     PlanBox* b = box_of<PlanBox>(env, a[0]);
     if (!b) return nullptr;
     if (!b->plan) return napi_throw_error(env, nullptr, "plan destroyed"), nullptr;
-    bool ok;
-    void* k = ptr_of(env, a[1], &ok);
-    void* v = ptr_of(env, a[2], &ok);
-    void* s = ptr_of(env, a[3], &ok);
+    PTR_ARG(env, k, a[1], "planSort(plan, keys, values, stream[, n]): bad keys");
+    PTR_ARG(env, v, a[2], "planSort: bad values");
+    PTR_ARG(env, s, a[3], "planSort: bad stream");
     if (argc >= 5) {
         uint64_t n = 0;
         if (!get_u64(env, a[4], &n)) return napi_throw_type_error(env, nullptr, "n"), nullptr;
@@ -366,6 +371,9 @@ napi_value PlanInfo(napi_env env, napi_callback_info info) {
     napi_create_uint32(env, inf.tile_keys, &x); napi_set_named_property(env, o, "tileKeys", x);
     napi_create_uint32(env, inf.grid_blocks, &x); napi_set_named_property(env, o, "gridBlocks", x);
     napi_create_double(env, (double)inf.workspace_bytes, &x); napi_set_named_property(env, o, "workspaceBytes", x);
+    napi_create_string_utf8(env, inf.rank_mode == 1 ? "ballot" : "lds_atomic", NAPI_AUTO_LENGTH, &x);
+    napi_set_named_property(env, o, "rankMode", x);
+    napi_create_int32(env, inf.lane_order_selftest, &x); napi_set_named_property(env, o, "laneOrderSelftest", x);
     napi_create_array_with_length(env, inf.passes, &arr);
     for (uint32_t i = 0; i < inf.passes && i < 16; ++i) {
         napi_create_uint32(env, inf.digit_bits[i], &x);
@@ -400,10 +408,54 @@ napi_value ScanPlanRun(napi_env env, napi_callback_info info) {
     if (!args(env, info, a)) return nullptr;
     ScanBox* b = box_of<ScanBox>(env, a[0]);
     if (!b || !b->plan) return napi_throw_error(env, nullptr, "plan destroyed"), nullptr;
-    bool ok;
-    void* d = ptr_of(env, a[1], &ok);
-    void* s = ptr_of(env, a[2], &ok);
+    PTR_ARG(env, d, a[1], "scanPlanRun(plan, data, stream): bad data");
+    PTR_ARG(env, s, a[2], "scanPlanRun: bad stream");
     RS_CALL(env, rs_scan_plan_run(b->plan, d, s), "dispatch");
+    return nullptr;
+}
+
+// scanPlanRunIndirect(plan, data, dispatchSizeBuffer, offsetBytes, stream)
+napi_value ScanPlanRunIndirect(napi_env env, napi_callback_info info) {
+    napi_value a[5];
+    if (!args(env, info, a)) return nullptr;
+    ScanBox* b = box_of<ScanBox>(env, a[0]);
+    if (!b || !b->plan) return napi_throw_error(env, nullptr, "plan destroyed"), nullptr;
+    PTR_ARG(env, d, a[1], "scanPlanRunIndirect: bad data");
+    PTR_ARG(env, buf, a[2], "scanPlanRunIndirect: bad dispatch size buffer");
+    uint64_t off = 0;
+    if (!get_u64(env, a[3], &off)) return napi_throw_type_error(env, nullptr, "scanPlanRunIndirect: bad offset"), nullptr;
+    PTR_ARG(env, s, a[4], "scanPlanRunIndirect: bad stream");
+    RS_CALL(env, rs_scan_plan_run_indirect(b->plan, d, buf, off, s), "dispatch");
+    return nullptr;
+}
+
+// scanPlanDispatchChain(plan) -> number[] (PrefixSumKernel.getDispatchChain)
+napi_value ScanPlanDispatchChain(napi_env env, napi_callback_info info) {
+    napi_value a[1];
+    if (!args(env, info, a)) return nullptr;
+    ScanBox* b = box_of<ScanBox>(env, a[0]);
+    if (!b || !b->plan) return napi_throw_error(env, nullptr, "plan destroyed"), nullptr;
+    const uint32_t n = rs_scan_plan_dispatch_chain(b->plan, nullptr, 0);
+    std::string buf(4 * (size_t)n, '\0');
+    uint32_t* w = reinterpret_cast<uint32_t*>(&buf[0]);
+    rs_scan_plan_dispatch_chain(b->plan, w, n);
+    napi_value arr, x;
+    napi_create_array_with_length(env, n, &arr);
+    for (uint32_t i = 0; i < n; ++i) {
+        napi_create_uint32(env, w[i], &x);
+        napi_set_element(env, arr, i, x);
+    }
+    return arr;
+}
+
+// planCheck(plan): waits for the plan's last sort; throws on a device-side failure since the
+// last check (rs_plan_check)
+napi_value PlanCheck(napi_env env, napi_callback_info info) {
+    napi_value a[1];
+    if (!args(env, info, a)) return nullptr;
+    PlanBox* b = box_of<PlanBox>(env, a[0]);
+    if (!b || !b->plan) return napi_throw_error(env, nullptr, "plan destroyed"), nullptr;
+    RS_CALL(env, rs_plan_check(b->plan), "check");
     return nullptr;
 }
 
@@ -445,6 +497,9 @@ napi_value Init(napi_env env, napi_value exports) {
     Define(env, exports, "planInfo", PlanInfo);
     Define(env, exports, "scanPlanCreate", ScanPlanCreate);
     Define(env, exports, "scanPlanRun", ScanPlanRun);
+    Define(env, exports, "scanPlanRunIndirect", ScanPlanRunIndirect);
+    Define(env, exports, "scanPlanDispatchChain", ScanPlanDispatchChain);
+    Define(env, exports, "planCheck", PlanCheck);
     Define(env, exports, "scanPlanDestroy", ScanPlanDestroy);
     napi_value v;
     napi_create_uint32(env, RS_FLAG_HAS_VALUES, &v); napi_set_named_property(env, exports, "FLAG_HAS_VALUES", v);

@@ -11,7 +11,18 @@ for (const name of ['RadixSortKernel', 'RadixSortBufferKernel', 'RadixSortTextur
 }
 assert.strictEqual(typeof rs.addon.planCreate, 'function');
 assert.strictEqual(rs.addon.FLAG_INTERLEAVED, 0x10);
-assert.strictEqual(rs.addon.version(), 1);
+assert.strictEqual(rs.addon.version(), 2);
+for (const f of ['planCheck', 'scanPlanRunIndirect', 'scanPlanDispatchChain']) {
+  assert.strictEqual(typeof rs.addon[f], 'function', f);
+}
+// argument conversion never truncates silently: negative / over-wide BigInts, fractional or
+// negative Numbers and option values above 2^32 - 1 are TypeErrors (before any device call)
+assert.throws(() => rs.addon.malloc(0, -1n), TypeError);
+assert.throws(() => rs.addon.malloc(0, 2n ** 64n), TypeError);
+assert.throws(() => rs.addon.malloc(0, 1.5), TypeError);
+assert.throws(() => rs.addon.free(-4096), TypeError);
+assert.throws(() => rs.addon.planCreate({ count: 10, bitCount: 2 ** 32 + 8 }), TypeError);
+assert.throws(() => rs.addon.planSort(undefined, 1n, null, null), TypeError);
 
 const fakeKeys = { ptr: 4096n };
 // PrefixSumKernel.ts:33-35: non power-of-two workgroups throw

@@ -21,6 +21,7 @@ RS_ERR_BIT_COUNT = 3
 RS_ERR_HIP = 4
 RS_ERR_OUT_OF_MEMORY = 5
 RS_ERR_CAPACITY = 6
+RS_ERR_DEVICE = 7
 
 RS_FLAG_HAS_VALUES = 0x1
 RS_FLAG_CHECK_ORDER = 0x2
@@ -51,7 +52,8 @@ class PlanDesc(ctypes.Structure):
 class PlanInfo(ctypes.Structure):
     _fields_ = [("passes", ctypes.c_uint32), ("digit_bits", ctypes.c_uint32 * 16),
                 ("tile_keys", ctypes.c_uint32), ("grid_blocks", ctypes.c_uint32),
-                ("workspace_bytes", ctypes.c_uint64)]
+                ("workspace_bytes", ctypes.c_uint64), ("rank_mode", ctypes.c_uint32),
+                ("lane_order_selftest", ctypes.c_int32)]
 
 
 _lib = None
@@ -74,11 +76,16 @@ _SIGS = {
                                             ctypes.POINTER(ctypes.c_uint64)]),
     "rs_plan_reset_kernel_times": (ctypes.c_int, [_VP]),
     "rs_plan_device_errors": (ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_uint32)]),
+    "rs_plan_check": (ctypes.c_int, [_VP]),
+    "rs_plan_set_wait_limit": (ctypes.c_int, [_VP, ctypes.c_uint32]),
     "rs_plan_destroy": (None, [_VP]),
     "rs_scan_plan_create": (ctypes.c_int, [ctypes.c_int32, ctypes.c_uint64, ctypes.c_uint32,
                                            ctypes.c_uint32, ctypes.c_uint32,
                                            ctypes.POINTER(_VP)]),
     "rs_scan_plan_run": (ctypes.c_int, [_VP, _VP, _VP]),
+    "rs_scan_plan_run_indirect": (ctypes.c_int, [_VP, _VP, _VP, ctypes.c_uint64, _VP]),
+    "rs_scan_plan_dispatch_chain": (ctypes.c_uint32, [_VP, ctypes.POINTER(ctypes.c_uint32),
+                                                      ctypes.c_uint32]),
     "rs_scan_plan_destroy": (None, [_VP]),
     "rs_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int32)]),
     "rs_malloc": (ctypes.c_int, [ctypes.c_int32, ctypes.c_uint64, ctypes.POINTER(_VP)]),

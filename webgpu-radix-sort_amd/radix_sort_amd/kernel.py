@@ -229,13 +229,21 @@ class RadixSortKernel:
         check(_lib.load().rs_plan_info_get(self._plan, ctypes.byref(inf)), "info")
         return {"passes": inf.passes, "digit_bits": list(inf.digit_bits[: inf.passes]),
                 "tile_keys": inf.tile_keys, "grid_blocks": inf.grid_blocks,
-                "workspace_bytes": inf.workspace_bytes}
+                "workspace_bytes": inf.workspace_bytes,
+                "rank_mode": "ballot" if inf.rank_mode == 1 else "lds_atomic",
+                "lane_order_selftest": inf.lane_order_selftest}
 
     def device_errors(self) -> int:
         """Device error word (synchronises): 0 = ok; non-zero = a bounded wait timed out."""
         e = ctypes.c_uint32(0)
         check(_lib.load().rs_plan_device_errors(self._plan, ctypes.byref(e)), "device_errors")
         return e.value
+
+    def check(self) -> None:
+        """Wait for the last dispatch and raise :class:`RadixSortError` (status RS_ERR_DEVICE) if
+        any sort on this kernel failed on the device since the last check (a timed-out
+        look-back wait: that sort's output is invalid).  Reported once."""
+        check(_lib.load().rs_plan_check(self._plan), "check")
 
     def set_profiling(self, enable: bool) -> None:
         check(_lib.load().rs_plan_set_profiling(self._plan, 1 if enable else 0), "profiling")
@@ -342,11 +350,28 @@ class PrefixSumKernel:
         self._plan = plan
 
     def dispatch(self, pass_=None, dispatch_size_buffer=None, offset: int = 0) -> None:
-        if dispatch_size_buffer is not None:
-            raise RadixSortError(_lib.RS_ERR_INVALID_ARG,
-                                 "indirect dispatch buffers are not used by the HIP backend")
+        """In-place exclusive scan on stream ``pass_``.  With ``dispatch_size_buffer`` (device
+        memory of u32 (x, y, z) triples, e.g. :meth:`get_dispatch_chain` written to the device) the
+        dispatch is indirect (PrefixSumKernel.ts:147-158): the scan runs iff the triple at byte
+        ``offset`` has no zero entry, decided on the device."""
         s = _stream_handle(pass_, self._uses_torch, self.device)
-        check(_lib.load().rs_scan_plan_run(self._plan, self._ptr, s), "dispatch")
+        if dispatch_size_buffer is None:
+            check(_lib.load().rs_scan_plan_run(self._plan, self._ptr, s), "dispatch")
+            return
+        bptr, _, _ = _buffer_info(dispatch_size_buffer, "dispatch_size_buffer")
+        check(_lib.load().rs_scan_plan_run_indirect(self._plan, self._ptr, bptr, int(offset), s),
+              "dispatch")
+
+    def get_dispatch_chain(self) -> list:
+        """The reference's dispatch chain (PrefixSumKernel.getDispatchChain, :135-137):
+        [x, y, 1] per pipeline, flattened."""
+        L = _lib.load()
+        n = L.rs_scan_plan_dispatch_chain(self._plan, None, 0)
+        out = (ctypes.c_uint32 * max(n, 1))()
+        L.rs_scan_plan_dispatch_chain(self._plan, out, n)
+        return list(out[:n])
+
+    getDispatchChain = get_dispatch_chain
 
     def destroy(self) -> None:
         if getattr(self, "_plan", None):

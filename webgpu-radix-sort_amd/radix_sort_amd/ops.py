@@ -63,6 +63,11 @@ class SortPlan:
                                          None if values is None else values.data_ptr(), n,
                                          _stream(keys, stream)), "rs_plan_sort_n")
 
+    def check(self) -> None:
+        """Wait for the plan's last sort; raise on a device-side failure since the last check
+        (rs_plan_check)."""
+        check(_lib.load().rs_plan_check(self._plan), "rs_plan_check")
+
     def partition(self, in_keys, in_values, out_keys, out_values, n: int, shift: int, bits: int,
                   hist=None, stream=None) -> None:
         """Stable one-digit scatter in -> out; hist (device u32[2^bits]) gets digit totals."""

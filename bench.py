@@ -10,8 +10,9 @@ A step = one full sort of one batch of synthetic input resident in HBM:
   different pre-generated batch (sorting already-sorted data would be a different workload).
 * N > 1 (torch.distributed.run, one process per GPU, RCCL): BASELINE configs[4] shape with
   2^28 keys+values per rank (2^31 at 8 GPUs): histogram all_gather -> stable top-byte partition
-  -> 4 rounds of RCCL all_to_all over xGMI (bucket groups), each group sorted locally (LSD)
-  while the later rounds are in flight.  Weak scaling.
+  into (key, value) records -> 4 rounds of batched RCCL point-to-point record messages over
+  xGMI (bucket groups), each group sorted locally (LSD) while the later rounds are in flight.
+  Weak scaling.
 
 Rank 0 prints ONE JSON line.  `value` = keys sorted by all ranks / max-over-ranks wall time.
 `roofline` is for the dominant kernel (the scatter pass): algorithmic bytes per launch
@@ -55,38 +56,71 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(n_log2: int, seed: int) -> dict:
-    """Reference CPU path timed in Node on this host (kind 'reference'); falls back to the C
-    oracle's single-threaded stable sort (kind 'port') when Node is absent."""
+def _node_sort(keys) -> dict:
+    with tempfile.TemporaryDirectory() as td:
+        p = os.path.join(td, "keys.bin")
+        keys.tofile(p)
+        out = subprocess.run(["node", os.path.join(ROOT, "oracle", "cpu_sort_ref.js"), p],
+                             capture_output=True, text=True, timeout=600, check=True)
+    r = json.loads(out.stdout.strip().splitlines()[-1])
+    assert r["sorted"]
+    return r
+
+
+def cpu_baseline(sizes_log2, seed: int, target_log2: int = 28) -> dict:
+    """Reference CPU path timed in Node on this host (kind 'reference'): the samples of
+    BASELINE.md §3 / SURVEY §8(d) (2^20 mandatory, then larger ones up to ~10-30 s of CPU work),
+    `value` = the rate at the largest sample, plus two clearly labelled extrapolations to the
+    workload size (never measured: the comparator sort at 2^28 would take hours).  Falls back to
+    the C oracle's single-threaded stable sort (kind 'port') when Node is absent."""
+    import math
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import numpy as np
     import oracle as O
-    n = 1 << n_log2
-    keys = O.gen_u32(seed, n)
+    sizes_log2 = sorted(sizes_log2)
     try:
-        with tempfile.TemporaryDirectory() as td:
-            p = os.path.join(td, "keys.bin")
-            keys.tofile(p)
-            out = subprocess.run(["node", os.path.join(ROOT, "oracle", "cpu_sort_ref.js"), p],
-                                 capture_output=True, text=True, timeout=600, check=True)
-        r = json.loads(out.stdout.strip().splitlines()[-1])
-        assert r["sorted"]
-        return {"value": n / (r["ms"] / 1e3) / 1e9, "unit": "Gkeys/s", "cores": 1,
-                "kind": "reference",
-                "sample": (f"2^{n_log2} uniform u32 keys (keys only, as the reference's demo times "
-                           f"it), Uint32Array.sort((a,b)=>a-b) in Node {r['node']} on "
+        points = []
+        for lg in sizes_log2:
+            r = _node_sort(O.gen_u32(seed, 1 << lg))
+            points.append({"n": 1 << lg, "seconds": round(r["ms"] / 1e3, 4),
+                           "gkeys_per_s": (1 << lg) / (r["ms"] / 1e3) / 1e9})
+        big = points[-1]
+        n_t = 1 << target_log2
+        # n log n from the largest sample, and a power law fitted through all samples (the
+        # comparator sort is super-linear beyond n log n here: cache misses grow with n)
+        t_nlogn = big["seconds"] * (n_t * target_log2) / (big["n"] * math.log2(big["n"]))
+        xs = [math.log(p["n"]) for p in points]
+        ys = [math.log(p["seconds"]) for p in points]
+        if len(points) > 1:
+            mx, my = sum(xs) / len(xs), sum(ys) / len(ys)
+            b = sum((x - mx) * (y - my) for x, y in zip(xs, ys)) / sum((x - mx) ** 2 for x in xs)
+            t_pow = math.exp(my + b * (math.log(n_t) - mx))
+        else:
+            b, t_pow = 1.0, t_nlogn
+        return {"value": big["gkeys_per_s"], "unit": "Gkeys/s", "cores": 1, "kind": "reference",
+                "sample": (f"2^{sizes_log2[-1]} uniform u32 keys (keys only, as the reference's demo "
+                           f"times it), Uint32Array.sort((a,b)=>a-b) in Node {r['node']} on "
                            f"'{r['cpu_model']}' ({r['cpus']} host cpus, 1 used); "
-                           f"{r['ms'] / 1e3:.2f} s; the comparator sort is super-linear, so the "
-                           f"rate at 2^28 is lower still"),
-                "seconds": r["ms"] / 1e3}
+                           f"{big['seconds']:.2f} s"),
+                "seconds": big["seconds"], "points": points,
+                "extrapolated_to_workload": {
+                    "n": n_t, "measured": False,
+                    "nlogn_from_largest_sample_s": round(t_nlogn, 1),
+                    "nlogn_gkeys_per_s": n_t / t_nlogn / 1e9,
+                    "power_law_fit_s": round(t_pow, 1), "power_law_exponent": round(b, 3),
+                    "power_law_gkeys_per_s": n_t / t_pow / 1e9,
+                    "note": "EXTRAPOLATED, not measured"}}
     except (OSError, subprocess.SubprocessError, ValueError, AssertionError) as e:
         log(f"node baseline unavailable ({e!r}); timing the C oracle instead")
+        lg = sizes_log2[-1]
+        n = 1 << lg
+        keys = O.gen_u32(seed, n)
         vals = np.arange(n, dtype=np.uint32)
         t = time.perf_counter()
         O.stable_sort_masked_c(keys, vals, 32)
         dt = time.perf_counter() - t
         return {"value": n / dt / 1e9, "unit": "Gkeys/s", "cores": 1, "kind": "port",
-                "sample": f"2^{n_log2} u32 keys + values, oracle/rs_oracle.c stable LSD, 1 thread",
+                "sample": f"2^{lg} u32 keys + values, oracle/rs_oracle.c stable LSD, 1 thread",
                 "seconds": dt}
 
 
@@ -153,6 +187,30 @@ def make_kernel(RadixSortKernel, RadixSortTextureKernel, wl, local, k, v, n, rad
                            radix_bits=radix_bits)
 
 
+def verify_batch(torch, ops, wl, n, seed, batch, dev) -> None:
+    """The sorted batch against its regenerated input: keys sorted (unsigned), values a
+    permutation with keys_out == keys_in[values_out] (values start as iota), equal keys in input
+    order.  Raises SystemExit on any mismatch."""
+    kin, _ = make_input(torch, ops, wl, n, seed, 0, dev)
+    if wl.get("layout") == "aos":
+        kin = kin[:, 0].contiguous()
+        ko, vo = batch[0][:, 0].contiguous(), batch[0][:, 1].contiguous()
+    else:
+        ko, vo = batch
+    if not ops.is_sorted(ko):
+        raise SystemExit("bench: output not sorted")
+    if vo is None:
+        return
+    v = vo.long()
+    if not torch.equal(torch.bincount(v, minlength=n), torch.ones(n, dtype=torch.long, device=dev)):
+        raise SystemExit("bench: values are not a permutation")
+    if not torch.equal(kin[v], ko):
+        raise SystemExit("bench: keys_out != keys_in[values_out]")
+    eq = ko[1:] == ko[:-1]
+    if not bool((v[1:][eq] > v[:-1][eq]).all()):
+        raise SystemExit("bench: equal keys out of input order (not stable)")
+
+
 def main() -> None:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
@@ -164,7 +222,8 @@ def main() -> None:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--distributed", action="store_true",
                     help="use the bucket-exchange path even at world size 1 (testing)")
-    ap.add_argument("--cpu-log2", type=int, default=24)
+    ap.add_argument("--cpu-log2", default="20,22,24",
+                    help="CPU baseline sample sizes (log2, comma-separated; 2^20 mandatory)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per scatter launch (tools/pmc_traffic.py)")
     args = ap.parse_args()
@@ -240,12 +299,12 @@ def main() -> None:
                 acc = kernel_ms.setdefault(name, {"ms": 0.0, "launches": 0})
                 acc["ms"] += v["ms"]
                 acc["launches"] += v["launches"]
-        # sanity: the last sorted batch really is sorted (outside the timed region)
-        lk = batches[(K - 1) % nb][0]
-        if wl.get("layout") == "aos":
-            lk = lk[:, 0].contiguous()
-        if not ops.is_sorted(lk):
-            raise SystemExit("bench: output not sorted")
+        # outside the timed region: no sort failed on the device (a timed-out look-back wait
+        # would make its output invalid), and the last batch is a stable sorted permutation
+        for k in kernels:
+            k.check()
+        last = (K - 1) % nb
+        verify_batch(torch, ops, wl, n, wl["seed"] + 7919 * last, batches[last], dev)
         info = kernels[0].info
         keys_per_step = n
         scatter_keys = n
@@ -269,6 +328,7 @@ def main() -> None:
         torch.cuda.synchronize()
         barrier()
         elapsed = time.perf_counter() - t0
+        lo.check()      # no local sort or partition failed on the device
         ms = (ctypes.c_double * 4)()
         cnt = (ctypes.c_uint64 * 4)()
         _lib.load().rs_plan_kernel_times(lo.plan._plan, ms, cnt)
@@ -331,7 +391,8 @@ def main() -> None:
 
     cpu = None
     if rank == 0 and not use_dist and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.cpu_log2, wl["seed"])
+        cpu = cpu_baseline([int(x) for x in str(args.cpu_log2).split(",")], wl["seed"],
+                           (n - 1).bit_length())
 
     if rank == 0:
         out = {

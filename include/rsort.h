@@ -125,6 +125,18 @@ rs_status rs_plan_partition(rs_plan* plan, const void* in_keys, const void* in_v
 rs_status rs_plan_partition_totals(rs_plan* plan, const void* in_keys, const void* in_values,
                                    void* out_keys, void* out_values, uint64_t n, uint32_t shift,
                                    uint32_t bits, const void* d_totals, void* stream);
+/* Multi-GPU record path.  rs_plan_partition_records: the stable partition of separate key / value
+ * arrays in[0..n) by the digit (key >> shift) & (2^bits - 1), bits <= 8, written as n 8-byte
+ * (key, value) records (one message per peer carries keys and values together); d_totals = the
+ * digit totals of the input (rs_histogram) or NULL (counted here).  rs_plan_sort_records: the
+ * whole stable sort of n records (the received buckets) into separate arrays keys_out /
+ * values_out; records[] is only read.  Both need a plan with RS_FLAG_HAS_VALUES and capacity >= n;
+ * check_order does not apply. */
+rs_status rs_plan_partition_records(rs_plan* plan, const void* in_keys, const void* in_values,
+                                    void* out_records, uint64_t n, uint32_t shift, uint32_t bits,
+                                    const void* d_totals, void* stream);
+rs_status rs_plan_sort_records(rs_plan* plan, const void* records, void* keys_out,
+                               void* values_out, uint64_t n, void* stream);
 rs_status rs_plan_info_get(const rs_plan* plan, rs_plan_info* info);
 /* Kernel timing: when enabled, every launch of the plan is bracketed by HIP events on the
  * launch stream and per-kind durations are accumulated (read after synchronising). */

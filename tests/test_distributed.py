@@ -19,7 +19,7 @@ from radix_sort_amd.distributed import (bucket_groups, bucket_owners, distribute
 
 
 class OracleLocalOps:
-    """Test-only local steps on CPU tensors (int32 views of u32 words)."""
+    """Test-only local steps on CPU tensors (int32 views of u32 words, int64 records)."""
 
     def empty(self, n, like):
         return torch.empty(n, dtype=like.dtype)
@@ -29,27 +29,42 @@ class OracleLocalOps:
         top = (k >> np.uint32(shift)) & np.uint32((1 << bits) - 1)
         return torch.from_numpy(np.bincount(top, minlength=1 << bits).astype(np.int32))
 
-    def partition(self, keys, values, shift, bits, out_keys=None, out_values=None, totals=None):
+    def partition(self, keys, values, shift, bits, totals):
         k = keys.numpy().view(np.uint32)
         top = (k >> np.uint32(shift)) & np.uint32((1 << bits) - 1)
+        assert (np.bincount(top, minlength=1 << bits) == totals.numpy()).all()
         perm = np.argsort(top, kind="stable")
-        sk = torch.from_numpy(k[perm].view(np.int32).copy())
-        sv = None if values is None else torch.from_numpy(values.numpy()[perm].copy())
-        if out_keys is not None:
-            out_keys.copy_(sk)
-            sk = out_keys
-        if sv is not None and out_values is not None:
-            out_values.copy_(sv)
-            sv = out_values
-        return sk, sv
+        if values is None:
+            return torch.from_numpy(k[perm].view(np.int32).copy())
+        v = values.numpy().view(np.uint32)[perm]
+        rec = k[perm].astype(np.uint64) | (v.astype(np.uint64) << np.uint64(32))
+        return torch.from_numpy(rec.view(np.int64))
 
-    def sort(self, keys, values, n):
+    def sort_records(self, records, keys_out, values_out):
+        r = records.numpy().view(np.uint64)
+        k = (r & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+        v = (r >> np.uint64(32)).astype(np.uint32)
+        ok, ov = O.stable_sort_masked(k, v, 32)
+        keys_out.numpy().view(np.uint32)[:] = ok
+        values_out.numpy().view(np.uint32)[:] = ov
+
+    def sort(self, keys, n):
         k = keys.numpy().view(np.uint32)
-        v = None if values is None else values.numpy().view(np.uint32)
-        ok, ov = O.stable_sort_masked(k[:n], None if v is None else v[:n], 32)
-        keys.numpy().view(np.uint32)[:n] = ok
-        if v is not None:
-            values.numpy().view(np.uint32)[:n] = ov
+        ok, _ = O.stable_sort_masked(k[:n].copy(), None, 32)
+        k[:n] = ok
+
+
+def _keys(kind, n, start):
+    u = O.gen_u32(9, n, start=start)
+    if kind == "uniform":
+        return u
+    if kind == "few":             # heavy duplicates: stability across ranks matters
+        return u % np.uint32(7) << np.uint32(29)
+    if kind == "skewed":          # everything in a handful of top-byte buckets
+        return u & np.uint32(0x03FFFFFF)
+    if kind == "one_bucket":      # one top-byte bucket: one rank receives everything
+        return u & np.uint32(0x00FFFFFF)
+    raise ValueError(kind)
 
 
 def _free_port():
@@ -60,35 +75,35 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, n_per_rank, kind, q, chunks):
+def _worker(rank, world, port, n_per_rank, kind, q, chunks, kv):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        if kind == "uniform":
-            k = O.gen_u32(9, n_per_rank, start=rank * n_per_rank)
-        elif kind == "few":   # heavy duplicates: stability across ranks matters
-            k = O.gen_u32(9, n_per_rank, start=rank * n_per_rank) % np.uint32(7) << np.uint32(29)
-        else:                 # skewed: everything in a handful of top-byte buckets
-            k = O.gen_u32(9, n_per_rank, start=rank * n_per_rank) & np.uint32(0x03FFFFFF)
+        k = _keys(kind, n_per_rank, rank * n_per_rank)
         v = np.arange(rank * n_per_rank, (rank + 1) * n_per_rank, dtype=np.uint32)
         r = distributed_sort(torch.from_numpy(k.view(np.int32).copy()),
-                             torch.from_numpy(v.view(np.int32).copy()), OracleLocalOps(),
-                             chunks=chunks)
+                             torch.from_numpy(v.view(np.int32).copy()) if kv else None,
+                             OracleLocalOps(), chunks=chunks)
         q.put((rank, r.keys[: r.n].numpy().view(np.uint32).copy(),
-               r.values[: r.n].numpy().view(np.uint32).copy(), r.send_sizes, r.recv_sizes))
+               r.values[: r.n].numpy().view(np.uint32).copy() if kv else None,
+               r.send_sizes, r.recv_sizes))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("kind,world,chunks", [("uniform", 2, 4), ("few", 2, 3), ("skewed", 2, 1),
-                                               ("uniform", 3, 4), ("few", 3, 2)])
-def test_gloo_bucket_exchange_is_global_stable_sort(kind, world, chunks):
+@pytest.mark.parametrize("kind,world,chunks,kv", [
+    ("uniform", 2, 4, True), ("few", 2, 3, True), ("skewed", 2, 1, True), ("uniform", 3, 4, True),
+    ("few", 3, 2, True), ("one_bucket", 3, 4, True), ("one_bucket", 2, 2, False),
+    ("uniform", 3, 3, False)])
+def test_gloo_bucket_exchange_is_global_stable_sort(kind, world, chunks, kv):
+    """The exchange code RCCL runs (exchange_round: batched point-to-point record messages, the
+    own segment copied locally), here over gloo with oracle local steps."""
     n = 20_000
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n, kind, q, chunks))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, kind, q, chunks, kv))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -97,18 +112,18 @@ def test_gloo_bucket_exchange_is_global_stable_sort(kind, world, chunks):
         p.join(timeout=60)
         assert p.exitcode == 0
     keys = np.concatenate([o[1] for o in outs])
-    vals = np.concatenate([o[2] for o in outs])
-    all_k = np.concatenate([
-        (O.gen_u32(9, n, start=r * n) if kind == "uniform" else
-         O.gen_u32(9, n, start=r * n) % np.uint32(7) << np.uint32(29) if kind == "few" else
-         O.gen_u32(9, n, start=r * n) & np.uint32(0x03FFFFFF)) for r in range(world)])
+    all_k = np.concatenate([_keys(kind, n, r * n) for r in range(world)])
     ek, ev = O.stable_sort_masked(all_k, np.arange(world * n, dtype=np.uint32), 32)
-    assert (keys == ek).all() and (vals == ev).all()
+    assert (keys == ek).all()
+    if kv:
+        assert (np.concatenate([o[2] for o in outs]) == ev).all()
     # every rank sent exactly its input, received what others sent it
     for r in range(world):
         assert sum(outs[r][3]) == n
-        for s in range(world):
-            assert outs[r][4][s] == outs[s][3][r]
+        for s_ in range(world):
+            assert outs[r][4][s_] == outs[s_][3][r]
+    if kind == "one_bucket":      # one rank holds the whole result, the others nothing
+        assert sorted(len(o[1]) for o in outs) == [0] * (world - 1) + [world * n]
 
 
 def test_bucket_owners_balanced_and_whole():
@@ -164,10 +179,18 @@ def test_rccl_world1_hip_local_ops_round_trip(chunks):
         ops = HipLocalOps(0, n, True)
         r = distributed_sort(kt, vt, ops, chunks=chunks)
         torch.cuda.synchronize()
+        ops.check()
         ek, ev = O.stable_sort_masked(k, v, 32)
         assert r.n == n
         assert (r.keys.cpu().numpy().view(np.uint32) == ek).all()
         assert (r.values.cpu().numpy().view(np.uint32) == ev).all()
+        # keys only: the exchange carries the keys themselves
+        kt2 = torch.from_numpy(k.view(np.int32)).cuda()
+        ops2 = HipLocalOps(0, n, False)
+        r2 = distributed_sort(kt2, None, ops2, chunks=chunks)
+        torch.cuda.synchronize()
+        ops2.check()
+        assert r2.n == n and (r2.keys.cpu().numpy().view(np.uint32) == ek).all()
     finally:
         dist.destroy_process_group()
 

@@ -1231,6 +1231,19 @@ __global__ __launch_bounds__(kBlock) void k_finalize(const uint32_t* __restrict_
     }
 }
 
+// (key, value) records -> two arrays (small sorts from records; the records' last pass writes the
+// arrays itself on larger ones).
+__global__ __launch_bounds__(kBlock) void k_split_records(const uint2* __restrict__ rec,
+                                                          uint32_t* __restrict__ k,
+                                                          uint32_t* __restrict__ v, uint64_t n) {
+    const uint32_t stride = gridDim.x * kBlock;
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+        const uint2 r = rec[i];
+        k[i] = r.x;
+        v[i] = r.y;
+    }
+}
+
 // ---- prefix sum (PrefixSumKernel) ---------------------------------------------------------
 // Three kernels, reduce-then-scan: chunk sums -> scan of chunk sums -> rescan with carry.
 // ind (may be null): the caller's indirect dispatch triple (x, y, z workgroups,

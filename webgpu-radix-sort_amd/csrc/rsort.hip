@@ -747,6 +747,10 @@ RS_EXPORT rs_status rs_plan_sort(rs_plan* p, void* keys, void* values, void* str
     return rs_plan_sort_n(p, keys, values, p->capacity, stream);
 }
 
+static rs_status onesweep_digit_pass(rs_plan* p, const uint32_t* ik, const uint32_t* iv,
+                                     uint32_t* ok, uint32_t* ov, uint64_t n, uint32_t shift,
+                                     uint32_t bits, int LL, const void* d_totals, hipStream_t s);
+
 RS_EXPORT rs_status rs_plan_partition(rs_plan* p, const void* in_keys, const void* in_values,
                                       void* out_keys, void* out_values, uint64_t n,
                                       uint32_t shift, uint32_t bits, void* d_hist, void* stream) {
@@ -787,19 +791,142 @@ RS_EXPORT rs_status rs_plan_partition_totals(rs_plan* p, const void* in_keys, co
         return rs_plan_partition(p, in_keys, in_values, out_keys, out_values, n, shift, bits,
                                  nullptr, stream);
     if (!in_keys || !out_keys) return fail(RS_ERR_INVALID_ARG, "rs_plan_partition_totals: null keys");
-    DeviceGuard guard(p->desc.device);
-    hipStream_t s = (hipStream_t)stream;
-    // run as the plan's last pass: no next-pass totals, its own ticket and totals slot
-    const int pass = (int)p->passes - 1;
     if (rs_status st = take_device_error(p, "rs_plan_partition_totals")) return st;
+    DeviceGuard guard(p->desc.device);
+    const int L = p->layout;
+    return onesweep_digit_pass(p, (const uint32_t*)in_keys, (const uint32_t*)in_values,
+                               (uint32_t*)out_keys, (uint32_t*)out_values, n, shift, bits,
+                               layout_pair(L, L), d_totals, (hipStream_t)stream);
+}
+
+// One stable one-sweep pass in -> out by the digit (key >> shift) & (2^bits - 1), run as the
+// plan's last pass (no next-pass totals): digit totals copied from d_totals, or counted here
+// (one read of the keys) when d_totals is null.  LL = layout_pair(in, out).
+static rs_status onesweep_digit_pass(rs_plan* p, const uint32_t* ik, const uint32_t* iv,
+                                     uint32_t* ok, uint32_t* ov, uint64_t n, uint32_t shift,
+                                     uint32_t bits, int LL, const void* d_totals, hipStream_t s) {
+    const int pass = (int)p->passes - 1;
+    uint32_t* slot = p->ptot + p->ptot_off[pass];   // 2^bits words fit: kTotalsMax >= off + 256
     HIP_TRY(hipMemsetAsync(p->tickets + pass, 0, 4, s));
     HIP_TRY(hipMemsetAsync(p->tickets + 16, 0, 4, s));
-    HIP_TRY(hipMemcpyAsync(p->ptot + p->ptot_off[pass], d_totals, 4u << bits,
-                           hipMemcpyDeviceToDevice, s));
-    const int L = p->layout;
-    return run_pass(p, (const uint32_t*)in_keys, (const uint32_t*)in_values, (uint32_t*)out_keys,
-                    (uint32_t*)out_values, (uint32_t)n, shift, bits, layout_pair(L, L), nullptr,
-                    pass, s, /*onesweep=*/true);
+    if (d_totals) {
+        HIP_TRY(hipMemcpyAsync(slot, d_totals, 4u << bits, hipMemcpyDeviceToDevice, s));
+    } else {
+        HIP_TRY(hipMemsetAsync(slot, 0, 4u << bits, s));
+        rs::PassList pl{};
+        pl.count = 1;
+        pl.width[0] = bits;
+        const uint32_t grid = (uint32_t)std::min<uint64_t>((uint64_t)RS_TOT_PER_CU * p->cus,
+                                                           (n + 4ull * RS_TOT_BLOCK - 1) / (4ull * RS_TOT_BLOCK));
+        if ((LL & 15) == rs::LAYOUT_AOS)
+            hipLaunchKernelGGL(rs::k_pass_totals<2>, dim3(grid), dim3(RS_TOT_BLOCK), 0, s, ik, (uint32_t)n, pl, shift, slot);
+        else
+            hipLaunchKernelGGL(rs::k_pass_totals<1>, dim3(grid), dim3(RS_TOT_BLOCK), 0, s, ik, (uint32_t)n, pl, shift, slot);
+        HIP_TRY(hipGetLastError());
+    }
+    return run_pass(p, ik, iv, ok, ov, (uint32_t)n, shift, bits, LL, nullptr, pass, s, /*onesweep=*/true);
+}
+
+RS_EXPORT rs_status rs_plan_partition_records(rs_plan* p, const void* in_keys, const void* in_values,
+                                              void* out_records, uint64_t n, uint32_t shift,
+                                              uint32_t bits, const void* d_totals, void* stream) {
+    if (!p) return fail(RS_ERR_INVALID_ARG, "rs_plan_partition_records: null plan");
+    if (p->layout != rs::LAYOUT_SOA)
+        return fail(RS_ERR_INVALID_ARG, "rs_plan_partition_records: needs a plan with separate values (RS_FLAG_HAS_VALUES)");
+    if (n > p->capacity)
+        return fail(RS_ERR_CAPACITY, "count %llu exceeds plan capacity %llu",
+                    (unsigned long long)n, (unsigned long long)p->capacity);
+    if (bits == 0 || bits > 8 || shift + bits > 32)
+        return fail(RS_ERR_INVALID_ARG, "partition digit must satisfy 1 <= bits <= 8, shift+bits <= 32");
+    if (n == 0) return RS_OK;
+    if (!in_keys || !in_values || !out_records)
+        return fail(RS_ERR_INVALID_ARG, "rs_plan_partition_records: null buffer");
+    if ((uintptr_t)out_records & 7) return fail(RS_ERR_INVALID_ARG, "records must be 8-byte aligned");
+    if (rs_status st = take_device_error(p, "rs_plan_partition_records")) return st;
+    DeviceGuard guard(p->desc.device);
+    return onesweep_digit_pass(p, (const uint32_t*)in_keys, (const uint32_t*)in_values,
+                               (uint32_t*)out_records, nullptr, n, shift, bits,
+                               layout_pair(rs::LAYOUT_SOA, rs::LAYOUT_AOS), d_totals, (hipStream_t)stream);
+}
+
+// Whole sort of n (key, value) records into two arrays: pass 0 reads the records, the last pass
+// writes the arrays; the passes between go through the plan's records buffers (R1 <-> R2), or
+// alternate with the output arrays when there is no second records buffer.  One-sweep passes at
+// every size (tiles of the size's configuration).
+static rs_status enqueue_sort_records(rs_plan* p, const uint32_t* rec, uint32_t* uk, uint32_t* uv,
+                                      uint64_t n, hipStream_t s) {
+    const uint32_t n32 = (uint32_t)n;
+    HIP_TRY(hipMemsetAsync(p->ptot, 0, 4ull * (rs::kTotalsMax + 32), s));
+    {
+        rs::PassList pl{};
+        pl.count = 1;
+        pl.width[0] = p->widths[0];
+        const uint32_t grid = (uint32_t)std::min<uint64_t>((uint64_t)RS_TOT_PER_CU * p->cus,
+                                                           (n + 4ull * RS_TOT_BLOCK - 1) / (4ull * RS_TOT_BLOCK));
+        p->timer.run(RS_KERNEL_HISTOGRAM, s, [&] {
+            hipLaunchKernelGGL(rs::k_pass_totals<2>, dim3(grid), dim3(RS_TOT_BLOCK), 0, s, rec, n32, pl, 0u, p->ptot);
+        });
+        HIP_TRY(hipGetLastError());
+    }
+    constexpr int A = rs::LAYOUT_AOS, S = rs::LAYOUT_SOA;
+    uint32_t* r1 = p->tmp_k;
+    uint32_t* r2 = p->tmp2;
+    uint32_t shift = 0;
+    for (uint32_t i = 0; i < p->passes; ++i) {
+        const bool last = i + 1 == p->passes, odd = (i & 1u) != 0;
+        const uint32_t* ik;
+        const uint32_t* iv = nullptr;
+        uint32_t* ok;
+        uint32_t* ov = nullptr;
+        int LL;
+        if (r2) {            // rec -> R1 -> R2 -> R1 ... -> arrays
+            ik = i == 0 ? rec : (odd ? r1 : r2);
+            if (last) { ok = uk; ov = uv; LL = layout_pair(A, S); }
+            else { ok = odd ? r2 : r1; LL = layout_pair(A, A); }
+        } else {             // rec -> R1 -> arrays -> R1 -> arrays
+            if (i == 0) { ik = rec; ok = r1; LL = layout_pair(A, A); }
+            else if (odd) { ik = r1; ok = uk; ov = uv; LL = layout_pair(A, S); }
+            else { ik = uk; iv = uv; ok = r1; LL = layout_pair(S, A); }
+        }
+        rs_status st = run_pass(p, ik, iv, ok, ov, n32, shift, p->widths[i], LL, nullptr, (int)i, s,
+                                /*onesweep=*/true);
+        if (st != RS_OK) return st;
+        shift += p->widths[i];
+    }
+    return RS_OK;
+}
+
+RS_EXPORT rs_status rs_plan_sort_records(rs_plan* p, const void* records, void* keys_out,
+                                         void* values_out, uint64_t n, void* stream) {
+    if (!p) return fail(RS_ERR_INVALID_ARG, "rs_plan_sort_records: null plan");
+    if (p->layout != rs::LAYOUT_SOA)
+        return fail(RS_ERR_INVALID_ARG, "rs_plan_sort_records: needs a plan with separate values (RS_FLAG_HAS_VALUES)");
+    if (n > p->capacity)
+        return fail(RS_ERR_CAPACITY, "count %llu exceeds plan capacity %llu",
+                    (unsigned long long)n, (unsigned long long)p->capacity);
+    if (n == 0) return RS_OK;
+    if (!records || !keys_out || !values_out)
+        return fail(RS_ERR_INVALID_ARG, "rs_plan_sort_records: null buffer");
+    if (((uintptr_t)records & 7) || ((uintptr_t)keys_out & 3) || ((uintptr_t)values_out & 3))
+        return fail(RS_ERR_INVALID_ARG, "records must be 8-byte and arrays 4-byte aligned");
+    if (rs_status st = take_device_error(p, "rs_plan_sort_records")) return st;
+    DeviceGuard guard(p->desc.device);
+    hipStream_t s = (hipStream_t)stream;
+    uint32_t* uk = (uint32_t*)keys_out;
+    uint32_t* uv = (uint32_t*)values_out;
+    rs_status st;
+    if (n <= kTinyMax) {
+        hipLaunchKernelGGL(rs::k_split_records, dim3((uint32_t)((n + rs::kBlock - 1) / rs::kBlock)),
+                           dim3(rs::kBlock), 0, s, (const uint2*)records, uk, uv, n);
+        HIP_TRY(hipGetLastError());
+        st = n > 1 ? run_tiny(p, uk, uv, (uint32_t)n, s) : RS_OK;
+    } else {
+        st = enqueue_sort_records(p, (const uint32_t*)records, uk, uv, n, s);
+    }
+    if (st != RS_OK) return st;
+    HIP_TRY(hipEventRecord(p->done, s));
+    p->done_recorded = true;
+    return RS_OK;
 }
 
 RS_EXPORT rs_status rs_plan_device_errors(rs_plan* p, uint32_t* errors) {

@@ -9,17 +9,19 @@ same sort for inputs spread over the GPUs of one node (BASELINE config 5):
    every rank computes the same bucket -> rank assignment on whole-bucket boundaries (equal
    keys never split), and splits every rank's buckets into G consecutive groups of about equal
    key counts (again whole buckets);
-4. a stable partition of the slice by the top digit (one scatter pass of the radix sort,
-   ``rs_plan_partition_totals``: given the step-2 counts it is the one-sweep pass, one key read),
-   overlapped with the host's wait for the counts: every (peer, group) send segment is now one
-   contiguous range of buckets;
-5. G exchange rounds, round g an asynchronous all-to-all (RCCL: each rank sends to all peers at
-   once, over all 7 xGMI links of a rank) of every rank's group-g buckets, keys and values.  The
-   receiver lays round g out as [source 0's segment, source 1's, ...] in its group-g region,
-   which is therefore complete once round g lands: it holds every key of those buckets,
-   equal keys in (source rank, input position) order = global input order;
+4. a stable partition of the slice by the top digit (one scatter pass of the radix sort, the
+   one-sweep pass fed the step-2 counts: one key read), written as 8-byte (key, value) records
+   (``rs_plan_partition_records``; keys only: ``rs_plan_partition_totals``), overlapped with the
+   host's wait for the counts: every (peer, group) send segment is now one contiguous range;
+5. G exchange rounds: round g is one batch of point-to-point messages (``batch_isend_irecv``;
+   RCCL sends to all peers at once, over all 7 xGMI links of a rank), one message per peer with
+   its group-g buckets' records.  The receiver lays round g out as [source 0's segment,
+   source 1's, ...] in its group-g region, which is therefore complete once round g lands: it
+   holds every key of those buckets, equal keys in (source rank, input position) order = global
+   input order;
 6. as soon as round g has landed, the group-g region is sorted locally (stable LSD, the same
-   plan), while rounds g+1.. are still on the wire: the local sort hides under the exchange,
+   plan; ``rs_plan_sort_records``: records in, separate key / value arrays out), while rounds
+   g+1.. are still on the wire: the local sort hides under the exchange,
    and only the last group's sort is exposed.  Groups hold increasing buckets, so the regions
    concatenated are rank r's part of the global stable order.
 
@@ -27,9 +29,12 @@ Stability: the partition is stable, segments are placed in source-rank order, th
 is stable, and a bucket never spans two groups or two ranks.
 
 The local compute is injected (`LocalOps`): the product uses :class:`HipLocalOps` (librsort);
-the CPU gloo tests inject an oracle-backed implementation to exercise the orchestration.  gloo
-has no list all-to-all, so there (and only there) a round's send segments are gathered into one
-staging buffer for ``all_to_all_single``.
+the CPU gloo tests inject an oracle-backed implementation.  The exchange itself
+(:func:`exchange_round`: point-to-point messages batched per round, the own segment copied
+locally) is ONE code path for every backend, so the gloo world-2/3 tests run exactly what RCCL
+runs on the GPUs.  With values, a message is a run of 8-byte (key, value) records (the partition
+writes records, the local sort reads them and writes separate arrays): one message per peer per
+round instead of two.
 """
 from __future__ import annotations
 
@@ -41,17 +46,19 @@ class LocalOps(Protocol):
     def histogram(self, keys, shift: int, bits: int):
         """-> hist[2^bits] int32 tensor on the keys' device (top-digit counts of keys)."""
 
-    def partition(self, keys, values, shift: int, bits: int, out_keys=None, out_values=None,
-                  totals=None):
-        """Stable partition by (key >> shift) & (2^bits - 1) -> (keys_out, values_out); written
-        into out_keys / out_values when given.  totals (optional): histogram() of the same keys,
-        which lets the pass skip its own digit count."""
+    def partition(self, keys, values, shift: int, bits: int, totals):
+        """Stable partition by (key >> shift) & (2^bits - 1) -> the send buffer: with values, one
+        int64 (key, value) record per key (key | value << 32, the interleaved layout: one message
+        per peer carries both); keys only, the int32 keys.  totals: histogram() of the same keys."""
 
-    def sort(self, keys, values, n: int) -> None:
-        """Stable in-place sort of keys[:n] (and values[:n]) by the full 32-bit key."""
+    def sort_records(self, records, keys_out, values_out) -> None:
+        """Stable sort of the int64 records by their 32-bit key into keys_out / values_out."""
+
+    def sort(self, keys, n: int) -> None:
+        """Stable in-place sort of keys[:n] (keys only) by the full 32-bit key."""
 
     def empty(self, n: int, like):
-        """Uninitialised buffer of n 32-bit words on like's device."""
+        """Uninitialised buffer of n elements of like's dtype on like's device."""
 
 
 def _split_whole(counts, lo: int, hi: int, parts: int):
@@ -154,7 +161,7 @@ def distributed_sort(keys, values, ops: LocalOps, group=None, bits: int = 8,
 
     On the GPU the work runs on a side stream (ordered after the caller's current stream, and
     the caller's stream after it): the legacy default stream would serialise every local sort
-    with the in-flight all-to-alls and undo the overlap."""
+    with the in-flight exchange and undo the overlap."""
     import torch
 
     if keys.is_cuda:
@@ -181,6 +188,31 @@ def _side_stream(device):
     return _SIDE[device]
 
 
+def exchange_round(send, recv, plan: GroupPlan, g: int, rank: int, world: int, group=None):
+    """Round g of the bucket exchange, the same code on every backend (gloo on CPU, RCCL on the
+    GPUs): one point-to-point message per peer carrying that peer's round-g buckets (records or
+    keys), received into the peer's source slot of the round-g region; the rank's own segment is
+    a local copy (RCCL moves a self segment through a few channels at ~0.3 TB/s, measured).
+    Both sides skip empty messages (they compute the same sizes).  -> the round's works."""
+    import torch.distributed as dist
+    a, b = plan.send[g][rank]
+    o = plan.off[g][rank]
+    if b > a and recv.data_ptr() != send.data_ptr():
+        recv[o:o + (b - a)].copy_(send[a:b])
+    p2p = []
+    for q in range(world):
+        if q == rank:
+            continue
+        a, b = plan.send[g][q]
+        if b > a:
+            p2p.append(dist.P2POp(dist.isend, send[a:b], q, group))
+        m = plan.recv[g][q]
+        if m:
+            o = plan.off[g][q]
+            p2p.append(dist.P2POp(dist.irecv, recv[o:o + m], q, group))
+    return dist.batch_isend_irecv(p2p) if p2p else []
+
+
 def _distributed_sort(keys, values, ops, group, bits, chunks) -> ExchangeResult:
     import torch
     import torch.distributed as dist
@@ -193,13 +225,6 @@ def _distributed_sort(keys, values, ops, group, bits, chunks) -> ExchangeResult:
     hist = ops.histogram(keys, shift, bits)                     # [2^bits]
     gathered = [torch.empty_like(hist) for _ in range(world)]
     dist.all_gather(gathered, hist, group=group)
-    sk = ops.empty(n_local, keys)
-    sv = None if values is None else ops.empty(n_local, values)
-
-    def partition():
-        if n_local:
-            ops.partition(keys, values, shift, bits, sk, sv, totals=hist)
-
     if keys.is_cuda:
         # the counts travel to the host while the slice is partitioned (the partition needs no
         # bucket ownership): copy, mark, enqueue the partition, then wait for the mark only
@@ -207,49 +232,35 @@ def _distributed_sort(keys, values, ops, group, bits, chunks) -> ExchangeResult:
         hcpu.copy_(torch.stack(gathered), non_blocking=True)
         ready = torch.cuda.Event()
         ready.record()
-        partition()
+        send = ops.partition(keys, values, shift, bits, hist)
         ready.synchronize()
         hist_all = hcpu.tolist()
     else:
         hist_all = torch.stack(gathered).tolist()
-        partition()
+        send = ops.partition(keys, values, shift, bits, hist)
     bounds = bucket_owners(hist_all, world)
     cuts = bucket_groups(hist_all, bounds, G)
     plan = group_plan(hist_all, cuts, rank, world)
     n_recv = plan.base[G]
-    rk = ops.empty(n_recv, keys)
-    rv = None if values is None else ops.empty(n_recv, values)
-    list_a2a = dist.get_backend(group) != "gloo"
-    rounds = []
-    for g in range(G):
-        works = []
-        for src, dst in ((sk, rk), (sv, rv)):
-            if src is None:
-                continue
-            ins = [src[a:b] for a, b in plan.send[g]]
-            region = dst[plan.base[g]:plan.base[g + 1]]
-            if list_a2a:
-                outs = [dst[plan.off[g][s]:plan.off[g][s] + plan.recv[g][s]] for s in range(world)]
-                # this rank's own segment is a local device copy (RCCL moves a self segment
-                # through a few channels at ~0.3 TB/s: 0.8 ms per 256 MiB, measured)
-                outs[rank].copy_(ins[rank])
-                if world > 1:
-                    ins[rank], outs[rank] = ins[rank][:0], outs[rank][:0]
-                    works.append(dist.all_to_all(outs, ins, group=group, async_op=True))
-            else:
-                dist.all_to_all_single(region, torch.cat(ins), output_split_sizes=plan.recv[g],
-                                       input_split_sizes=[b - a for a, b in plan.send[g]],
-                                       group=group)
-        rounds.append(works)
+    # one rank: the receive layout is the partitioned slice itself (no copy)
+    recv = send if world == 1 else ops.empty(n_recv, send)
+    rounds = [exchange_round(send, recv, plan, g, rank, world, group) for g in range(G)]
+    if values is None:
+        out_k, out_v = recv, None
+    else:
+        out_k, out_v = ops.empty(n_recv, keys), ops.empty(n_recv, values)
     # round g's local sort waits for round g only (the stream waits, not the host); later rounds
-    # keep moving on RCCL's stream meanwhile
+    # keep moving meanwhile
     for g in range(G):
         for w in rounds[g]:
             w.wait()
         a, b = plan.base[g], plan.base[g + 1]
         if b > a:
-            ops.sort(rk[a:b], None if rv is None else rv[a:b], b - a)
-    return ExchangeResult(rk, rv, n_recv,
+            if values is None:
+                ops.sort(recv[a:b], b - a)
+            else:
+                ops.sort_records(recv[a:b], out_k[a:b], out_v[a:b])
+    return ExchangeResult(out_k, out_v, n_recv,
                           [sum(b - a for a, b in (plan.send[g][q] for g in range(G))) for q in range(world)],
                           [sum(plan.recv[g][s] for g in range(G)) for s in range(world)])
 
@@ -277,33 +288,46 @@ class HipLocalOps:
         histogram(keys, keys.numel(), shift, bits, h)
         return h
 
-    def partition(self, keys, values, shift: int, bits: int, out_keys=None, out_values=None,
-                  totals=None):
+    def partition(self, keys, values, shift: int, bits: int, totals):
         import torch
         n = keys.numel()
-        sk = torch.empty_like(keys) if out_keys is None else out_keys
-        sv = None if values is None else (torch.empty_like(values) if out_values is None else out_values)
         if self.part_plan is None or self.part_plan.capacity < n:
             from .ops import SortPlan
             if self.part_plan is not None:
                 self.part_plan.destroy()
             self.part_plan = SortPlan(self.device, max(n, 1), self.has_values, 32, self.radix_bits)
-        if totals is not None:
-            self.part_plan.partition_totals(keys, values, sk, sv, n, shift, bits, totals)
-        else:
-            self.part_plan.partition(keys, values, sk, sv, n, shift, bits, None)
-        return sk, sv
+        if values is None:
+            sk = torch.empty_like(keys)
+            self.part_plan.partition_totals(keys, None, sk, None, n, shift, bits, totals)
+            return sk
+        rec = torch.empty(n, dtype=torch.int64, device=keys.device)
+        self.part_plan.partition_records(keys, values, rec, n, shift, bits, totals)
+        return rec
+
+    def _grow(self, n: int) -> None:
+        if n > self.capacity:
+            from .ops import SortPlan
+            self.plan.destroy()
+            self.capacity = int(n * 1.125)
+            self.plan = SortPlan(self.device, self.capacity, self.has_values, 32, self.radix_bits)
+
+    def sort(self, keys, n: int) -> None:
+        self._grow(n)
+        self.plan.sort(keys, None, n)
+
+    def sort_records(self, records, keys_out, values_out) -> None:
+        n = records.numel()
+        self._grow(n)
+        self.plan.sort_records(records, keys_out, values_out, n)
+
+    def check(self) -> None:
+        """Raise if a local sort or partition failed on the device (rs_plan_check)."""
+        self.plan.check()
+        if self.part_plan is not None:
+            self.part_plan.check()
 
     def destroy(self) -> None:
         self.plan.destroy()
         if self.part_plan is not None:
             self.part_plan.destroy()
             self.part_plan = None
-
-    def sort(self, keys, values, n: int) -> None:
-        if n > self.capacity:
-            from .ops import SortPlan
-            self.plan.destroy()
-            self.capacity = int(n * 1.125)
-            self.plan = SortPlan(self.device, self.capacity, self.has_values, 32, self.radix_bits)
-        self.plan.sort(keys, values, n)

@@ -86,6 +86,23 @@ class SortPlan:
             out_keys.data_ptr(), None if out_values is None else out_values.data_ptr(), n, shift,
             bits, totals.data_ptr(), _stream(in_keys, stream)), "rs_plan_partition_totals")
 
+    def partition_records(self, in_keys, in_values, out_records, n: int, shift: int, bits: int,
+                          totals=None, stream=None) -> None:
+        """Stable one-digit partition of separate arrays into (key, value) records
+        (out_records: int64 tensor, record i = key | value << 32)."""
+        check(_lib.load().rs_plan_partition_records(
+            self._plan, in_keys.data_ptr(), in_values.data_ptr(), out_records.data_ptr(), n, shift,
+            bits, None if totals is None else totals.data_ptr(), _stream(in_keys, stream)),
+            "rs_plan_partition_records")
+
+    def sort_records(self, records, keys_out, values_out, n: int | None = None,
+                     stream=None) -> None:
+        """Stable sort of n (key, value) records into separate key / value arrays."""
+        n = records.numel() if n is None else n
+        check(_lib.load().rs_plan_sort_records(self._plan, records.data_ptr(), keys_out.data_ptr(),
+                                               values_out.data_ptr(), n, _stream(records, stream)),
+              "rs_plan_sort_records")
+
     def destroy(self) -> None:
         if getattr(self, "_plan", None):
             _lib.load().rs_plan_destroy(self._plan)

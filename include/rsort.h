@@ -178,6 +178,58 @@ rs_status rs_scan_plan_run_indirect(rs_scan_plan* plan, void* data, const void* 
 uint32_t  rs_scan_plan_dispatch_chain(const rs_scan_plan* plan, uint32_t* out, uint32_t max_words);
 void      rs_scan_plan_destroy(rs_scan_plan* plan);
 
+/* ---- multi-GPU group sort (one process, several devices) ------------
+ * The reference has no multi-device path; this is the sharded form of the same sort for an
+ * input spread over the GPUs of one node (BASELINE config 5), callable from a single host
+ * process (the Node addon, a C/C++ host) the way ncclCommInitAll + ncclGroupStart/End drive
+ * several devices from one thread.  Rank r's input is keys[r][0..counts[r]) (+ values[r]) on
+ * devices[r]; after rs_group_sort, rank r holds slice r of the global stable ascending order by
+ * the 32-bit key (rank-ordered concatenation = the sorted whole).  Steps: top-`top_bits`
+ * histogram per rank -> counts to the host -> whole-bucket ownership (~1/world of the keys per
+ * rank, equal keys never split) -> stable partition by the top digit (records with values) ->
+ * `rounds` exchange rounds of point-to-point messages (one per peer per round) -> each round's
+ * region sorted locally as soon as it has landed, while later rounds are on the wire. */
+typedef struct rs_group rs_group;
+
+#define RS_TRANSPORT_RCCL 0u   /* ncclCommInitAll + ncclGroupStart / ncclSend / ncclRecv (xGMI) */
+#define RS_TRANSPORT_COPY 1u   /* peer copies (hipMemcpyPeerAsync, DMA over xGMI); the only one
+                                  that accepts a device listed twice (virtual ranks on one GPU) */
+
+typedef struct rs_group_desc {
+    uint64_t capacity;      /* largest counts[r] a sort may pass (partition workspace); receive
+                               buffers and local sort plans grow on demand */
+    uint32_t flags;         /* RS_FLAG_HAS_VALUES or 0 (keys only); nothing else */
+    uint32_t transport;     /* RS_TRANSPORT_* */
+    uint32_t top_bits;      /* exchange digit width, 1..8; 0 -> 8 (256 buckets) */
+    uint32_t rounds;        /* exchange rounds (bucket groups per rank), 1..16; 0 -> 4 */
+} rs_group_desc;
+
+/* Create the communicators / streams / plans for `world` ranks on devices[0..world). */
+rs_status rs_group_create(int32_t world, const int32_t* devices, const rs_group_desc* desc,
+                          rs_group** out);
+/* Sort.  keys[r] / values[r] (values NULL without RS_FLAG_HAS_VALUES) are device pointers on
+ * devices[r], only read.  streams: NULL, or world hipStream_t (as void*): the group's work is
+ * ordered after each caller stream and each caller stream after the group's work.  Blocks the
+ * host until the bucket counts are known (the exchange sizes, as ncclAllToAllv's host size
+ * arrays); the exchange and the local sorts stay asynchronous. */
+rs_status rs_group_sort(rs_group* g, void* const* keys, void* const* values,
+                        const uint64_t* counts, void* const* streams);
+/* Rank r's slice of the last sort: group-owned device buffers (valid until the next sort or
+ * destroy), *count keys.  Read them after rs_group_synchronize or on a stream passed to the
+ * sort.  values is NULL for a keys-only group. */
+rs_status rs_group_result(const rs_group* g, int32_t rank, void** keys, void** values,
+                          uint64_t* count);
+/* Wait for the last sort on every rank; RS_ERR_DEVICE if any of its kernels failed on the
+ * device (rs_plan_check of every rank's plans). */
+rs_status rs_group_synchronize(rs_group* g);
+void      rs_group_destroy(rs_group* g);
+/* The host-side bucket plan, a pure function (identical on every rank; no device needed):
+ * hist_all[r * buckets + b] = rank r's count of bucket b.  Writes bounds[0..world] (rank q owns
+ * buckets [bounds[q], bounds[q+1])) and cuts[q * (rounds + 1) + i], i <= rounds (round i of rank
+ * q = buckets [cuts[.. + i], cuts[.. + i + 1])), whole buckets of ~equal global key counts. */
+rs_status rs_group_plan(int32_t world, uint32_t buckets, uint32_t rounds, const uint64_t* hist_all,
+                        uint32_t* bounds, uint32_t* cuts);
+
 /* ---- device memory / streams (the reference's createBuffers / queue analogue) ---------- */
 rs_status rs_device_count(int32_t* n);
 rs_status rs_malloc(int32_t device, uint64_t bytes, void** ptr);

@@ -1,0 +1,121 @@
+"""GPU: the single-process multi-GPU sort through the C ABI (rs_group_*).
+
+RCCL transport at world size 1 (the box has one GPU; ncclCommInitAll over one device), and the
+peer-copy transport with device 0 listed 2-4 times: virtual ranks that run the whole multi-rank
+path on one GPU — per-rank top-digit histograms, the host bucket plan, the stable partition into
+records, every exchange round with uneven and empty segments, the region sorts behind the round
+events — with only the wire differing from RCCL.  Checked against the oracle: the rank-ordered
+concatenation equals the stable sort of the concatenated input, values = global input index
+(so stability across ranks is checked too)."""
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+from radix_sort_amd import RadixSortError, RadixSortGroup, _lib
+
+pytestmark = pytest.mark.gpu
+
+
+def _keys(kind, n, seed):
+    u = O.gen_u32(seed, n)
+    if kind == "uniform":
+        return u
+    if kind == "one_bucket":          # every key in the top bucket: one rank receives all
+        return (u & np.uint32(0x00FFFFFF)) | np.uint32(0xFF000000)
+    if kind == "dups":                # 64 distinct keys over 8 buckets
+        return (u % np.uint32(64)) * np.uint32(0x04000001)
+    if kind == "two_buckets":
+        return np.where(u & np.uint32(1), u | np.uint32(0xF0000000), u & np.uint32(0x0FFFFFFF)).astype(np.uint32)
+    raise ValueError(kind)
+
+
+def _run(group, counts, kind, has_values, seed=11, stream=None):
+    dev = torch.device("cuda", 0)
+    host_k = [_keys(kind, n, seed + r) for r, n in enumerate(counts)]
+    starts = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+    host_v = [np.arange(starts[r], starts[r + 1], dtype=np.uint32) for r in range(len(counts))]
+    kt = [torch.from_numpy(k.view(np.int32)).to(dev) for k in host_k]
+    vt = [torch.from_numpy(v.view(np.int32)).to(dev) for v in host_v] if has_values else None
+    keep = [k.clone() for k in kt]
+    if stream is not None:
+        torch.cuda.synchronize()
+        with torch.cuda.stream(stream):
+            out = group.sort(kt, vt)
+    else:
+        out = group.sort(kt, vt)
+    for a, b in zip(kt, keep):                     # inputs are only read
+        assert torch.equal(a, b)
+    all_k = np.concatenate(host_k) if counts else np.zeros(0, np.uint32)
+    all_v = np.concatenate(host_v) if counts else np.zeros(0, np.uint32)
+    ek, ev = O.stable_sort_masked_c(all_k, all_v, 32)
+    gk = np.concatenate([o[0].cpu().numpy().view(np.uint32) for o in out])
+    assert gk.size == ek.size
+    assert np.array_equal(gk, ek)
+    if has_values:
+        gv = np.concatenate([o[1].cpu().numpy().view(np.uint32) for o in out])
+        assert np.array_equal(gv, ev)
+    return [o[0].numel() for o in out]
+
+
+@pytest.mark.parametrize("has_values", [True, False])
+@pytest.mark.parametrize("n", [0, 1, 1000, 16387, 1 << 20, 13 << 20])
+def test_rccl_world1(n, has_values):
+    g = RadixSortGroup([0], capacity=max(n, 1), has_values=has_values, transport="rccl")
+    try:
+        _run(g, [n], "uniform", has_values)
+    finally:
+        g.destroy()
+
+
+@pytest.mark.parametrize("kind", ["uniform", "one_bucket", "dups", "two_buckets"])
+@pytest.mark.parametrize("world", [2, 3, 4])
+@pytest.mark.parametrize("has_values", [True, False])
+def test_virtual_ranks(world, kind, has_values):
+    counts = [300_000 + 777 * r for r in range(world)]
+    counts[-1] = 5000 if world > 2 else counts[-1]        # ragged slices
+    g = RadixSortGroup([0] * world, capacity=max(counts), has_values=has_values, transport="copy",
+                       rounds=3)
+    try:
+        got = _run(g, counts, kind, has_values, seed=world)
+        if kind == "one_bucket":      # a bucket never splits: one rank receives every key
+            assert max(got) == sum(counts)
+    finally:
+        g.destroy()
+
+
+@pytest.mark.parametrize("has_values", [True, False])
+def test_virtual_ranks_one_sweep_sizes(has_values):
+    # > 12M keys per rank: the partition runs the one-sweep records pass, the regions the
+    # records sort; 4 rounds, the second sort reuses (and regrows) the group's buffers
+    counts = [13 << 20, (12 << 20) + 5]
+    g = RadixSortGroup([0, 0], capacity=max(counts), has_values=has_values, transport="copy")
+    try:
+        _run(g, counts, "uniform", has_values, seed=3)
+        _run(g, [1 << 20, 13 << 20], "two_buckets", has_values, seed=4)
+    finally:
+        g.destroy()
+
+
+def test_empty_rank_and_caller_stream():
+    g = RadixSortGroup([0] * 3, capacity=100_000, has_values=True, transport="copy", rounds=2)
+    s = torch.cuda.Stream(0)
+    try:
+        _run(g, [100_000, 0, 4321], "uniform", True, stream=s)
+        _run(g, [0, 0, 0], "uniform", True)
+    finally:
+        g.destroy()
+
+
+def test_capacity_and_duplicate_device_errors():
+    g = RadixSortGroup([0, 0], capacity=1000, has_values=True, transport="copy")
+    try:
+        k = [torch.zeros(2000, dtype=torch.int32, device="cuda:0")] * 2
+        with pytest.raises(RadixSortError) as e:
+            g.sort_async(k, k)
+        assert e.value.status == _lib.RS_ERR_CAPACITY
+    finally:
+        g.destroy()
+    with pytest.raises(RadixSortError) as e:
+        RadixSortGroup([0, 0], capacity=10, transport="rccl")
+    assert "listed twice" in str(e.value)

@@ -34,6 +34,12 @@ def test_node_reference_flow_on_gpu():
     assert "node sort checks ok" in _run("sort.js", 300)
 
 
+@pytest.mark.gpu
+def test_node_group_sort_on_gpu():
+    """RadixSortGroup (rs_group_* through the addon): RCCL world 1 and 3 virtual ranks."""
+    assert "node group checks ok" in _run("group.js", 300)
+
+
 def _demo(*args, timeout=300):
     r = subprocess.run(["node", os.path.join(NODE_DIR, "demo.js"), *args], capture_output=True,
                        text=True, timeout=timeout, cwd=NODE_DIR)

@@ -23,6 +23,7 @@
 #include <vector>
 
 #include "../../include/rsort.h"
+#include "rs_internal.h"
 #include "rs_kernels.hpp"
 
 #define RS_EXPORT extern "C" __attribute__((visibility("default")))
@@ -148,6 +149,8 @@ struct KernelTimer {
 };
 
 }  // namespace
+
+rs_status rs_internal_fail(rs_status s, const char* msg) { return fail(s, "%s", msg); }
 
 struct rs_plan {
     rs_plan_desc desc{};
@@ -620,7 +623,10 @@ RS_EXPORT void rs_plan_destroy(rs_plan* p) {
 }
 
 // Enqueue every launch of one sort (n > kTinyMax) on stream s.
-static rs_status enqueue_sort(rs_plan* p, uint32_t* uk, uint32_t* uv, uint64_t n, hipStream_t s) {
+// in_k0 / in_v0 (optional): pass 0 reads them instead of uk / uv (out-of-place sort; the
+// caller's input is only read, the result lands in uk / uv; check_order not supported).
+static rs_status enqueue_sort(rs_plan* p, uint32_t* uk, uint32_t* uv, uint64_t n, hipStream_t s,
+                              const uint32_t* in_k0 = nullptr, const uint32_t* in_v0 = nullptr) {
     const int L = p->layout;
     const uint32_t n32 = (uint32_t)n;
     const uint32_t* gate = p->check_order ? p->flags : nullptr;
@@ -640,11 +646,12 @@ static rs_status enqueue_sort(rs_plan* p, uint32_t* uk, uint32_t* uv, uint64_t n
         // on that pass's k_onesweep), so no k_check launch at all
         uint32_t* chk0 = (p->check_order && p->fused_check) ? p->flags : nullptr;
         const uint32_t fm = full_mask(p->bit_count);
+        const uint32_t* src = in_k0 ? in_k0 : uk;
         p->timer.run(RS_KERNEL_HISTOGRAM, s, [&] {
             if (L == rs::LAYOUT_AOS)
-                hipLaunchKernelGGL(rs::k_pass_totals<2>, dim3(grid), dim3(RS_TOT_BLOCK), 0, s, uk, n32, pl, 0u, p->ptot, chk0, fm);
+                hipLaunchKernelGGL(rs::k_pass_totals<2>, dim3(grid), dim3(RS_TOT_BLOCK), 0, s, src, n32, pl, 0u, p->ptot, chk0, fm);
             else
-                hipLaunchKernelGGL(rs::k_pass_totals<1>, dim3(grid), dim3(RS_TOT_BLOCK), 0, s, uk, n32, pl, 0u, p->ptot, chk0, fm);
+                hipLaunchKernelGGL(rs::k_pass_totals<1>, dim3(grid), dim3(RS_TOT_BLOCK), 0, s, src, n32, pl, 0u, p->ptot, chk0, fm);
         });
         HIP_TRY(hipGetLastError());
     }
@@ -666,6 +673,10 @@ static rs_status enqueue_sort(rs_plan* p, uint32_t* uk, uint32_t* uv, uint64_t n
         uint32_t* ov = even ? (recs ? nullptr : p->tmp_v) : uv;
         int in_layout = (recs && !even) ? A : L;
         int LL = recs ? (even ? layout_pair(L, A) : layout_pair(A, L)) : layout_pair(L, L);
+        if (i == 0 && in_k0) {
+            ik = in_k0;
+            if (iv) iv = in_v0;
+        }
         if (r2 && i > 0 && i + 1 < p->passes) {
             ik = even ? r2 : p->tmp_k;
             ok = even ? p->tmp_k : r2;
@@ -729,6 +740,39 @@ RS_EXPORT rs_status rs_plan_sort_n(rs_plan* p, void* keys, void* values, uint64_
     if (rs_status st = take_device_error(p, "rs_plan_sort")) return st;
     const rs_status st = n <= kTinyMax ? run_tiny(p, uk, uv, n32, s)   // one launch; check_order moot
                                        : enqueue_sort(p, uk, uv, n, s);
+    if (st != RS_OK) return st;
+    HIP_TRY(hipEventRecord(p->done, s));
+    p->done_recorded = true;
+    return RS_OK;
+}
+
+// Out-of-place sort for the multi-GPU group at world size 1 (rs_group.hip): in[0..n) is only
+// read, the sorted result is written to out[0..n) (separate arrays or keys only).
+rs_status rs_internal_sort_from(rs_plan* p, const void* in_k, const void* in_v, void* out_k,
+                                void* out_v, uint64_t n, void* stream) {
+    if (!p) return fail(RS_ERR_INVALID_ARG, "rs_internal_sort_from: null plan");
+    if (n > p->capacity)
+        return fail(RS_ERR_CAPACITY, "count %llu exceeds plan capacity %llu",
+                    (unsigned long long)n, (unsigned long long)p->capacity);
+    if (p->layout == rs::LAYOUT_AOS || p->check_order)
+        return fail(RS_ERR_INVALID_ARG, "rs_internal_sort_from: separate arrays, no check_order");
+    const bool kv = p->layout == rs::LAYOUT_SOA;
+    if (n == 0) return RS_OK;
+    if (!in_k || !out_k || (kv && (!in_v || !out_v)))
+        return fail(RS_ERR_INVALID_ARG, "rs_internal_sort_from: null buffer");
+    if (rs_status st = take_device_error(p, "rs_group_sort")) return st;
+    DeviceGuard guard(p->desc.device);
+    hipStream_t s = (hipStream_t)stream;
+    uint32_t* uk = (uint32_t*)out_k;
+    uint32_t* uv = kv ? (uint32_t*)out_v : nullptr;
+    rs_status st;
+    if (n <= kTinyMax) {
+        HIP_TRY(hipMemcpyAsync(uk, in_k, 4 * n, hipMemcpyDeviceToDevice, s));
+        if (kv) HIP_TRY(hipMemcpyAsync(uv, in_v, 4 * n, hipMemcpyDeviceToDevice, s));
+        st = n > 1 ? run_tiny(p, uk, uv, (uint32_t)n, s) : RS_OK;
+    } else {
+        st = enqueue_sort(p, uk, uv, n, s, (const uint32_t*)in_k, kv ? (const uint32_t*)in_v : nullptr);
+    }
     if (st != RS_OK) return st;
     HIP_TRY(hipEventRecord(p->done, s));
     p->done_recorded = true;

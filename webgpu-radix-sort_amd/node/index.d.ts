@@ -148,3 +148,36 @@ export declare class PrefixSumKernel {
   getDispatchChain(): number[];
   destroy(): void;
 }
+
+/** A device range owned by a RadixSortGroup (one rank's slice of the last sort). */
+export declare class GroupBuffer {
+  readonly device: Device;
+  readonly ptr: bigint;
+  readonly size: number;
+  readonly host: false;
+}
+
+/**
+ * Multi-GPU sort from one process (no reference counterpart; SURVEY.md §8(b)/(e)): rank r's
+ * slice on devices[r]; after sort() + synchronize(), result(r) is rank r's slice of the global
+ * stable sorted order.  C ABI: rs_group_create / rs_group_sort / rs_group_result.
+ */
+export interface RadixSortGroupOptions {
+  devices: Array<Device | number>;
+  capacity: number;
+  hasValues?: boolean;
+  transport?: 'rccl' | 'copy';
+  topBits?: number;
+  rounds?: number;
+}
+export declare class RadixSortGroup {
+  constructor(options: RadixSortGroupOptions);
+  readonly devices: Device[];
+  readonly world: number;
+  readonly hasValues: boolean;
+  sort(slices: Array<{ keys: DeviceBuffer | GroupBuffer; values?: DeviceBuffer | GroupBuffer; count?: number }>): void;
+  synchronize(): void;
+  result(rank: number): { keys: GroupBuffer; values: GroupBuffer | null; count: number };
+  results(): Array<{ keys: GroupBuffer; values: GroupBuffer | null; count: number }>;
+  destroy(): void;
+}

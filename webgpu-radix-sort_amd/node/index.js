@@ -456,7 +456,90 @@ class PrefixSumKernel {
   }
 }
 
+// A device range owned by a RadixSortGroup (one rank's slice of the last sort): usable as the
+// source of copyBufferToBuffer or as a kernel's keys/values buffer.
+class GroupBuffer {
+  constructor(device, ptr, size) {
+    this.device = device;
+    this.ptr = ptr;
+    this.size = size;
+    this.host = false;
+  }
+}
+
+class RadixSortGroup {
+  /**
+   * Multi-GPU sort of an input spread over the GPUs of one node, driven from this one process
+   * (the reference has no multi-device path; SURVEY.md §8(b)/(e), BASELINE config 5):
+   * {devices: [Device | ordinal, ...], capacity, hasValues = true, transport = 'rccl' | 'copy',
+   * topBits = 8, rounds = 4}.  Rank r's slice lives on devices[r].  'rccl' opens one RCCL
+   * communicator per device (ncclCommInitAll); 'copy' moves the exchange by peer DMA and also
+   * accepts a device listed several times (virtual ranks).
+   */
+  constructor(options) {
+    const opts = options || {};
+    const devs = opts.devices;
+    if (!Array.isArray(devs) || devs.length === 0) throw new TypeError('devices must be a non-empty array');
+    this.devices = devs.map((d) => (d instanceof Device ? d : new Device(d)));
+    this.world = this.devices.length;
+    this.capacity = opts.capacity;
+    if (!(this.capacity >= 0)) throw new TypeError('capacity is required');
+    this.hasValues = opts.hasValues === undefined ? true : !!opts.hasValues;
+    this._group = addon.groupCreate(this.devices.map((d) => d.ordinal), {
+      capacity: this.capacity,
+      hasValues: this.hasValues,
+      transport: opts.transport || 'rccl',
+      topBits: opts.topBits || 0,
+      rounds: opts.rounds || 0,
+    });
+  }
+
+  /**
+   * slices: one {keys, values?, count?} per rank (device buffers on devices[r]; count defaults to
+   * keys.size / 4).  The inputs are only read.  Runs on each device's stream after the work
+   * already submitted there; returns once the exchange sizes are known (the rest is
+   * asynchronous: results() after synchronize(), or copies submitted on the devices' queues).
+   */
+  sort(slices) {
+    if (!Array.isArray(slices) || slices.length !== this.world) {
+      throw new TypeError(`sort: expected ${this.world} slices`);
+    }
+    const keys = slices.map((s, r) => bufferPtr(s.keys, `slices[${r}].keys`));
+    const values = this.hasValues ? slices.map((s, r) => {
+      const v = bufferPtr(s.values, `slices[${r}].values`);
+      if (v === null) throw new TypeError(`slices[${r}].values is required (hasValues)`);
+      return v;
+    }) : null;
+    const counts = slices.map((s) => (s.count !== undefined ? s.count : Math.floor(s.keys.size / 4)));
+    addon.groupSort(this._group, keys, values, counts, this.devices.map((d) => d.stream));
+  }
+
+  /** Wait for the last sort on every device; throws if any of its kernels failed on the device. */
+  synchronize() { addon.groupSynchronize(this._group); }
+
+  /** Rank r's slice of the global sorted order: {keys, values, count} (group-owned, valid until
+   * the next sort or destroy). */
+  result(rank) {
+    const r = addon.groupResult(this._group, rank);
+    const dev = this.devices[rank];
+    return {
+      keys: new GroupBuffer(dev, r.keys, r.count * 4),
+      values: r.values === null ? null : new GroupBuffer(dev, r.values, r.count * 4),
+      count: r.count,
+    };
+  }
+
+  results() { return this.devices.map((_, r) => this.result(r)); }
+
+  destroy() {
+    if (this._group) addon.groupDestroy(this._group);
+    this._group = null;
+  }
+}
+
 module.exports = {
+  RadixSortGroup,
+  GroupBuffer,
   RadixSortKernel,
   RadixSortBufferKernel,
   RadixSortTextureKernel,

@@ -10,6 +10,7 @@
 #include <cstdint>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "../../include/rsort.h"
 
@@ -469,6 +470,175 @@ napi_value ScanPlanDestroy(napi_env env, napi_callback_info info) {
     return nullptr;
 }
 
+// ---- multi-GPU group (rs_group_*) ----------------------------------------------------------
+struct GroupBox { rs_group* group; };
+
+void group_finalize(napi_env, void* data, void*) {
+    auto* b = static_cast<GroupBox*>(data);
+    if (b->group) rs_group_destroy(b->group);
+    delete b;
+}
+
+// Array of pointers / counts (BigInt or Number each); null/undefined -> empty (ok stays true).
+bool u64_array(napi_env env, napi_value v, std::vector<uint64_t>* out, bool* present) {
+    napi_valuetype t;
+    out->clear();
+    *present = false;
+    if (napi_typeof(env, v, &t) != napi_ok) return false;
+    if (t == napi_null || t == napi_undefined) return true;
+    bool isarr = false;
+    if (napi_is_array(env, v, &isarr) != napi_ok || !isarr) return false;
+    uint32_t len = 0;
+    napi_get_array_length(env, v, &len);
+    for (uint32_t i = 0; i < len; ++i) {
+        napi_value e;
+        uint64_t x = 0;
+        if (napi_get_element(env, v, i, &e) != napi_ok || !get_u64(env, e, &x)) return false;
+        out->push_back(x);
+    }
+    *present = true;
+    return true;
+}
+
+// groupCreate([devices], {capacity, hasValues, transport: 'rccl'|'copy', topBits, rounds})
+napi_value GroupCreate(napi_env env, napi_callback_info info) {
+    napi_value a[2];
+    if (!args(env, info, a)) return nullptr;
+    std::vector<uint64_t> devs;
+    bool present = false;
+    if (!u64_array(env, a[0], &devs, &present) || devs.empty())
+        return napi_throw_type_error(env, nullptr, "groupCreate: devices must be a non-empty array"), nullptr;
+    std::vector<int32_t> d32;
+    for (uint64_t d : devs) {
+        if (d > 0x7FFFFFFF) return napi_throw_type_error(env, nullptr, "groupCreate: bad device"), nullptr;
+        d32.push_back((int32_t)d);
+    }
+    rs_group_desc d;
+    memset(&d, 0, sizeof(d));
+    uint32_t has_values = 1;
+    bool has = false;
+    napi_has_named_property(env, a[1], "capacity", &has);
+    if (has) {
+        napi_value c;
+        napi_get_named_property(env, a[1], "capacity", &c);
+        if (!get_u64(env, c, &d.capacity)) return napi_throw_type_error(env, nullptr, "capacity"), nullptr;
+    }
+    napi_has_named_property(env, a[1], "hasValues", &has);
+    if (has) {
+        napi_value hv;
+        bool bv = true;
+        napi_get_named_property(env, a[1], "hasValues", &hv);
+        if (napi_get_value_bool(env, hv, &bv) != napi_ok)
+            return napi_throw_type_error(env, nullptr, "hasValues must be a boolean"), nullptr;
+        has_values = bv ? 1u : 0u;
+    }
+    napi_has_named_property(env, a[1], "transport", &has);
+    if (has) {
+        napi_value tv;
+        char buf[16] = {0};
+        size_t len = 0;
+        napi_get_named_property(env, a[1], "transport", &tv);
+        if (napi_get_value_string_utf8(env, tv, buf, sizeof(buf), &len) != napi_ok)
+            return napi_throw_type_error(env, nullptr, "transport must be 'rccl' or 'copy'"), nullptr;
+        if (strcmp(buf, "rccl") == 0) d.transport = RS_TRANSPORT_RCCL;
+        else if (strcmp(buf, "copy") == 0) d.transport = RS_TRANSPORT_COPY;
+        else return napi_throw_type_error(env, nullptr, "transport must be 'rccl' or 'copy'"), nullptr;
+    }
+    if (!get_u32_prop(env, a[1], "topBits", &d.top_bits, 0) ||
+        !get_u32_prop(env, a[1], "rounds", &d.rounds, 0))
+        return napi_throw_type_error(env, nullptr, "groupCreate: bad option"), nullptr;
+    d.flags = has_values ? RS_FLAG_HAS_VALUES : 0u;
+    rs_group* g = nullptr;
+    RS_CALL(env, rs_group_create((int32_t)d32.size(), d32.data(), &d, &g), "RadixSortGroup");
+    napi_value ext;
+    auto* box = new GroupBox{g};
+    if (napi_create_external(env, box, group_finalize, nullptr, &ext) != napi_ok) {
+        group_finalize(env, box, nullptr);
+        return napi_throw_error(env, nullptr, "external"), nullptr;
+    }
+    return ext;
+}
+
+GroupBox* group_of(napi_env env, napi_value v) {
+    void* p = nullptr;
+    if (napi_get_value_external(env, v, &p) != napi_ok || !p) {
+        napi_throw_type_error(env, nullptr, "expected a group handle");
+        return nullptr;
+    }
+    auto* b = static_cast<GroupBox*>(p);
+    if (!b->group) {
+        napi_throw_error(env, nullptr, "group destroyed");
+        return nullptr;
+    }
+    return b;
+}
+
+// groupSort(group, [keysPtr], [valuesPtr]|null, [count], [stream]|null)
+napi_value GroupSort(napi_env env, napi_callback_info info) {
+    napi_value a[5];
+    if (!args(env, info, a)) return nullptr;
+    GroupBox* b = group_of(env, a[0]);
+    if (!b) return nullptr;
+    std::vector<uint64_t> k, v, n, s;
+    bool hk, hv, hn, hs;
+    if (!u64_array(env, a[1], &k, &hk) || !u64_array(env, a[2], &v, &hv) ||
+        !u64_array(env, a[3], &n, &hn) || !u64_array(env, a[4], &s, &hs) || !hk || !hn ||
+        n.size() != k.size() || (hv && v.size() != k.size()) || (hs && s.size() != k.size()))
+        return napi_throw_type_error(env, nullptr, "groupSort(group, keys[], values[]|null, counts[], streams[]|null): bad arrays"), nullptr;
+    std::vector<void*> kp(k.size()), vp(v.size()), sp(s.size());
+    for (size_t i = 0; i < k.size(); ++i) kp[i] = (void*)(uintptr_t)k[i];
+    for (size_t i = 0; i < v.size(); ++i) vp[i] = (void*)(uintptr_t)v[i];
+    for (size_t i = 0; i < s.size(); ++i) sp[i] = (void*)(uintptr_t)s[i];
+    RS_CALL(env, rs_group_sort(b->group, kp.data(), hv ? vp.data() : nullptr, n.data(),
+                               hs ? sp.data() : nullptr), "RadixSortGroup.sort");
+    return nullptr;
+}
+
+// groupResult(group, rank) -> {keys: BigInt, values: BigInt|null, count: Number}
+napi_value GroupResult(napi_env env, napi_callback_info info) {
+    napi_value a[2];
+    if (!args(env, info, a)) return nullptr;
+    GroupBox* b = group_of(env, a[0]);
+    if (!b) return nullptr;
+    uint64_t rank = 0;
+    if (!get_u64(env, a[1], &rank) || rank > 0x7FFFFFFF)
+        return napi_throw_type_error(env, nullptr, "groupResult: bad rank"), nullptr;
+    void* kp = nullptr;
+    void* vp = nullptr;
+    uint64_t n = 0;
+    RS_CALL(env, rs_group_result(b->group, (int32_t)rank, &kp, &vp, &n), "groupResult");
+    napi_value o, x;
+    napi_create_object(env, &o);
+    napi_set_named_property(env, o, "keys", bigint(env, (uint64_t)(uintptr_t)kp));
+    if (vp) x = bigint(env, (uint64_t)(uintptr_t)vp);
+    else napi_get_null(env, &x);
+    napi_set_named_property(env, o, "values", x);
+    napi_create_double(env, (double)n, &x);
+    napi_set_named_property(env, o, "count", x);
+    return o;
+}
+
+napi_value GroupSynchronize(napi_env env, napi_callback_info info) {
+    napi_value a[1];
+    if (!args(env, info, a)) return nullptr;
+    GroupBox* b = group_of(env, a[0]);
+    if (!b) return nullptr;
+    RS_CALL(env, rs_group_synchronize(b->group), "RadixSortGroup.synchronize");
+    return nullptr;
+}
+
+napi_value GroupDestroy(napi_env env, napi_callback_info info) {
+    napi_value a[1];
+    if (!args(env, info, a)) return nullptr;
+    void* p = nullptr;
+    if (napi_get_value_external(env, a[0], &p) != napi_ok || !p)
+        return napi_throw_type_error(env, nullptr, "expected a group handle"), nullptr;
+    auto* b = static_cast<GroupBox*>(p);
+    if (b->group) rs_group_destroy(b->group);
+    b->group = nullptr;
+    return nullptr;
+}
+
 napi_value Define(napi_env env, napi_value exports, const char* name, napi_callback cb) {
     napi_value fn;
     napi_create_function(env, name, NAPI_AUTO_LENGTH, cb, nullptr, &fn);
@@ -501,6 +671,11 @@ napi_value Init(napi_env env, napi_value exports) {
     Define(env, exports, "scanPlanDispatchChain", ScanPlanDispatchChain);
     Define(env, exports, "planCheck", PlanCheck);
     Define(env, exports, "scanPlanDestroy", ScanPlanDestroy);
+    Define(env, exports, "groupCreate", GroupCreate);
+    Define(env, exports, "groupSort", GroupSort);
+    Define(env, exports, "groupResult", GroupResult);
+    Define(env, exports, "groupSynchronize", GroupSynchronize);
+    Define(env, exports, "groupDestroy", GroupDestroy);
     napi_value v;
     napi_create_uint32(env, RS_FLAG_HAS_VALUES, &v); napi_set_named_property(env, exports, "FLAG_HAS_VALUES", v);
     napi_create_uint32(env, RS_FLAG_CHECK_ORDER, &v); napi_set_named_property(env, exports, "FLAG_CHECK_ORDER", v);

@@ -40,4 +40,15 @@ assert.throws(() => new rs.RadixSortKernel({ keys: fakeKeys }), /count is requir
 assert.throws(() => new rs.RadixSortTextureKernel({ count: 10 }), /texture is required/);
 assert.throws(() => new rs.RadixSortTextureKernel({ data: { texture: { ptr: 4096n, format: 'r32uint' } }, count: 10 }),
   /rg32uint/);
+// multi-GPU group: options validated before any device call (rs_group_create)
+assert.strictEqual(typeof rs.RadixSortGroup, 'function');
+for (const f of ['groupCreate', 'groupSort', 'groupResult', 'groupSynchronize', 'groupDestroy']) {
+  assert.strictEqual(typeof rs.addon[f], 'function', f);
+}
+assert.throws(() => new rs.RadixSortGroup({ devices: [], capacity: 10 }), TypeError);
+assert.throws(() => new rs.RadixSortGroup({ devices: [0], capacity: 10, topBits: 9 }), /top_bits/);
+assert.throws(() => new rs.RadixSortGroup({ devices: [0], capacity: 10, rounds: 17 }), /rounds/);
+assert.throws(() => new rs.RadixSortGroup({ devices: [0], capacity: 10, transport: 'tcp' }), TypeError);
+assert.throws(() => new rs.RadixSortGroup({ devices: [0], capacity: 2 ** 32 }), /capacity/);
+assert.throws(() => rs.addon.groupSort(undefined, [], null, [], null), TypeError);
 console.log('node api checks ok');

@@ -11,7 +11,8 @@ from ._lib import RadixSortError, load as load_library  # noqa: F401
 from .kernel import (DeviceBuffer, PrefixSumKernel, RadixSortBufferKernel,  # noqa: F401
                      RadixSortKernel, RadixSortTextureKernel)
 from . import ops  # noqa: F401
+from .group import RadixSortGroup  # noqa: F401
 
 __all__ = ["RadixSortKernel", "RadixSortBufferKernel", "RadixSortTextureKernel", "PrefixSumKernel",
-           "DeviceBuffer",
+           "DeviceBuffer", "RadixSortGroup",
            "RadixSortError", "load_library", "ops"]

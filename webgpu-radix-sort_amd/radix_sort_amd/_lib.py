@@ -56,6 +56,15 @@ class PlanInfo(ctypes.Structure):
                 ("lane_order_selftest", ctypes.c_int32)]
 
 
+class GroupDesc(ctypes.Structure):
+    _fields_ = [("capacity", ctypes.c_uint64), ("flags", ctypes.c_uint32),
+                ("transport", ctypes.c_uint32), ("top_bits", ctypes.c_uint32),
+                ("rounds", ctypes.c_uint32)]
+
+
+RS_TRANSPORT_RCCL = 0
+RS_TRANSPORT_COPY = 1
+
 _lib = None
 
 _VP = ctypes.c_void_p
@@ -90,6 +99,18 @@ _SIGS = {
     "rs_scan_plan_dispatch_chain": (ctypes.c_uint32, [_VP, ctypes.POINTER(ctypes.c_uint32),
                                                       ctypes.c_uint32]),
     "rs_scan_plan_destroy": (None, [_VP]),
+    "rs_group_create": (ctypes.c_int, [ctypes.c_int32, ctypes.POINTER(ctypes.c_int32),
+                                       ctypes.POINTER(GroupDesc), ctypes.POINTER(_VP)]),
+    "rs_group_sort": (ctypes.c_int, [_VP, ctypes.POINTER(_VP), ctypes.POINTER(_VP),
+                                     ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(_VP)]),
+    "rs_group_result": (ctypes.c_int, [_VP, ctypes.c_int32, ctypes.POINTER(_VP),
+                                       ctypes.POINTER(_VP), ctypes.POINTER(ctypes.c_uint64)]),
+    "rs_group_synchronize": (ctypes.c_int, [_VP]),
+    "rs_group_destroy": (None, [_VP]),
+    "rs_group_plan": (ctypes.c_int, [ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint32,
+                                     ctypes.POINTER(ctypes.c_uint64),
+                                     ctypes.POINTER(ctypes.c_uint32),
+                                     ctypes.POINTER(ctypes.c_uint32)]),
     "rs_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int32)]),
     "rs_malloc": (ctypes.c_int, [ctypes.c_int32, ctypes.c_uint64, ctypes.POINTER(_VP)]),
     "rs_free": (ctypes.c_int, [_VP]),

@@ -886,73 +886,18 @@ __device__ __forceinline__ bool wave_inversion(const uint32_t (&k)[KPT], uint32_
     return __ballot(bad) != 0ull;
 }
 
-// ---- cross-tile line carry (k_onesweep CY = 1) -------------------------------------------------
-// A 128-B output line holding the end of tile t's digit-d run and the start of tile t+1's is
-// otherwise written half by each tile, at different times from different CUs; such a partial line
-// costs as much as a third more than a whole one (tools/line_probe.hip, line_probe2.hip: 2^28
-// records as 512-B runs, 1.17 ms per pass with the shared lines written half and half, 0.92 with
-// every line written whole and the tails carried through a small ring).  With the carry, tile t
-// writes only the whole lines of its run; the kout < LINE records of its last, shared line go to
-// its ring slot (one whole-line store per digit, its last record the header kout), and tile t+1
-// writes that line whole: the carried records + its own head records, after t's ring flag.  Only
-// a run that ends inside the line it started in (fewer records than the line's rest) still
-// writes a partial line.  Ring: kCarryRing slots of RADIX lines of LINE records; a slot is reused
-// only after its consumer acknowledged it.  Hand-off (MI355X_MICROARCH.md, cross-XCD hand-offs):
-// sc1 stores, s_waitcnt vmcnt(0) in every storing wave, barrier, one lane's sc1 flag store;
-// the consumer polls the flag with sc1 loads, barrier, sc1 loads of the slot.
-#ifndef RS_CY_ABL
-#define RS_CY_ABL 0   // timing ablations of the carry (results invalid): 1 no store drain before the
-                      // flag, 2 no wait for the predecessor's flag, 4 plain carry stores / loads,
-                      // 8 no carry stores, 16 no carry loads
-#endif
-constexpr uint32_t kCarryRing = 1024;
-struct CarryRing {
-    unsigned long long* rec;    // [kCarryRing][256][LINE] (key | value << 32)
-    unsigned long long* flag;   // [kCarryRing] (epoch << 32) | tile: slot published by tile
-    unsigned long long* ack;    // [kCarryRing] (epoch << 32) | tile: tile's slot consumed
-};
-
-__device__ __forceinline__ unsigned long long ld_sc1(const unsigned long long* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_sc1(unsigned long long* p, unsigned long long v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ unsigned long long ld_carry(const unsigned long long* p) {
-    return (RS_CY_ABL & 4) ? *p : ld_sc1(p);
-}
-__device__ __forceinline__ void st_carry(unsigned long long* p, unsigned long long v) {
-    if (RS_CY_ABL & 4) *p = v;
-    else st_sc1(p, v);
-}
-
-// Bounded wait until *p == want (one lane); a timeout sets the error words (never a hang).
-__device__ __forceinline__ void wait_word(const unsigned long long* p, unsigned long long want,
-                                          uint32_t spin_max, uint32_t* err, uint32_t* host_err) {
-    uint32_t spins = 0;
-    while (ld_sc1(p) != want) {
-        if (++spins > spin_max ||
-            ((spins & 255u) == 0u && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
-            atomicOr(err, 2u);
-            if (host_err) __hip_atomic_fetch_or(host_err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            return;
-        }
-        __builtin_amdgcn_s_sleep(1);
-    }
-}
-
 // SR > 1: the tile is SR times the LDS staging area (32K-key tiles from 1024 threads x 32 keys
 // with values, staged and scattered in two rounds of 16K positions).  Longer digit runs per tile
 // mean fewer 128-B lines shared by two tiles' runs; such a line reaches memory as two partial
 // writes, and those cost as much as a third more than whole lines (tools/line_probe.hip).
-template <int R, int BLOCK, int KPT, int L, int RANK, int LO = L, int SR = 1, int CY = 0>
+template <int R, int BLOCK, int KPT, int L, int RANK, int LO = L, int SR = 1>
 __global__ __launch_bounds__(BLOCK, pass_min_waves(BLOCK, KPT)) void k_onesweep(
     const uint32_t* __restrict__ in_k, const uint32_t* __restrict__ in_v,
     uint32_t* __restrict__ out_k, uint32_t* __restrict__ out_v, uint32_t n, uint32_t shift,
     uint32_t mask, uint32_t ntiles, const uint32_t* __restrict__ dtot,
     unsigned long long* status, uint32_t* ticket, uint32_t* err, uint32_t* __restrict__ ntot,
     uint32_t nshift, uint32_t nmask, uint32_t epoch, const uint32_t* gate, int pass,
-    uint32_t* chk, uint32_t fmask, uint32_t spin_max, uint32_t* host_err, CarryRing cring) {
+    uint32_t* chk, uint32_t fmask, uint32_t spin_max, uint32_t* host_err) {
     // ntot (may be null): whole-array totals of the NEXT pass's digit (key >> nshift) & nmask,
     // counted here from the keys this workgroup stages, so only pass 0 needs k_pass_totals.
     // chk (may be null, check_order, pass > 0): the order check of this pass's input, fused:
@@ -968,16 +913,8 @@ __global__ __launch_bounds__(BLOCK, pass_min_waves(BLOCK, KPT)) void k_onesweep(
     constexpr int WAVE_KEYS = 64 * KPT;
     static_assert(RADIX <= BLOCK, "one digit per thread");
     static_assert(SR == 1 || TILE <= 65536, "packed 16-bit tile positions");
-    static_assert(!CY || (SR == 1 && HAS_VALUES && RADIX == 256 && BLOCK > RADIX && TILE < 65536),
-                  "line carry: one staging round, values, 8-bit digits, a spare wave");
-    constexpr uint32_t LINE = LO == LAYOUT_AOS ? 16u : 32u;   // output positions per 128-B line
     __shared__ uint32_t s_whist[NW][RADIX];
     __shared__ uint32_t s_gdelta[RADIX];
-    // CY: s_lim[d] = staged-index range [lo, hi) of the records written in the interior scatter;
-    // s_gs[d] = first output position of the tile's run; s_ck[d] = count | kout << 16 | hown << 24
-    __shared__ uint32_t s_lim[CY ? RADIX : 1];
-    __shared__ uint32_t s_gs[CY ? RADIX : 1];
-    __shared__ uint32_t s_ck[CY ? RADIX : 1];
     __shared__ uint32_t s_dbase[RADIX];
     __shared__ uint32_t s_scratch[NW];
     __shared__ uint32_t s_next;
@@ -1120,122 +1057,16 @@ __global__ __launch_bounds__(BLOCK, pass_min_waves(BLOCK, KPT)) void k_onesweep(
                 st_store(st, (epoch << 2) | kStInclusive, excl + c);
             }
             s_gdelta[tid] = excl - tstart;
-            if (CY) {
-                // gs..ge: this tile's run of digit tid.  kout: records of the run's last line
-                // carried to tile T+1 (the line is shared and the run holds its start);
-                // hown: own records in the head line (written with the carry in, phase 2)
-                const uint32_t gs = excl, ge = excl + c;
-                const uint32_t hl = (gs + LINE - 1u) & ~(LINE - 1u);
-                const uint32_t kout = (T + 1 < ntiles && (ge & (LINE - 1u)) && (ge & ~(LINE - 1u)) >= gs)
-                                          ? (ge & (LINE - 1u)) : 0u;
-                const uint32_t own_end = ge - kout;
-                const uint32_t lo = hl < own_end ? hl : own_end;
-                const uint32_t hown = lo - gs;
-                s_gs[tid] = gs;
-                s_ck[tid] = c | (kout << 16) | (hown << 24);
-                s_lim[tid] = (lo - gs + tstart) | ((own_end - gs + tstart) << 16);
-            }
 #if RS_SCATTER_DEBUG >= 2
             // ablation (write-pattern study, n a power of 2): every (tile, digit) run starts on
             // its own 512-B-aligned slot; mode 2 also fills the run's last line with padding
             s_gdelta[tid] = ((((uint32_t)tid * ntiles + T) * 64u) & (n - 1u)) - tstart;
 #endif
         }
-        if (CY && tid == (uint32_t)RADIX && T + 1 < ntiles && T >= kCarryRing) {
-            // the ring slot this tile writes was last written by tile T - kCarryRing: its
-            // consumer must have read it (tickets run ahead of slow workgroups)
-            wait_word(cring.ack + T % kCarryRing,
-                      ((unsigned long long)epoch << 32) | (T - kCarryRing), spin_max, err, host_err);
-        }
         if (RS_PREFETCH == 1 && SR == 1 && Tn < ntiles) load(Tn * (uint32_t)TILE);
         __syncthreads();
         if (RS_PREFETCH == 2 && SR == 1 && Tn < ntiles) load(Tn * (uint32_t)TILE);
         RS_STAMP(pass, ntiles, T, 4, __builtin_amdgcn_s_memtime());
-        if constexpr (CY) {
-            constexpr uint32_t GROUPS = BLOCK / LINE;
-            const uint32_t grp = tid / LINE, lj = tid % LINE;
-            const uint32_t hlane = (lane_id() & ~(LINE - 1u)) + LINE - 1u;   // group's last lane
-            // phase 0: carry out - every digit whose run's last line is shared with the next tile
-            // writes that line's slot whole (records [0, kout), header kout in the last record)
-            if (T + 1 < ntiles) {
-                unsigned long long* slot = cring.rec + (size_t)(T % kCarryRing) * RADIX * LINE;
-                for (uint32_t d = grp; d < (uint32_t)RADIX; d += GROUPS) {
-                    const uint32_t ck = s_ck[d];
-                    const uint32_t ge = s_gs[d] + (ck & 0xFFFFu);
-                    if (ge & (LINE - 1u)) {
-                        const uint32_t kout = (ck >> 16) & 0xFFu;
-                        unsigned long long r = kout;   // header (last lane) / filler
-                        if (lj < kout) {
-                            const uint2 kv = s_kv[(ge & ~(LINE - 1u)) + lj - s_gdelta[d]];
-                            r = (unsigned long long)kv.x | ((unsigned long long)kv.y << 32);
-                        }
-                        if (!(RS_CY_ABL & 8)) st_carry(slot + (size_t)d * LINE + lj, r);
-                    }
-                }
-                if (!(RS_CY_ABL & 1)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
-            __syncthreads();
-            if (tid == 0 && T + 1 < ntiles)
-                st_sc1(cring.flag + T % kCarryRing, ((unsigned long long)epoch << 32) | T);
-            // phase 1: the interior lines (every record outside the head line and the carry)
-#pragma unroll 4
-            for (uint32_t i = tid; i < nvalid; i += BLOCK) {
-                const uint2 kv = s_kv[i];
-                const uint32_t d = (kv.x >> shift) & mask;
-                const uint32_t lim = s_lim[d];
-                if (i >= (lim & 0xFFFFu) && i < (lim >> 16)) {
-                    const uint32_t pos = s_gdelta[d] + i;
-                    if (pos < n) {
-                        if (LO == LAYOUT_AOS)
-                            st_out(reinterpret_cast<unsigned long long*>(out_k) + pos,
-                                   (unsigned long long)kv.x | ((unsigned long long)kv.y << 32));
-                        else {
-                            st_out(out_k + pos, kv.x);
-                            st_out(out_v + pos, kv.y);
-                        }
-                    }
-                }
-            }
-            // phase 2: the head lines - the predecessor's carried records + this tile's own
-            if (tid == 0 && T > 0 && !(RS_CY_ABL & 2))
-                wait_word(cring.flag + (T - 1) % kCarryRing,
-                          ((unsigned long long)epoch << 32) | (T - 1), spin_max, err, host_err);
-            __syncthreads();
-            const unsigned long long* pslot = cring.rec + (size_t)((T + kCarryRing - 1) % kCarryRing) * RADIX * LINE;
-            for (uint32_t d = grp; d < (uint32_t)RADIX; d += GROUPS) {
-                const uint32_t gs = s_gs[d];
-                if (!(gs & (LINE - 1u))) continue;
-                const uint32_t lb = gs & ~(LINE - 1u);
-                unsigned long long cr = 0ull;
-                uint32_t hin = 0;
-                if (T > 0 && !(RS_CY_ABL & 16)) {
-                    cr = ld_carry(pslot + (size_t)d * LINE + lj);
-                    hin = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(hlane << 2), (int)(uint32_t)cr);
-                    if (hin != 0u && hin != gs - lb && lj == 0) atomicOr(err, 4u);   // never
-                }
-                const uint32_t hown = s_ck[d] >> 24;
-                const uint32_t pos = lb + lj;
-                const bool carried = lj < hin;
-                const bool own = pos >= gs && pos < gs + hown;
-                if ((carried || own) && pos < n) {
-                    uint2 kv;
-                    if (carried) kv = make_uint2((uint32_t)cr, (uint32_t)(cr >> 32));
-                    else kv = s_kv[pos - s_gdelta[d]];
-                    if (LO == LAYOUT_AOS)
-                        st_out(reinterpret_cast<unsigned long long*>(out_k) + pos,
-                               (unsigned long long)kv.x | ((unsigned long long)kv.y << 32));
-                    else {
-                        st_out(out_k + pos, kv.x);
-                        st_out(out_v + pos, kv.y);
-                    }
-                }
-            }
-            __syncthreads();
-            // the predecessor's slot has been read (every load above was consumed before the
-            // barrier): it may be reused
-            if (tid == 0 && T > 0)
-                st_sc1(cring.ack + (T - 1) % kCarryRing, ((unsigned long long)epoch << 32) | (T - 1));
-        } else
 #pragma unroll
         for (int h = 0; h < SR; ++h) {
             if (h > 0) {   // the previous round's scatter has read the staging area

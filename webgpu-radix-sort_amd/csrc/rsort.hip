@@ -184,9 +184,6 @@ struct rs_plan {
     uint32_t* tickets = nullptr;   // = ptot + kTotalsMax: [16] per-pass tile tickets, [16] error
     uint32_t epoch = 0;            // tag of the last k_onesweep launch's status words
     uint32_t spin_max = 1u << 20;  // look-back wait bound in sleeps (RSORT_SPIN_MAX; tests force 0)
-    bool carry = false;            // one-sweep 16K-tile passes: shared output lines written whole
-                                   // by the later tile (k_onesweep CY; RSORT_CARRY=1: on; measured slower)
-    rs::CarryRing cring{};         // its ring (allocated with the one-sweep workspace)
     uint32_t* host_err = nullptr;  // host-mapped error word: set by a timed-out look-back wait,
     uint32_t* host_err_dev = nullptr;   // read + cleared by rs_plan_check / the next rs_plan_sort
     hipEvent_t done = nullptr;     // recorded after every sort (rs_plan_check waits for it)
@@ -269,11 +266,11 @@ uint32_t resident_per_cu(F kernel, int block) {
     return (uint32_t)api;
 }
 
-template <int R, int BLOCK, int KPT, int L, int RANK, int LO, int SR, int CY>
+template <int R, int BLOCK, int KPT, int L, int RANK, int LO, int SR>
 void launch_onesweep_t(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint32_t* ok,
                        uint32_t* ov, uint32_t n, uint32_t shift, uint32_t mask, uint32_t ntiles,
                        const uint32_t* gate, int pass, hipStream_t s) {
-    auto kern = rs::k_onesweep<R, BLOCK, KPT, L, RANK, LO, SR, CY>;
+    auto kern = rs::k_onesweep<R, BLOCK, KPT, L, RANK, LO, SR>;
     static const uint32_t per_cu = resident_per_cu(kern, BLOCK);   // per instantiation
     // RSORT_OS_GRID caps the persistent grid (tiles come from tickets, so any grid >= 1 is correct)
     static const uint32_t cap = [] { const char* g = getenv("RSORT_OS_GRID"); return g ? (uint32_t)atoi(g) : 0u; }();
@@ -288,18 +285,17 @@ void launch_onesweep_t(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint3
     hipLaunchKernelGGL(kern, dim3(grid), dim3(BLOCK), 0, s, ik, iv, ok, ov, n, shift, mask, ntiles,
                        p->ptot + p->ptot_off[pass], p->status, p->tickets + pass,
                        p->tickets + 16, ntot, nshift, nmask, p->epoch, gate, pass, chk,
-                       full_mask(p->bit_count), p->spin_max, p->host_err_dev,
-                       CY ? p->cring : rs::CarryRing{});
+                       full_mask(p->bit_count), p->spin_max, p->host_err_dev);
 }
 
-template <int R, int BLOCK, int KPT, int L, int LO, int SR, int CY = 0>
+template <int R, int BLOCK, int KPT, int L, int LO, int SR>
 void launch_onesweep_l(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint32_t* ok,
                        uint32_t* ov, uint32_t n, uint32_t shift, uint32_t mask, uint32_t ntiles,
                        const uint32_t* gate, int pass, hipStream_t s) {
     if (p->rank_mode == rs::RANK_BALLOT)
-        launch_onesweep_t<R, BLOCK, KPT, L, rs::RANK_BALLOT, LO, SR, CY>(p, ik, iv, ok, ov, n, shift, mask, ntiles, gate, pass, s);
+        launch_onesweep_t<R, BLOCK, KPT, L, rs::RANK_BALLOT, LO, SR>(p, ik, iv, ok, ov, n, shift, mask, ntiles, gate, pass, s);
     else
-        launch_onesweep_t<R, BLOCK, KPT, L, rs::RANK_LDS_ATOMIC, LO, SR, CY>(p, ik, iv, ok, ov, n, shift, mask, ntiles, gate, pass, s);
+        launch_onesweep_t<R, BLOCK, KPT, L, rs::RANK_LDS_ATOMIC, LO, SR>(p, ik, iv, ok, ov, n, shift, mask, ntiles, gate, pass, s);
 }
 
 // Layout pair of one pass: input layout | output layout << 4 (they differ only on the one-sweep
@@ -321,22 +317,10 @@ rs_status run_pass_cfg(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint3
     if (onesweep) {
         if (++p->epoch >= (1u << 30)) {   // tag space exhausted: clear the words, restart tags
             HIP_TRY(hipMemsetAsync(p->status, 0, 8ull * p->status_words, s));
-            if (p->cring.flag) HIP_TRY(hipMemsetAsync(p->cring.flag, 0, 16ull * rs::kCarryRing, s));
             p->epoch = 1;
         }
         constexpr int K = rs::LAYOUT_KEYS, S = rs::LAYOUT_SOA, A = rs::LAYOUT_AOS;
         p->timer.run(RS_KERNEL_SCATTER, s, [&] {
-            if constexpr (R == 8 && BLOCK == kLarge.block && KPT == kLarge.kpt && SR == 1 && !KEYS_ONLY) {
-                if (p->carry && p->cring.rec && LL != layout_pair(K, K)) {
-                    switch (LL) {
-                        case layout_pair(A, A): launch_onesweep_l<R, BLOCK, KPT, A, A, SR, 1>(p, ik, iv, ok, ov, n, shift, mask, ntiles, gate, pass, s); break;
-                        case layout_pair(S, S): launch_onesweep_l<R, BLOCK, KPT, S, S, SR, 1>(p, ik, iv, ok, ov, n, shift, mask, ntiles, gate, pass, s); break;
-                        case layout_pair(S, A): launch_onesweep_l<R, BLOCK, KPT, S, A, SR, 1>(p, ik, iv, ok, ov, n, shift, mask, ntiles, gate, pass, s); break;
-                        default: launch_onesweep_l<R, BLOCK, KPT, A, S, SR, 1>(p, ik, iv, ok, ov, n, shift, mask, ntiles, gate, pass, s);
-                    }
-                    return;
-                }
-            }
             if constexpr (KEYS_ONLY) {
                 launch_onesweep_l<R, BLOCK, KPT, K, K, SR>(p, ik, iv, ok, ov, n, shift, mask, ntiles, gate, pass, s);
             } else {
@@ -555,7 +539,6 @@ RS_EXPORT rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out) {
     if (const char* hg = getenv("RSORT_HUGE")) p->huge_tiles = atoi(hg);
     if (const char* kc = getenv("RSORT_KV_CFG")) p->kv_cfg = atoi(kc);
     if (const char* fc = getenv("RSORT_FUSED_CHECK")) p->fused_check = strcmp(fc, "0") != 0;
-    if (const char* cy = getenv("RSORT_CARRY")) p->carry = strcmp(cy, "0") != 0;
     if (const char* sm = getenv("RSORT_SPIN_MAX")) p->spin_max = (uint32_t)strtoul(sm, nullptr, 10);
     // Even number of passes so the result lands in the caller's buffers, like the reference's
     // bit_count/2 passes with ping-pong on bit % 4 (AbstractRadixSortKernel.ts:93-107).
@@ -609,22 +592,6 @@ RS_EXPORT rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out) {
         (e = alloc((uint32_t**)&p->status, 8ull * p->status_words)) != hipSuccess)
         return cleanup(fail(e == hipErrorOutOfMemory ? RS_ERR_OUT_OF_MEMORY : RS_ERR_HIP,
                             "rs_plan_create: hipMalloc failed: %s", hipGetErrorString(e)));
-    // line-carry ring of the 16K-tile one-sweep passes with values: 1024 slots x 256 digits x
-    // 32 records (64 MiB) + flag / ack words
-    if (p->carry && p->onesweep_mode != 0 && p->layout != rs::LAYOUT_KEYS && !use_small_tiles(d.count) &&
-        d.count > kTinyMax) {
-        const uint64_t rec_bytes = 8ull * rs::kCarryRing * 256 * 32;
-        unsigned long long* ring = nullptr;
-        if ((e = hipMalloc((void**)&ring, rec_bytes + 16ull * rs::kCarryRing)) != hipSuccess)
-            return cleanup(fail(e == hipErrorOutOfMemory ? RS_ERR_OUT_OF_MEMORY : RS_ERR_HIP,
-                                "rs_plan_create: hipMalloc failed: %s", hipGetErrorString(e)));
-        p->workspace += rec_bytes + 16ull * rs::kCarryRing;
-        p->cring.rec = ring;
-        p->cring.flag = ring + rec_bytes / 8;
-        p->cring.ack = p->cring.flag + rs::kCarryRing;
-        if ((e = hipMemset(p->cring.flag, 0, 16ull * rs::kCarryRing)) != hipSuccess)
-            return cleanup(fail(RS_ERR_HIP, "rs_plan_create: hipMemset failed: %s", hipGetErrorString(e)));
-    }
     p->tickets = p->ptot + rs::kTotalsMax;   // [16] tickets, [16] error word
     if ((e = hipHostMalloc((void**)&p->host_err, 4, hipHostMallocMapped)) != hipSuccess ||
         (e = hipHostGetDevicePointer((void**)&p->host_err_dev, p->host_err, 0)) != hipSuccess ||
@@ -650,7 +617,6 @@ RS_EXPORT void rs_plan_destroy(rs_plan* p) {
     (void)hipFree(p->flags);
     (void)hipFree(p->ptot);
     (void)hipFree(p->status);
-    (void)hipFree(p->cring.rec);
     if (p->host_err) (void)hipHostFree(p->host_err);
     if (p->done) (void)hipEventDestroy(p->done);
     delete p;

@@ -112,6 +112,12 @@ rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out);
 rs_status rs_plan_sort(rs_plan* plan, void* keys, void* values, void* stream);
 /* Same, for n <= the plan's count (multi-GPU receive buffers vary per call). */
 rs_status rs_plan_sort_n(rs_plan* plan, void* keys, void* values, uint64_t n, void* stream);
+/* Out-of-place sort: in_keys[0..n) (+ in_values) are only read; the stable sorted result is
+ * written to out_keys[0..n) (+ out_values).  A plan with separate arrays or keys only, without
+ * check_order; n <= capacity.  Pass 0 reads the input, the last pass writes the output: the same
+ * HBM traffic as rs_plan_sort, no copy (the multi-GPU sorts at world size 1 use it). */
+rs_status rs_plan_sort_copy(rs_plan* plan, const void* in_keys, const void* in_values,
+                            void* out_keys, void* out_values, uint64_t n, void* stream);
 /* One stable scatter pass by digit (key >> shift) & (2^bits - 1), bits <= 8, out of place:
  * in[0..n) -> out[0..n).  Writes the 2^bits digit totals (u32) to d_hist (device, may be
  * NULL).  The bucket-exchange partition step of the multi-GPU sort. */

@@ -48,6 +48,14 @@ class OracleLocalOps:
         keys_out.numpy().view(np.uint32)[:] = ok
         values_out.numpy().view(np.uint32)[:] = ov
 
+    def sort_copy(self, keys, values, keys_out, values_out):
+        k = keys.numpy().view(np.uint32)
+        v = None if values is None else values.numpy().view(np.uint32)
+        ok, ov = O.stable_sort_masked(k, v, 32)
+        keys_out.numpy().view(np.uint32)[:] = ok
+        if values_out is not None:
+            values_out.numpy().view(np.uint32)[:] = ov
+
     def sort(self, keys, n):
         k = keys.numpy().view(np.uint32)
         ok, _ = O.stable_sort_masked(k[:n].copy(), None, 32)
@@ -95,10 +103,11 @@ def _worker(rank, world, port, n_per_rank, kind, q, chunks, kv):
 @pytest.mark.parametrize("kind,world,chunks,kv", [
     ("uniform", 2, 4, True), ("few", 2, 3, True), ("skewed", 2, 1, True), ("uniform", 3, 4, True),
     ("few", 3, 2, True), ("one_bucket", 3, 4, True), ("one_bucket", 2, 2, False),
-    ("uniform", 3, 3, False)])
+    ("uniform", 3, 3, False), ("uniform", 1, 4, True), ("few", 1, 2, False)])
 def test_gloo_bucket_exchange_is_global_stable_sort(kind, world, chunks, kv):
     """The exchange code RCCL runs (exchange_round: batched point-to-point record messages, the
-    own segment copied locally), here over gloo with oracle local steps."""
+    own segment copied locally), here over gloo with oracle local steps; world size 1 takes the
+    no-exchange path (one out-of-place sort)."""
     n = 20_000
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

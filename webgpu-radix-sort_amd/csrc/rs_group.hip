@@ -18,7 +18,7 @@
 //   5. the sort stream waits for round g only, then sorts region g (rs_plan_sort_records: records
 //      in, separate arrays out; keys only: rs_plan_sort_n in place) while later rounds move.
 // At world size 1 nothing is exchanged: the slice is sorted straight from the input into the
-// output (rs_internal_sort_from), no partition pass.
+// output (rs_plan_sort_copy), no partition pass.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -294,12 +294,12 @@ static rs_status group_sort_world1(rs_group* g, void* const* keys, void* const* 
     if (g->kv) {
         G_TRY(grow((void**)&k.out_k, &k.out_k_cap, 4 * n));
         G_TRY(grow((void**)&k.out_v, &k.out_v_cap, 4 * n));
-        G_TRY(rs_internal_sort_from(k.local, keys[0], values[0], k.out_k, k.out_v, n, k.sort_s));
+        G_TRY(rs_plan_sort_copy(k.local, keys[0], values[0], k.out_k, k.out_v, n, k.sort_s));
         k.res_k = k.out_k;
         k.res_v = k.out_v;
     } else {
         G_TRY(grow(&k.recv, &k.recv_cap, 4 * n));
-        G_TRY(rs_internal_sort_from(k.local, keys[0], nullptr, k.recv, nullptr, n, k.sort_s));
+        G_TRY(rs_plan_sort_copy(k.local, keys[0], nullptr, k.recv, nullptr, n, k.sort_s));
         k.res_k = k.recv;
         k.res_v = nullptr;
     }

@@ -746,21 +746,23 @@ RS_EXPORT rs_status rs_plan_sort_n(rs_plan* p, void* keys, void* values, uint64_
     return RS_OK;
 }
 
-// Out-of-place sort for the multi-GPU group at world size 1 (rs_group.hip): in[0..n) is only
-// read, the sorted result is written to out[0..n) (separate arrays or keys only).
-rs_status rs_internal_sort_from(rs_plan* p, const void* in_k, const void* in_v, void* out_k,
-                                void* out_v, uint64_t n, void* stream) {
-    if (!p) return fail(RS_ERR_INVALID_ARG, "rs_internal_sort_from: null plan");
+// Out-of-place sort (rsort.h; the multi-GPU paths at world size 1): in[0..n) is only read, the
+// sorted result is written to out[0..n): pass 0 reads the input, the last pass writes the output.
+RS_EXPORT rs_status rs_plan_sort_copy(rs_plan* p, const void* in_k, const void* in_v, void* out_k,
+                                      void* out_v, uint64_t n, void* stream) {
+    if (!p) return fail(RS_ERR_INVALID_ARG, "rs_plan_sort_copy: null plan");
     if (n > p->capacity)
         return fail(RS_ERR_CAPACITY, "count %llu exceeds plan capacity %llu",
                     (unsigned long long)n, (unsigned long long)p->capacity);
     if (p->layout == rs::LAYOUT_AOS || p->check_order)
-        return fail(RS_ERR_INVALID_ARG, "rs_internal_sort_from: separate arrays, no check_order");
+        return fail(RS_ERR_INVALID_ARG, "rs_plan_sort_copy: needs a plan with separate arrays (not interleaved) and no check_order");
     const bool kv = p->layout == rs::LAYOUT_SOA;
     if (n == 0) return RS_OK;
     if (!in_k || !out_k || (kv && (!in_v || !out_v)))
-        return fail(RS_ERR_INVALID_ARG, "rs_internal_sort_from: null buffer");
-    if (rs_status st = take_device_error(p, "rs_group_sort")) return st;
+        return fail(RS_ERR_INVALID_ARG, "rs_plan_sort_copy: null buffer");
+    if (((uintptr_t)in_k | (uintptr_t)out_k | (kv ? ((uintptr_t)in_v | (uintptr_t)out_v) : 0)) & 3)
+        return fail(RS_ERR_INVALID_ARG, "keys/values must be 4-byte aligned");
+    if (rs_status st = take_device_error(p, "rs_plan_sort_copy")) return st;
     DeviceGuard guard(p->desc.device);
     hipStream_t s = (hipStream_t)stream;
     uint32_t* uk = (uint32_t*)out_k;

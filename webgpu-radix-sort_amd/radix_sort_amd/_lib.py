@@ -75,6 +75,7 @@ _SIGS = {
     "rs_plan_create": (ctypes.c_int, [ctypes.POINTER(PlanDesc), ctypes.POINTER(_VP)]),
     "rs_plan_sort": (ctypes.c_int, [_VP, _VP, _VP, _VP]),
     "rs_plan_sort_n": (ctypes.c_int, [_VP, _VP, _VP, ctypes.c_uint64, _VP]),
+    "rs_plan_sort_copy": (ctypes.c_int, [_VP, _VP, _VP, _VP, _VP, ctypes.c_uint64, _VP]),
     "rs_plan_partition": (ctypes.c_int, [_VP, _VP, _VP, _VP, _VP, ctypes.c_uint64,
                                          ctypes.c_uint32, ctypes.c_uint32, _VP, _VP]),
     "rs_plan_partition_totals": (ctypes.c_int, [_VP, _VP, _VP, _VP, _VP, ctypes.c_uint64,

@@ -57,6 +57,10 @@ class LocalOps(Protocol):
     def sort(self, keys, n: int) -> None:
         """Stable in-place sort of keys[:n] (keys only) by the full 32-bit key."""
 
+    def sort_copy(self, keys, values, keys_out, values_out) -> None:
+        """Stable out-of-place sort of (keys, values) by the 32-bit key into keys_out /
+        values_out (values None: keys only); the input is only read."""
+
     def empty(self, n: int, like):
         """Uninitialised buffer of n elements of like's dtype on like's device."""
 
@@ -220,6 +224,13 @@ def _distributed_sort(keys, values, ops, group, bits, chunks) -> ExchangeResult:
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     n_local = keys.numel()
+    if world == 1:
+        # one rank holds the whole array: nothing to exchange, so no partition either - one
+        # out-of-place sort (pass 0 reads the input, the last pass writes the result)
+        out_k = ops.empty(n_local, keys)
+        out_v = None if values is None else ops.empty(n_local, values)
+        ops.sort_copy(keys, values, out_k, out_v)
+        return ExchangeResult(out_k, out_v, n_local, [n_local], [n_local])
     G = max(1, int(chunks))
     shift = 32 - bits
     hist = ops.histogram(keys, shift, bits)                     # [2^bits]
@@ -319,6 +330,11 @@ class HipLocalOps:
         n = records.numel()
         self._grow(n)
         self.plan.sort_records(records, keys_out, values_out, n)
+
+    def sort_copy(self, keys, values, keys_out, values_out) -> None:
+        n = keys.numel()
+        self._grow(n)
+        self.plan.sort_copy(keys, values, keys_out, values_out, n)
 
     def check(self) -> None:
         """Raise if a local sort or partition failed on the device (rs_plan_check)."""

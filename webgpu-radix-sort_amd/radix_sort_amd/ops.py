@@ -63,6 +63,15 @@ class SortPlan:
                                          None if values is None else values.data_ptr(), n,
                                          _stream(keys, stream)), "rs_plan_sort_n")
 
+    def sort_copy(self, in_keys, in_values, out_keys, out_values=None, n: int | None = None,
+                  stream=None) -> None:
+        """Out-of-place stable sort in -> out (the input is only read)."""
+        n = in_keys.numel() if n is None else n
+        check(_lib.load().rs_plan_sort_copy(
+            self._plan, in_keys.data_ptr(), None if in_values is None else in_values.data_ptr(),
+            out_keys.data_ptr(), None if out_values is None else out_values.data_ptr(), n,
+            _stream(in_keys, stream)), "rs_plan_sort_copy")
+
     def check(self) -> None:
         """Wait for the plan's last sort; raise on a device-side failure since the last check
         (rs_plan_check)."""

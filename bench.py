@@ -341,14 +341,20 @@ def main() -> None:
             raise SystemExit(f"bench: rank {rank} output not sorted")
         info = {"passes": 4}
         keys_per_step = n * world
-        # the local sort runs as `chunks` group sorts per step: a pass launch handles one group
-        scatter_keys = r.n / EXCHANGE_ROUNDS
         extra["recv_keys_rank0"] = r.n
-        extra["partition"] = (f"top 8 bits, whole-bucket split; {EXCHANGE_ROUNDS} exchange rounds of "
-                              "bucket groups, each sorted while the later rounds are on the wire")
-        extra["roofline_scope"] = ("local group sorts of the received keys (rank 0; a pass launch "
-                                   f"handles one of the {EXCHANGE_ROUNDS} bucket groups)")
-        extra["group_sorts_per_step"] = EXCHANGE_ROUNDS
+        if world == 1:
+            # one rank: nothing to exchange - the slice is sorted out of place in one sort
+            scatter_keys = r.n
+            extra["partition"] = "none (world size 1: one out-of-place sort of the slice)"
+            extra["roofline_scope"] = "the rank's whole sort"
+        else:
+            # the local sort runs as `chunks` group sorts per step: a pass launch handles one group
+            scatter_keys = r.n / EXCHANGE_ROUNDS
+            extra["partition"] = (f"top 8 bits, whole-bucket split; {EXCHANGE_ROUNDS} exchange rounds "
+                                  "of bucket groups, each sorted while the later rounds are on the wire")
+            extra["roofline_scope"] = ("local group sorts of the received keys (rank 0; a pass launch "
+                                       f"handles one of the {EXCHANGE_ROUNDS} bucket groups)")
+            extra["group_sorts_per_step"] = EXCHANGE_ROUNDS
 
     value = keys_per_step * K / elapsed / 1e9
     sc = kernel_ms.get("scatter", {"ms": 0.0, "launches": 0})
@@ -409,7 +415,7 @@ def main() -> None:
                        "local_shuffle": wl["local_shuffle"], "check_order": wl["check_order"],
                        "radix_bits": args.radix_bits or 8,
                        "parallelism": "single GPU" if world == 1 else
-                       f"{world} ranks, top-byte bucket exchange (RCCL all_to_all)"},
+                       f"{world} ranks, top-byte bucket exchange (RCCL point-to-point rounds)"},
             "roofline": roof, "cpu_baseline": cpu, **extra,
         }
         print(json.dumps(out), flush=True)

@@ -1,0 +1,219 @@
+// Host-side AddressSanitizer / UBSan driver (SURVEY.md §5 "sanitizers"): exercises every C-ABI
+// entry point of a librsort built with host-only sanitizers (make -C webgpu-radix-sort_amd/csrc
+// asan: `-Xarch_host -fsanitize=address,undefined`; device code is not instrumented), so plan
+// creation, the launch/schedule code, the multi-GPU group planner and its buffer management run
+// under ASan on a GPU box.  Every result is checked on the host (sorted, a stable permutation).
+// Exit status 0 = all checks passed and the sanitizers reported nothing.
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "../include/rsort.h"
+
+static int g_fail = 0;
+#define CHECK(c, ...)                                  \
+    do {                                               \
+        if (!(c)) {                                    \
+            fprintf(stderr, "FAIL %s:%d: ", __FILE__, __LINE__); \
+            fprintf(stderr, __VA_ARGS__);              \
+            fprintf(stderr, "\n");                     \
+            ++g_fail;                                  \
+        }                                              \
+    } while (0)
+#define OK(call) CHECK((call) == RS_OK, "%s -> %s", #call, rs_last_error())
+
+static uint32_t mix(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return (uint32_t)(z ^ (z >> 31));
+}
+
+// keys sorted ascending; values[i] = original index, stable (equal keys keep index order)
+static bool verify(const std::vector<uint32_t>& in, const std::vector<uint32_t>& k,
+                   const std::vector<uint32_t>* v, size_t n) {
+    for (size_t i = 0; i + 1 < n; ++i)
+        if (k[i] > k[i + 1]) return false;
+    if (v) {
+        for (size_t i = 0; i < n; ++i) {
+            if ((*v)[i] >= n || in[(*v)[i]] != k[i]) return false;
+            if (i + 1 < n && k[i] == k[i + 1] && (*v)[i] >= (*v)[i + 1]) return false;
+        }
+    }
+    return true;
+}
+
+static void sort_case(size_t n, bool kv, uint32_t flags_extra, uint32_t key_mask) {
+    std::vector<uint32_t> hk(n), hv(n);
+    for (size_t i = 0; i < n; ++i) { hk[i] = mix(i * 7 + n) & key_mask; hv[i] = (uint32_t)i; }
+    void *dk = nullptr, *dv = nullptr;
+    OK(rs_malloc(0, 4 * n, &dk));
+    OK(rs_malloc(0, 4 * n, &dv));
+    OK(rs_memcpy_h2d(dk, hk.data(), 4 * n, nullptr));
+    OK(rs_memcpy_h2d(dv, hv.data(), 4 * n, nullptr));
+    rs_plan_desc d{};
+    d.device = 0;
+    d.count = n;
+    d.flags = (kv ? RS_FLAG_HAS_VALUES : 0u) | flags_extra;
+    rs_plan* p = nullptr;
+    OK(rs_plan_create(&d, &p));
+    if (p) {
+        OK(rs_plan_sort(p, dk, kv ? dv : nullptr, nullptr));
+        OK(rs_plan_check(p));
+        std::vector<uint32_t> ok(n), ov(n);
+        OK(rs_memcpy_d2h(ok.data(), dk, 4 * n, nullptr));
+        OK(rs_memcpy_d2h(ov.data(), dv, 4 * n, nullptr));
+        CHECK(verify(hk, ok, kv ? &ov : nullptr, n), "sort n=%zu kv=%d flags=%x", n, kv, flags_extra);
+        rs_plan_info info;
+        OK(rs_plan_info_get(p, &info));
+        rs_plan_destroy(p);
+    }
+    OK(rs_free(dk));
+    OK(rs_free(dv));
+}
+
+static void copy_and_records(size_t n) {
+    std::vector<uint32_t> hk(n), hv(n);
+    for (size_t i = 0; i < n; ++i) { hk[i] = mix(i ^ 0x5555); hv[i] = (uint32_t)i; }
+    void *ik, *iv, *ok, *ov, *rec;
+    OK(rs_malloc(0, 4 * n, &ik));
+    OK(rs_malloc(0, 4 * n, &iv));
+    OK(rs_malloc(0, 4 * n, &ok));
+    OK(rs_malloc(0, 4 * n, &ov));
+    OK(rs_malloc(0, 8 * n, &rec));
+    OK(rs_memcpy_h2d(ik, hk.data(), 4 * n, nullptr));
+    OK(rs_memcpy_h2d(iv, hv.data(), 4 * n, nullptr));
+    rs_plan_desc d{};
+    d.count = n;
+    d.flags = RS_FLAG_HAS_VALUES;
+    rs_plan* p = nullptr;
+    OK(rs_plan_create(&d, &p));
+    std::vector<uint32_t> gk(n), gv(n);
+    if (p) {
+        OK(rs_plan_sort_copy(p, ik, iv, ok, ov, n, nullptr));
+        OK(rs_plan_check(p));
+        OK(rs_memcpy_d2h(gk.data(), ok, 4 * n, nullptr));
+        OK(rs_memcpy_d2h(gv.data(), ov, 4 * n, nullptr));
+        CHECK(verify(hk, gk, &gv, n), "sort_copy n=%zu", n);
+        OK(rs_plan_partition_records(p, ik, iv, rec, n, 24, 8, nullptr, nullptr));
+        OK(rs_plan_sort_records(p, rec, ok, ov, n, nullptr));
+        OK(rs_plan_check(p));
+        OK(rs_memcpy_d2h(gk.data(), ok, 4 * n, nullptr));
+        OK(rs_memcpy_d2h(gv.data(), ov, 4 * n, nullptr));
+        CHECK(verify(hk, gk, &gv, n), "partition+sort_records n=%zu", n);
+        rs_plan_destroy(p);
+    }
+    for (void* q : {ik, iv, ok, ov, rec}) OK(rs_free(q));
+}
+
+static void scan_case(size_t n) {
+    std::vector<uint32_t> h(n), out(n);
+    for (size_t i = 0; i < n; ++i) h[i] = mix(i) & 0xFF;
+    void* dd;
+    OK(rs_malloc(0, 4 * n, &dd));
+    OK(rs_memcpy_h2d(dd, h.data(), 4 * n, nullptr));
+    rs_scan_plan* s = nullptr;
+    OK(rs_scan_plan_create(0, n, 16, 16, 0, &s));
+    if (s) {
+        OK(rs_scan_plan_run(s, dd, nullptr));
+        OK(rs_memcpy_d2h(out.data(), dd, 4 * n, nullptr));
+        uint32_t acc = 0;
+        bool good = true;
+        for (size_t i = 0; i < n; ++i) { good &= out[i] == acc; acc += h[i]; }
+        CHECK(good, "scan n=%zu", n);
+        uint32_t chain[64];
+        CHECK(rs_scan_plan_dispatch_chain(s, chain, 64) > 0, "dispatch chain");
+        rs_scan_plan_destroy(s);
+    }
+    OK(rs_free(dd));
+}
+
+static void group_case(int world, uint32_t transport, bool kv, size_t n_per) {
+    std::vector<int32_t> devs(world, 0);
+    rs_group_desc gd{};
+    gd.capacity = n_per;
+    gd.flags = kv ? RS_FLAG_HAS_VALUES : 0u;
+    gd.transport = transport;
+    gd.rounds = 3;
+    rs_group* g = nullptr;
+    OK(rs_group_create(world, devs.data(), &gd, &g));
+    if (!g) return;
+    std::vector<void*> k(world), v(world);
+    std::vector<uint64_t> cnt(world);
+    std::vector<uint32_t> all, allv;
+    for (int r = 0; r < world; ++r) {
+        cnt[r] = n_per - (size_t)r * 1000;
+        std::vector<uint32_t> hk(cnt[r]), hv(cnt[r]);
+        for (size_t i = 0; i < cnt[r]; ++i) {
+            hk[i] = mix(all.size() + 99) & 0xFF00FFFFu;
+            hv[i] = (uint32_t)all.size();
+            all.push_back(hk[i]);
+        }
+        OK(rs_malloc(0, 4 * cnt[r], &k[r]));
+        OK(rs_malloc(0, 4 * cnt[r], &v[r]));
+        OK(rs_memcpy_h2d(k[r], hk.data(), 4 * cnt[r], nullptr));
+        OK(rs_memcpy_h2d(v[r], hv.data(), 4 * cnt[r], nullptr));
+    }
+    OK(rs_group_sort(g, k.data(), kv ? v.data() : nullptr, cnt.data(), nullptr));
+    OK(rs_group_synchronize(g));
+    std::vector<uint32_t> gk, gv;
+    for (int r = 0; r < world; ++r) {
+        void *rk, *rv;
+        uint64_t m;
+        OK(rs_group_result(g, r, &rk, &rv, &m));
+        std::vector<uint32_t> a(m), b(m);
+        if (m) OK(rs_memcpy_d2h(a.data(), rk, 4 * m, nullptr));
+        if (m && kv) OK(rs_memcpy_d2h(b.data(), rv, 4 * m, nullptr));
+        gk.insert(gk.end(), a.begin(), a.end());
+        gv.insert(gv.end(), b.begin(), b.end());
+    }
+    CHECK(gk.size() == all.size(), "group sizes");
+    if (gk.size() == all.size())
+        CHECK(verify(all, gk, kv ? &gv : nullptr, all.size()), "group world=%d transport=%u kv=%d", world,
+              transport, kv);
+    rs_group_destroy(g);
+    for (int r = 0; r < world; ++r) { OK(rs_free(k[r])); OK(rs_free(v[r])); }
+}
+
+static void error_paths() {
+    rs_plan_desc d{};
+    d.count = 10;
+    d.workgroup_x = 3;
+    rs_plan* p = nullptr;
+    CHECK(rs_plan_create(&d, &p) == RS_ERR_NOT_POW2 && !p, "non-pow2 workgroup");
+    d.workgroup_x = 16;
+    d.bit_count = 6;
+    CHECK(rs_plan_create(&d, &p) == RS_ERR_BIT_COUNT, "bit_count 6");
+    CHECK(rs_plan_sort(nullptr, nullptr, nullptr, nullptr) == RS_ERR_INVALID_ARG, "null plan");
+    rs_group_desc gd{};
+    gd.top_bits = 9;
+    int32_t dev = 0;
+    rs_group* g = nullptr;
+    CHECK(rs_group_create(1, &dev, &gd, &g) == RS_ERR_INVALID_ARG && !g, "top_bits 9");
+    CHECK(strlen(rs_last_error()) > 0, "error message");
+    uint64_t h[8] = {1, 2, 3, 4, 5, 6, 7, 8};
+    uint32_t bounds[3], cuts[6];
+    OK(rs_group_plan(2, 4, 2, h, bounds, cuts));
+    CHECK(bounds[0] == 0 && bounds[2] == 4, "plan bounds");
+}
+
+int main() {
+    error_paths();
+    for (size_t n : {1ul, 2ul, 1000ul, 16385ul, 300000ul, 5000000ul, 13000000ul}) {
+        sort_case(n, true, 0, ~0u);
+        sort_case(n, false, 0, ~0u);
+    }
+    sort_case(20000, true, RS_FLAG_CHECK_ORDER, 0xFFu);          // duplicate-heavy + check_order
+    sort_case(13000000, true, RS_FLAG_CHECK_ORDER | RS_FLAG_LOCAL_SHUFFLE, ~0u);
+    copy_and_records(70000);
+    copy_and_records(13000000);
+    scan_case(1000);
+    scan_case(3000017);
+    group_case(1, RS_TRANSPORT_RCCL, true, 200000);
+    group_case(3, RS_TRANSPORT_COPY, true, 300000);
+    group_case(2, RS_TRANSPORT_COPY, false, 13000000);
+    printf("asan driver: %d failure(s)\n", g_fail);
+    return g_fail ? 1 : 0;
+}

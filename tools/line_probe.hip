@@ -27,6 +27,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>
+#include <cstring>
 #pragma clang diagnostic ignored "-Wunused-value"
 #pragma clang diagnostic ignored "-Wunused-result"
 
@@ -97,7 +98,7 @@ float run(const uint2* s, uint2* d, uint32_t ntiles, int grid) {
     return ms / 10;
 }
 
-int main() {
+int main(int argc, char** argv) {
     const uint32_t ntiles = 16384;
     const size_t n = (size_t)ntiles * 16384;   // 2^28 records, 2 GiB
     uint2 *s, *d;
@@ -105,6 +106,20 @@ int main() {
     hipMemset(s, 1, n * 8);
     hipMemset(d, 0, n * 8 + 4096);
     if (hipMalloc(&g_side, (size_t)ntiles * 256 * 128) != hipSuccess) return 1;
+    if (argc > 1 && strcmp(argv[1], "runs") == 0) {
+        // run length series (digit width go/no-go: 11-bit digits leave ~8-record runs per 16K tile)
+        for (int rep = 0; rep < 2; ++rep) {
+            const float t[8] = {run<1, 8>(s, d, ntiles, 256), run<2, 8>(s, d, ntiles, 256),
+                                run<1, 16>(s, d, ntiles, 256), run<2, 16>(s, d, ntiles, 256),
+                                run<1, 32>(s, d, ntiles, 256), run<2, 32>(s, d, ntiles, 256),
+                                run<1, 64>(s, d, ntiles, 256), run<2, 64>(s, d, ntiles, 256)};
+            const int rl[8] = {8, 8, 16, 16, 32, 32, 64, 64};
+            for (int m = 0; m < 8; ++m)
+                printf("{\"probe\": \"line_probe\", \"mode\": \"%s\", \"run_records\": %d, \"grid\": 256, \"ms\": %.4f, \"rw_GBs\": %.1f}\n",
+                       (m & 1) ? "runs_shifted" : "runs_line_aligned", rl[m], t[m], 2.0 * n * 8 / (t[m] * 1e-3) / 1e9);
+        }
+        return 0;
+    }
     for (int grid : {256, 512, 1024}) {
         const float t0 = run<0>(s, d, ntiles, grid);
         const float t1 = run<1>(s, d, ntiles, grid);

@@ -37,7 +37,7 @@
 #define RS_SCATTER_DEBUG 0   // ablation (tools/sweep.py): 1 = linear writes (output pos = input pos)
 #endif
 #ifndef RS_NT_STORE
-#define RS_NT_STORE 0        // 1: pass outputs stored non-temporal (streamed, read back next pass)
+#define RS_NT_STORE 0        // pass output stores: 1 non-temporal, 2 write-through (sc1), 3 system scope
 #endif
 #ifndef RS_NT_LOAD
 #define RS_NT_LOAD 0         // 1: pass inputs (full tiles) loaded non-temporal (read once per pass)
@@ -83,8 +83,13 @@ __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
 // Stream accesses of the pass kernels (cache policy per RS_NT_STORE / RS_NT_LOAD).
 template <class T>
 __device__ __forceinline__ void st_out(T* p, T v) {
-#if RS_NT_STORE
+#if RS_NT_STORE == 1
     __builtin_nontemporal_store(v, p);
+#elif RS_NT_STORE == 2
+    // write-through (sc1) stores: agent-scope relaxed atomic stores
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#elif RS_NT_STORE == 3
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 #else
     *p = v;
 #endif

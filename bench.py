@@ -329,8 +329,8 @@ def main() -> None:
         barrier()
         elapsed = time.perf_counter() - t0
         lo.check()      # no local sort or partition failed on the device
-        ms = (ctypes.c_double * 4)()
-        cnt = (ctypes.c_uint64 * 4)()
+        ms = (ctypes.c_double * _lib.RS_KERNEL_KINDS)()
+        cnt = (ctypes.c_uint64 * _lib.RS_KERNEL_KINDS)()
         _lib.load().rs_plan_kernel_times(lo.plan._plan, ms, cnt)
         for i, name in enumerate(_lib.KERNEL_NAMES):
             kernel_ms[name] = {"ms": ms[i], "launches": int(cnt[i])}
@@ -358,11 +358,31 @@ def main() -> None:
 
     value = keys_per_step * K / elapsed / 1e9
     sc = kernel_ms.get("scatter", {"ms": 0.0, "launches": 0})
+    bk = kernel_ms.get("bucket", {"ms": 0.0, "launches": 0})
+    fb = kernel_ms.get("fallback", {"ms": 0.0, "launches": 0})
     hist_launches = kernel_ms.get("histogram", {"launches": 0})["launches"]
+    # the hybrid MSD path (separate arrays >= 12M keys): two one-sweep passes (top byte, next byte
+    # within top-byte segments) and the in-LDS 16-bit bucket pass; its LSD fallbacks are enqueued
+    # too and gated off on the device unless the keys are too skewed (then they carry the time)
+    msd = bk["launches"] > 0 and bk["ms"] > fb["ms"]
+    if bk["launches"] and not msd:
+        sc = fb        # the device took the LSD fallback: its passes are the pass launches
     # one-sweep path: one digit-count launch per sort instead of one per pass
-    onesweep = 0 < hist_launches < sc["launches"]
+    onesweep = msd or 0 < hist_launches < sc["launches"]
     bytes_per_key = 16 if wl["values"] else 8
     roof = None
+    if msd:
+        # the gated-off fallback launches are not pass launches: the scatter kind holds the two
+        # MSD passes exactly
+        extra["path"] = ("hybrid MSD: top-byte one-sweep pass, 16-bit bucket histogram, next-byte "
+                         "one-sweep pass per top-byte segment, in-LDS sort of every 16-bit bucket")
+        extra["bucket_pass"] = {
+            "kernel": "k_bucket_sort (one workgroup per 16-bit bucket, 2 LDS passes, contiguous writes)",
+            "ms_per_sort": round(bk["ms"] / max(K, 1), 4),
+            "achieved_GBs": round(scatter_keys * bytes_per_key / (bk["ms"] / max(K, 1) / 1e3) / 1e9, 1),
+            "frac": round(scatter_keys * bytes_per_key / (bk["ms"] / max(K, 1) / 1e3) / 1e9 / HBM_PEAK_GBS, 4)}
+    elif bk["launches"]:
+        extra["path"] = "LSD one-sweep passes (the hybrid MSD path's device-side fallback: skewed keys)"
     if sc["launches"]:
         avg_ms = sc["ms"] / sc["launches"]
         achieved = scatter_keys * bytes_per_key / (avg_ms / 1e3) / 1e9
@@ -388,6 +408,9 @@ def main() -> None:
     hist_reads = max(1, round(hist / max(K, 1))) if hist else passes
     if use_dist and hist:
         hist_reads = 1   # one totals read per group sort: each key once per step
+    if msd:
+        passes = 3       # MSD pass 0, MSD pass 1, bucket pass; key reads: top-byte totals, hist16
+        hist_reads = 2
     sort_bytes = keys_per_step / max(world, 1) * (passes * (8 + 8 * (1 if wl["values"] else 0))
                                                   + 4 * hist_reads)
     extra["digit_count_reads_per_sort"] = hist_reads

@@ -26,7 +26,7 @@ extern "C" {
 #endif
 
 #define RSORT_VERSION_MAJOR 0
-#define RSORT_VERSION_MINOR 2
+#define RSORT_VERSION_MINOR 3
 
 typedef enum rs_status {
     RS_OK = 0,
@@ -94,7 +94,10 @@ enum {
     RS_KERNEL_SCATTER = 2,      /* rank + local shuffle + scatter     (RadixSortReorder.ts:80-102,
                                                                        RadixSortLocalShuffle.ts) */
     RS_KERNEL_CHECK = 3,        /* order check                        (CheckSort.ts:70-145) */
-    RS_KERNEL_KINDS = 4
+    RS_KERNEL_BUCKET = 4,       /* hybrid MSD path: in-LDS sort of every 16-bit bucket */
+    RS_KERNEL_FALLBACK = 5,     /* hybrid MSD path: the LSD passes it enqueues as its fallback
+                                   (gated off on the device unless the keys are too skewed) */
+    RS_KERNEL_KINDS = 6
 };
 
 /* ---- errors / versions ------------------------------------------------------------------ */

@@ -744,15 +744,19 @@ constexpr int kTotalsMax = 1024;
 #ifndef RS_TOT_U
 #define RS_TOT_U 1           // k_pass_totals 16-byte loads per lane issued together
 #endif
+// only (bit p): count pass p's digit (its slot of out stays as it is otherwise).
 template <int KS, int BLOCK = RS_TOT_BLOCK>
 __global__ __launch_bounds__(BLOCK) void k_pass_totals(const uint32_t* __restrict__ keys,
                                                        uint32_t n, PassList pl, uint32_t shift0,
                                                        uint32_t* __restrict__ out,
                                                        uint32_t* chk = nullptr,
-                                                       uint32_t fmask = 0xFFFFFFFFu) {
+                                                       uint32_t fmask = 0xFFFFFFFFu,
+                                                       uint32_t only = 0xFFFFu,
+                                                       const uint32_t* gate = nullptr) {
     // pass p's digit starts at bit shift0 + sum(width[<p]) (shift0 = 0 for a sort)
     constexpr int NWT = BLOCK / 64;
     __shared__ uint32_t hist[NWT][kTotalsMax];
+    if (gate && gated_off(gate, 0)) return;
     const uint32_t tid = threadIdx.x, w = tid >> 6;
     uint32_t total = 0;
     for (uint32_t p = 0; p < pl.count; ++p) total += 1u << pl.width[p];
@@ -763,7 +767,7 @@ __global__ __launch_bounds__(BLOCK) void k_pass_totals(const uint32_t* __restric
         uint32_t off = 0, shift = shift0;
         for (uint32_t p = 0; p < pl.count; ++p) {
             const uint32_t wd = pl.width[p];
-            atomicAdd(&h[off + ((key >> shift) & ((1u << wd) - 1u))], 1u);
+            if ((only >> p) & 1u) atomicAdd(&h[off + ((key >> shift) & ((1u << wd) - 1u))], 1u);
             off += 1u << wd;
             shift += wd;
         }
@@ -895,14 +899,21 @@ __device__ __forceinline__ bool wave_inversion(const uint32_t (&k)[KPT], uint32_
 // with values, staged and scattered in two rounds of 16K positions).  Longer digit runs per tile
 // mean fewer 128-B lines shared by two tiles' runs; such a line reaches memory as two partial
 // writes, and those cost as much as a third more than whole lines (tools/line_probe.hip).
-template <int R, int BLOCK, int KPT, int L, int RANK, int LO = L, int SR = 1>
+// SEG (the hybrid MSD path's second pass, see k_msd_plan): the input is cut into segments (the
+// top-byte buckets of the first MSD pass); tiles never straddle a segment, a segment's last tile
+// may be partial, and every segment has its own digit bases (base16[(seg << 8) | d]) and its own
+// look-back chain (its first tile publishes an inclusive prefix at once).  segtab = [257] first
+// tile of every segment (+ the total), [256] segment starts, [256] segment ends; the tile count is
+// segtab[256] (ntiles is only its bound).
+template <int R, int BLOCK, int KPT, int L, int RANK, int LO = L, int SR = 1, int SEG = 0>
 __global__ __launch_bounds__(BLOCK, pass_min_waves(BLOCK, KPT)) void k_onesweep(
     const uint32_t* __restrict__ in_k, const uint32_t* __restrict__ in_v,
     uint32_t* __restrict__ out_k, uint32_t* __restrict__ out_v, uint32_t n, uint32_t shift,
     uint32_t mask, uint32_t ntiles, const uint32_t* __restrict__ dtot,
     unsigned long long* status, uint32_t* ticket, uint32_t* err, uint32_t* __restrict__ ntot,
     uint32_t nshift, uint32_t nmask, uint32_t epoch, const uint32_t* gate, int pass,
-    uint32_t* chk, uint32_t fmask, uint32_t spin_max, uint32_t* host_err) {
+    uint32_t* chk, uint32_t fmask, uint32_t spin_max, uint32_t* host_err,
+    const uint32_t* __restrict__ segtab = nullptr, const uint32_t* __restrict__ base16 = nullptr) {
     // ntot (may be null): whole-array totals of the NEXT pass's digit (key >> nshift) & nmask,
     // counted here from the keys this workgroup stages, so only pass 0 needs k_pass_totals.
     // chk (may be null, check_order, pass > 0): the order check of this pass's input, fused:
@@ -927,13 +938,18 @@ __global__ __launch_bounds__(BLOCK, pass_min_waves(BLOCK, KPT)) void k_onesweep(
     __shared__ uint32_t s_keys[HAS_VALUES ? 1 : STAGE];
     __shared__ uint2 s_kv[HAS_VALUES ? STAGE : 1];
     __shared__ uint32_t s_inv;
+    constexpr bool SG = SEG != 0;
+    static_assert(!SG || (SR == 1 && RADIX == 256), "segmented pass: one staging round, 8-bit digits");
+    __shared__ uint32_t s_seg[SG ? 769 : 1];
 
     if (gated_off(gate, chk ? pass - 1 : pass)) return;
     const uint32_t tid = threadIdx.x, w = tid >> 6;
     for (uint32_t d = tid; d < 256u; d += BLOCK) s_ntot[d] = 0u;
+    if (SG)
+        for (uint32_t i = tid; i < 769u; i += BLOCK) s_seg[i] = segtab[i];
     if (tid == 0) s_inv = 0u;
     {   // first output position of every digit
-        const uint32_t c = (tid < (uint32_t)RADIX && tid <= mask) ? dtot[tid] : 0u;
+        const uint32_t c = (!SG && tid < (uint32_t)RADIX && tid <= mask) ? dtot[tid] : 0u;
         uint32_t all;
         const uint32_t ex = block_excl_scan_n<NW>(c, s_scratch, all);
         if (tid < (uint32_t)RADIX) s_dbase[tid] = ex;
@@ -941,26 +957,56 @@ __global__ __launch_bounds__(BLOCK, pass_min_waves(BLOCK, KPT)) void k_onesweep(
         __syncthreads();
     }
     uint32_t T = s_next;
+    const uint32_t nt = SG ? s_seg[256] : ntiles;   // SEG: the tile count the plan kernel wrote
+    // first record and end of tile t (and, SEG, its segment and the segment's first tile)
+    auto geom = [&](uint32_t t, uint32_t& t0, uint32_t& tend, uint32_t& seg, uint32_t& first) {
+        if (SG) {
+            uint32_t lo = 0, hi = 256;                   // s_seg[lo] <= t < s_seg[hi]
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (s_seg[mid] <= t) lo = mid;
+                else hi = mid;
+            }
+            seg = lo;
+            first = s_seg[lo];
+            t0 = s_seg[257 + lo] + (t - first) * (uint32_t)TILE;
+            const uint32_t e = s_seg[513 + lo];
+            tend = e - t0 < (uint32_t)TILE ? e : t0 + (uint32_t)TILE;
+        } else {
+            seg = 0;
+            first = 0;
+            t0 = t * (uint32_t)TILE;
+            tend = (uint64_t)t0 + TILE <= n ? t0 + (uint32_t)TILE : n;
+        }
+    };
     uint32_t k[KPT];
     uint32_t v[HAS_VALUES ? KPT : 1];
     // SR > 1: no per-slot load branches (they spilled).  Records come from a plan-owned buffer
     // padded to whole tiles: whole-tile loads, and the slots past n are set to kPadKey once the
     // tile has arrived.  Arrays (the caller's) load with clamped indices.
-    auto load = [&](uint32_t t0) {
+    auto load_at = [&](uint32_t t0, uint32_t bound) {
         if (SR > 1 && L == LAYOUT_AOS)
-            load_tile<KPT, L>(in_k, in_v, (uint64_t)t0 + w * WAVE_KEYS, n, true, k, v);
+            load_tile<KPT, L>(in_k, in_v, (uint64_t)t0 + w * WAVE_KEYS, bound, true, k, v);
         else
-            load_tile<KPT, L, (SR > 1)>(in_k, in_v, (uint64_t)t0 + w * WAVE_KEYS, n, (uint64_t)t0 + TILE <= n, k, v);
+            load_tile<KPT, L, (SR > 1)>(in_k, in_v, (uint64_t)t0 + w * WAVE_KEYS, bound, (uint64_t)t0 + TILE <= bound, k, v);
     };
-    if (T < ntiles) load(T * (uint32_t)TILE);
-    while (T < ntiles) {
+    auto load = [&](uint32_t t) {
+        uint32_t t0, tend, sg, fi;
+        geom(t, t0, tend, sg, fi);
+        load_at(t0, SG ? tend : n);
+    };
+    if (T < nt) load(T);
+    while (T < nt) {
         RS_STAMP(pass, ntiles, T, 0, __builtin_amdgcn_s_memtime());
         RS_STAMP(pass, ntiles, T, 7, blockIdx.x);
         uint32_t early_ticket = 0;
         if (RS_EARLY_TICKET && tid == 0) early_ticket = atomicAdd(ticket, 1u);
-        const uint32_t tile0 = T * (uint32_t)TILE;
-        const bool full = (uint64_t)tile0 + TILE <= n;
-        const uint32_t nvalid = full ? (uint32_t)TILE : n - tile0;
+        uint32_t tile0, tend, seg, seg_first;
+        geom(T, tile0, tend, seg, seg_first);
+        const bool full = tend - tile0 == (uint32_t)TILE;
+        const uint32_t nvalid = tend - tile0;
+        const bool first_tile = T == seg_first;   // publishes an inclusive prefix at once
+        if (SG && tid < (uint32_t)RADIX) s_dbase[tid] = base16[(seg << 8) | tid];
         if (SR > 1 && L == LAYOUT_AOS && !full) {
             const uint64_t wb = (uint64_t)tile0 + w * WAVE_KEYS + lane_id();
 #pragma unroll
@@ -985,7 +1031,7 @@ __global__ __launch_bounds__(BLOCK, pass_min_waves(BLOCK, KPT)) void k_onesweep(
         // in flight while we wait.
         unsigned long long* st = status + (size_t)T * RADIX + tid;
         if (tid < (uint32_t)RADIX) {
-            if (T == 0) st_store(st, (epoch << 2) | kStInclusive, s_dbase[tid] + c);
+            if (first_tile) st_store(st, (epoch << 2) | kStInclusive, s_dbase[tid] + c);
             else st_store(st, (epoch << 2) | kStAggregate, c);
             set_wave_offsets<R, NW>(s_whist, tstart);
         }
@@ -1007,10 +1053,10 @@ __global__ __launch_bounds__(BLOCK, pass_min_waves(BLOCK, KPT)) void k_onesweep(
         const uint32_t Tn = s_next;
         RS_STAMP(pass, ntiles, T, 3, __builtin_amdgcn_s_memtime());
         // prefetch (RS_PREFETCH): hides under the look-back and this scatter
-        if (RS_PREFETCH == 0 && SR == 1 && Tn < ntiles) load(Tn * (uint32_t)TILE);
+        if (RS_PREFETCH == 0 && SR == 1 && Tn < nt) load(Tn);
         if (tid < (uint32_t)RADIX) {
             uint32_t excl = s_dbase[tid];
-            if (T != 0) {
+            if (!first_tile) {
                 // windowed look-back: kLookback predecessors loaded at once, consumed in order
                 // (aggregates summed) up to the first inclusive prefix; a not-yet-published
                 // word stops the window and is re-read next round
@@ -1068,16 +1114,16 @@ __global__ __launch_bounds__(BLOCK, pass_min_waves(BLOCK, KPT)) void k_onesweep(
             s_gdelta[tid] = ((((uint32_t)tid * ntiles + T) * 64u) & (n - 1u)) - tstart;
 #endif
         }
-        if (RS_PREFETCH == 1 && SR == 1 && Tn < ntiles) load(Tn * (uint32_t)TILE);
+        if (RS_PREFETCH == 1 && SR == 1 && Tn < nt) load(Tn);
         __syncthreads();
-        if (RS_PREFETCH == 2 && SR == 1 && Tn < ntiles) load(Tn * (uint32_t)TILE);
+        if (RS_PREFETCH == 2 && SR == 1 && Tn < nt) load(Tn);
         RS_STAMP(pass, ntiles, T, 4, __builtin_amdgcn_s_memtime());
 #pragma unroll
         for (int h = 0; h < SR; ++h) {
             if (h > 0) {   // the previous round's scatter has read the staging area
                 stage_round<KPT, HAS_VALUES, STAGE>(k, v, rank, s_keys, s_kv, h * (uint32_t)STAGE);
                 __syncthreads();
-                if (h == SR - 1 && Tn < ntiles) load(Tn * (uint32_t)TILE);   // registers free: prefetch
+                if (h == SR - 1 && Tn < nt) load(Tn);   // registers free: prefetch
             }
             const uint32_t lo = h * (uint32_t)STAGE;
             if (lo < nvalid)
@@ -1182,6 +1228,245 @@ __global__ __launch_bounds__(BLOCK) void k_sort_small(uint32_t* __restrict__ key
                 if (HAS_VALUES) values[p2] = v[j];
             }
         }
+    }
+}
+
+// ---- hybrid MSD path (uniformly spread keys; rsort.hip enqueue_sort_msd) --------------------
+// 1. k_pass_totals counts all four byte digits from one read of the input (mtot[256 p + d]);
+// 2. k_msd_decide picks the path on the device: MSD when no top-byte bucket holds more than
+//    max_top keys (else the four LSD passes run, gated the other way);
+// 3. MSD pass 0 (k_onesweep, top byte) writes the input partitioned by its top byte (R1, arrays);
+// 4. k_hist16 counts hist16[key >> 16] over R1 (every top-byte bucket is contiguous there);
+// 5. k_msd_plan scans hist16 into base16 (the first output position of every 16-bit bucket),
+//    lays out the segmented tiles of pass 2, and gates the bucket pass on max(hist16) <= the
+//    bucket capacity (else the LSD passes sort R1: still the stable sort of the input);
+// 6. MSD pass 1 (k_onesweep SEG, next byte within every top-byte segment) writes records R2 in
+//    16-bit bucket order;
+// 7. k_bucket_sort: one workgroup per 16-bit bucket sorts it by its low 16 bits in LDS and writes
+//    it as one contiguous run of the output.  Every step is stable, so the result is the stable
+//    sort of the input.  Gate words: g[0..15] MSD chosen, g[16..31] LSD on the input,
+//    g[32..47] bucket pass, g[48..63] LSD on R1 (each word repeated: gated_off reads 0..pass).
+constexpr uint32_t kGateMsd = 0, kGateLsd = 16, kGateBucket = 32, kGateLsdR1 = 48;
+
+__device__ __forceinline__ void set_gate(uint32_t* g, uint32_t v) {
+    if (threadIdx.x < 16u) g[threadIdx.x] = v;
+}
+
+__global__ __launch_bounds__(256) void k_msd_decide(const uint32_t* __restrict__ top_tot,
+                                                    uint32_t max_top, uint32_t* gates) {
+    __shared__ uint32_t s_bad;
+    if (threadIdx.x == 0) s_bad = 0u;
+    __syncthreads();
+    if (top_tot[threadIdx.x] > max_top) atomicOr(&s_bad, 1u);
+    __syncthreads();
+    const uint32_t msd = s_bad ? 0u : 1u;
+    set_gate(gates + kGateMsd, msd);
+    set_gate(gates + kGateLsd, 1u - msd);
+    if (!msd) {   // the plan kernel is gated off with the MSD path: close its gates here
+        set_gate(gates + kGateBucket, 0u);
+        set_gate(gates + kGateLsdR1, 0u);
+    }
+}
+
+// hist16[key >> 16] over keys[0..n) sorted by their top byte: each workgroup takes a contiguous
+// chunk, counts the (at most 4) top bytes that start it in LDS rows, any later ones with global
+// atomics (only in chunks crossing many small buckets), then adds its rows to hist16.
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void k_hist16(const uint32_t* __restrict__ keys, uint32_t n,
+                                                  uint32_t* __restrict__ hist16, const uint32_t* gate) {
+    __shared__ uint32_t h[4][256];
+    __shared__ uint32_t s_top0;
+    if (gated_off(gate, 0)) return;
+    const uint32_t chunk = ((n + gridDim.x - 1) / gridDim.x + 3u) & ~3u;
+    const uint64_t lo = (uint64_t)blockIdx.x * chunk;
+    if (lo >= n) return;
+    const uint32_t hi = lo + chunk < n ? (uint32_t)(lo + chunk) : n;
+    for (uint32_t i = threadIdx.x; i < 4u * 256u; i += BLOCK) (&h[0][0])[i] = 0u;
+    if (threadIdx.x == 0) s_top0 = keys[lo] >> 24;
+    __syncthreads();
+    const uint32_t top0 = s_top0;
+    auto count = [&](uint32_t key) {
+        const uint32_t r = (key >> 24) - top0;
+        if (r < 4u) atomicAdd(&h[r][(key >> 16) & 255u], 1u);
+        else atomicAdd(&hist16[key >> 16], 1u);
+    };
+    // lo is a multiple of 4: 16-byte loads for the whole vectors of the chunk, 4 in flight
+    const uint4* k4 = reinterpret_cast<const uint4*>(keys + lo);
+    const uint32_t nv = (uint32_t)((hi - lo) / 4u);
+    uint32_t i = threadIdx.x;
+    for (; i + 3u * BLOCK < nv; i += 4u * BLOCK) {
+        uint4 q[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) q[u] = k4[i + u * BLOCK];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) { count(q[u].x); count(q[u].y); count(q[u].z); count(q[u].w); }
+    }
+    for (; i < nv; i += BLOCK) {
+        const uint4 q = k4[i];
+        count(q.x); count(q.y); count(q.z); count(q.w);
+    }
+    for (uint64_t i = lo + 4ull * nv + threadIdx.x; i < hi; i += BLOCK) count(keys[i]);
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < 4u * 256u; i += BLOCK) {
+        const uint32_t r = i >> 8, c = (&h[0][0])[i];
+        if (c && top0 + r < 256u) atomicAdd(&hist16[((top0 + r) << 8) | (i & 255u)], c);
+    }
+}
+
+// One workgroup: base16 = exclusive scan of hist16 (65536 buckets in key order), the segmented
+// tile table of MSD pass 1 (segment = top byte: [257] first tile + total, [256] start, [256]
+// end), and the bucket / LSD-on-R1 gates (bucket pass iff every 16-bit bucket fits its tile).
+// Buckets larger than `small` (the population-sized bucket tile) are listed in over[1..]
+// (over[0] = their number; at most kOverMax, else the bucket pass is gated off too).
+constexpr uint32_t kOverMax = 4096;
+template <int TILE>
+__global__ __launch_bounds__(1024) void k_msd_plan(const uint32_t* __restrict__ hist16,
+                                                   const uint32_t* __restrict__ top_tot,
+                                                   uint32_t* __restrict__ base16,
+                                                   uint32_t* __restrict__ segtab, uint32_t cap,
+                                                   uint32_t small, uint32_t* __restrict__ over,
+                                                   uint32_t* gates) {
+    constexpr int NW = 16;
+    __shared__ uint32_t s_scratch[NW];
+    __shared__ uint32_t s_big, s_nover;
+    if (gated_off(gates + kGateMsd, 0)) return;
+    const uint32_t tid = threadIdx.x;
+    if (tid == 0) { s_big = 0u; s_nover = 0u; }
+    // 64 consecutive buckets per thread, held in registers (16 loads of 16 bytes in flight)
+    uint4 c4[16];
+    const uint4* h4 = reinterpret_cast<const uint4*>(hist16) + tid * 16u;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) c4[j] = h4[j];
+    uint32_t sum = 0, mx = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        sum += c4[j].x + c4[j].y + c4[j].z + c4[j].w;
+        mx = max(mx, max(max(c4[j].x, c4[j].y), max(c4[j].z, c4[j].w)));
+    }
+    uint32_t total;
+    uint32_t run = block_excl_scan_n<NW>(sum, s_scratch, total);
+    uint4* b4 = reinterpret_cast<uint4*>(base16) + tid * 16u;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        uint4 o;
+        o.x = run; run += c4[j].x;
+        o.y = run; run += c4[j].y;
+        o.z = run; run += c4[j].z;
+        o.w = run; run += c4[j].w;
+        b4[j] = o;
+    }
+    if (mx > small) {   // list the buckets the population-sized tile cannot take
+        for (uint32_t j = 0; j < 64u; ++j) {
+            const uint32_t c = hist16[tid * 64u + j];
+            if (c > small) {
+                const uint32_t slot = atomicAdd(&s_nover, 1u);
+                if (slot < kOverMax) over[1 + slot] = tid * 64u + j;
+            }
+        }
+    }
+    if (mx > cap) atomicOr(&s_big, 1u);
+    // segments: tiles of TILE records per top-byte bucket
+    const uint32_t cnt = tid < 256u ? top_tot[tid] : 0u;
+    const uint32_t tiles = (cnt + TILE - 1) / TILE;
+    uint32_t ttot;
+    const uint32_t tbase = block_excl_scan_n<NW>(tiles, s_scratch, ttot);
+    uint32_t stot;
+    const uint32_t sbase = block_excl_scan_n<NW>(cnt, s_scratch, stot);
+    if (tid < 256u) {
+        segtab[tid] = tbase;
+        segtab[257 + tid] = sbase;
+        segtab[513 + tid] = sbase + cnt;
+    }
+    if (tid == 0) segtab[256] = ttot;
+    __syncthreads();
+    if (tid == 0) over[0] = s_nover < kOverMax ? s_nover : kOverMax;
+    const uint32_t ok = (s_big || s_nover > kOverMax) ? 0u : 1u;
+    set_gate(gates + kGateBucket, ok);
+    set_gate(gates + kGateLsdR1, 1u - ok);
+}
+
+// One workgroup per 16-bit bucket (blockIdx.x = key >> 16): its records (R2, contiguous, at most
+// BLOCK * KPT) sorted stably by their low 16 bits in two 8-bit LDS passes, then written to the
+// output arrays as one contiguous run (whole 128-B lines but at the two ends).
+// Two launches share the buckets: a tile sized to the bucket population (about 1.15x the mean
+// bucket) takes every bucket of at most BLOCK * KPT records (min_cnt = 0), and a 16K-record tile
+// takes the rest (min_cnt = the first launch's tile); k_msd_plan gates this pass off when a
+// bucket exceeds the large tile.
+template <int BLOCK, int KPT, int RANK>
+__global__ __launch_bounds__(BLOCK) void k_bucket_sort(const uint32_t* __restrict__ rec,
+                                                       const uint32_t* __restrict__ hist16,
+                                                       const uint32_t* __restrict__ base16,
+                                                       uint32_t* __restrict__ out_k,
+                                                       uint32_t* __restrict__ out_v,
+                                                       const uint32_t* gate, uint32_t* err,
+                                                       uint32_t min_cnt,
+                                                       const uint32_t* __restrict__ over = nullptr) {
+    constexpr int R = 8, RADIX = 256;
+    constexpr int NW = BLOCK / 64;
+    constexpr int TILE = BLOCK * KPT;
+    constexpr int WAVE_KEYS = 64 * KPT;
+    __shared__ uint32_t s_whist[NW][RADIX];
+    __shared__ uint32_t s_scratch[NW];
+    __shared__ uint2 s_kv[TILE];
+    if (gated_off(gate, 0)) return;
+    // over (the large-tile launch): workgroup i takes listed buckets i, i + grid, ...
+    const uint32_t nb = over ? over[0] : 1u;
+    for (uint32_t it = over ? blockIdx.x : 0u; it < nb; it += gridDim.x) {
+    const uint32_t b = over ? over[1 + it] : blockIdx.x;
+    const uint32_t cnt = hist16[b];
+    if (cnt == 0u || cnt <= min_cnt) continue;   // empty, or the smaller tile's launch took it
+    if (cnt > (uint32_t)TILE) {
+        if (over && threadIdx.x == 0) atomicOr(err, 8u);   // the largest tile: never (gated)
+        continue;                                          // else: the large-tile launch's
+    }
+    const uint32_t base = base16[b];
+    const uint32_t tid = threadIdx.x, w = tid >> 6, lane = lane_id();
+    const uint32_t wbase = w * WAVE_KEYS;
+    uint32_t k[KPT], v[KPT];
+    load_tile<KPT, LAYOUT_AOS>(rec + 2ull * base, nullptr, wbase, cnt, false, k, v);
+    if (cnt > 1u) {
+        for (uint32_t p = 0, shift = 0; p < 2u; ++p, shift += 8u) {
+            const uint32_t mask = 255u;
+            for (uint32_t d = lane; d < (uint32_t)RADIX; d += 64) s_whist[w][d] = 0u;
+            Slots<KPT, false> rank;
+            rank_slots<R, KPT, RANK>(k, rank, s_whist[w], shift, mask);   // pads included
+            __syncthreads();
+            uint32_t c = 0, wc[NW];
+            if (tid < (uint32_t)RADIX) {
+#pragma unroll
+                for (int q = 0; q < NW; ++q) { wc[q] = s_whist[q][tid]; c += wc[q]; }
+            }
+            uint32_t ttot;
+            const uint32_t tstart = block_excl_scan_n<NW>(c, s_scratch, ttot);
+            if (tid < (uint32_t)RADIX) {
+                uint32_t o = tstart;
+#pragma unroll
+                for (int q = 0; q < NW; ++q) { s_whist[q][tid] = o; o += wc[q]; }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < KPT; ++j)
+                s_kv[s_whist[w][(k[j] >> shift) & mask] + rank.get(j)] = make_uint2(k[j], v[j]);
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) {
+                const uint2 kv = s_kv[wbase + j * 64 + lane];
+                k[j] = kv.x;
+                v[j] = kv.y;
+            }
+            __syncthreads();
+        }
+    }
+    // slot j of lane l of wave w holds sorted position w * WAVE_KEYS + j * 64 + l
+#pragma unroll
+    for (int j = 0; j < KPT; ++j) {
+        const uint32_t p2 = wbase + j * 64 + lane;
+        if (p2 < cnt) {
+            out_k[(size_t)base + p2] = k[j];
+            out_v[(size_t)base + p2] = v[j];
+        }
+    }
+    __syncthreads();   // the next listed bucket reuses s_whist / s_kv
     }
 }
 

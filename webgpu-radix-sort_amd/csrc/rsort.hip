@@ -93,6 +93,18 @@ constexpr TileCfg kKv512x24{512, 24, 12288, 1024};
 constexpr uint32_t kMinOnesweepTile = 8192;   // finest one-sweep tile (status words per plan)
 constexpr uint64_t kRecPad = 49152;           // records buffers: whole tiles of every config
 constexpr uint32_t kTinyMax = 1024 * 16;
+// Hybrid MSD path (enqueue_sort_msd): used for separate key/value arrays of >= kMsdMin keys when
+// no top-byte bucket exceeds kMsdMaxTop keys (decided on the device); 16-bit buckets of up to
+// kBucketCap records are sorted in LDS (k_bucket_sort<kBucketBlock, kBucketKpt>).
+#ifndef RS_MSD_DEFAULT
+#define RS_MSD_DEFAULT 1
+#endif
+constexpr uint64_t kMsdMin = 12ull << 20;
+constexpr uint32_t kMsdMaxTop = 3u << 19;
+constexpr int kBucketBlock = 1024, kBucketKpt = 16;    // the large bucket tile (overflow launch)
+constexpr uint32_t kBucketCap = kBucketBlock * kBucketKpt;
+constexpr uint64_t kMsdWords = 65536ull * 2 + 1024 + 64 + 1024 + 1 + rs::kOverMax;   // hist16, base16,
+                                                                    // segtab, gates, mtot, over
 constexpr uint32_t kHistGrid = 2048;
 constexpr int kCheckGrid = 2048;
 
@@ -112,8 +124,8 @@ struct KernelTimer {
     struct Rec { int kind; hipEvent_t a, b; };
     std::vector<Rec> pending;
     std::vector<hipEvent_t> pool;
-    double ms[RS_KERNEL_KINDS] = {0, 0, 0, 0};
-    uint64_t launches[RS_KERNEL_KINDS] = {0, 0, 0, 0};
+    double ms[RS_KERNEL_KINDS] = {};
+    uint64_t launches[RS_KERNEL_KINDS] = {};
 
     hipEvent_t get() {
         if (!pool.empty()) { hipEvent_t e = pool.back(); pool.pop_back(); return e; }
@@ -184,6 +196,9 @@ struct rs_plan {
     uint32_t* tickets = nullptr;   // = ptot + kTotalsMax: [16] per-pass tile tickets, [16] error
     uint32_t epoch = 0;            // tag of the last k_onesweep launch's status words
     uint32_t spin_max = 1u << 20;  // look-back wait bound in sleeps (RSORT_SPIN_MAX; tests force 0)
+    int msd_mode = RS_MSD_DEFAULT;   // hybrid MSD path for separate arrays (RSORT_MSD=0/1)
+    uint32_t* msd = nullptr;         // its workspace: hist16 | base16 | segtab | gates | mtot
+    int scatter_kind = RS_KERNEL_SCATTER;   // timer kind of the pass launches being enqueued
     uint32_t* host_err = nullptr;  // host-mapped error word: set by a timed-out look-back wait,
     uint32_t* host_err_dev = nullptr;   // read + cleared by rs_plan_check / the next rs_plan_sort
     hipEvent_t done = nullptr;     // recorded after every sort (rs_plan_check waits for it)
@@ -281,11 +296,12 @@ void launch_onesweep_t(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint3
     const uint32_t nshift = last ? 0u : shift + p->widths[pass];
     const uint32_t nmask = last ? 0u : (1u << p->widths[pass + 1]) - 1u;
     // check_order: passes > 0 check their own input (k_check runs before pass 0 only)
-    uint32_t* chk = (gate && pass > 0 && p->fused_check) ? p->flags : nullptr;
+    uint32_t* chk = (p->check_order && gate && pass > 0 && p->fused_check) ? p->flags : nullptr;
     hipLaunchKernelGGL(kern, dim3(grid), dim3(BLOCK), 0, s, ik, iv, ok, ov, n, shift, mask, ntiles,
                        p->ptot + p->ptot_off[pass], p->status, p->tickets + pass,
                        p->tickets + 16, ntot, nshift, nmask, p->epoch, gate, pass, chk,
-                       full_mask(p->bit_count), p->spin_max, p->host_err_dev);
+                       full_mask(p->bit_count), p->spin_max, p->host_err_dev,
+                       (const uint32_t*)nullptr, (const uint32_t*)nullptr);
 }
 
 template <int R, int BLOCK, int KPT, int L, int LO, int SR>
@@ -296,6 +312,35 @@ void launch_onesweep_l(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint3
         launch_onesweep_t<R, BLOCK, KPT, L, rs::RANK_BALLOT, LO, SR>(p, ik, iv, ok, ov, n, shift, mask, ntiles, gate, pass, s);
     else
         launch_onesweep_t<R, BLOCK, KPT, L, rs::RANK_LDS_ATOMIC, LO, SR>(p, ik, iv, ok, ov, n, shift, mask, ntiles, gate, pass, s);
+}
+
+// A new tag for the look-back status words of the next k_onesweep launch.
+rs_status next_epoch(rs_plan* p, hipStream_t s) {
+    if (++p->epoch >= (1u << 30)) {   // tag space exhausted: clear the words, restart tags
+        HIP_TRY(hipMemsetAsync(p->status, 0, 8ull * p->status_words, s));
+        p->epoch = 1;
+    }
+    return RS_OK;
+}
+
+// One pass of the hybrid MSD path (16K-record tiles, 8-bit digit at `shift`): SEG = 0 the
+// top-byte pass over the whole input, SEG = 1 the next-byte pass inside every top-byte segment.
+template <int L, int LO, int SEG>
+void launch_msd_pass(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint32_t* ok, uint32_t* ov,
+                     uint32_t n, uint32_t shift, uint32_t ntiles, const uint32_t* dtot, uint32_t* ticket,
+                     const uint32_t* gate, const uint32_t* segtab, const uint32_t* base16,
+                     hipStream_t s) {
+    auto go = [&](auto kern) {
+        static const uint32_t per_cu = resident_per_cu(kern, kLarge.block);
+        const uint32_t grid = std::min<uint32_t>(ntiles, p->cus * per_cu);
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(kLarge.block), 0, s, ik, iv, ok, ov, n, shift, 255u,
+                           ntiles, dtot, p->status, ticket, p->tickets + 16, nullptr, 0u, 0u, p->epoch,
+                           gate, 0, nullptr, 0xFFFFFFFFu, p->spin_max, p->host_err_dev, segtab, base16);
+    };
+    if (p->rank_mode == rs::RANK_BALLOT)
+        go(rs::k_onesweep<8, kLarge.block, kLarge.kpt, L, rs::RANK_BALLOT, LO, 1, SEG>);
+    else
+        go(rs::k_onesweep<8, kLarge.block, kLarge.kpt, L, rs::RANK_LDS_ATOMIC, LO, 1, SEG>);
 }
 
 // Layout pair of one pass: input layout | output layout << 4 (they differ only on the one-sweep
@@ -315,12 +360,9 @@ rs_status run_pass_cfg(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint3
     const uint32_t grid = std::min<uint32_t>(ntiles, max_grid);
     const int L = LL & 15;
     if (onesweep) {
-        if (++p->epoch >= (1u << 30)) {   // tag space exhausted: clear the words, restart tags
-            HIP_TRY(hipMemsetAsync(p->status, 0, 8ull * p->status_words, s));
-            p->epoch = 1;
-        }
+        if (rs_status st = next_epoch(p, s)) return st;
         constexpr int K = rs::LAYOUT_KEYS, S = rs::LAYOUT_SOA, A = rs::LAYOUT_AOS;
-        p->timer.run(RS_KERNEL_SCATTER, s, [&] {
+        p->timer.run(p->scatter_kind, s, [&] {
             if constexpr (KEYS_ONLY) {
                 launch_onesweep_l<R, BLOCK, KPT, K, K, SR>(p, ik, iv, ok, ov, n, shift, mask, ntiles, gate, pass, s);
             } else {
@@ -434,6 +476,13 @@ bool use_onesweep(const rs_plan* p, uint64_t n) {
     return p->layout != rs::LAYOUT_KEYS && !use_small_tiles(n);
 }
 
+// The hybrid MSD path applies (the device still falls back to the LSD passes for skewed keys).
+bool use_msd(const rs_plan* p, uint64_t n) {
+    return p->msd && p->msd_mode != 0 && p->layout == rs::LAYOUT_SOA && !p->check_order &&
+           p->bit_count == 32 && p->radix_bits == 8 && p->tmp2 && p->aos_tmp && use_onesweep(p, n) &&
+           !use_small_tiles(n) && n >= kMsdMin && p->kv_cfg == 0 && !p->huge_tiles;
+}
+
 // Lane-order self-test of the device's LDS atomics (k_lane_order_selftest), once per device
 // per process: 1 passed, 0 failed (plans then rank with RANK_BALLOT), -1 could not run.
 // RSORT_SELFTEST=fail simulates a failure (tests), RSORT_SELFTEST=0 skips it (counts as passed).
@@ -539,6 +588,7 @@ RS_EXPORT rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out) {
     if (const char* hg = getenv("RSORT_HUGE")) p->huge_tiles = atoi(hg);
     if (const char* kc = getenv("RSORT_KV_CFG")) p->kv_cfg = atoi(kc);
     if (const char* fc = getenv("RSORT_FUSED_CHECK")) p->fused_check = strcmp(fc, "0") != 0;
+    if (const char* ms = getenv("RSORT_MSD")) p->msd_mode = strcmp(ms, "0") != 0 ? 1 : 0;
     if (const char* sm = getenv("RSORT_SPIN_MAX")) p->spin_max = (uint32_t)strtoul(sm, nullptr, 10);
     // Even number of passes so the result lands in the caller's buffers, like the reference's
     // bit_count/2 passes with ping-pong on bit % 4 (AbstractRadixSortKernel.ts:93-107).
@@ -592,6 +642,10 @@ RS_EXPORT rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out) {
         (e = alloc((uint32_t**)&p->status, 8ull * p->status_words)) != hipSuccess)
         return cleanup(fail(e == hipErrorOutOfMemory ? RS_ERR_OUT_OF_MEMORY : RS_ERR_HIP,
                             "rs_plan_create: hipMalloc failed: %s", hipGetErrorString(e)));
+    if (p->msd_mode != 0 && p->layout == rs::LAYOUT_SOA && p->tmp2 && d.count >= kMsdMin &&
+        (e = alloc(&p->msd, 4ull * kMsdWords)) != hipSuccess)
+        return cleanup(fail(e == hipErrorOutOfMemory ? RS_ERR_OUT_OF_MEMORY : RS_ERR_HIP,
+                            "rs_plan_create: hipMalloc failed: %s", hipGetErrorString(e)));
     p->tickets = p->ptot + rs::kTotalsMax;   // [16] tickets, [16] error word
     if ((e = hipHostMalloc((void**)&p->host_err, 4, hipHostMallocMapped)) != hipSuccess ||
         (e = hipHostGetDevicePointer((void**)&p->host_err_dev, p->host_err, 0)) != hipSuccess ||
@@ -617,16 +671,152 @@ RS_EXPORT void rs_plan_destroy(rs_plan* p) {
     (void)hipFree(p->flags);
     (void)hipFree(p->ptot);
     (void)hipFree(p->status);
+    (void)hipFree(p->msd);
     if (p->host_err) (void)hipHostFree(p->host_err);
     if (p->done) (void)hipEventDestroy(p->done);
     delete p;
 }
 
 // Enqueue every launch of one sort (n > kTinyMax) on stream s.
+// The four LSD passes of a separate-arrays sort gated on `gate` (the hybrid MSD path's fallbacks):
+// src (arrays) -> records -> records -> records -> uk / uv, through the plan's two records
+// buffers; pass 0's totals must be in ptot, later passes count theirs.  When src is the plan's
+// own array pair (tmp_k / tmp_v: R1 of the MSD path), pass 0 writes tmp2 first.
+static rs_status enqueue_lsd_gated(rs_plan* p, const uint32_t* sk, const uint32_t* sv, uint32_t* uk,
+                                   uint32_t* uv, uint32_t n, const uint32_t* gate, hipStream_t s) {
+    constexpr int A = rs::LAYOUT_AOS, S = rs::LAYOUT_SOA;
+    uint32_t* ra = sk == p->tmp_k ? p->tmp2 : p->tmp_k;    // never overwrite the source early
+    uint32_t* rb = ra == p->tmp2 ? p->tmp_k : p->tmp2;
+    struct Step { const uint32_t* ik; const uint32_t* iv; uint32_t* ok; uint32_t* ov; int LL; };
+    const Step steps[4] = {{sk, sv, ra, nullptr, layout_pair(S, A)},
+                           {ra, nullptr, rb, nullptr, layout_pair(A, A)},
+                           {rb, nullptr, ra, nullptr, layout_pair(A, A)},
+                           {ra, nullptr, uk, uv, layout_pair(A, S)}};
+    p->scatter_kind = RS_KERNEL_FALLBACK;
+    uint32_t shift = 0;
+    rs_status st = RS_OK;
+    for (uint32_t i = 0; i < 4 && st == RS_OK; ++i, shift += 8)
+        st = run_pass(p, steps[i].ik, steps[i].iv, steps[i].ok, steps[i].ov, n, shift, 8, steps[i].LL,
+                      gate, (int)i, s, /*onesweep=*/true);
+    p->scatter_kind = RS_KERNEL_SCATTER;
+    return st;
+}
+
+// The hybrid MSD path (rs_kernels.hpp, "hybrid MSD path"): digit totals of all four bytes from
+// one read, the device's choice, top-byte pass -> 16-bit bucket histogram -> plan -> segmented
+// next-byte pass -> in-LDS bucket sort; the LSD passes enqueued behind, gated on the device
+// (on the input when the top byte is skewed, on R1 when a 16-bit bucket exceeds kBucketCap).
+static rs_status enqueue_sort_msd(rs_plan* p, uint32_t* uk, uint32_t* uv, uint64_t n, hipStream_t s,
+                                  const uint32_t* ik0, const uint32_t* iv0) {
+    constexpr int A = rs::LAYOUT_AOS, S = rs::LAYOUT_SOA;
+    const uint32_t n32 = (uint32_t)n;
+    const uint32_t* sk = ik0 ? ik0 : uk;
+    const uint32_t* sv = ik0 ? iv0 : uv;
+    uint32_t* hist16 = p->msd;
+    uint32_t* base16 = hist16 + 65536;
+    uint32_t* segtab = base16 + 65536;
+    uint32_t* gates = segtab + 1024;
+    uint32_t* mtot = gates + 64;
+    uint32_t* over = mtot + 1024;
+    const uint32_t* top_tot = mtot + 768;
+    const uint32_t ntiles = (uint32_t)((n + kLarge.tile - 1) / kLarge.tile);
+    HIP_TRY(hipMemsetAsync(p->ptot, 0, 4ull * (rs::kTotalsMax + 32), s));
+    HIP_TRY(hipMemsetAsync(hist16, 0, 4ull * 65536, s));
+    HIP_TRY(hipMemsetAsync(mtot, 0, 4ull * 1024, s));
+    rs::PassList pl{};
+    pl.count = 1;
+    pl.width[0] = 8;
+    const uint32_t tgrid = (uint32_t)std::min<uint64_t>((uint64_t)RS_TOT_PER_CU * p->cus,
+                                                        (n + 4ull * RS_TOT_BLOCK - 1) / (4ull * RS_TOT_BLOCK));
+    p->timer.run(RS_KERNEL_HISTOGRAM, s, [&] {
+        // the top byte only (the LSD fallbacks count byte 0 for themselves, gated)
+        hipLaunchKernelGGL(rs::k_pass_totals<1>, dim3(tgrid), dim3(RS_TOT_BLOCK), 0, s, sk, n32, pl, 24u,
+                           mtot + 768, (uint32_t*)nullptr, 0xFFFFFFFFu, 0x1u, (const uint32_t*)nullptr);
+    });
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(rs::k_msd_decide, dim3(1), dim3(256), 0, s, top_tot, kMsdMaxTop, gates);
+    HIP_TRY(hipGetLastError());
+    // MSD pass 0: input arrays -> R1 arrays (tmp_k / tmp_v), partitioned by the top byte
+    if (rs_status st = next_epoch(p, s)) return st;
+    p->timer.run(RS_KERNEL_SCATTER, s, [&] {
+        launch_msd_pass<S, S, 0>(p, sk, sv, p->tmp_k, p->tmp_v, n32, 24, ntiles, top_tot, p->tickets + 4,
+                                 gates + rs::kGateMsd, nullptr, nullptr, s);
+    });
+    HIP_TRY(hipGetLastError());
+    p->timer.run(RS_KERNEL_HISTOGRAM, s, [&] {
+        hipLaunchKernelGGL(rs::k_hist16<256>, dim3(8 * p->cus), dim3(256), 0, s, p->tmp_k, n32, hist16,
+                           gates + rs::kGateMsd);
+    });
+    HIP_TRY(hipGetLastError());
+    // 16-bit buckets: a tile sized to the mean bucket + 6 sigma of a uniform population takes
+    // every bucket that fits it, the large tile the listed rest
+    const double mean = (double)n / 65536.0;
+    static const double slack = [] { const char* e = getenv("RSORT_BUCKET_SLACK"); return e ? atof(e) : 1.0; }();
+    const uint32_t want = (uint32_t)(mean * slack + 6.0 * std::sqrt(mean) + 64.0);
+    uint32_t small_cap = 0;
+    for (uint32_t kpt : {4u, 8u, 12u, 18u, 24u})
+        if (!small_cap && want <= 256u * kpt) small_cap = 256u * kpt;
+    p->timer.run(RS_KERNEL_SCAN, s, [&] {
+        hipLaunchKernelGGL(rs::k_msd_plan<kLarge.tile>, dim3(1), dim3(1024), 0, s, hist16, top_tot, base16,
+                           segtab, kBucketCap, small_cap, over, gates);
+    });
+    HIP_TRY(hipGetLastError());
+    // MSD pass 1: R1 arrays -> R2 records (tmp2), by the next byte inside every top-byte segment
+    if (rs_status st = next_epoch(p, s)) return st;
+    p->timer.run(RS_KERNEL_SCATTER, s, [&] {
+        launch_msd_pass<S, A, 1>(p, p->tmp_k, p->tmp_v, p->tmp2, nullptr, n32, 16, ntiles + 257, nullptr,
+                                 p->tickets + 5, gates + rs::kGateBucket, segtab, base16, s);
+    });
+    HIP_TRY(hipGetLastError());
+    const uint32_t g_b = rs::kGateBucket;
+    const bool ballot = p->rank_mode == rs::RANK_BALLOT;
+    constexpr int A0 = rs::RANK_LDS_ATOMIC, B0 = rs::RANK_BALLOT;
+    p->timer.run(RS_KERNEL_BUCKET, s, [&] {
+        auto small = [&](auto kern) {
+            hipLaunchKernelGGL(kern, dim3(65536), dim3(256), 0, s, p->tmp2, hist16, base16, uk, uv,
+                               gates + g_b, p->tickets + 16, 0u, (const uint32_t*)nullptr);
+        };
+        switch (small_cap) {
+            case 256 * 4: ballot ? small(rs::k_bucket_sort<256, 4, B0>) : small(rs::k_bucket_sort<256, 4, A0>); break;
+            case 256 * 8: ballot ? small(rs::k_bucket_sort<256, 8, B0>) : small(rs::k_bucket_sort<256, 8, A0>); break;
+            case 256 * 12: ballot ? small(rs::k_bucket_sort<256, 12, B0>) : small(rs::k_bucket_sort<256, 12, A0>); break;
+            case 256 * 18: ballot ? small(rs::k_bucket_sort<256, 18, B0>) : small(rs::k_bucket_sort<256, 18, A0>); break;
+            case 256 * 24: ballot ? small(rs::k_bucket_sort<256, 24, B0>) : small(rs::k_bucket_sort<256, 24, A0>); break;
+            default: break;   // every bucket goes to the listed large-tile launch
+        }
+        // the listed buckets (none for uniform keys): a small persistent grid over the list
+        auto large = [&](auto kern) {
+            hipLaunchKernelGGL(kern, dim3(256), dim3(kBucketBlock), 0, s, p->tmp2, hist16, base16, uk, uv,
+                               gates + g_b, p->tickets + 16, small_cap, (const uint32_t*)over);
+        };
+        ballot ? large(rs::k_bucket_sort<kBucketBlock, kBucketKpt, B0>)
+               : large(rs::k_bucket_sort<kBucketBlock, kBucketKpt, A0>);
+    });
+    HIP_TRY(hipGetLastError());
+    // fallbacks (gated off on the device unless taken), each counting its pass 0 totals first
+    // (the byte-0 digit totals of the input; R1 is a permutation of it)
+    rs::PassList p0{};
+    p0.count = 1;
+    p0.width[0] = 8;
+    for (int f = 0; f < 2; ++f) {
+        const uint32_t* fk = f == 0 ? sk : p->tmp_k;
+        const uint32_t* fv = f == 0 ? sv : p->tmp_v;
+        const uint32_t* fg = gates + (f == 0 ? rs::kGateLsd : rs::kGateLsdR1);
+        p->timer.run(RS_KERNEL_FALLBACK, s, [&] {
+            hipLaunchKernelGGL(rs::k_pass_totals<1>, dim3(tgrid), dim3(RS_TOT_BLOCK), 0, s, fk, n32, p0, 0u,
+                               p->ptot + p->ptot_off[0], (uint32_t*)nullptr, 0xFFFFFFFFu, 0x1u, fg);
+        });
+        HIP_TRY(hipGetLastError());
+        if (rs_status st = enqueue_lsd_gated(p, fk, fv, uk, uv, n32, fg, s)) return st;
+    }
+    return RS_OK;
+}
+
 // in_k0 / in_v0 (optional): pass 0 reads them instead of uk / uv (out-of-place sort; the
 // caller's input is only read, the result lands in uk / uv; check_order not supported).
 static rs_status enqueue_sort(rs_plan* p, uint32_t* uk, uint32_t* uv, uint64_t n, hipStream_t s,
                               const uint32_t* in_k0 = nullptr, const uint32_t* in_v0 = nullptr) {
+    if (use_msd(p, n)) return enqueue_sort_msd(p, uk, uv, n, s, in_k0, in_v0);
     const int L = p->layout;
     const uint32_t n32 = (uint32_t)n;
     const uint32_t* gate = p->check_order ? p->flags : nullptr;

@@ -29,9 +29,10 @@ RS_FLAG_LOCAL_SHUFFLE = 0x4
 RS_FLAG_AVOID_BANK_CONFLICTS = 0x8
 RS_FLAG_INTERLEAVED = 0x10
 
-RS_KERNEL_HISTOGRAM, RS_KERNEL_SCAN, RS_KERNEL_SCATTER, RS_KERNEL_CHECK = range(4)
-RS_KERNEL_KINDS = 4
-KERNEL_NAMES = ("histogram", "scan", "scatter", "check")
+(RS_KERNEL_HISTOGRAM, RS_KERNEL_SCAN, RS_KERNEL_SCATTER, RS_KERNEL_CHECK, RS_KERNEL_BUCKET,
+ RS_KERNEL_FALLBACK) = range(6)
+RS_KERNEL_KINDS = 6
+KERNEL_NAMES = ("histogram", "scan", "scatter", "check", "bucket", "fallback")
 
 
 class RadixSortError(RuntimeError):

@@ -1,5 +1,6 @@
 """GPU: the hybrid MSD path (rsort.hip enqueue_sort_msd; rs_kernels.hpp "hybrid MSD path") —
-separate key / value arrays of >= 12M keys: top-byte pass, 16-bit bucket histogram, segmented
+separate key / value arrays and interleaved records (RadixSortTextureKernel, sorted in place) of
+>= 12M keys: top-byte pass, 16-bit bucket histogram, segmented
 next-byte pass, in-LDS bucket sort — and both of its device-side fallbacks to the LSD passes
 (top byte too skewed: LSD on the input; a 16-bit bucket over the large tile: LSD on R1).
 Parity is the same contract as every other path: the stable sort of the input, bit-exact
@@ -105,3 +106,37 @@ def test_msd_repeated_sorts_on_one_plan():
         kern.check()
         assert ops.is_sorted(k) and torch.equal(kin[v.long()], k)
     kern.destroy()
+
+
+def _sort_tex_and_check(n, kind, seed=7):
+    """The texture layout (records in place: R2 is the caller's buffer)."""
+    from radix_sort_amd import RadixSortTextureKernel
+    k = _keys(n, kind, seed)
+    rec = torch.empty((n, 2), dtype=torch.int32, device=DEV)
+    rec[:, 0] = k
+    rec[:, 1] = torch.arange(n, dtype=torch.int32, device=DEV)
+    kern = RadixSortTextureKernel(texture=rec, count=n)
+    kern.set_profiling(True)
+    kern.dispatch()
+    torch.cuda.synchronize()
+    kern.check()
+    times = kern.kernel_times()
+    ek, ev = O.stable_sort_masked_c(k.cpu().numpy().view(np.uint32), np.arange(n, dtype=np.uint32), 32)
+    got = rec.cpu().numpy().view(np.uint32)
+    assert np.array_equal(got[:, 0], ek)
+    assert np.array_equal(got[:, 1], ev)
+    kern.destroy()
+    return times
+
+
+@pytest.mark.parametrize("n", [(12 << 20) + 1, (1 << 24) + 7])
+def test_msd_records_uniform_matches_oracle(n):
+    t = _sort_tex_and_check(n, "uniform")
+    assert t["bucket"]["ms"] > 0.05 and t["fallback"]["ms"] < t["bucket"]["ms"]
+
+
+@pytest.mark.parametrize("kind", ["top0", "low0", "few_big", "dups"])
+def test_msd_records_fallbacks_and_overflow(kind):
+    t = _sort_tex_and_check((1 << 24) + 1, kind)
+    if kind in ("top0", "low0"):
+        assert t["fallback"]["ms"] > 5 * t["bucket"]["ms"]

@@ -1392,11 +1392,14 @@ __global__ __launch_bounds__(1024) void k_msd_plan(const uint32_t* __restrict__ 
 // bucket) takes every bucket of at most BLOCK * KPT records (min_cnt = 0), and a 16K-record tile
 // takes the rest (min_cnt = the first launch's tile); k_msd_plan gates this pass off when a
 // bucket exceeds the large tile.
-template <int BLOCK, int KPT, int RANK>
-__global__ __launch_bounds__(BLOCK) void k_bucket_sort(const uint32_t* __restrict__ rec,
+// LO: output layout (LAYOUT_SOA: the caller's two arrays; LAYOUT_AOS: records - the texture
+// layout, sorted in place: R2 is then the caller's buffer itself, and every workgroup has read its
+// whole bucket before it writes the same range).
+template <int BLOCK, int KPT, int RANK, int LO = LAYOUT_SOA>
+__global__ __launch_bounds__(BLOCK) void k_bucket_sort(const uint32_t* rec,
                                                        const uint32_t* __restrict__ hist16,
                                                        const uint32_t* __restrict__ base16,
-                                                       uint32_t* __restrict__ out_k,
+                                                       uint32_t* out_k,
                                                        uint32_t* __restrict__ out_v,
                                                        const uint32_t* gate, uint32_t* err,
                                                        uint32_t min_cnt,
@@ -1462,12 +1465,30 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_sort(const uint32_t* __restric
     for (int j = 0; j < KPT; ++j) {
         const uint32_t p2 = wbase + j * 64 + lane;
         if (p2 < cnt) {
-            out_k[(size_t)base + p2] = k[j];
-            out_v[(size_t)base + p2] = v[j];
+            if (LO == LAYOUT_AOS) {
+                reinterpret_cast<uint2*>(out_k)[(size_t)base + p2] = make_uint2(k[j], v[j]);
+            } else {
+                out_k[(size_t)base + p2] = k[j];
+                out_v[(size_t)base + p2] = v[j];
+            }
         }
     }
     __syncthreads();   // the next listed bucket reuses s_whist / s_kv
     }
+}
+
+// dst[0..n) = src[0..n) (8-byte records, 16 bytes per load) when the gate is open (the texture
+// layout's LSD-on-R1 fallback, whose fourth pass ends in the plan's buffer).
+__global__ __launch_bounds__(kBlock) void k_copy_gated(const uint2* __restrict__ src,
+                                                       uint2* __restrict__ dst, uint64_t n,
+                                                       const uint32_t* gate) {
+    if (gated_off(gate, 0)) return;
+    const uint64_t n16 = n >> 1;
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    const uint64_t i0 = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    for (uint64_t i = i0; i < n16; i += stride)
+        reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(src)[i];
+    if ((n & 1) && i0 == 0) dst[n - 1] = src[n - 1];
 }
 
 // ---- order check -------------------------------------------------------------------------

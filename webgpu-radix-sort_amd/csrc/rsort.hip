@@ -16,6 +16,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <type_traits>
 #include <map>
 #include <mutex>
 #include <new>
@@ -93,7 +94,7 @@ constexpr TileCfg kKv512x24{512, 24, 12288, 1024};
 constexpr uint32_t kMinOnesweepTile = 8192;   // finest one-sweep tile (status words per plan)
 constexpr uint64_t kRecPad = 49152;           // records buffers: whole tiles of every config
 constexpr uint32_t kTinyMax = 1024 * 16;
-// Hybrid MSD path (enqueue_sort_msd): used for separate key/value arrays of >= kMsdMin keys when
+// Hybrid MSD path (enqueue_sort_msd): used for key/value arrays and records of >= kMsdMin keys when
 // no top-byte bucket exceeds kMsdMaxTop keys (decided on the device); 16-bit buckets of up to
 // kBucketCap records are sorted in LDS (k_bucket_sort<kBucketBlock, kBucketKpt>).
 #ifndef RS_MSD_DEFAULT
@@ -196,7 +197,7 @@ struct rs_plan {
     uint32_t* tickets = nullptr;   // = ptot + kTotalsMax: [16] per-pass tile tickets, [16] error
     uint32_t epoch = 0;            // tag of the last k_onesweep launch's status words
     uint32_t spin_max = 1u << 20;  // look-back wait bound in sleeps (RSORT_SPIN_MAX; tests force 0)
-    int msd_mode = RS_MSD_DEFAULT;   // hybrid MSD path for separate arrays (RSORT_MSD=0/1)
+    int msd_mode = RS_MSD_DEFAULT;   // hybrid MSD path for values (RSORT_MSD=0/1)
     uint32_t* msd = nullptr;         // its workspace: hist16 | base16 | segtab | gates | mtot
     int scatter_kind = RS_KERNEL_SCATTER;   // timer kind of the pass launches being enqueued
     uint32_t* host_err = nullptr;  // host-mapped error word: set by a timed-out look-back wait,
@@ -478,9 +479,10 @@ bool use_onesweep(const rs_plan* p, uint64_t n) {
 
 // The hybrid MSD path applies (the device still falls back to the LSD passes for skewed keys).
 bool use_msd(const rs_plan* p, uint64_t n) {
-    return p->msd && p->msd_mode != 0 && p->layout == rs::LAYOUT_SOA && !p->check_order &&
-           p->bit_count == 32 && p->radix_bits == 8 && p->tmp2 && p->aos_tmp && use_onesweep(p, n) &&
-           !use_small_tiles(n) && n >= kMsdMin && p->kv_cfg == 0 && !p->huge_tiles;
+    const bool bufs = p->layout == rs::LAYOUT_AOS || (p->layout == rs::LAYOUT_SOA && p->tmp2 && p->aos_tmp);
+    return p->msd && p->msd_mode != 0 && bufs && !p->check_order && p->bit_count == 32 &&
+           p->radix_bits == 8 && use_onesweep(p, n) && !use_small_tiles(n) && n >= kMsdMin &&
+           p->kv_cfg == 0 && !p->huge_tiles;
 }
 
 // Lane-order self-test of the device's LDS atomics (k_lane_order_selftest), once per device
@@ -642,7 +644,8 @@ RS_EXPORT rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out) {
         (e = alloc((uint32_t**)&p->status, 8ull * p->status_words)) != hipSuccess)
         return cleanup(fail(e == hipErrorOutOfMemory ? RS_ERR_OUT_OF_MEMORY : RS_ERR_HIP,
                             "rs_plan_create: hipMalloc failed: %s", hipGetErrorString(e)));
-    if (p->msd_mode != 0 && p->layout == rs::LAYOUT_SOA && p->tmp2 && d.count >= kMsdMin &&
+    if (p->msd_mode != 0 && (p->layout == rs::LAYOUT_AOS || (p->layout == rs::LAYOUT_SOA && p->tmp2)) &&
+        d.count >= kMsdMin &&
         (e = alloc(&p->msd, 4ull * kMsdWords)) != hipSuccess)
         return cleanup(fail(e == hipErrorOutOfMemory ? RS_ERR_OUT_OF_MEMORY : RS_ERR_HIP,
                             "rs_plan_create: hipMalloc failed: %s", hipGetErrorString(e)));
@@ -702,16 +705,22 @@ static rs_status enqueue_lsd_gated(rs_plan* p, const uint32_t* sk, const uint32_
     return st;
 }
 
-// The hybrid MSD path (rs_kernels.hpp, "hybrid MSD path"): digit totals of all four bytes from
-// one read, the device's choice, top-byte pass -> 16-bit bucket histogram -> plan -> segmented
-// next-byte pass -> in-LDS bucket sort; the LSD passes enqueued behind, gated on the device
-// (on the input when the top byte is skewed, on R1 when a 16-bit bucket exceeds kBucketCap).
+// The hybrid MSD path (rs_kernels.hpp, "hybrid MSD path"): top-byte totals, the device's choice,
+// top-byte pass -> 16-bit bucket histogram -> plan -> segmented next-byte pass -> in-LDS bucket
+// sort; the LSD passes enqueued behind, gated on the device (on the input when the top byte is
+// skewed, on R1 when a 16-bit bucket exceeds kBucketCap).  Separate arrays: R1 = tmp_k / tmp_v,
+// R2 = tmp2, the result in uk / uv.  Records (the texture layout, sorted in place): R1 = the
+// two halves of tmp_k, R2 = the caller's buffer itself (consumed by pass 0).
 static rs_status enqueue_sort_msd(rs_plan* p, uint32_t* uk, uint32_t* uv, uint64_t n, hipStream_t s,
                                   const uint32_t* ik0, const uint32_t* iv0) {
     constexpr int A = rs::LAYOUT_AOS, S = rs::LAYOUT_SOA;
+    const bool aos = p->layout == A;
     const uint32_t n32 = (uint32_t)n;
     const uint32_t* sk = ik0 ? ik0 : uk;
-    const uint32_t* sv = ik0 ? iv0 : uv;
+    const uint32_t* sv = aos ? nullptr : (ik0 ? iv0 : uv);
+    uint32_t* r1k = p->tmp_k;
+    uint32_t* r1v = p->tmp_k + p->capacity;      // = tmp_v of a separate-arrays plan
+    uint32_t* r2 = aos ? uk : p->tmp2;
     uint32_t* hist16 = p->msd;
     uint32_t* base16 = hist16 + 65536;
     uint32_t* segtab = base16 + 65536;
@@ -728,23 +737,32 @@ static rs_status enqueue_sort_msd(rs_plan* p, uint32_t* uk, uint32_t* uv, uint64
     pl.width[0] = 8;
     const uint32_t tgrid = (uint32_t)std::min<uint64_t>((uint64_t)RS_TOT_PER_CU * p->cus,
                                                         (n + 4ull * RS_TOT_BLOCK - 1) / (4ull * RS_TOT_BLOCK));
-    p->timer.run(RS_KERNEL_HISTOGRAM, s, [&] {
-        // the top byte only (the LSD fallbacks count byte 0 for themselves, gated)
-        hipLaunchKernelGGL(rs::k_pass_totals<1>, dim3(tgrid), dim3(RS_TOT_BLOCK), 0, s, sk, n32, pl, 24u,
-                           mtot + 768, (uint32_t*)nullptr, 0xFFFFFFFFu, 0x1u, (const uint32_t*)nullptr);
-    });
+    auto totals = [&](const uint32_t* keys, bool records, uint32_t shift, uint32_t* out, const uint32_t* gate) {
+        if (records)
+            hipLaunchKernelGGL(rs::k_pass_totals<2>, dim3(tgrid), dim3(RS_TOT_BLOCK), 0, s, keys, n32, pl, shift,
+                               out, (uint32_t*)nullptr, 0xFFFFFFFFu, 0x1u, gate);
+        else
+            hipLaunchKernelGGL(rs::k_pass_totals<1>, dim3(tgrid), dim3(RS_TOT_BLOCK), 0, s, keys, n32, pl, shift,
+                               out, (uint32_t*)nullptr, 0xFFFFFFFFu, 0x1u, gate);
+    };
+    // the top byte only (the LSD fallbacks count byte 0 for themselves, gated)
+    p->timer.run(RS_KERNEL_HISTOGRAM, s, [&] { totals(sk, aos, 24u, mtot + 768, nullptr); });
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(rs::k_msd_decide, dim3(1), dim3(256), 0, s, top_tot, kMsdMaxTop, gates);
     HIP_TRY(hipGetLastError());
-    // MSD pass 0: input arrays -> R1 arrays (tmp_k / tmp_v), partitioned by the top byte
+    // MSD pass 0: input -> R1 arrays, partitioned by the top byte
     if (rs_status st = next_epoch(p, s)) return st;
     p->timer.run(RS_KERNEL_SCATTER, s, [&] {
-        launch_msd_pass<S, S, 0>(p, sk, sv, p->tmp_k, p->tmp_v, n32, 24, ntiles, top_tot, p->tickets + 4,
-                                 gates + rs::kGateMsd, nullptr, nullptr, s);
+        if (aos)
+            launch_msd_pass<A, S, 0>(p, sk, nullptr, r1k, r1v, n32, 24, ntiles, top_tot, p->tickets + 4,
+                                     gates + rs::kGateMsd, nullptr, nullptr, s);
+        else
+            launch_msd_pass<S, S, 0>(p, sk, sv, r1k, r1v, n32, 24, ntiles, top_tot, p->tickets + 4,
+                                     gates + rs::kGateMsd, nullptr, nullptr, s);
     });
     HIP_TRY(hipGetLastError());
     p->timer.run(RS_KERNEL_HISTOGRAM, s, [&] {
-        hipLaunchKernelGGL(rs::k_hist16<256>, dim3(8 * p->cus), dim3(256), 0, s, p->tmp_k, n32, hist16,
+        hipLaunchKernelGGL(rs::k_hist16<256>, dim3(8 * p->cus), dim3(256), 0, s, r1k, n32, hist16,
                            gates + rs::kGateMsd);
     });
     HIP_TRY(hipGetLastError());
@@ -761,10 +779,10 @@ static rs_status enqueue_sort_msd(rs_plan* p, uint32_t* uk, uint32_t* uv, uint64
                            segtab, kBucketCap, small_cap, over, gates);
     });
     HIP_TRY(hipGetLastError());
-    // MSD pass 1: R1 arrays -> R2 records (tmp2), by the next byte inside every top-byte segment
+    // MSD pass 1: R1 arrays -> R2 records, by the next byte inside every top-byte segment
     if (rs_status st = next_epoch(p, s)) return st;
     p->timer.run(RS_KERNEL_SCATTER, s, [&] {
-        launch_msd_pass<S, A, 1>(p, p->tmp_k, p->tmp_v, p->tmp2, nullptr, n32, 16, ntiles + 257, nullptr,
+        launch_msd_pass<S, A, 1>(p, r1k, r1v, r2, nullptr, n32, 16, ntiles + 257, nullptr,
                                  p->tickets + 5, gates + rs::kGateBucket, segtab, base16, s);
     });
     HIP_TRY(hipGetLastError());
@@ -773,42 +791,67 @@ static rs_status enqueue_sort_msd(rs_plan* p, uint32_t* uk, uint32_t* uv, uint64
     constexpr int A0 = rs::RANK_LDS_ATOMIC, B0 = rs::RANK_BALLOT;
     p->timer.run(RS_KERNEL_BUCKET, s, [&] {
         auto small = [&](auto kern) {
-            hipLaunchKernelGGL(kern, dim3(65536), dim3(256), 0, s, p->tmp2, hist16, base16, uk, uv,
+            hipLaunchKernelGGL(kern, dim3(65536), dim3(256), 0, s, r2, hist16, base16, uk, uv,
                                gates + g_b, p->tickets + 16, 0u, (const uint32_t*)nullptr);
         };
-        switch (small_cap) {
-            case 256 * 4: ballot ? small(rs::k_bucket_sort<256, 4, B0>) : small(rs::k_bucket_sort<256, 4, A0>); break;
-            case 256 * 8: ballot ? small(rs::k_bucket_sort<256, 8, B0>) : small(rs::k_bucket_sort<256, 8, A0>); break;
-            case 256 * 12: ballot ? small(rs::k_bucket_sort<256, 12, B0>) : small(rs::k_bucket_sort<256, 12, A0>); break;
-            case 256 * 18: ballot ? small(rs::k_bucket_sort<256, 18, B0>) : small(rs::k_bucket_sort<256, 18, A0>); break;
-            case 256 * 24: ballot ? small(rs::k_bucket_sort<256, 24, B0>) : small(rs::k_bucket_sort<256, 24, A0>); break;
-            default: break;   // every bucket goes to the listed large-tile launch
-        }
-        // the listed buckets (none for uniform keys): a small persistent grid over the list
         auto large = [&](auto kern) {
-            hipLaunchKernelGGL(kern, dim3(256), dim3(kBucketBlock), 0, s, p->tmp2, hist16, base16, uk, uv,
+            hipLaunchKernelGGL(kern, dim3(256), dim3(kBucketBlock), 0, s, r2, hist16, base16, uk, uv,
                                gates + g_b, p->tickets + 16, small_cap, (const uint32_t*)over);
         };
-        ballot ? large(rs::k_bucket_sort<kBucketBlock, kBucketKpt, B0>)
-               : large(rs::k_bucket_sort<kBucketBlock, kBucketKpt, A0>);
+        auto both = [&](auto lo) {
+            constexpr int LO = decltype(lo)::value;
+            switch (small_cap) {
+                case 256 * 4: ballot ? small(rs::k_bucket_sort<256, 4, B0, LO>) : small(rs::k_bucket_sort<256, 4, A0, LO>); break;
+                case 256 * 8: ballot ? small(rs::k_bucket_sort<256, 8, B0, LO>) : small(rs::k_bucket_sort<256, 8, A0, LO>); break;
+                case 256 * 12: ballot ? small(rs::k_bucket_sort<256, 12, B0, LO>) : small(rs::k_bucket_sort<256, 12, A0, LO>); break;
+                case 256 * 18: ballot ? small(rs::k_bucket_sort<256, 18, B0, LO>) : small(rs::k_bucket_sort<256, 18, A0, LO>); break;
+                case 256 * 24: ballot ? small(rs::k_bucket_sort<256, 24, B0, LO>) : small(rs::k_bucket_sort<256, 24, A0, LO>); break;
+                default: break;   // every bucket goes to the listed large-tile launch
+            }
+            // the listed buckets (none for uniform keys): a small persistent grid over the list
+            ballot ? large(rs::k_bucket_sort<kBucketBlock, kBucketKpt, B0, LO>)
+                   : large(rs::k_bucket_sort<kBucketBlock, kBucketKpt, A0, LO>);
+        };
+        if (aos) both(std::integral_constant<int, A>{});
+        else both(std::integral_constant<int, S>{});
     });
     HIP_TRY(hipGetLastError());
     // fallbacks (gated off on the device unless taken), each counting its pass 0 totals first
     // (the byte-0 digit totals of the input; R1 is a permutation of it)
-    rs::PassList p0{};
-    p0.count = 1;
-    p0.width[0] = 8;
-    for (int f = 0; f < 2; ++f) {
-        const uint32_t* fk = f == 0 ? sk : p->tmp_k;
-        const uint32_t* fv = f == 0 ? sv : p->tmp_v;
-        const uint32_t* fg = gates + (f == 0 ? rs::kGateLsd : rs::kGateLsdR1);
-        p->timer.run(RS_KERNEL_FALLBACK, s, [&] {
-            hipLaunchKernelGGL(rs::k_pass_totals<1>, dim3(tgrid), dim3(RS_TOT_BLOCK), 0, s, fk, n32, p0, 0u,
-                               p->ptot + p->ptot_off[0], (uint32_t*)nullptr, 0xFFFFFFFFu, 0x1u, fg);
-        });
+    const uint32_t* g_lsd = gates + rs::kGateLsd;
+    const uint32_t* g_r1 = gates + rs::kGateLsdR1;
+    uint32_t* t0 = p->ptot + p->ptot_off[0];
+    if (!aos) {
+        p->timer.run(RS_KERNEL_FALLBACK, s, [&] { totals(sk, false, 0u, t0, g_lsd); });
         HIP_TRY(hipGetLastError());
-        if (rs_status st = enqueue_lsd_gated(p, fk, fv, uk, uv, n32, fg, s)) return st;
+        if (rs_status st = enqueue_lsd_gated(p, sk, sv, uk, uv, n32, g_lsd, s)) return st;
+        p->timer.run(RS_KERNEL_FALLBACK, s, [&] { totals(r1k, false, 0u, t0, g_r1); });
+        HIP_TRY(hipGetLastError());
+        return enqueue_lsd_gated(p, r1k, r1v, uk, uv, n32, g_r1, s);
     }
+    // records: on the input, uk -> tmp_k -> uk -> tmp_k -> uk; on R1 (the arrays in tmp_k),
+    // R1 -> uk -> tmp_k -> uk -> tmp_k, then tmp_k copied back to uk
+    p->scatter_kind = RS_KERNEL_FALLBACK;
+    rs_status st = RS_OK;
+    p->timer.run(RS_KERNEL_FALLBACK, s, [&] { totals(uk, true, 0u, t0, g_lsd); });
+    for (uint32_t i = 0; i < 4 && st == RS_OK; ++i)
+        st = run_pass(p, (i & 1) ? p->tmp_k : uk, nullptr, (i & 1) ? uk : p->tmp_k, nullptr, n32, 8 * i, 8,
+                      layout_pair(A, A), g_lsd, (int)i, s, /*onesweep=*/true);
+    if (st == RS_OK) p->timer.run(RS_KERNEL_FALLBACK, s, [&] { totals(r1k, false, 0u, t0, g_r1); });
+    for (uint32_t i = 0; i < 4 && st == RS_OK; ++i) {
+        const uint32_t* ik = i == 0 ? r1k : ((i & 1) ? uk : p->tmp_k);
+        uint32_t* ok = (i & 1) ? p->tmp_k : uk;
+        st = run_pass(p, ik, i == 0 ? r1v : nullptr, ok, nullptr, n32, 8 * i, 8,
+                      i == 0 ? layout_pair(S, A) : layout_pair(A, A), g_r1, (int)i, s, /*onesweep=*/true);
+    }
+    p->scatter_kind = RS_KERNEL_SCATTER;
+    if (st != RS_OK) return st;
+    const uint32_t cgrid = (uint32_t)std::min<uint64_t>(8ull * p->cus, (n / 2 + rs::kBlock - 1) / rs::kBlock + 1);
+    p->timer.run(RS_KERNEL_FALLBACK, s, [&] {
+        hipLaunchKernelGGL(rs::k_copy_gated, dim3(cgrid), dim3(rs::kBlock), 0, s, (const uint2*)p->tmp_k,
+                           (uint2*)uk, n, g_r1);
+    });
+    HIP_TRY(hipGetLastError());
     return RS_OK;
 }
 

@@ -1232,90 +1232,126 @@ __global__ __launch_bounds__(BLOCK) void k_sort_small(uint32_t* __restrict__ key
 }
 
 // ---- hybrid MSD path (uniformly spread keys; rsort.hip enqueue_sort_msd) --------------------
-// 1. k_pass_totals counts all four byte digits from one read of the input (mtot[256 p + d]);
-// 2. k_msd_decide picks the path on the device: MSD when no top-byte bucket holds more than
-//    max_top keys (else the four LSD passes run, gated the other way);
-// 3. MSD pass 0 (k_onesweep, top byte) writes the input partitioned by its top byte (R1, arrays);
-// 4. k_hist16 counts hist16[key >> 16] over R1 (every top-byte bucket is contiguous there);
-// 5. k_msd_plan scans hist16 into base16 (the first output position of every 16-bit bucket),
-//    lays out the segmented tiles of pass 2, and gates the bucket pass on max(hist16) <= the
-//    bucket capacity (else the LSD passes sort R1: still the stable sort of the input);
-// 6. MSD pass 1 (k_onesweep SEG, next byte within every top-byte segment) writes records R2 in
+// 1. k_hist16_in counts hist16[key >> 16] over the input (one row per workgroup), k_hist16_reduce
+//    adds the rows and the top-byte totals (the digit totals of pass 0);
+// 2. k_msd_plan scans hist16 into base16 (the first output position of every 16-bit bucket), lays
+//    out the segmented tiles of pass 2, and picks the path on the device: MSD when every 16-bit
+//    bucket fits the bucket tile and no top-byte bucket holds more than max_top keys, else the
+//    four LSD passes (enqueued behind, gated the other way) sort the input;
+// 3. MSD pass 0 (k_onesweep, top byte) writes the input partitioned by its top byte (R1, records);
+// 4. MSD pass 1 (k_onesweep SEG, next byte within every top-byte segment) writes records R2 in
 //    16-bit bucket order;
-// 7. k_bucket_sort: one workgroup per 16-bit bucket sorts it by its low 16 bits in LDS and writes
+// 5. k_bucket_sort: one workgroup per 16-bit bucket sorts it by its low 16 bits in LDS and writes
 //    it as one contiguous run of the output.  Every step is stable, so the result is the stable
-//    sort of the input.  Gate words: g[0..15] MSD chosen, g[16..31] LSD on the input,
-//    g[32..47] bucket pass, g[48..63] LSD on R1 (each word repeated: gated_off reads 0..pass).
-constexpr uint32_t kGateMsd = 0, kGateLsd = 16, kGateBucket = 32, kGateLsdR1 = 48;
+//    sort of the input.  Gate words: g[0..15] MSD chosen, g[16..31] LSD on the input
+//    (each word repeated: gated_off reads 0..pass).
+constexpr uint32_t kGateMsd = 0, kGateLsd = 16;
 
 __device__ __forceinline__ void set_gate(uint32_t* g, uint32_t v) {
     if (threadIdx.x < 16u) g[threadIdx.x] = v;
 }
 
-__global__ __launch_bounds__(256) void k_msd_decide(const uint32_t* __restrict__ top_tot,
-                                                    uint32_t max_top, uint32_t* gates) {
-    __shared__ uint32_t s_bad;
-    if (threadIdx.x == 0) s_bad = 0u;
-    __syncthreads();
-    if (top_tot[threadIdx.x] > max_top) atomicOr(&s_bad, 1u);
-    __syncthreads();
-    const uint32_t msd = s_bad ? 0u : 1u;
-    set_gate(gates + kGateMsd, msd);
-    set_gate(gates + kGateLsd, 1u - msd);
-    if (!msd) {   // the plan kernel is gated off with the MSD path: close its gates here
-        set_gate(gates + kGateBucket, 0u);
-        set_gate(gates + kGateLsdR1, 0u);
-    }
-}
-
-// hist16[key >> 16] over keys[0..n) sorted by their top byte: each workgroup takes a contiguous
-// chunk, counts the (at most 4) top bytes that start it in LDS rows, any later ones with global
-// atomics (only in chunks crossing many small buckets), then adds its rows to hist16.
-template <int BLOCK>
-__global__ __launch_bounds__(BLOCK) void k_hist16(const uint32_t* __restrict__ keys, uint32_t n,
-                                                  uint32_t* __restrict__ hist16, const uint32_t* gate) {
-    __shared__ uint32_t h[4][256];
-    __shared__ uint32_t s_top0;
-    if (gated_off(gate, 0)) return;
+// hist16[key >> 16] of keys[0..n) (L = LAYOUT_AOS: the keys of n 8-byte records), one 1024-thread
+// workgroup per CU over a contiguous chunk.  All 65536 buckets live in LDS as the 16-bit halves of
+// 32768 words (128 KB, one ds_add per key); after every kRound keys (fewer than 2^16: no half can
+// wrap) each thread adds its 32 words' halves into 64 u32 registers and clears them.  The
+// workgroup's 65536 counts go to rows[blockIdx.x] (k_hist16_reduce adds the rows).
+template <int L>
+__global__ __launch_bounds__(1024) void k_hist16_in(const uint32_t* __restrict__ keys, uint32_t n,
+                                                     uint32_t* __restrict__ rows) {
+    constexpr uint32_t B = 1024, W = 32768, PER = W / B;
+    constexpr uint32_t KPL = L == LAYOUT_AOS ? 2u : 4u;          // keys per 16-byte load
+    constexpr uint32_t STEPS = 61440u / (B * KPL);                // loads per thread per round
+    constexpr uint32_t FLY = 5;                                    // loads in flight
+    static_assert(STEPS % FLY == 0, "whole load groups per round");
+    __shared__ uint32_t h[W];
+    const uint32_t tid = threadIdx.x;
+    uint32_t acc[2 * PER];
+#pragma unroll
+    for (uint32_t i = 0; i < PER; ++i) { h[tid + B * i] = 0u; acc[2 * i] = 0u; acc[2 * i + 1] = 0u; }
     const uint32_t chunk = ((n + gridDim.x - 1) / gridDim.x + 3u) & ~3u;
     const uint64_t lo = (uint64_t)blockIdx.x * chunk;
-    if (lo >= n) return;
-    const uint32_t hi = lo + chunk < n ? (uint32_t)(lo + chunk) : n;
-    for (uint32_t i = threadIdx.x; i < 4u * 256u; i += BLOCK) (&h[0][0])[i] = 0u;
-    if (threadIdx.x == 0) s_top0 = keys[lo] >> 24;
-    __syncthreads();
-    const uint32_t top0 = s_top0;
+    const uint64_t hi = lo + chunk < n ? lo + chunk : (lo < n ? n : lo);
+    const uint64_t nv = (hi - lo) / KPL;                          // whole 16-byte vectors
+    const uint4* v4 = reinterpret_cast<const uint4*>(keys + (L == LAYOUT_AOS ? 2 : 1) * lo);
     auto count = [&](uint32_t key) {
-        const uint32_t r = (key >> 24) - top0;
-        if (r < 4u) atomicAdd(&h[r][(key >> 16) & 255u], 1u);
-        else atomicAdd(&hist16[key >> 16], 1u);
+        const uint32_t b = key >> 16;
+        atomicAdd(&h[b >> 1], 1u << ((b & 1u) << 4));
     };
-    // lo is a multiple of 4: 16-byte loads for the whole vectors of the chunk, 4 in flight
-    const uint4* k4 = reinterpret_cast<const uint4*>(keys + lo);
-    const uint32_t nv = (uint32_t)((hi - lo) / 4u);
-    uint32_t i = threadIdx.x;
-    for (; i + 3u * BLOCK < nv; i += 4u * BLOCK) {
-        uint4 q[4];
+    auto flush = [&]() {
+        __syncthreads();
 #pragma unroll
-        for (int u = 0; u < 4; ++u) q[u] = k4[i + u * BLOCK];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) { count(q[u].x); count(q[u].y); count(q[u].z); count(q[u].w); }
-    }
-    for (; i < nv; i += BLOCK) {
-        const uint4 q = k4[i];
-        count(q.x); count(q.y); count(q.z); count(q.w);
-    }
-    for (uint64_t i = lo + 4ull * nv + threadIdx.x; i < hi; i += BLOCK) count(keys[i]);
+        for (uint32_t i = 0; i < PER; ++i) {
+            const uint32_t x = h[tid + B * i];
+            acc[2 * i] += x & 0xFFFFu;
+            acc[2 * i + 1] += x >> 16;
+            h[tid + B * i] = 0u;
+        }
+        __syncthreads();
+    };
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < 4u * 256u; i += BLOCK) {
-        const uint32_t r = i >> 8, c = (&h[0][0])[i];
-        if (c && top0 + r < 256u) atomicAdd(&hist16[((top0 + r) << 8) | (i & 255u)], c);
+    for (uint64_t base = 0; base < nv; base += (uint64_t)STEPS * B) {
+        for (uint32_t s0 = 0; s0 < STEPS; s0 += FLY) {
+            uint4 q[FLY];
+#pragma unroll
+            for (uint32_t u = 0; u < FLY; ++u) {
+                const uint64_t i = base + (uint64_t)(s0 + u) * B + tid;
+                q[u] = i < nv ? v4[i] : make_uint4(0u, 0u, 0u, 0u);
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < FLY; ++u) {
+                if (base + (uint64_t)(s0 + u) * B + tid < nv) {
+                    if (L == LAYOUT_AOS) { count(q[u].x); count(q[u].z); }
+                    else { count(q[u].x); count(q[u].y); count(q[u].z); count(q[u].w); }
+                }
+            }
+        }
+        flush();
+    }
+    // the last (hi - lo) % KPL keys of the chunk
+    const uint64_t rest = lo + nv * KPL;
+    if (rest + tid < hi) count(keys[(L == LAYOUT_AOS ? 2 : 1) * (rest + tid)]);
+    flush();
+    uint2* row = reinterpret_cast<uint2*>(rows + (size_t)blockIdx.x * 65536u);
+#pragma unroll
+    for (uint32_t i = 0; i < PER; ++i) row[tid + B * i] = make_uint2(acc[2 * i], acc[2 * i + 1]);
+}
+
+// hist16 = the sum of nrows rows of 65536 counts; top_tot[t] = the sum of hist16[t << 8 ..] (the
+// top-byte digit totals).  One workgroup per top byte: 64 columns of 4 buckets x 16 row groups.
+__global__ __launch_bounds__(1024) void k_hist16_reduce(const uint32_t* __restrict__ rows, uint32_t nrows,
+                                                         uint32_t* __restrict__ hist16,
+                                                         uint32_t* __restrict__ top_tot) {
+    __shared__ uint4 s_part[16][64];
+    const uint32_t tid = threadIdx.x, c = tid & 63u, g = tid >> 6;
+    const uint4* r4 = reinterpret_cast<const uint4*>(rows) + (size_t)blockIdx.x * 64u + c;
+    constexpr size_t RS = 65536 / 4;    // row stride in 16-byte words
+    uint4 a = make_uint4(0u, 0u, 0u, 0u);
+    auto add = [](uint4& x, const uint4 y) { x.x += y.x; x.y += y.y; x.z += y.z; x.w += y.w; };
+    uint32_t r = g;
+    for (; r + 48u < nrows; r += 64u) {
+        const uint4 q0 = r4[r * RS], q1 = r4[(r + 16u) * RS], q2 = r4[(r + 32u) * RS], q3 = r4[(r + 48u) * RS];
+        add(a, q0); add(a, q1); add(a, q2); add(a, q3);
+    }
+    for (; r < nrows; r += 16u) add(a, r4[r * RS]);
+    s_part[g][c] = a;
+    __syncthreads();
+    if (tid < 64u) {
+        uint4 t = s_part[0][tid];
+#pragma unroll
+        for (int j = 1; j < 16; ++j) add(t, s_part[j][tid]);
+        reinterpret_cast<uint4*>(hist16)[blockIdx.x * 64u + tid] = t;
+        uint32_t sum = t.x + t.y + t.z + t.w;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) sum += __shfl_down(sum, off, 64);
+        if (tid == 0) top_tot[blockIdx.x] = sum;
     }
 }
 
 // One workgroup: base16 = exclusive scan of hist16 (65536 buckets in key order), the segmented
 // tile table of MSD pass 1 (segment = top byte: [257] first tile + total, [256] start, [256]
-// end), and the bucket / LSD-on-R1 gates (bucket pass iff every 16-bit bucket fits its tile).
+// end), and the path: MSD iff every 16-bit bucket fits the bucket tile (cap) and every top-byte
+// bucket holds at most max_top keys, else the LSD passes on the input.
 // Buckets larger than `small` (the population-sized bucket tile) are listed in over[1..]
 // (over[0] = their number; at most kOverMax, else the bucket pass is gated off too).
 constexpr uint32_t kOverMax = 4096;
@@ -1324,12 +1360,11 @@ __global__ __launch_bounds__(1024) void k_msd_plan(const uint32_t* __restrict__ 
                                                    const uint32_t* __restrict__ top_tot,
                                                    uint32_t* __restrict__ base16,
                                                    uint32_t* __restrict__ segtab, uint32_t cap,
-                                                   uint32_t small, uint32_t* __restrict__ over,
-                                                   uint32_t* gates) {
+                                                   uint32_t small, uint32_t max_top,
+                                                   uint32_t* __restrict__ over, uint32_t* gates) {
     constexpr int NW = 16;
     __shared__ uint32_t s_scratch[NW];
     __shared__ uint32_t s_big, s_nover;
-    if (gated_off(gates + kGateMsd, 0)) return;
     const uint32_t tid = threadIdx.x;
     if (tid == 0) { s_big = 0u; s_nover = 0u; }
     // 64 consecutive buckets per thread, held in registers (16 loads of 16 bytes in flight)
@@ -1367,6 +1402,7 @@ __global__ __launch_bounds__(1024) void k_msd_plan(const uint32_t* __restrict__ 
     if (mx > cap) atomicOr(&s_big, 1u);
     // segments: tiles of TILE records per top-byte bucket
     const uint32_t cnt = tid < 256u ? top_tot[tid] : 0u;
+    if (cnt > max_top) atomicOr(&s_big, 1u);
     const uint32_t tiles = (cnt + TILE - 1) / TILE;
     uint32_t ttot;
     const uint32_t tbase = block_excl_scan_n<NW>(tiles, s_scratch, ttot);
@@ -1381,8 +1417,8 @@ __global__ __launch_bounds__(1024) void k_msd_plan(const uint32_t* __restrict__ 
     __syncthreads();
     if (tid == 0) over[0] = s_nover < kOverMax ? s_nover : kOverMax;
     const uint32_t ok = (s_big || s_nover > kOverMax) ? 0u : 1u;
-    set_gate(gates + kGateBucket, ok);
-    set_gate(gates + kGateLsdR1, 1u - ok);
+    set_gate(gates + kGateMsd, ok);
+    set_gate(gates + kGateLsd, 1u - ok);
 }
 
 // One workgroup per 16-bit bucket (blockIdx.x = key >> 16): its records (R2, contiguous, at most
@@ -1390,7 +1426,7 @@ __global__ __launch_bounds__(1024) void k_msd_plan(const uint32_t* __restrict__ 
 // output arrays as one contiguous run (whole 128-B lines but at the two ends).
 // Two launches share the buckets: a tile sized to the bucket population (about 1.15x the mean
 // bucket) takes every bucket of at most BLOCK * KPT records (min_cnt = 0), and a 16K-record tile
-// takes the rest (min_cnt = the first launch's tile); k_msd_plan gates this pass off when a
+// takes the rest (min_cnt = the first launch's tile); k_msd_plan gates the path off when a
 // bucket exceeds the large tile.
 // LO: output layout (LAYOUT_SOA: the caller's two arrays; LAYOUT_AOS: records - the texture
 // layout, sorted in place: R2 is then the caller's buffer itself, and every workgroup has read its
@@ -1475,20 +1511,6 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_sort(const uint32_t* rec,
     }
     __syncthreads();   // the next listed bucket reuses s_whist / s_kv
     }
-}
-
-// dst[0..n) = src[0..n) (8-byte records, 16 bytes per load) when the gate is open (the texture
-// layout's LSD-on-R1 fallback, whose fourth pass ends in the plan's buffer).
-__global__ __launch_bounds__(kBlock) void k_copy_gated(const uint2* __restrict__ src,
-                                                       uint2* __restrict__ dst, uint64_t n,
-                                                       const uint32_t* gate) {
-    if (gated_off(gate, 0)) return;
-    const uint64_t n16 = n >> 1;
-    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
-    const uint64_t i0 = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    for (uint64_t i = i0; i < n16; i += stride)
-        reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(src)[i];
-    if ((n & 1) && i0 == 0) dst[n - 1] = src[n - 1];
 }
 
 // ---- order check -------------------------------------------------------------------------

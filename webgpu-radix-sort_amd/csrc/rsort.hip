@@ -479,7 +479,8 @@ bool use_onesweep(const rs_plan* p, uint64_t n) {
 
 // The hybrid MSD path applies (the device still falls back to the LSD passes for skewed keys).
 bool use_msd(const rs_plan* p, uint64_t n) {
-    const bool bufs = p->layout == rs::LAYOUT_AOS || (p->layout == rs::LAYOUT_SOA && p->tmp2 && p->aos_tmp);
+    const bool bufs = (p->layout == rs::LAYOUT_AOS || (p->layout == rs::LAYOUT_SOA && p->tmp2 && p->aos_tmp)) &&
+                      (uint64_t)p->cus * 65536ull <= 2ull * n;   // the histogram rows fit in tmp_k
     return p->msd && p->msd_mode != 0 && bufs && !p->check_order && p->bit_count == 32 &&
            p->radix_bits == 8 && use_onesweep(p, n) && !use_small_tiles(n) && n >= kMsdMin &&
            p->kv_cfg == 0 && !p->huge_tiles;
@@ -681,15 +682,14 @@ RS_EXPORT void rs_plan_destroy(rs_plan* p) {
 }
 
 // Enqueue every launch of one sort (n > kTinyMax) on stream s.
-// The four LSD passes of a separate-arrays sort gated on `gate` (the hybrid MSD path's fallbacks):
+// The four LSD passes of a separate-arrays sort gated on `gate` (the hybrid MSD path's fallback):
 // src (arrays) -> records -> records -> records -> uk / uv, through the plan's two records
-// buffers; pass 0's totals must be in ptot, later passes count theirs.  When src is the plan's
-// own array pair (tmp_k / tmp_v: R1 of the MSD path), pass 0 writes tmp2 first.
+// buffers; pass 0's totals must be in ptot, later passes count theirs.
 static rs_status enqueue_lsd_gated(rs_plan* p, const uint32_t* sk, const uint32_t* sv, uint32_t* uk,
                                    uint32_t* uv, uint32_t n, const uint32_t* gate, hipStream_t s) {
     constexpr int A = rs::LAYOUT_AOS, S = rs::LAYOUT_SOA;
-    uint32_t* ra = sk == p->tmp_k ? p->tmp2 : p->tmp_k;    // never overwrite the source early
-    uint32_t* rb = ra == p->tmp2 ? p->tmp_k : p->tmp2;
+    uint32_t* ra = p->tmp_k;
+    uint32_t* rb = p->tmp2;
     struct Step { const uint32_t* ik; const uint32_t* iv; uint32_t* ok; uint32_t* ov; int LL; };
     const Step steps[4] = {{sk, sv, ra, nullptr, layout_pair(S, A)},
                            {ra, nullptr, rb, nullptr, layout_pair(A, A)},
@@ -705,12 +705,12 @@ static rs_status enqueue_lsd_gated(rs_plan* p, const uint32_t* sk, const uint32_
     return st;
 }
 
-// The hybrid MSD path (rs_kernels.hpp, "hybrid MSD path"): top-byte totals, the device's choice,
-// top-byte pass -> 16-bit bucket histogram -> plan -> segmented next-byte pass -> in-LDS bucket
-// sort; the LSD passes enqueued behind, gated on the device (on the input when the top byte is
-// skewed, on R1 when a 16-bit bucket exceeds kBucketCap).  Separate arrays: R1 = tmp_k / tmp_v,
-// R2 = tmp2, the result in uk / uv.  Records (the texture layout, sorted in place): R1 = the
-// two halves of tmp_k, R2 = the caller's buffer itself (consumed by pass 0).
+// The hybrid MSD path (rs_kernels.hpp, "hybrid MSD path"): the 16-bit bucket histogram of the
+// input and the device's choice first, then top-byte pass -> segmented next-byte pass -> in-LDS
+// bucket sort; the LSD passes on the input enqueued behind, gated the other way (skewed keys).
+// R1 = records in tmp_k (which holds the histogram rows before that); R2 = records in tmp2
+// (separate arrays, the result in uk / uv) or the caller's buffer itself (records, the texture
+// layout sorted in place: the input is consumed by pass 0).
 static rs_status enqueue_sort_msd(rs_plan* p, uint32_t* uk, uint32_t* uv, uint64_t n, hipStream_t s,
                                   const uint32_t* ik0, const uint32_t* iv0) {
     constexpr int A = rs::LAYOUT_AOS, S = rs::LAYOUT_SOA;
@@ -718,8 +718,7 @@ static rs_status enqueue_sort_msd(rs_plan* p, uint32_t* uk, uint32_t* uv, uint64
     const uint32_t n32 = (uint32_t)n;
     const uint32_t* sk = ik0 ? ik0 : uk;
     const uint32_t* sv = aos ? nullptr : (ik0 ? iv0 : uv);
-    uint32_t* r1k = p->tmp_k;
-    uint32_t* r1v = p->tmp_k + p->capacity;      // = tmp_v of a separate-arrays plan
+    uint32_t* r1 = p->tmp_k;
     uint32_t* r2 = aos ? uk : p->tmp2;
     uint32_t* hist16 = p->msd;
     uint32_t* base16 = hist16 + 65536;
@@ -727,43 +726,17 @@ static rs_status enqueue_sort_msd(rs_plan* p, uint32_t* uk, uint32_t* uv, uint64
     uint32_t* gates = segtab + 1024;
     uint32_t* mtot = gates + 64;
     uint32_t* over = mtot + 1024;
-    const uint32_t* top_tot = mtot + 768;
+    uint32_t* top_tot = mtot + 768;
     const uint32_t ntiles = (uint32_t)((n + kLarge.tile - 1) / kLarge.tile);
     HIP_TRY(hipMemsetAsync(p->ptot, 0, 4ull * (rs::kTotalsMax + 32), s));
-    HIP_TRY(hipMemsetAsync(hist16, 0, 4ull * 65536, s));
-    HIP_TRY(hipMemsetAsync(mtot, 0, 4ull * 1024, s));
-    rs::PassList pl{};
-    pl.count = 1;
-    pl.width[0] = 8;
-    const uint32_t tgrid = (uint32_t)std::min<uint64_t>((uint64_t)RS_TOT_PER_CU * p->cus,
-                                                        (n + 4ull * RS_TOT_BLOCK - 1) / (4ull * RS_TOT_BLOCK));
-    auto totals = [&](const uint32_t* keys, bool records, uint32_t shift, uint32_t* out, const uint32_t* gate) {
-        if (records)
-            hipLaunchKernelGGL(rs::k_pass_totals<2>, dim3(tgrid), dim3(RS_TOT_BLOCK), 0, s, keys, n32, pl, shift,
-                               out, (uint32_t*)nullptr, 0xFFFFFFFFu, 0x1u, gate);
-        else
-            hipLaunchKernelGGL(rs::k_pass_totals<1>, dim3(tgrid), dim3(RS_TOT_BLOCK), 0, s, keys, n32, pl, shift,
-                               out, (uint32_t*)nullptr, 0xFFFFFFFFu, 0x1u, gate);
-    };
-    // the top byte only (the LSD fallbacks count byte 0 for themselves, gated)
-    p->timer.run(RS_KERNEL_HISTOGRAM, s, [&] { totals(sk, aos, 24u, mtot + 768, nullptr); });
-    HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(rs::k_msd_decide, dim3(1), dim3(256), 0, s, top_tot, kMsdMaxTop, gates);
-    HIP_TRY(hipGetLastError());
-    // MSD pass 0: input -> R1 arrays, partitioned by the top byte
-    if (rs_status st = next_epoch(p, s)) return st;
-    p->timer.run(RS_KERNEL_SCATTER, s, [&] {
-        if (aos)
-            launch_msd_pass<A, S, 0>(p, sk, nullptr, r1k, r1v, n32, 24, ntiles, top_tot, p->tickets + 4,
-                                     gates + rs::kGateMsd, nullptr, nullptr, s);
-        else
-            launch_msd_pass<S, S, 0>(p, sk, sv, r1k, r1v, n32, 24, ntiles, top_tot, p->tickets + 4,
-                                     gates + rs::kGateMsd, nullptr, nullptr, s);
-    });
-    HIP_TRY(hipGetLastError());
+    // one histogram row per CU in tmp_k (R1 is written only after the rows are added)
     p->timer.run(RS_KERNEL_HISTOGRAM, s, [&] {
-        hipLaunchKernelGGL(rs::k_hist16<256>, dim3(8 * p->cus), dim3(256), 0, s, r1k, n32, hist16,
-                           gates + rs::kGateMsd);
+        if (aos)
+            hipLaunchKernelGGL(rs::k_hist16_in<A>, dim3(p->cus), dim3(1024), 0, s, sk, n32, p->tmp_k);
+        else
+            hipLaunchKernelGGL(rs::k_hist16_in<S>, dim3(p->cus), dim3(1024), 0, s, sk, n32, p->tmp_k);
+        hipLaunchKernelGGL(rs::k_hist16_reduce, dim3(256), dim3(1024), 0, s, (const uint32_t*)p->tmp_k,
+                           (uint32_t)p->cus, hist16, top_tot);
     });
     HIP_TRY(hipGetLastError());
     // 16-bit buckets: a tile sized to the mean bucket + 6 sigma of a uniform population takes
@@ -771,43 +744,60 @@ static rs_status enqueue_sort_msd(rs_plan* p, uint32_t* uk, uint32_t* uv, uint64
     const double mean = (double)n / 65536.0;
     static const double slack = [] { const char* e = getenv("RSORT_BUCKET_SLACK"); return e ? atof(e) : 1.0; }();
     const uint32_t want = (uint32_t)(mean * slack + 6.0 * std::sqrt(mean) + 64.0);
-    uint32_t small_cap = 0;
-    for (uint32_t kpt : {4u, 8u, 12u, 18u, 24u})
-        if (!small_cap && want <= 256u * kpt) small_cap = 256u * kpt;
+    static const uint32_t bb = [] { const char* e = getenv("RSORT_BUCKET_BLOCK"); return e ? (uint32_t)atoi(e) : 256u; }();
+    static const uint32_t kpts256[] = {4, 8, 12, 18, 24}, kpts512[] = {2, 4, 6, 9, 12}, kpts1024[] = {1, 2, 3, 5, 6},
+                          kpts128[] = {8, 16, 24, 36, 48};
+    const uint32_t* kpts = bb == 512 ? kpts512 : bb == 1024 ? kpts1024 : bb == 128 ? kpts128 : kpts256;
+    uint32_t small_cap = 0, small_kpt = 0;
+    for (int q = 0; q < 5; ++q)
+        if (!small_cap && want <= bb * kpts[q]) { small_cap = bb * kpts[q]; small_kpt = kpts[q]; }
     p->timer.run(RS_KERNEL_SCAN, s, [&] {
-        hipLaunchKernelGGL(rs::k_msd_plan<kLarge.tile>, dim3(1), dim3(1024), 0, s, hist16, top_tot, base16,
-                           segtab, kBucketCap, small_cap, over, gates);
+        hipLaunchKernelGGL(rs::k_msd_plan<kLarge.tile>, dim3(1), dim3(1024), 0, s, (const uint32_t*)hist16,
+                           (const uint32_t*)top_tot, base16, segtab, kBucketCap, small_cap, kMsdMaxTop, over,
+                           gates);
     });
     HIP_TRY(hipGetLastError());
-    // MSD pass 1: R1 arrays -> R2 records, by the next byte inside every top-byte segment
+    const uint32_t* g_msd = gates + rs::kGateMsd;
+    // MSD pass 0: input -> R1 records, partitioned by the top byte
     if (rs_status st = next_epoch(p, s)) return st;
     p->timer.run(RS_KERNEL_SCATTER, s, [&] {
-        launch_msd_pass<S, A, 1>(p, r1k, r1v, r2, nullptr, n32, 16, ntiles + 257, nullptr,
-                                 p->tickets + 5, gates + rs::kGateBucket, segtab, base16, s);
+        if (aos)
+            launch_msd_pass<A, A, 0>(p, sk, nullptr, r1, nullptr, n32, 24, ntiles, top_tot, p->tickets + 4,
+                                     g_msd, nullptr, nullptr, s);
+        else
+            launch_msd_pass<S, A, 0>(p, sk, sv, r1, nullptr, n32, 24, ntiles, top_tot, p->tickets + 4,
+                                     g_msd, nullptr, nullptr, s);
     });
     HIP_TRY(hipGetLastError());
-    const uint32_t g_b = rs::kGateBucket;
+    // MSD pass 1: R1 -> R2 records, by the next byte inside every top-byte segment
+    if (rs_status st = next_epoch(p, s)) return st;
+    p->timer.run(RS_KERNEL_SCATTER, s, [&] {
+        launch_msd_pass<A, A, 1>(p, r1, nullptr, r2, nullptr, n32, 16, ntiles + 257, nullptr,
+                                 p->tickets + 5, g_msd, segtab, base16, s);
+    });
+    HIP_TRY(hipGetLastError());
     const bool ballot = p->rank_mode == rs::RANK_BALLOT;
     constexpr int A0 = rs::RANK_LDS_ATOMIC, B0 = rs::RANK_BALLOT;
     p->timer.run(RS_KERNEL_BUCKET, s, [&] {
         auto small = [&](auto kern) {
-            hipLaunchKernelGGL(kern, dim3(65536), dim3(256), 0, s, r2, hist16, base16, uk, uv,
-                               gates + g_b, p->tickets + 16, 0u, (const uint32_t*)nullptr);
+            hipLaunchKernelGGL(kern, dim3(65536), dim3(bb), 0, s, r2, hist16, base16, uk, uv, g_msd,
+                               p->tickets + 16, 0u, (const uint32_t*)nullptr);
         };
         auto large = [&](auto kern) {
-            hipLaunchKernelGGL(kern, dim3(256), dim3(kBucketBlock), 0, s, r2, hist16, base16, uk, uv,
-                               gates + g_b, p->tickets + 16, small_cap, (const uint32_t*)over);
+            hipLaunchKernelGGL(kern, dim3(256), dim3(kBucketBlock), 0, s, r2, hist16, base16, uk, uv, g_msd,
+                               p->tickets + 16, small_cap, (const uint32_t*)over);
         };
         auto both = [&](auto lo) {
             constexpr int LO = decltype(lo)::value;
-            switch (small_cap) {
-                case 256 * 4: ballot ? small(rs::k_bucket_sort<256, 4, B0, LO>) : small(rs::k_bucket_sort<256, 4, A0, LO>); break;
-                case 256 * 8: ballot ? small(rs::k_bucket_sort<256, 8, B0, LO>) : small(rs::k_bucket_sort<256, 8, A0, LO>); break;
-                case 256 * 12: ballot ? small(rs::k_bucket_sort<256, 12, B0, LO>) : small(rs::k_bucket_sort<256, 12, A0, LO>); break;
-                case 256 * 18: ballot ? small(rs::k_bucket_sort<256, 18, B0, LO>) : small(rs::k_bucket_sort<256, 18, A0, LO>); break;
-                case 256 * 24: ballot ? small(rs::k_bucket_sort<256, 24, B0, LO>) : small(rs::k_bucket_sort<256, 24, A0, LO>); break;
+#define RS_BK(BB, KP) case BB * 100 + KP: ballot ? small(rs::k_bucket_sort<BB, KP, B0, LO>) : small(rs::k_bucket_sort<BB, KP, A0, LO>); break;
+            switch (bb * 100 + small_kpt) {
+                RS_BK(256, 4) RS_BK(256, 8) RS_BK(256, 12) RS_BK(256, 18) RS_BK(256, 24)
+                RS_BK(512, 2) RS_BK(512, 4) RS_BK(512, 6) RS_BK(512, 9) RS_BK(512, 12)
+                RS_BK(1024, 1) RS_BK(1024, 2) RS_BK(1024, 3) RS_BK(1024, 5) RS_BK(1024, 6)
+                RS_BK(128, 8) RS_BK(128, 16) RS_BK(128, 24) RS_BK(128, 36) RS_BK(128, 48)
                 default: break;   // every bucket goes to the listed large-tile launch
             }
+#undef RS_BK
             // the listed buckets (none for uniform keys): a small persistent grid over the list
             ballot ? large(rs::k_bucket_sort<kBucketBlock, kBucketKpt, B0, LO>)
                    : large(rs::k_bucket_sort<kBucketBlock, kBucketKpt, A0, LO>);
@@ -816,43 +806,33 @@ static rs_status enqueue_sort_msd(rs_plan* p, uint32_t* uk, uint32_t* uv, uint64
         else both(std::integral_constant<int, S>{});
     });
     HIP_TRY(hipGetLastError());
-    // fallbacks (gated off on the device unless taken), each counting its pass 0 totals first
-    // (the byte-0 digit totals of the input; R1 is a permutation of it)
+    // the fallback (gated off on the device unless taken): pass 0's byte-0 totals, then the four
+    // LSD passes on the input
     const uint32_t* g_lsd = gates + rs::kGateLsd;
-    const uint32_t* g_r1 = gates + rs::kGateLsdR1;
     uint32_t* t0 = p->ptot + p->ptot_off[0];
-    if (!aos) {
-        p->timer.run(RS_KERNEL_FALLBACK, s, [&] { totals(sk, false, 0u, t0, g_lsd); });
-        HIP_TRY(hipGetLastError());
-        if (rs_status st = enqueue_lsd_gated(p, sk, sv, uk, uv, n32, g_lsd, s)) return st;
-        p->timer.run(RS_KERNEL_FALLBACK, s, [&] { totals(r1k, false, 0u, t0, g_r1); });
-        HIP_TRY(hipGetLastError());
-        return enqueue_lsd_gated(p, r1k, r1v, uk, uv, n32, g_r1, s);
-    }
-    // records: on the input, uk -> tmp_k -> uk -> tmp_k -> uk; on R1 (the arrays in tmp_k),
-    // R1 -> uk -> tmp_k -> uk -> tmp_k, then tmp_k copied back to uk
+    rs::PassList pl{};
+    pl.count = 1;
+    pl.width[0] = 8;
+    const uint32_t tgrid = (uint32_t)std::min<uint64_t>((uint64_t)RS_TOT_PER_CU * p->cus,
+                                                        (n + 4ull * RS_TOT_BLOCK - 1) / (4ull * RS_TOT_BLOCK));
+    p->timer.run(RS_KERNEL_FALLBACK, s, [&] {
+        if (aos)
+            hipLaunchKernelGGL(rs::k_pass_totals<2>, dim3(tgrid), dim3(RS_TOT_BLOCK), 0, s, sk, n32, pl, 0u, t0,
+                               (uint32_t*)nullptr, 0xFFFFFFFFu, 0x1u, g_lsd);
+        else
+            hipLaunchKernelGGL(rs::k_pass_totals<1>, dim3(tgrid), dim3(RS_TOT_BLOCK), 0, s, sk, n32, pl, 0u, t0,
+                               (uint32_t*)nullptr, 0xFFFFFFFFu, 0x1u, g_lsd);
+    });
+    HIP_TRY(hipGetLastError());
+    if (!aos) return enqueue_lsd_gated(p, sk, sv, uk, uv, n32, g_lsd, s);
+    // records: uk -> tmp_k -> uk -> tmp_k -> uk
     p->scatter_kind = RS_KERNEL_FALLBACK;
     rs_status st = RS_OK;
-    p->timer.run(RS_KERNEL_FALLBACK, s, [&] { totals(uk, true, 0u, t0, g_lsd); });
     for (uint32_t i = 0; i < 4 && st == RS_OK; ++i)
         st = run_pass(p, (i & 1) ? p->tmp_k : uk, nullptr, (i & 1) ? uk : p->tmp_k, nullptr, n32, 8 * i, 8,
                       layout_pair(A, A), g_lsd, (int)i, s, /*onesweep=*/true);
-    if (st == RS_OK) p->timer.run(RS_KERNEL_FALLBACK, s, [&] { totals(r1k, false, 0u, t0, g_r1); });
-    for (uint32_t i = 0; i < 4 && st == RS_OK; ++i) {
-        const uint32_t* ik = i == 0 ? r1k : ((i & 1) ? uk : p->tmp_k);
-        uint32_t* ok = (i & 1) ? p->tmp_k : uk;
-        st = run_pass(p, ik, i == 0 ? r1v : nullptr, ok, nullptr, n32, 8 * i, 8,
-                      i == 0 ? layout_pair(S, A) : layout_pair(A, A), g_r1, (int)i, s, /*onesweep=*/true);
-    }
     p->scatter_kind = RS_KERNEL_SCATTER;
-    if (st != RS_OK) return st;
-    const uint32_t cgrid = (uint32_t)std::min<uint64_t>(8ull * p->cus, (n / 2 + rs::kBlock - 1) / rs::kBlock + 1);
-    p->timer.run(RS_KERNEL_FALLBACK, s, [&] {
-        hipLaunchKernelGGL(rs::k_copy_gated, dim3(cgrid), dim3(rs::kBlock), 0, s, (const uint2*)p->tmp_k,
-                           (uint2*)uk, n, g_r1);
-    });
-    HIP_TRY(hipGetLastError());
-    return RS_OK;
+    return st;
 }
 
 // in_k0 / in_v0 (optional): pass 0 reads them instead of uk / uv (out-of-place sort; the

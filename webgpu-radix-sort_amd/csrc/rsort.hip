@@ -739,18 +739,17 @@ static rs_status enqueue_sort_msd(rs_plan* p, uint32_t* uk, uint32_t* uv, uint64
                            (uint32_t)p->cus, hist16, top_tot);
     });
     HIP_TRY(hipGetLastError());
-    // 16-bit buckets: a tile sized to the mean bucket + 6 sigma of a uniform population takes
-    // every bucket that fits it, the large tile the listed rest
+    // 16-bit buckets: a tile sized to the mean bucket + 4 sigma of a uniform population takes
+    // every bucket that fits it (at 2^28 keys: 4352 records, ~2 buckets over it), the large tile
+    // the listed rest
     const double mean = (double)n / 65536.0;
     static const double slack = [] { const char* e = getenv("RSORT_BUCKET_SLACK"); return e ? atof(e) : 1.0; }();
-    const uint32_t want = (uint32_t)(mean * slack + 6.0 * std::sqrt(mean) + 64.0);
-    static const uint32_t bb = [] { const char* e = getenv("RSORT_BUCKET_BLOCK"); return e ? (uint32_t)atoi(e) : 256u; }();
-    static const uint32_t kpts256[] = {4, 8, 12, 18, 24}, kpts512[] = {2, 4, 6, 9, 12}, kpts1024[] = {1, 2, 3, 5, 6},
-                          kpts128[] = {8, 16, 24, 36, 48};
-    const uint32_t* kpts = bb == 512 ? kpts512 : bb == 1024 ? kpts1024 : bb == 128 ? kpts128 : kpts256;
+    const uint32_t want = (uint32_t)(mean * slack + 4.0 * std::sqrt(mean));
+    constexpr uint32_t bb = 256;
+    static const uint32_t kpts[] = {4, 8, 12, 17, 18, 24};
     uint32_t small_cap = 0, small_kpt = 0;
-    for (int q = 0; q < 5; ++q)
-        if (!small_cap && want <= bb * kpts[q]) { small_cap = bb * kpts[q]; small_kpt = kpts[q]; }
+    for (uint32_t kpt : kpts)
+        if (!small_cap && want <= bb * kpt) { small_cap = bb * kpt; small_kpt = kpt; }
     p->timer.run(RS_KERNEL_SCAN, s, [&] {
         hipLaunchKernelGGL(rs::k_msd_plan<kLarge.tile>, dim3(1), dim3(1024), 0, s, (const uint32_t*)hist16,
                            (const uint32_t*)top_tot, base16, segtab, kBucketCap, small_cap, kMsdMaxTop, over,
@@ -789,12 +788,9 @@ static rs_status enqueue_sort_msd(rs_plan* p, uint32_t* uk, uint32_t* uv, uint64
         };
         auto both = [&](auto lo) {
             constexpr int LO = decltype(lo)::value;
-#define RS_BK(BB, KP) case BB * 100 + KP: ballot ? small(rs::k_bucket_sort<BB, KP, B0, LO>) : small(rs::k_bucket_sort<BB, KP, A0, LO>); break;
-            switch (bb * 100 + small_kpt) {
-                RS_BK(256, 4) RS_BK(256, 8) RS_BK(256, 12) RS_BK(256, 18) RS_BK(256, 24)
-                RS_BK(512, 2) RS_BK(512, 4) RS_BK(512, 6) RS_BK(512, 9) RS_BK(512, 12)
-                RS_BK(1024, 1) RS_BK(1024, 2) RS_BK(1024, 3) RS_BK(1024, 5) RS_BK(1024, 6)
-                RS_BK(128, 8) RS_BK(128, 16) RS_BK(128, 24) RS_BK(128, 36) RS_BK(128, 48)
+#define RS_BK(KP) case KP: ballot ? small(rs::k_bucket_sort<bb, KP, B0, LO, (KP <= 18 ? 3 : 1)>) : small(rs::k_bucket_sort<bb, KP, A0, LO, (KP <= 18 ? 3 : 1)>); break;
+            switch (small_kpt) {
+                RS_BK(4) RS_BK(8) RS_BK(12) RS_BK(17) RS_BK(18) RS_BK(24)
                 default: break;   // every bucket goes to the listed large-tile launch
             }
 #undef RS_BK

@@ -26,7 +26,7 @@ extern "C" {
 #endif
 
 #define RSORT_VERSION_MAJOR 0
-#define RSORT_VERSION_MINOR 3
+#define RSORT_VERSION_MINOR 4
 
 typedef enum rs_status {
     RS_OK = 0,
@@ -146,6 +146,13 @@ rs_status rs_plan_partition_records(rs_plan* plan, const void* in_keys, const vo
                                     const void* d_totals, void* stream);
 rs_status rs_plan_sort_records(rs_plan* plan, const void* records, void* keys_out,
                                void* values_out, uint64_t n, void* stream);
+/* rs_plan_sort_records with a hint: every key lies in [key_lo, key_hi] (a group sort's received
+ * top-digit buckets).  The sort may then work on the range-relative bits key - key_lo only (the
+ * hybrid MSD path over a rank's buckets); a key outside the range is detected on the device and
+ * the 32-bit passes run instead, so the result is always the stable sort.  key_lo <= key_hi. */
+rs_status rs_plan_sort_records_range(rs_plan* plan, const void* records, void* keys_out,
+                                     void* values_out, uint64_t n, uint32_t key_lo, uint32_t key_hi,
+                                     void* stream);
 rs_status rs_plan_info_get(const rs_plan* plan, rs_plan_info* info);
 /* Kernel timing: when enabled, every launch of the plan is bracketed by HIP events on the
  * launch stream and per-kind durations are accumulated (read after synchronising). */

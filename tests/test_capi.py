@@ -20,7 +20,7 @@ def test_library_exports_every_header_symbol():
 
 def test_version_and_status_strings():
     L = _lib.load()
-    assert L.rs_version() == (0 << 16) | 3
+    assert L.rs_version() == (0 << 16) | 4
     assert L.rs_status_string(_lib.RS_ERR_NOT_POW2).decode().startswith("workgroup")
     assert "device-side failure" in L.rs_status_string(_lib.RS_ERR_DEVICE).decode()
 

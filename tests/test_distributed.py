@@ -40,10 +40,12 @@ class OracleLocalOps:
         rec = k[perm].astype(np.uint64) | (v.astype(np.uint64) << np.uint64(32))
         return torch.from_numpy(rec.view(np.int64))
 
-    def sort_records(self, records, keys_out, values_out):
+    def sort_records(self, records, keys_out, values_out, key_range=None):
         r = records.numpy().view(np.uint64)
         k = (r & np.uint64(0xFFFFFFFF)).astype(np.uint32)
         v = (r >> np.uint64(32)).astype(np.uint32)
+        if key_range is not None and k.size:   # the hint the exchange passes is exact
+            assert key_range[0] <= int(k.min()) and int(k.max()) <= key_range[1]
         ok, ov = O.stable_sort_masked(k, v, 32)
         keys_out.numpy().view(np.uint32)[:] = ok
         values_out.numpy().view(np.uint32)[:] = ov

@@ -140,3 +140,77 @@ def test_msd_records_fallbacks_and_overflow(kind):
     t = _sort_tex_and_check((1 << 24) + 1, kind)
     if kind in ("top0", "low0"):
         assert t["fallback"]["ms"] > 5 * t["bucket"]["ms"]
+
+
+def _records_sort(keys_u32, key_range=None, profile=False):
+    """SortPlan.sort_records (records in, arrays out) of (key, index) records."""
+    from radix_sort_amd.ops import SortPlan
+    n = keys_u32.size
+    k = torch.from_numpy(keys_u32.view(np.int32)).to(DEV)
+    rec = torch.empty((n, 2), dtype=torch.int32, device=DEV)
+    rec[:, 0] = k
+    rec[:, 1] = torch.arange(n, dtype=torch.int32, device=DEV)
+    rec = rec.view(torch.int64).view(-1)
+    plan = SortPlan(0, n, True)
+    plan.set_profiling(True)
+    ok_, ov_ = torch.empty_like(k), torch.empty_like(k)
+    plan.sort_records(rec, ok_, ov_, n, key_range=key_range)
+    torch.cuda.synchronize()
+    plan.check()
+    times = plan.kernel_times()
+    plan.destroy()
+    ek, ev = O.stable_sort_masked_c(keys_u32, np.arange(n, dtype=np.uint32), 32)
+    assert np.array_equal(ok_.cpu().numpy().view(np.uint32), ek)
+    assert np.array_equal(ov_.cpu().numpy().view(np.uint32), ev)
+    return times
+
+
+def test_msd_records_to_arrays_full_range():
+    # rs_plan_sort_records (the group sorts' records -> arrays form) takes the MSD path itself
+    u = O.gen_u32(21, (1 << 24) + 3)
+    t = _records_sort(u)
+    assert t["bucket"]["ms"] > 0.05 and t["fallback"]["ms"] < t["bucket"]["ms"]
+
+
+@pytest.mark.parametrize("lo_hi", [(0x20000000, 0x27FFFFFF),      # 8 aligned top-byte buckets (27 bits)
+                                   (0x1E000000, 0x25FFFFFF),      # 8 unaligned buckets (key - lo: 27 bits)
+                                   (0x12345678, 0x1234F677),      # a 16-bit-wide range
+                                   (0x00000000, 0xFFFFFFFF)])
+def test_msd_records_key_range(lo_hi):
+    lo, hi = lo_hi
+    u = O.gen_u32(22, 1 << 24).astype(np.uint64)
+    keys = (np.uint64(lo) + u % np.uint64(hi - lo + 1)).astype(np.uint32)
+    keys[:5] = lo                      # both ends of the range present
+    keys[5:9] = hi
+    t = _records_sort(keys, key_range=(lo, hi))
+    if hi - lo >= (1 << 24):           # populated 16-bit buckets: the MSD path ran
+        assert t["bucket"]["ms"] > 0.05 and t["fallback"]["ms"] < t["bucket"]["ms"]
+
+
+@pytest.mark.parametrize("outside", ["below", "above"])
+def test_msd_records_key_outside_range_falls_back(outside):
+    lo, hi = 0x40000000, 0x47FFFFFF
+    u = O.gen_u32(23, 1 << 24)
+    keys = (np.uint32(lo) + (u & np.uint32(0x07FFFFFF))).astype(np.uint32)
+    keys[12345] = lo - 1 if outside == "below" else hi + 1     # the hint is wrong for one key
+    t = _records_sort(keys, key_range=(lo, hi))
+    assert t["fallback"]["ms"] > 5 * t["bucket"]["ms"]           # the 32-bit LSD passes ran
+
+
+def test_msd_group_regions_use_key_range():
+    # virtual ranks with one exchange round: every rank's region (>= 12M records) is sorted with
+    # its buckets' key range (rs_plan_sort_records_range) - parity against the oracle
+    from radix_sort_amd import RadixSortGroup
+    counts = [13 << 20, (13 << 20) + 11]
+    host_k = [O.gen_u32(30 + r, c) for r, c in enumerate(counts)]
+    starts = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+    host_v = [np.arange(starts[r], starts[r + 1], dtype=np.uint32) for r in range(2)]
+    g = RadixSortGroup([0, 0], capacity=max(counts), has_values=True, transport="copy", rounds=1)
+    try:
+        out = g.sort([torch.from_numpy(k.view(np.int32)).to(DEV) for k in host_k],
+                     [torch.from_numpy(v.view(np.int32)).to(DEV) for v in host_v])
+        ek, ev = O.stable_sort_masked_c(np.concatenate(host_k), np.concatenate(host_v), 32)
+        assert np.array_equal(np.concatenate([o[0].cpu().numpy().view(np.uint32) for o in out]), ek)
+        assert np.array_equal(np.concatenate([o[1].cpu().numpy().view(np.uint32) for o in out]), ev)
+    finally:
+        g.destroy()

@@ -454,8 +454,14 @@ RS_EXPORT rs_status rs_group_sort(rs_group* g, void* const* keys, void* const* v
                 }
                 const uint64_t a = base[(size_t)q * (G + 1) + j], b = base[(size_t)q * (G + 1) + j + 1];
                 if (b <= a) continue;
+                // every key of round j lies in its buckets' range: the local sort may work on the
+                // range-relative bits (the hybrid MSD path over this rank's buckets)
+                const uint32_t ca = g->cuts[(size_t)q * (G + 1) + j], cb = g->cuts[(size_t)q * (G + 1) + j + 1];
+                const uint32_t klo = ca << (32 - bits);
+                const uint32_t khi = cb >= B ? 0xFFFFFFFFu : (cb << (32 - bits)) - 1u;
                 if (g->kv)
-                    G_TRY(rs_plan_sort_records(k.local, (char*)k.recv + 8 * a, k.out_k + a, k.out_v + a, b - a, k.sort_s));
+                    G_TRY(rs_plan_sort_records_range(k.local, (char*)k.recv + 8 * a, k.out_k + a, k.out_v + a, b - a,
+                                                     klo, khi, k.sort_s));
                 else
                     G_TRY(rs_plan_sort_n(k.local, (uint32_t*)k.recv + a, nullptr, b - a, k.sort_s));
             }

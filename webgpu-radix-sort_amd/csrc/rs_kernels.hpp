@@ -19,6 +19,7 @@
 // reference's block_sums[b * WORKGROUP_COUNT + WORKGROUP_ID] (RadixSort.ts:113).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <type_traits>
 #include <stdint.h>
 
 #ifndef RS_XCD_GROUP
@@ -905,7 +906,9 @@ __device__ __forceinline__ bool wave_inversion(const uint32_t (&k)[KPT], uint32_
 // look-back chain (its first tile publishes an inclusive prefix at once).  segtab = [257] first
 // tile of every segment (+ the total), [256] segment starts, [256] segment ends; the tile count is
 // segtab[256] (ntiles is only its bound).
-template <int R, int BLOCK, int KPT, int L, int RANK, int LO = L, int SR = 1, int SEG = 0>
+// KB (the hybrid MSD path's first pass over a known key range): every real key is replaced by
+// key - kbase as it is loaded, so the digits and the output are of the range-relative keys.
+template <int R, int BLOCK, int KPT, int L, int RANK, int LO = L, int SR = 1, int SEG = 0, bool KB = false>
 __global__ __launch_bounds__(BLOCK, pass_min_waves(BLOCK, KPT)) void k_onesweep(
     const uint32_t* __restrict__ in_k, const uint32_t* __restrict__ in_v,
     uint32_t* __restrict__ out_k, uint32_t* __restrict__ out_v, uint32_t n, uint32_t shift,
@@ -913,7 +916,8 @@ __global__ __launch_bounds__(BLOCK, pass_min_waves(BLOCK, KPT)) void k_onesweep(
     unsigned long long* status, uint32_t* ticket, uint32_t* err, uint32_t* __restrict__ ntot,
     uint32_t nshift, uint32_t nmask, uint32_t epoch, const uint32_t* gate, int pass,
     uint32_t* chk, uint32_t fmask, uint32_t spin_max, uint32_t* host_err,
-    const uint32_t* __restrict__ segtab = nullptr, const uint32_t* __restrict__ base16 = nullptr) {
+    const uint32_t* __restrict__ segtab = nullptr, const uint32_t* __restrict__ base16 = nullptr,
+    uint32_t kbase = 0) {
     // ntot (may be null): whole-array totals of the NEXT pass's digit (key >> nshift) & nmask,
     // counted here from the keys this workgroup stages, so only pass 0 needs k_pass_totals.
     // chk (may be null, check_order, pass > 0): the order check of this pass's input, fused:
@@ -1012,6 +1016,12 @@ __global__ __launch_bounds__(BLOCK, pass_min_waves(BLOCK, KPT)) void k_onesweep(
 #pragma unroll
             for (int j = 0; j < KPT; ++j)
                 if (wb + j * 64 >= n) k[j] = kPadKey;
+        }
+        if (KB) {   // range-relative keys (the pads past nvalid stay kPadKey)
+            const uint32_t wb = w * WAVE_KEYS + lane_id();
+#pragma unroll
+            for (int j = 0; j < KPT; ++j)
+                if (wb + j * 64 < nvalid) k[j] -= kbase;
         }
         const uint32_t npad = (uint32_t)TILE - nvalid;
         uint32_t bkey = kPadKey;   // the key after this wave's slots (next wave or next tile)
@@ -1256,14 +1266,20 @@ __device__ __forceinline__ void set_gate(uint32_t* g, uint32_t v) {
 // 32768 words (128 KB, one ds_add per key); after every kRound keys (fewer than 2^16: no half can
 // wrap) each thread adds its 32 words' halves into 64 u32 registers and clears them.  The
 // workgroup's 65536 counts go to rows[blockIdx.x] (k_hist16_reduce adds the rows).
+// Range form (the multi-GPU group sorts): the buckets are of key - kbase >> shift, and a key
+// outside [kbase, kbase + range] sets the workgroup's flag word (rows[gridDim.x * 65536 + block];
+// k_msd_plan then picks the LSD passes over the whole 32-bit keys).  Records load 8 bytes per lane
+// (a receive region is only 8-byte aligned), arrays 16.
 template <int L>
 __global__ __launch_bounds__(1024) void k_hist16_in(const uint32_t* __restrict__ keys, uint32_t n,
-                                                     uint32_t* __restrict__ rows) {
+                                                     uint32_t* __restrict__ rows, uint32_t kbase,
+                                                     uint32_t range, uint32_t shift) {
     constexpr uint32_t B = 1024, W = 32768, PER = W / B;
-    constexpr uint32_t KPL = L == LAYOUT_AOS ? 2u : 4u;          // keys per 16-byte load
+    constexpr uint32_t KPL = L == LAYOUT_AOS ? 1u : 4u;          // keys per load
     constexpr uint32_t STEPS = 61440u / (B * KPL);                // loads per thread per round
     constexpr uint32_t FLY = 5;                                    // loads in flight
     static_assert(STEPS % FLY == 0, "whole load groups per round");
+    using Vec = typename std::conditional<L == LAYOUT_AOS, uint2, uint4>::type;
     __shared__ uint32_t h[W];
     const uint32_t tid = threadIdx.x;
     uint32_t acc[2 * PER];
@@ -1272,10 +1288,13 @@ __global__ __launch_bounds__(1024) void k_hist16_in(const uint32_t* __restrict__
     const uint32_t chunk = ((n + gridDim.x - 1) / gridDim.x + 3u) & ~3u;
     const uint64_t lo = (uint64_t)blockIdx.x * chunk;
     const uint64_t hi = lo + chunk < n ? lo + chunk : (lo < n ? n : lo);
-    const uint64_t nv = (hi - lo) / KPL;                          // whole 16-byte vectors
-    const uint4* v4 = reinterpret_cast<const uint4*>(keys + (L == LAYOUT_AOS ? 2 : 1) * lo);
+    const uint64_t nv = (hi - lo) / KPL;                          // whole vectors
+    const Vec* v4 = reinterpret_cast<const Vec*>(keys + (L == LAYOUT_AOS ? 2 : 1) * lo);
+    bool bad = false;
     auto count = [&](uint32_t key) {
-        const uint32_t b = key >> 16;
+        const uint32_t rk = key - kbase;
+        bad |= rk > range;
+        const uint32_t b = (rk >> shift) & 0xFFFFu;
         atomicAdd(&h[b >> 1], 1u << ((b & 1u) << 4));
     };
     auto flush = [&]() {
@@ -1292,16 +1311,16 @@ __global__ __launch_bounds__(1024) void k_hist16_in(const uint32_t* __restrict__
     __syncthreads();
     for (uint64_t base = 0; base < nv; base += (uint64_t)STEPS * B) {
         for (uint32_t s0 = 0; s0 < STEPS; s0 += FLY) {
-            uint4 q[FLY];
+            Vec q[FLY];
 #pragma unroll
             for (uint32_t u = 0; u < FLY; ++u) {
                 const uint64_t i = base + (uint64_t)(s0 + u) * B + tid;
-                q[u] = i < nv ? v4[i] : make_uint4(0u, 0u, 0u, 0u);
+                if (i < nv) q[u] = v4[i];
             }
 #pragma unroll
             for (uint32_t u = 0; u < FLY; ++u) {
                 if (base + (uint64_t)(s0 + u) * B + tid < nv) {
-                    if (L == LAYOUT_AOS) { count(q[u].x); count(q[u].z); }
+                    if constexpr (L == LAYOUT_AOS) { count(q[u].x); }
                     else { count(q[u].x); count(q[u].y); count(q[u].z); count(q[u].w); }
                 }
             }
@@ -1315,15 +1334,23 @@ __global__ __launch_bounds__(1024) void k_hist16_in(const uint32_t* __restrict__
     uint2* row = reinterpret_cast<uint2*>(rows + (size_t)blockIdx.x * 65536u);
 #pragma unroll
     for (uint32_t i = 0; i < PER; ++i) row[tid + B * i] = make_uint2(acc[2 * i], acc[2 * i + 1]);
+    const int any_bad = __syncthreads_or(bad ? 1 : 0);
+    if (tid == 0) rows[(size_t)gridDim.x * 65536u + blockIdx.x] = any_bad ? 1u : 0u;
 }
 
 // hist16 = the sum of nrows rows of 65536 counts; top_tot[t] = the sum of hist16[t << 8 ..] (the
-// top-byte digit totals).  One workgroup per top byte: 64 columns of 4 buckets x 16 row groups.
+// top-byte digit totals).  One workgroup per top byte: 64 columns of 4 buckets x 16 row groups
+// (nrows <= 1024).
 __global__ __launch_bounds__(1024) void k_hist16_reduce(const uint32_t* __restrict__ rows, uint32_t nrows,
                                                          uint32_t* __restrict__ hist16,
-                                                         uint32_t* __restrict__ top_tot) {
+                                                         uint32_t* __restrict__ top_tot,
+                                                         uint32_t* __restrict__ range_bad) {
     __shared__ uint4 s_part[16][64];
     const uint32_t tid = threadIdx.x, c = tid & 63u, g = tid >> 6;
+    if (blockIdx.x == 0) {   // any key outside the range (the rows' flag words)
+        const int bad = __syncthreads_or(tid < nrows && rows[(size_t)nrows * 65536u + tid] != 0u);
+        if (tid == 0) *range_bad = bad ? 1u : 0u;
+    }
     const uint4* r4 = reinterpret_cast<const uint4*>(rows) + (size_t)blockIdx.x * 64u + c;
     constexpr size_t RS = 65536 / 4;    // row stride in 16-byte words
     uint4 a = make_uint4(0u, 0u, 0u, 0u);
@@ -1361,7 +1388,8 @@ __global__ __launch_bounds__(1024) void k_msd_plan(const uint32_t* __restrict__ 
                                                    uint32_t* __restrict__ base16,
                                                    uint32_t* __restrict__ segtab, uint32_t cap,
                                                    uint32_t small, uint32_t max_top,
-                                                   uint32_t* __restrict__ over, uint32_t* gates) {
+                                                   uint32_t* __restrict__ over, uint32_t* gates,
+                                                   const uint32_t* __restrict__ range_bad) {
     constexpr int NW = 16;
     __shared__ uint32_t s_scratch[NW];
     __shared__ uint32_t s_big, s_nover;
@@ -1416,7 +1444,7 @@ __global__ __launch_bounds__(1024) void k_msd_plan(const uint32_t* __restrict__ 
     if (tid == 0) segtab[256] = ttot;
     __syncthreads();
     if (tid == 0) over[0] = s_nover < kOverMax ? s_nover : kOverMax;
-    const uint32_t ok = (s_big || s_nover > kOverMax) ? 0u : 1u;
+    const uint32_t ok = (s_big || s_nover > kOverMax || *range_bad) ? 0u : 1u;
     set_gate(gates + kGateMsd, ok);
     set_gate(gates + kGateLsd, 1u - ok);
 }
@@ -1444,7 +1472,8 @@ __global__ __launch_bounds__(BLOCK, MW) void k_bucket_sort(const uint32_t* rec,
                                                        uint32_t* __restrict__ out_v,
                                                        const uint32_t* gate, uint32_t* err,
                                                        uint32_t min_cnt,
-                                                       const uint32_t* __restrict__ over = nullptr) {
+                                                       const uint32_t* __restrict__ over = nullptr,
+                                                       uint32_t kbase = 0) {
     constexpr int R = 8, RADIX = 256;
     constexpr int NW = BLOCK / 64;
     constexpr int TILE = BLOCK * KPT;
@@ -1519,9 +1548,9 @@ __global__ __launch_bounds__(BLOCK, MW) void k_bucket_sort(const uint32_t* rec,
             const uint32_t p2 = wbase + j * 64 + lane;
             if (p2 < cnt) {
                 if (LO == LAYOUT_AOS) {
-                    reinterpret_cast<uint2*>(out_k)[(size_t)base + p2] = make_uint2(k[j], v[j]);
+                    reinterpret_cast<uint2*>(out_k)[(size_t)base + p2] = make_uint2(k[j] + kbase, v[j]);
                 } else {
-                    out_k[(size_t)base + p2] = k[j];
+                    out_k[(size_t)base + p2] = k[j] + kbase;
                     out_v[(size_t)base + p2] = v[j];
                 }
             }

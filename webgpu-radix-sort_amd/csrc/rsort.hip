@@ -302,7 +302,7 @@ void launch_onesweep_t(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint3
                        p->ptot + p->ptot_off[pass], p->status, p->tickets + pass,
                        p->tickets + 16, ntot, nshift, nmask, p->epoch, gate, pass, chk,
                        full_mask(p->bit_count), p->spin_max, p->host_err_dev,
-                       (const uint32_t*)nullptr, (const uint32_t*)nullptr);
+                       (const uint32_t*)nullptr, (const uint32_t*)nullptr, 0u);
 }
 
 template <int R, int BLOCK, int KPT, int L, int LO, int SR>
@@ -326,22 +326,22 @@ rs_status next_epoch(rs_plan* p, hipStream_t s) {
 
 // One pass of the hybrid MSD path (16K-record tiles, 8-bit digit at `shift`): SEG = 0 the
 // top-byte pass over the whole input, SEG = 1 the next-byte pass inside every top-byte segment.
-template <int L, int LO, int SEG>
+template <int L, int LO, int SEG, bool KB = false>
 void launch_msd_pass(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint32_t* ok, uint32_t* ov,
                      uint32_t n, uint32_t shift, uint32_t ntiles, const uint32_t* dtot, uint32_t* ticket,
                      const uint32_t* gate, const uint32_t* segtab, const uint32_t* base16,
-                     hipStream_t s) {
+                     hipStream_t s, uint32_t kbase = 0) {
     auto go = [&](auto kern) {
         static const uint32_t per_cu = resident_per_cu(kern, kLarge.block);
         const uint32_t grid = std::min<uint32_t>(ntiles, p->cus * per_cu);
         hipLaunchKernelGGL(kern, dim3(grid), dim3(kLarge.block), 0, s, ik, iv, ok, ov, n, shift, 255u,
                            ntiles, dtot, p->status, ticket, p->tickets + 16, nullptr, 0u, 0u, p->epoch,
-                           gate, 0, nullptr, 0xFFFFFFFFu, p->spin_max, p->host_err_dev, segtab, base16);
+                           gate, 0, nullptr, 0xFFFFFFFFu, p->spin_max, p->host_err_dev, segtab, base16, kbase);
     };
     if (p->rank_mode == rs::RANK_BALLOT)
-        go(rs::k_onesweep<8, kLarge.block, kLarge.kpt, L, rs::RANK_BALLOT, LO, 1, SEG>);
+        go(rs::k_onesweep<8, kLarge.block, kLarge.kpt, L, rs::RANK_BALLOT, LO, 1, SEG, KB>);
     else
-        go(rs::k_onesweep<8, kLarge.block, kLarge.kpt, L, rs::RANK_LDS_ATOMIC, LO, 1, SEG>);
+        go(rs::k_onesweep<8, kLarge.block, kLarge.kpt, L, rs::RANK_LDS_ATOMIC, LO, 1, SEG, KB>);
 }
 
 // Layout pair of one pass: input layout | output layout << 4 (they differ only on the one-sweep
@@ -683,15 +683,16 @@ RS_EXPORT void rs_plan_destroy(rs_plan* p) {
 
 // Enqueue every launch of one sort (n > kTinyMax) on stream s.
 // The four LSD passes of a separate-arrays sort gated on `gate` (the hybrid MSD path's fallback):
-// src (arrays) -> records -> records -> records -> uk / uv, through the plan's two records
+// src (arrays, or records) -> records -> records -> records -> uk / uv, through the plan's two records
 // buffers; pass 0's totals must be in ptot, later passes count theirs.
-static rs_status enqueue_lsd_gated(rs_plan* p, const uint32_t* sk, const uint32_t* sv, uint32_t* uk,
-                                   uint32_t* uv, uint32_t n, const uint32_t* gate, hipStream_t s) {
+static rs_status enqueue_lsd_gated(rs_plan* p, const uint32_t* sk, const uint32_t* sv, bool in_aos,
+                                   uint32_t* uk, uint32_t* uv, uint32_t n, const uint32_t* gate,
+                                   hipStream_t s) {
     constexpr int A = rs::LAYOUT_AOS, S = rs::LAYOUT_SOA;
     uint32_t* ra = p->tmp_k;
     uint32_t* rb = p->tmp2;
     struct Step { const uint32_t* ik; const uint32_t* iv; uint32_t* ok; uint32_t* ov; int LL; };
-    const Step steps[4] = {{sk, sv, ra, nullptr, layout_pair(S, A)},
+    const Step steps[4] = {{sk, sv, ra, nullptr, layout_pair(in_aos ? A : S, A)},
                            {ra, nullptr, rb, nullptr, layout_pair(A, A)},
                            {rb, nullptr, ra, nullptr, layout_pair(A, A)},
                            {ra, nullptr, uk, uv, layout_pair(A, S)}};
@@ -708,18 +709,21 @@ static rs_status enqueue_lsd_gated(rs_plan* p, const uint32_t* sk, const uint32_
 // The hybrid MSD path (rs_kernels.hpp, "hybrid MSD path"): the 16-bit bucket histogram of the
 // input and the device's choice first, then top-byte pass -> segmented next-byte pass -> in-LDS
 // bucket sort; the LSD passes on the input enqueued behind, gated the other way (skewed keys).
-// R1 = records in tmp_k (which holds the histogram rows before that); R2 = records in tmp2
-// (separate arrays, the result in uk / uv) or the caller's buffer itself (records, the texture
-// layout sorted in place: the input is consumed by pass 0).
-static rs_status enqueue_sort_msd(rs_plan* p, uint32_t* uk, uint32_t* uv, uint64_t n, hipStream_t s,
-                                  const uint32_t* ik0, const uint32_t* iv0) {
+// Input (sk, sv): arrays, or records (in_aos: the texture layout in place, or a group sort's
+// received region).  Output (uk, uv): arrays, or records in place (out_aos).  R1 = records in
+// tmp_k (which holds the histogram rows before that); R2 = records in tmp2, or the caller's
+// buffer itself when the records are sorted in place (the input is consumed by pass 0).
+// Keys known to lie in [kbase, kbase + 2^vbits) (a group sort's received buckets) are sorted by
+// their vbits range-relative bits: digits of key - kbase at vbits - 8 and vbits - 16 (a key
+// outside the range sends the device to the 32-bit LSD passes).
+static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t* sv, bool in_aos,
+                                  uint32_t* uk, uint32_t* uv, bool out_aos, uint64_t n, hipStream_t s,
+                                  uint32_t kbase = 0, uint32_t vbits = 32) {
     constexpr int A = rs::LAYOUT_AOS, S = rs::LAYOUT_SOA;
-    const bool aos = p->layout == A;
     const uint32_t n32 = (uint32_t)n;
-    const uint32_t* sk = ik0 ? ik0 : uk;
-    const uint32_t* sv = aos ? nullptr : (ik0 ? iv0 : uv);
+    const uint32_t range = vbits >= 32 ? 0xFFFFFFFFu : (1u << vbits) - 1u;
     uint32_t* r1 = p->tmp_k;
-    uint32_t* r2 = aos ? uk : p->tmp2;
+    uint32_t* r2 = out_aos ? uk : p->tmp2;
     uint32_t* hist16 = p->msd;
     uint32_t* base16 = hist16 + 65536;
     uint32_t* segtab = base16 + 65536;
@@ -730,13 +734,16 @@ static rs_status enqueue_sort_msd(rs_plan* p, uint32_t* uk, uint32_t* uv, uint64
     const uint32_t ntiles = (uint32_t)((n + kLarge.tile - 1) / kLarge.tile);
     HIP_TRY(hipMemsetAsync(p->ptot, 0, 4ull * (rs::kTotalsMax + 32), s));
     // one histogram row per CU in tmp_k (R1 is written only after the rows are added)
+    uint32_t* range_bad = mtot;
     p->timer.run(RS_KERNEL_HISTOGRAM, s, [&] {
-        if (aos)
-            hipLaunchKernelGGL(rs::k_hist16_in<A>, dim3(p->cus), dim3(1024), 0, s, sk, n32, p->tmp_k);
+        if (in_aos)
+            hipLaunchKernelGGL(rs::k_hist16_in<A>, dim3(p->cus), dim3(1024), 0, s, sk, n32, p->tmp_k, kbase,
+                               range, vbits - 16);
         else
-            hipLaunchKernelGGL(rs::k_hist16_in<S>, dim3(p->cus), dim3(1024), 0, s, sk, n32, p->tmp_k);
+            hipLaunchKernelGGL(rs::k_hist16_in<S>, dim3(p->cus), dim3(1024), 0, s, sk, n32, p->tmp_k, kbase,
+                               range, vbits - 16);
         hipLaunchKernelGGL(rs::k_hist16_reduce, dim3(256), dim3(1024), 0, s, (const uint32_t*)p->tmp_k,
-                           (uint32_t)p->cus, hist16, top_tot);
+                           (uint32_t)p->cus, hist16, top_tot, range_bad);
     });
     HIP_TRY(hipGetLastError());
     // 16-bit buckets: a tile sized to the mean bucket + 4 sigma of a uniform population takes
@@ -753,25 +760,31 @@ static rs_status enqueue_sort_msd(rs_plan* p, uint32_t* uk, uint32_t* uv, uint64
     p->timer.run(RS_KERNEL_SCAN, s, [&] {
         hipLaunchKernelGGL(rs::k_msd_plan<kLarge.tile>, dim3(1), dim3(1024), 0, s, (const uint32_t*)hist16,
                            (const uint32_t*)top_tot, base16, segtab, kBucketCap, small_cap, kMsdMaxTop, over,
-                           gates);
+                           gates, (const uint32_t*)range_bad);
     });
     HIP_TRY(hipGetLastError());
     const uint32_t* g_msd = gates + rs::kGateMsd;
     // MSD pass 0: input -> R1 records, partitioned by the top byte
     if (rs_status st = next_epoch(p, s)) return st;
     p->timer.run(RS_KERNEL_SCATTER, s, [&] {
-        if (aos)
-            launch_msd_pass<A, A, 0>(p, sk, nullptr, r1, nullptr, n32, 24, ntiles, top_tot, p->tickets + 4,
-                                     g_msd, nullptr, nullptr, s);
+        if (in_aos && kbase)
+            launch_msd_pass<A, A, 0, true>(p, sk, nullptr, r1, nullptr, n32, vbits - 8, ntiles, top_tot,
+                                           p->tickets + 4, g_msd, nullptr, nullptr, s, kbase);
+        else if (in_aos)
+            launch_msd_pass<A, A, 0>(p, sk, nullptr, r1, nullptr, n32, vbits - 8, ntiles, top_tot,
+                                     p->tickets + 4, g_msd, nullptr, nullptr, s);
+        else if (kbase)
+            launch_msd_pass<S, A, 0, true>(p, sk, sv, r1, nullptr, n32, vbits - 8, ntiles, top_tot,
+                                           p->tickets + 4, g_msd, nullptr, nullptr, s, kbase);
         else
-            launch_msd_pass<S, A, 0>(p, sk, sv, r1, nullptr, n32, 24, ntiles, top_tot, p->tickets + 4,
+            launch_msd_pass<S, A, 0>(p, sk, sv, r1, nullptr, n32, vbits - 8, ntiles, top_tot, p->tickets + 4,
                                      g_msd, nullptr, nullptr, s);
     });
     HIP_TRY(hipGetLastError());
     // MSD pass 1: R1 -> R2 records, by the next byte inside every top-byte segment
     if (rs_status st = next_epoch(p, s)) return st;
     p->timer.run(RS_KERNEL_SCATTER, s, [&] {
-        launch_msd_pass<A, A, 1>(p, r1, nullptr, r2, nullptr, n32, 16, ntiles + 257, nullptr,
+        launch_msd_pass<A, A, 1>(p, r1, nullptr, r2, nullptr, n32, vbits - 16, ntiles + 257, nullptr,
                                  p->tickets + 5, g_msd, segtab, base16, s);
     });
     HIP_TRY(hipGetLastError());
@@ -780,11 +793,11 @@ static rs_status enqueue_sort_msd(rs_plan* p, uint32_t* uk, uint32_t* uv, uint64
     p->timer.run(RS_KERNEL_BUCKET, s, [&] {
         auto small = [&](auto kern) {
             hipLaunchKernelGGL(kern, dim3(65536), dim3(bb), 0, s, r2, hist16, base16, uk, uv, g_msd,
-                               p->tickets + 16, 0u, (const uint32_t*)nullptr);
+                               p->tickets + 16, 0u, (const uint32_t*)nullptr, kbase);
         };
         auto large = [&](auto kern) {
             hipLaunchKernelGGL(kern, dim3(256), dim3(kBucketBlock), 0, s, r2, hist16, base16, uk, uv, g_msd,
-                               p->tickets + 16, small_cap, (const uint32_t*)over);
+                               p->tickets + 16, small_cap, (const uint32_t*)over, kbase);
         };
         auto both = [&](auto lo) {
             constexpr int LO = decltype(lo)::value;
@@ -798,7 +811,7 @@ static rs_status enqueue_sort_msd(rs_plan* p, uint32_t* uk, uint32_t* uv, uint64
             ballot ? large(rs::k_bucket_sort<kBucketBlock, kBucketKpt, B0, LO>)
                    : large(rs::k_bucket_sort<kBucketBlock, kBucketKpt, A0, LO>);
         };
-        if (aos) both(std::integral_constant<int, A>{});
+        if (out_aos) both(std::integral_constant<int, A>{});
         else both(std::integral_constant<int, S>{});
     });
     HIP_TRY(hipGetLastError());
@@ -812,7 +825,7 @@ static rs_status enqueue_sort_msd(rs_plan* p, uint32_t* uk, uint32_t* uv, uint64
     const uint32_t tgrid = (uint32_t)std::min<uint64_t>((uint64_t)RS_TOT_PER_CU * p->cus,
                                                         (n + 4ull * RS_TOT_BLOCK - 1) / (4ull * RS_TOT_BLOCK));
     p->timer.run(RS_KERNEL_FALLBACK, s, [&] {
-        if (aos)
+        if (in_aos)
             hipLaunchKernelGGL(rs::k_pass_totals<2>, dim3(tgrid), dim3(RS_TOT_BLOCK), 0, s, sk, n32, pl, 0u, t0,
                                (uint32_t*)nullptr, 0xFFFFFFFFu, 0x1u, g_lsd);
         else
@@ -820,8 +833,8 @@ static rs_status enqueue_sort_msd(rs_plan* p, uint32_t* uk, uint32_t* uv, uint64
                                (uint32_t*)nullptr, 0xFFFFFFFFu, 0x1u, g_lsd);
     });
     HIP_TRY(hipGetLastError());
-    if (!aos) return enqueue_lsd_gated(p, sk, sv, uk, uv, n32, g_lsd, s);
-    // records: uk -> tmp_k -> uk -> tmp_k -> uk
+    if (!out_aos) return enqueue_lsd_gated(p, sk, sv, in_aos, uk, uv, n32, g_lsd, s);
+    // records in place: uk -> tmp_k -> uk -> tmp_k -> uk
     p->scatter_kind = RS_KERNEL_FALLBACK;
     rs_status st = RS_OK;
     for (uint32_t i = 0; i < 4 && st == RS_OK; ++i)
@@ -835,7 +848,10 @@ static rs_status enqueue_sort_msd(rs_plan* p, uint32_t* uk, uint32_t* uv, uint64
 // caller's input is only read, the result lands in uk / uv; check_order not supported).
 static rs_status enqueue_sort(rs_plan* p, uint32_t* uk, uint32_t* uv, uint64_t n, hipStream_t s,
                               const uint32_t* in_k0 = nullptr, const uint32_t* in_v0 = nullptr) {
-    if (use_msd(p, n)) return enqueue_sort_msd(p, uk, uv, n, s, in_k0, in_v0);
+    if (use_msd(p, n)) {
+        const bool aos = p->layout == rs::LAYOUT_AOS;
+        return enqueue_sort_msd(p, in_k0 ? in_k0 : uk, aos ? nullptr : (in_k0 ? in_v0 : uv), aos, uk, uv, aos, n, s);
+    }
     const int L = p->layout;
     const uint32_t n32 = (uint32_t)n;
     const uint32_t* gate = p->check_order ? p->flags : nullptr;
@@ -1151,8 +1167,8 @@ static rs_status enqueue_sort_records(rs_plan* p, const uint32_t* rec, uint32_t*
     return RS_OK;
 }
 
-RS_EXPORT rs_status rs_plan_sort_records(rs_plan* p, const void* records, void* keys_out,
-                                         void* values_out, uint64_t n, void* stream) {
+static rs_status sort_records_impl(rs_plan* p, const void* records, void* keys_out, void* values_out,
+                                   uint64_t n, uint32_t key_lo, uint32_t key_hi, void* stream) {
     if (!p) return fail(RS_ERR_INVALID_ARG, "rs_plan_sort_records: null plan");
     if (p->layout != rs::LAYOUT_SOA)
         return fail(RS_ERR_INVALID_ARG, "rs_plan_sort_records: needs a plan with separate values (RS_FLAG_HAS_VALUES)");
@@ -1175,6 +1191,11 @@ RS_EXPORT rs_status rs_plan_sort_records(rs_plan* p, const void* records, void* 
                            dim3(rs::kBlock), 0, s, (const uint2*)records, uk, uv, n);
         HIP_TRY(hipGetLastError());
         st = n > 1 ? run_tiny(p, uk, uv, (uint32_t)n, s) : RS_OK;
+    } else if (use_msd(p, n) && key_lo <= key_hi && key_hi - key_lo >= 0xFFFFu) {
+        // the hybrid MSD path over the range-relative bits of the keys
+        const uint32_t range = key_hi - key_lo;
+        const uint32_t vbits = 32u - (uint32_t)__builtin_clz(range);
+        st = enqueue_sort_msd(p, (const uint32_t*)records, nullptr, true, uk, uv, false, n, s, key_lo, vbits);
     } else {
         st = enqueue_sort_records(p, (const uint32_t*)records, uk, uv, n, s);
     }
@@ -1182,6 +1203,18 @@ RS_EXPORT rs_status rs_plan_sort_records(rs_plan* p, const void* records, void* 
     HIP_TRY(hipEventRecord(p->done, s));
     p->done_recorded = true;
     return RS_OK;
+}
+
+RS_EXPORT rs_status rs_plan_sort_records(rs_plan* p, const void* records, void* keys_out,
+                                         void* values_out, uint64_t n, void* stream) {
+    return sort_records_impl(p, records, keys_out, values_out, n, 0u, 0xFFFFFFFFu, stream);
+}
+
+RS_EXPORT rs_status rs_plan_sort_records_range(rs_plan* p, const void* records, void* keys_out,
+                                               void* values_out, uint64_t n, uint32_t key_lo,
+                                               uint32_t key_hi, void* stream) {
+    if (key_lo > key_hi) return fail(RS_ERR_INVALID_ARG, "rs_plan_sort_records_range: key_lo > key_hi");
+    return sort_records_impl(p, records, keys_out, values_out, n, key_lo, key_hi, stream);
 }
 
 RS_EXPORT rs_status rs_plan_device_errors(rs_plan* p, uint32_t* errors) {

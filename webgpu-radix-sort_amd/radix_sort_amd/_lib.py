@@ -84,6 +84,8 @@ _SIGS = {
     "rs_plan_partition_records": (ctypes.c_int, [_VP, _VP, _VP, _VP, ctypes.c_uint64,
                                                  ctypes.c_uint32, ctypes.c_uint32, _VP, _VP]),
     "rs_plan_sort_records": (ctypes.c_int, [_VP, _VP, _VP, _VP, ctypes.c_uint64, _VP]),
+    "rs_plan_sort_records_range": (ctypes.c_int, [_VP, _VP, _VP, _VP, ctypes.c_uint64, ctypes.c_uint32,
+                                                  ctypes.c_uint32, _VP]),
     "rs_plan_info_get": (ctypes.c_int, [_VP, ctypes.POINTER(PlanInfo)]),
     "rs_plan_set_profiling": (ctypes.c_int, [_VP, ctypes.c_int]),
     "rs_plan_kernel_times": (ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_double),

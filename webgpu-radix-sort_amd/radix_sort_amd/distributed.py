@@ -51,8 +51,9 @@ class LocalOps(Protocol):
         int64 (key, value) record per key (key | value << 32, the interleaved layout: one message
         per peer carries both); keys only, the int32 keys.  totals: histogram() of the same keys."""
 
-    def sort_records(self, records, keys_out, values_out) -> None:
-        """Stable sort of the int64 records by their 32-bit key into keys_out / values_out."""
+    def sort_records(self, records, keys_out, values_out, key_range=None) -> None:
+        """Stable sort of the int64 records by their 32-bit key into keys_out / values_out.
+        key_range: (lo, hi), every key in [lo, hi] (the round's top-digit buckets), a hint."""
 
     def sort(self, keys, n: int) -> None:
         """Stable in-place sort of keys[:n] (keys only) by the full 32-bit key."""
@@ -102,6 +103,14 @@ def bucket_groups(hist_all, bounds, groups: int):
     B = len(hist_all[0])
     totals = [sum(int(h[b]) for h in hist_all) for b in range(B)]
     return [_split_whole(totals, bounds[q], bounds[q + 1], groups) for q in range(len(bounds) - 1)]
+
+
+def round_key_range(cuts_rank, g: int, bits: int):
+    """[lo, hi] of every key in round g's buckets [cuts_rank[g], cuts_rank[g + 1]) of the
+    top-`bits` digit (the hint the group sort passes to the local sort)."""
+    shift = 32 - bits
+    a, b = int(cuts_rank[g]), int(cuts_rank[g + 1])
+    return a << shift, min((b << shift) - 1, 0xFFFFFFFF)
 
 
 def split_sizes(hist_all, bounds, rank: int, world: int):
@@ -270,7 +279,8 @@ def _distributed_sort(keys, values, ops, group, bits, chunks) -> ExchangeResult:
             if values is None:
                 ops.sort(recv[a:b], b - a)
             else:
-                ops.sort_records(recv[a:b], out_k[a:b], out_v[a:b])
+                ops.sort_records(recv[a:b], out_k[a:b], out_v[a:b],
+                                 key_range=round_key_range(cuts[rank], g, bits))
     return ExchangeResult(out_k, out_v, n_recv,
                           [sum(b - a for a, b in (plan.send[g][q] for g in range(G))) for q in range(world)],
                           [sum(plan.recv[g][s] for g in range(G)) for s in range(world)])
@@ -326,10 +336,10 @@ class HipLocalOps:
         self._grow(n)
         self.plan.sort(keys, None, n)
 
-    def sort_records(self, records, keys_out, values_out) -> None:
+    def sort_records(self, records, keys_out, values_out, key_range=None) -> None:
         n = records.numel()
         self._grow(n)
-        self.plan.sort_records(records, keys_out, values_out, n)
+        self.plan.sort_records(records, keys_out, values_out, n, key_range=key_range)
 
     def sort_copy(self, keys, values, keys_out, values_out) -> None:
         n = keys.numel()

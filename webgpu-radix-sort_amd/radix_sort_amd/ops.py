@@ -77,6 +77,16 @@ class SortPlan:
         (rs_plan_check)."""
         check(_lib.load().rs_plan_check(self._plan), "rs_plan_check")
 
+    def set_profiling(self, enable: bool) -> None:
+        check(_lib.load().rs_plan_set_profiling(self._plan, 1 if enable else 0), "profiling")
+
+    def kernel_times(self) -> dict:
+        """Accumulated per-kind kernel times of the plan's launches (after set_profiling)."""
+        ms = (ctypes.c_double * _lib.RS_KERNEL_KINDS)()
+        n = (ctypes.c_uint64 * _lib.RS_KERNEL_KINDS)()
+        check(_lib.load().rs_plan_kernel_times(self._plan, ms, n), "kernel_times")
+        return {name: {"ms": ms[i], "launches": n[i]} for i, name in enumerate(_lib.KERNEL_NAMES)}
+
     def partition(self, in_keys, in_values, out_keys, out_values, n: int, shift: int, bits: int,
                   hist=None, stream=None) -> None:
         """Stable one-digit scatter in -> out; hist (device u32[2^bits]) gets digit totals."""
@@ -105,12 +115,22 @@ class SortPlan:
             "rs_plan_partition_records")
 
     def sort_records(self, records, keys_out, values_out, n: int | None = None,
-                     stream=None) -> None:
-        """Stable sort of n (key, value) records into separate key / value arrays."""
+                     stream=None, key_range=None) -> None:
+        """Stable sort of n (key, value) records into separate key / value arrays.  key_range:
+        (lo, hi) with every key in [lo, hi] (rs_plan_sort_records_range: a hint, checked on the
+        device)."""
         n = records.numel() if n is None else n
-        check(_lib.load().rs_plan_sort_records(self._plan, records.data_ptr(), keys_out.data_ptr(),
-                                               values_out.data_ptr(), n, _stream(records, stream)),
-              "rs_plan_sort_records")
+        L = _lib.load()
+        if key_range is None:
+            check(L.rs_plan_sort_records(self._plan, records.data_ptr(), keys_out.data_ptr(),
+                                         values_out.data_ptr(), n, _stream(records, stream)),
+                  "rs_plan_sort_records")
+        else:
+            lo, hi = (int(x) for x in key_range)
+            check(L.rs_plan_sort_records_range(self._plan, records.data_ptr(), keys_out.data_ptr(),
+                                               values_out.data_ptr(), n, lo, hi,
+                                               _stream(records, stream)),
+                  "rs_plan_sort_records_range")
 
     def destroy(self) -> None:
         if getattr(self, "_plan", None):

@@ -13,7 +13,8 @@ A step = one full sort of one batch of synthetic input resident in HBM:
 * N > 1 (torch.distributed.run, one process per GPU, RCCL): BASELINE configs[4] shape with
   2^28 keys+values per rank (2^31 at 8 GPUs): histogram all_gather -> stable top-byte partition
   into (key, value) records -> 4 rounds of batched RCCL point-to-point record messages over
-  xGMI (bucket groups), each group sorted locally (LSD) while the later rounds are in flight.
+  xGMI (bucket groups), each group sorted locally while the later rounds are in flight (the
+  hybrid MSD path over the group's key range, rs_plan_sort_records_range).
   Weak scaling.
 
 Rank 0 prints ONE JSON line.  `value` = keys sorted by all ranks / max-over-ranks wall time.
@@ -411,8 +412,10 @@ def main() -> None:
     if use_dist and hist:
         hist_reads = 1   # one totals read per group sort: each key once per step
     if msd:
-        passes = 3       # MSD pass 0, MSD pass 1, bucket pass; key reads: top-byte totals, hist16
-        hist_reads = 2
+        # MSD pass 0, MSD pass 1, bucket pass; one read of the input for the 16-bit histogram
+        # (4 B/key arrays; records are read whole: 8 B/key = two 4-byte key reads)
+        passes = 3
+        hist_reads = 2 if wl.get("layout") == "aos" else 1
     sort_bytes = keys_per_step / max(world, 1) * (passes * (8 + 8 * (1 if wl["values"] else 0))
                                                   + 4 * hist_reads)
     extra["digit_count_reads_per_sort"] = hist_reads

@@ -108,6 +108,52 @@ static void copy_and_records(size_t n) {
     for (void* q : {ik, iv, ok, ov, rec}) OK(rs_free(q));
 }
 
+// records -> arrays with a key-range hint (the group sorts' form; hybrid MSD path over the range),
+// a wrong hint (one key outside: the device falls back), and the texture layout in place
+static void range_and_texture(size_t n) {
+    const uint32_t lo = 0x30000000u, hi = 0x37FFFFFFu;
+    std::vector<uint32_t> hk(n), hr(2 * n);
+    for (size_t i = 0; i < n; ++i) {
+        hk[i] = lo + (mix(i + 77) & (hi - lo));
+        hr[2 * i] = hk[i];
+        hr[2 * i + 1] = (uint32_t)i;
+    }
+    void *rec, *ok, *ov;
+    OK(rs_malloc(0, 8 * n, &rec));
+    OK(rs_malloc(0, 4 * n, &ok));
+    OK(rs_malloc(0, 4 * n, &ov));
+    rs_plan_desc d{};
+    d.count = n;
+    d.flags = RS_FLAG_HAS_VALUES;
+    rs_plan* p = nullptr;
+    OK(rs_plan_create(&d, &p));
+    std::vector<uint32_t> gk(n), gv(n);
+    for (int wrong = 0; wrong < 2 && p; ++wrong) {
+        if (wrong) { hk[n / 2] = hi + 1; hr[2 * (n / 2)] = hi + 1; }
+        OK(rs_memcpy_h2d(rec, hr.data(), 8 * n, nullptr));
+        OK(rs_plan_sort_records_range(p, rec, ok, ov, n, lo, hi, nullptr));
+        OK(rs_plan_check(p));
+        OK(rs_memcpy_d2h(gk.data(), ok, 4 * n, nullptr));
+        OK(rs_memcpy_d2h(gv.data(), ov, 4 * n, nullptr));
+        CHECK(verify(hk, gk, &gv, n), "sort_records_range n=%zu wrong_hint=%d", n, wrong);
+    }
+    if (p) rs_plan_destroy(p);
+    d.flags = RS_FLAG_INTERLEAVED;
+    p = nullptr;
+    OK(rs_plan_create(&d, &p));
+    if (p) {
+        OK(rs_memcpy_h2d(rec, hr.data(), 8 * n, nullptr));
+        OK(rs_plan_sort(p, rec, nullptr, nullptr));
+        OK(rs_plan_check(p));
+        std::vector<uint32_t> out(2 * n);
+        OK(rs_memcpy_d2h(out.data(), rec, 8 * n, nullptr));
+        for (size_t i = 0; i < n; ++i) { gk[i] = out[2 * i]; gv[i] = out[2 * i + 1]; }
+        CHECK(verify(hk, gk, &gv, n), "texture n=%zu", n);
+        rs_plan_destroy(p);
+    }
+    for (void* q : {rec, ok, ov}) OK(rs_free(q));
+}
+
 static void scan_case(size_t n) {
     std::vector<uint32_t> h(n), out(n);
     for (size_t i = 0; i < n; ++i) h[i] = mix(i) & 0xFF;
@@ -209,6 +255,7 @@ int main() {
     sort_case(13000000, true, RS_FLAG_CHECK_ORDER | RS_FLAG_LOCAL_SHUFFLE, ~0u);
     copy_and_records(70000);
     copy_and_records(13000000);
+    range_and_texture(13000001);
     scan_case(1000);
     scan_case(3000017);
     group_case(1, RS_TRANSPORT_RCCL, true, 200000);

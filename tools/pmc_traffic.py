@@ -4,7 +4,8 @@
 Follows MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE in separate --pmc passes (TCC slots),
 KB units; on gfx950 FETCH_SIZE reports 1/2 of the bytes of a coalesced streaming read, so it is
 doubled.  Both corrections are re-checked in the same run on kernels with a known byte count:
-k_fill_random writes exactly n*4 bytes, k_histogram / k_pass_totals read exactly n*4 bytes.
+k_fill_random writes exactly n*4 bytes, k_histogram / k_pass_totals / k_hist16_in (the hybrid MSD
+path's 16-bit bucket count) read exactly n*4 bytes.
 
     python3 tools/pmc_traffic.py [config3|config2] [out.json]
 
@@ -34,7 +35,8 @@ def run_pass(counter: str, wl: str, outdir: str) -> dict:
             # the pass kernel (k_scatter, or k_onesweep on the one-sweep path) and a kernel that
             # reads exactly the n keys once (k_histogram per pass, or k_pass_totals per sort)
             key = ("scatter" if ("k_scatter" in name or "k_onesweep" in name)
-                   else "histogram" if ("k_histogram" in name or "k_pass_totals" in name)
+                   else "histogram" if ("k_histogram" in name or "k_pass_totals" in name
+                                        or "k_hist16_in" in name)
                    else "bucket" if "k_bucket_sort" in name
                    else "fill_random" if "k_fill_random" in name else "scan" if "k_scan_rows" in name
                    else None)

@@ -214,3 +214,78 @@ def test_msd_group_regions_use_key_range():
         assert np.array_equal(np.concatenate([o[1].cpu().numpy().view(np.uint32) for o in out]), ev)
     finally:
         g.destroy()
+
+
+# ---- keys only (BASELINE config2's shape): R1 = the plan's key copy, R2 = the caller's keys ----
+
+def _sort_keys_and_check(n, kind, seed=21, copy=False, count=None):
+    """Keys-only hybrid MSD path (>= 16M keys: the histogram rows live in the plan's key copy);
+    `count` < n leaves the tail untouched.  Expected: the oracle's stable sort of the keys."""
+    count = n if count is None else count
+    k = _keys(n, kind, seed)
+    kin = k.clone()
+    kern = RadixSortKernel(keys=k, count=count, bit_count=32)
+    kern.set_profiling(True)
+    if copy:
+        from radix_sort_amd.ops import SortPlan
+        plan = SortPlan(0, count, False)
+        out = torch.full_like(k, -1)
+        plan.sort_copy(kin, None, out, None, count)
+        torch.cuda.synchronize()
+        plan.check()
+        got = out
+        plan.destroy()
+    else:
+        kern.dispatch()
+        torch.cuda.synchronize()
+        kern.check()
+        got = k
+    times = kern.kernel_times()
+    src = kin.cpu().numpy().view(np.uint32)
+    ek, _ = O.stable_sort_masked_c(src[:count].copy(), np.arange(count, dtype=np.uint32), 32)
+    g = got.cpu().numpy().view(np.uint32)
+    assert np.array_equal(g[:count], ek)
+    if not copy:
+        assert np.array_equal(g[count:], src[count:])
+    kern.destroy()
+    return times
+
+
+@pytest.mark.parametrize("n", [(1 << 24) + 4096, (1 << 25) + 12345, 1 << 26])
+def test_msd_keys_uniform_matches_oracle(n):
+    t = _sort_keys_and_check(n, "uniform")
+    # the MSD path ran: two one-sweep passes and the bucket pass; the gated LSD launches are short
+    assert t["bucket"]["launches"] == 1 and t["scatter"]["launches"] == 2
+    assert t["fallback"]["ms"] < t["bucket"]["ms"]
+
+
+@pytest.mark.parametrize("kind", ["top0", "low0"])
+def test_msd_keys_device_fallbacks(kind):
+    t = _sort_keys_and_check((1 << 24) + 4096, kind)
+    assert t["fallback"]["ms"] > 5 * t["bucket"]["ms"]
+
+
+@pytest.mark.parametrize("kind", ["dups", "few_big"])
+def test_msd_keys_duplicates_and_overflow_buckets(kind):
+    _sort_keys_and_check((1 << 24) + 4096, kind)
+
+
+def test_msd_keys_out_of_place_partial_count_and_ballot(monkeypatch):
+    _sort_keys_and_check((1 << 24) + 4099, "uniform", copy=True)
+    _sort_keys_and_check((1 << 25) + 3, "uniform", count=(1 << 24) + 5000)
+    monkeypatch.setenv("RSORT_RANK", "ballot")
+    _sort_keys_and_check((1 << 24) + 4096, "dups")
+
+
+@pytest.mark.parametrize("n", [(12 << 20) + 9, 1 << 24])
+def test_msd_keys_below_row_capacity_keeps_lsd(n):
+    # the 256 histogram rows of 65536 counts and their 256 flag words do not fit the key copy
+    # (n < 256 * 65537 on a 256-CU device): the histogram-path LSD sort
+    t = _sort_keys_and_check(n, "uniform")
+    assert t["bucket"]["launches"] == 0 and t["fallback"]["launches"] == 0
+
+
+def test_msd_keys_wide_tile_config(monkeypatch):
+    monkeypatch.setenv("RSORT_MSD_KEYS_CFG", "0")   # 1024 x 16 pass tiles instead of 512 x 32
+    t = _sort_keys_and_check(1 << 25, "uniform")
+    assert t["scatter"]["launches"] == 2

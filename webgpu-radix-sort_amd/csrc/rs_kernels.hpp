@@ -1463,8 +1463,11 @@ __global__ __launch_bounds__(1024) void k_msd_plan(const uint32_t* __restrict__ 
 // bucket exceeds the large tile.
 // LO: output layout (LAYOUT_SOA: the caller's two arrays; LAYOUT_AOS: records - the texture
 // layout, sorted in place: R2 is then the caller's buffer itself, and every workgroup has read its
-// whole bucket before it writes the same range).
-template <int BLOCK, int KPT, int RANK, int LO = LAYOUT_SOA, int MW = 1>
+// whole bucket before it writes the same range; LAYOUT_KEYS: keys only, in place as well - `rec`
+// is then a key array, R2 the caller's keys).
+// PF = 1: the next bucket's keys are loaded before the current bucket is sorted (a persistent grid;
+// keys only, where a bucket is a few KB and a workgroup's load latency is not hidden otherwise).
+template <int BLOCK, int KPT, int RANK, int LO = LAYOUT_SOA, int MW = 1, int PF = 0>
 __global__ __launch_bounds__(BLOCK, MW) void k_bucket_sort(const uint32_t* rec,
                                                        const uint32_t* __restrict__ hist16,
                                                        const uint32_t* __restrict__ base16,
@@ -1478,10 +1481,13 @@ __global__ __launch_bounds__(BLOCK, MW) void k_bucket_sort(const uint32_t* rec,
     constexpr int NW = BLOCK / 64;
     constexpr int TILE = BLOCK * KPT;
     constexpr int WAVE_KEYS = 64 * KPT;
+    constexpr bool KV = LO != LAYOUT_KEYS;
+    constexpr int LI = KV ? LAYOUT_AOS : LAYOUT_KEYS;   // R2: records, or keys
     static_assert(BLOCK >= RADIX, "one digit per thread in the scan");
     __shared__ uint32_t s_whist[NW][RADIX];
     __shared__ uint32_t s_scratch[NW];
-    __shared__ uint2 s_kv[TILE];
+    __shared__ uint2 s_kv[KV ? TILE : 1];
+    __shared__ uint32_t s_k[KV ? 1 : TILE];
     if (gated_off(gate, 0)) return;
     const uint32_t tid = threadIdx.x, w = tid >> 6, lane = lane_id();
     const uint32_t wbase = w * WAVE_KEYS;
@@ -1502,13 +1508,19 @@ __global__ __launch_bounds__(BLOCK, MW) void k_bucket_sort(const uint32_t* rec,
     uint32_t cnt = 0;
     uint32_t it = next_valid(blockIdx.x, cnt);
     if (it >= nb) return;
-    uint32_t k[KPT], v[KPT];
-    load_tile<KPT, LAYOUT_AOS>(rec + 2ull * base16[over ? over[1 + it] : it], nullptr, wbase, cnt, false, k, v);
+    uint32_t k[KPT], v[KV ? KPT : 1];
+    uint32_t k2[PF ? KPT : 1], v2[PF && KV ? KPT : 1];
+    load_tile<KPT, LI>(rec + (KV ? 2ull : 1ull) * base16[over ? over[1 + it] : it], nullptr, wbase, cnt, false, k, v);
     while (true) {
         const uint32_t b = over ? over[1 + it] : it;
         const uint32_t base = base16[b];
         uint32_t ncnt = 0;
         const uint32_t nit = next_valid(it + gridDim.x, ncnt);
+        if constexpr (PF != 0) {
+            if (nit < nb)
+                load_tile<KPT, LI>(rec + (KV ? 2ull : 1ull) * base16[over ? over[1 + nit] : nit], nullptr, wbase,
+                                   ncnt, false, k2, v2);
+        }
         if (cnt > 1u) {
             for (uint32_t p = 0, shift = 0; p < 2u; ++p, shift += 8u) {
                 const uint32_t mask = 255u;
@@ -1530,14 +1542,21 @@ __global__ __launch_bounds__(BLOCK, MW) void k_bucket_sort(const uint32_t* rec,
                 }
                 __syncthreads();
 #pragma unroll
-                for (int j = 0; j < KPT; ++j)
-                    s_kv[s_whist[w][(k[j] >> shift) & mask] + rank.get(j)] = make_uint2(k[j], v[j]);
+                for (int j = 0; j < KPT; ++j) {
+                    const uint32_t q = s_whist[w][(k[j] >> shift) & mask] + rank.get(j);
+                    if constexpr (KV) s_kv[q] = make_uint2(k[j], v[j]);
+                    else s_k[q] = k[j];
+                }
                 __syncthreads();
 #pragma unroll
                 for (int j = 0; j < KPT; ++j) {
-                    const uint2 kv = s_kv[wbase + j * 64 + lane];
-                    k[j] = kv.x;
-                    v[j] = kv.y;
+                    if constexpr (KV) {
+                        const uint2 kv = s_kv[wbase + j * 64 + lane];
+                        k[j] = kv.x;
+                        v[j] = kv.y;
+                    } else {
+                        k[j] = s_k[wbase + j * 64 + lane];
+                    }
                 }
                 __syncthreads();
             }
@@ -1547,8 +1566,10 @@ __global__ __launch_bounds__(BLOCK, MW) void k_bucket_sort(const uint32_t* rec,
         for (int j = 0; j < KPT; ++j) {
             const uint32_t p2 = wbase + j * 64 + lane;
             if (p2 < cnt) {
-                if (LO == LAYOUT_AOS) {
+                if constexpr (LO == LAYOUT_AOS) {
                     reinterpret_cast<uint2*>(out_k)[(size_t)base + p2] = make_uint2(k[j] + kbase, v[j]);
+                } else if constexpr (LO == LAYOUT_KEYS) {
+                    out_k[(size_t)base + p2] = k[j] + kbase;
                 } else {
                     out_k[(size_t)base + p2] = k[j] + kbase;
                     out_v[(size_t)base + p2] = v[j];
@@ -1559,7 +1580,74 @@ __global__ __launch_bounds__(BLOCK, MW) void k_bucket_sort(const uint32_t* rec,
         it = nit;
         cnt = ncnt;
         __syncthreads();   // s_whist / s_kv are reused
-        load_tile<KPT, LAYOUT_AOS>(rec + 2ull * base16[over ? over[1 + it] : it], nullptr, wbase, cnt, false, k, v);
+        if constexpr (PF != 0) {
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) {
+                k[j] = k2[j];
+                if constexpr (KV) v[j] = v2[j];
+            }
+        } else {
+            load_tile<KPT, LI>(rec + (KV ? 2ull : 1ull) * base16[over ? over[1 + it] : it], nullptr, wbase, cnt, false, k, v);
+        }
+    }
+}
+
+// Keys-only bucket pass with one WAVE per 16-bit bucket (buckets of at most 64 * KPT keys, sorted in
+// place): at ~1K keys per bucket (64M keys) a workgroup per bucket spends its time in barriers and
+// load latency, so here every wave sorts its own bucket in wave-private LDS (counters + staging)
+// with no workgroup barrier at all - one wave's LDS operations execute in order - and a CU holds
+// ~28 buckets in flight.  Two stable 8-bit passes (low byte, then the next), pads (kPadKey) after
+// every real key.  Buckets of more than 64 * KPT keys are listed by k_msd_plan for the large-tile
+// launch; empty and one-key buckets are skipped.
+template <int KPT, int RANK, int WPB>
+__global__ __launch_bounds__(64 * WPB) void k_bucket_sort_keys_wave(uint32_t* keys,
+                                                                 const uint32_t* __restrict__ hist16,
+                                                                 const uint32_t* __restrict__ base16,
+                                                                 const uint32_t* gate) {
+    constexpr uint32_t CAP = 64u * KPT;
+    __shared__ uint32_t s_h[WPB][256];
+    __shared__ uint32_t s_k[WPB][CAP];
+    if (gated_off(gate, 0)) return;
+    const uint32_t w = threadIdx.x >> 6, lane = lane_id();
+    uint32_t* h = s_h[w];
+    uint32_t* sk = s_k[w];
+    auto wave_sync = [] { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); __builtin_amdgcn_wave_barrier(); };
+    for (uint32_t b = blockIdx.x * WPB + w; b < 65536u; b += gridDim.x * WPB) {
+        const uint32_t cnt = hist16[b];
+        if (cnt <= 1u || cnt > CAP) continue;
+        uint32_t* src = keys + base16[b];
+        uint32_t k[KPT];
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) {
+            const uint32_t q = (uint32_t)j * 64u + lane;
+            k[j] = q < cnt ? src[q] : kPadKey;
+        }
+#pragma unroll 1
+        for (uint32_t shift = 0; shift < 16u; shift += 8u) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) h[lane * 4 + i] = 0u;
+            wave_sync();
+            Slots<KPT, false> rank;
+            rank_slots<8, KPT, RANK>(k, rank, h, shift, 255u);
+            wave_sync();
+            // exclusive scan of the 256 counters: lane l owns digits 4l .. 4l + 3
+            const uint4 c = *reinterpret_cast<const uint4*>(h + lane * 4);
+            const uint32_t sum = c.x + c.y + c.z + c.w;
+            const uint32_t ex = wave_incl_scan(sum) - sum;
+            *reinterpret_cast<uint4*>(h + lane * 4) = make_uint4(ex, ex + c.x, ex + c.x + c.y, ex + c.x + c.y + c.z);
+            wave_sync();
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) sk[h[(k[j] >> shift) & 255u] + rank.get(j)] = k[j];
+            wave_sync();
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) k[j] = sk[(uint32_t)j * 64u + lane];
+            wave_sync();
+        }
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) {
+            const uint32_t q = (uint32_t)j * 64u + lane;
+            if (q < cnt) src[q] = k[j];
+        }
     }
 }
 

@@ -326,22 +326,24 @@ rs_status next_epoch(rs_plan* p, hipStream_t s) {
 
 // One pass of the hybrid MSD path (16K-record tiles, 8-bit digit at `shift`): SEG = 0 the
 // top-byte pass over the whole input, SEG = 1 the next-byte pass inside every top-byte segment.
-template <int L, int LO, int SEG, bool KB = false>
+// BLOCK x KPT = 16K keys (kLarge; keys only: kLargeKeys, two workgroups per CU).
+template <int L, int LO, int SEG, bool KB = false, int BLOCK = kLarge.block, int KPT = kLarge.kpt>
 void launch_msd_pass(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint32_t* ok, uint32_t* ov,
                      uint32_t n, uint32_t shift, uint32_t ntiles, const uint32_t* dtot, uint32_t* ticket,
                      const uint32_t* gate, const uint32_t* segtab, const uint32_t* base16,
                      hipStream_t s, uint32_t kbase = 0) {
+    static_assert(BLOCK * KPT == kLarge.tile, "k_msd_plan lays out kLarge tiles");
     auto go = [&](auto kern) {
-        static const uint32_t per_cu = resident_per_cu(kern, kLarge.block);
+        static const uint32_t per_cu = resident_per_cu(kern, BLOCK);
         const uint32_t grid = std::min<uint32_t>(ntiles, p->cus * per_cu);
-        hipLaunchKernelGGL(kern, dim3(grid), dim3(kLarge.block), 0, s, ik, iv, ok, ov, n, shift, 255u,
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(BLOCK), 0, s, ik, iv, ok, ov, n, shift, 255u,
                            ntiles, dtot, p->status, ticket, p->tickets + 16, nullptr, 0u, 0u, p->epoch,
                            gate, 0, nullptr, 0xFFFFFFFFu, p->spin_max, p->host_err_dev, segtab, base16, kbase);
     };
     if (p->rank_mode == rs::RANK_BALLOT)
-        go(rs::k_onesweep<8, kLarge.block, kLarge.kpt, L, rs::RANK_BALLOT, LO, 1, SEG, KB>);
+        go(rs::k_onesweep<8, BLOCK, KPT, L, rs::RANK_BALLOT, LO, 1, SEG, KB>);
     else
-        go(rs::k_onesweep<8, kLarge.block, kLarge.kpt, L, rs::RANK_LDS_ATOMIC, LO, 1, SEG, KB>);
+        go(rs::k_onesweep<8, BLOCK, KPT, L, rs::RANK_LDS_ATOMIC, LO, 1, SEG, KB>);
 }
 
 // Layout pair of one pass: input layout | output layout << 4 (they differ only on the one-sweep
@@ -382,18 +384,20 @@ rs_status run_pass_cfg(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint3
     if constexpr (SR != 1) {
         return fail(RS_ERR_INVALID_ARG, "staging rounds are one-sweep only");
     } else {
-        p->timer.run(RS_KERNEL_HISTOGRAM, s, [&] {
+        // the gated LSD fallback of the hybrid MSD path times all its launches as one kind
+        const bool fb = p->scatter_kind == RS_KERNEL_FALLBACK;
+        p->timer.run(fb ? RS_KERNEL_FALLBACK : RS_KERNEL_HISTOGRAM, s, [&] {
             launch_histogram<R, TILE>(L, ik, n, shift, mask, ntiles, p->counts, gate, pass, s);
         });
         HIP_TRY(hipGetLastError());
-        p->timer.run(RS_KERNEL_SCAN, s, [&] {
+        p->timer.run(fb ? RS_KERNEL_FALLBACK : RS_KERNEL_SCAN, s, [&] {
             hipLaunchKernelGGL(rs::k_scan_rows, dim3(1u << R), dim3(rs::kBlock), 0, s, p->counts,
                                ntiles, p->totals, gate, pass);
         });
         HIP_TRY(hipGetLastError());
         // The scatter always stages the tile through LDS (the local shuffle,
         // RadixSortLocalShuffle.ts:94-116): it is what makes the writes coalesced.
-        p->timer.run(RS_KERNEL_SCATTER, s, [&] {
+        p->timer.run(fb ? RS_KERNEL_FALLBACK : RS_KERNEL_SCATTER, s, [&] {
             if constexpr (KEYS_ONLY)
                 launch_scatter_l<R, BLOCK, KPT, rs::LAYOUT_KEYS>(p->rank_mode, ik, iv, ok, ov, n, shift, mask,
                                                                  ntiles, grid, p->counts, p->totals, gate, pass, s);
@@ -479,11 +483,16 @@ bool use_onesweep(const rs_plan* p, uint64_t n) {
 
 // The hybrid MSD path applies (the device still falls back to the LSD passes for skewed keys).
 bool use_msd(const rs_plan* p, uint64_t n) {
+    if (!p->msd || p->msd_mode == 0 || p->check_order || p->bit_count != 32 || p->radix_bits != 8 ||
+        use_small_tiles(n) || n < kMsdMin)
+        return false;
+    // keys only: R1 = tmp_k (n words, which first holds the histogram rows), R2 = the caller's keys;
+    // the one-sweep passes of this path are its own (the keys-only LSD sort keeps the histogram path)
+    if (p->layout == rs::LAYOUT_KEYS)
+        return p->onesweep_mode != 0 && (uint64_t)p->cus * 65537ull <= n;   // rows + their flag words
     const bool bufs = (p->layout == rs::LAYOUT_AOS || (p->layout == rs::LAYOUT_SOA && p->tmp2 && p->aos_tmp)) &&
                       (uint64_t)p->cus * 65536ull <= 2ull * n;   // the histogram rows fit in tmp_k
-    return p->msd && p->msd_mode != 0 && bufs && !p->check_order && p->bit_count == 32 &&
-           p->radix_bits == 8 && use_onesweep(p, n) && !use_small_tiles(n) && n >= kMsdMin &&
-           p->kv_cfg == 0 && !p->huge_tiles;
+    return bufs && use_onesweep(p, n) && p->kv_cfg == 0 && !p->huge_tiles;
 }
 
 // Lane-order self-test of the device's LDS atomics (k_lane_order_selftest), once per device
@@ -645,8 +654,9 @@ RS_EXPORT rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out) {
         (e = alloc((uint32_t**)&p->status, 8ull * p->status_words)) != hipSuccess)
         return cleanup(fail(e == hipErrorOutOfMemory ? RS_ERR_OUT_OF_MEMORY : RS_ERR_HIP,
                             "rs_plan_create: hipMalloc failed: %s", hipGetErrorString(e)));
-    if (p->msd_mode != 0 && (p->layout == rs::LAYOUT_AOS || (p->layout == rs::LAYOUT_SOA && p->tmp2)) &&
-        d.count >= kMsdMin &&
+    if (p->msd_mode != 0 && d.count >= kMsdMin &&
+        (p->layout == rs::LAYOUT_AOS || p->layout == rs::LAYOUT_KEYS ||
+         (p->layout == rs::LAYOUT_SOA && p->tmp2)) &&
         (e = alloc(&p->msd, 4ull * kMsdWords)) != hipSuccess)
         return cleanup(fail(e == hipErrorOutOfMemory ? RS_ERR_OUT_OF_MEMORY : RS_ERR_HIP,
                             "rs_plan_create: hipMalloc failed: %s", hipGetErrorString(e)));
@@ -719,11 +729,12 @@ static rs_status enqueue_lsd_gated(rs_plan* p, const uint32_t* sk, const uint32_
 static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t* sv, bool in_aos,
                                   uint32_t* uk, uint32_t* uv, bool out_aos, uint64_t n, hipStream_t s,
                                   uint32_t kbase = 0, uint32_t vbits = 32) {
-    constexpr int A = rs::LAYOUT_AOS, S = rs::LAYOUT_SOA;
+    constexpr int A = rs::LAYOUT_AOS, S = rs::LAYOUT_SOA, K = rs::LAYOUT_KEYS;
+    const bool keys = p->layout == rs::LAYOUT_KEYS;   // keys only: R1 = tmp_k, R2 = the caller's keys
     const uint32_t n32 = (uint32_t)n;
     const uint32_t range = vbits >= 32 ? 0xFFFFFFFFu : (1u << vbits) - 1u;
     uint32_t* r1 = p->tmp_k;
-    uint32_t* r2 = out_aos ? uk : p->tmp2;
+    uint32_t* r2 = (out_aos || keys) ? uk : p->tmp2;
     uint32_t* hist16 = p->msd;
     uint32_t* base16 = hist16 + 65536;
     uint32_t* segtab = base16 + 65536;
@@ -735,15 +746,18 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
     HIP_TRY(hipMemsetAsync(p->ptot, 0, 4ull * (rs::kTotalsMax + 32), s));
     // one histogram row per CU in tmp_k (R1 is written only after the rows are added)
     uint32_t* range_bad = mtot;
+    // RSORT_HIST16_DIV: one row per `div` CUs (fewer rows to write and add; sweeps)
+    static const uint32_t hdiv = [] { const char* e = getenv("RSORT_HIST16_DIV"); return e ? std::max(1, atoi(e)) : 1; }();
+    const uint32_t hrows = std::max(1u, p->cus / hdiv);
     p->timer.run(RS_KERNEL_HISTOGRAM, s, [&] {
         if (in_aos)
-            hipLaunchKernelGGL(rs::k_hist16_in<A>, dim3(p->cus), dim3(1024), 0, s, sk, n32, p->tmp_k, kbase,
+            hipLaunchKernelGGL(rs::k_hist16_in<A>, dim3(hrows), dim3(1024), 0, s, sk, n32, p->tmp_k, kbase,
                                range, vbits - 16);
         else
-            hipLaunchKernelGGL(rs::k_hist16_in<S>, dim3(p->cus), dim3(1024), 0, s, sk, n32, p->tmp_k, kbase,
+            hipLaunchKernelGGL(rs::k_hist16_in<S>, dim3(hrows), dim3(1024), 0, s, sk, n32, p->tmp_k, kbase,
                                range, vbits - 16);
         hipLaunchKernelGGL(rs::k_hist16_reduce, dim3(256), dim3(1024), 0, s, (const uint32_t*)p->tmp_k,
-                           (uint32_t)p->cus, hist16, top_tot, range_bad);
+                           hrows, hist16, top_tot, range_bad);
     });
     HIP_TRY(hipGetLastError());
     // 16-bit buckets: a tile sized to the mean bucket + 4 sigma of a uniform population takes
@@ -754,9 +768,19 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
     const uint32_t want = (uint32_t)(mean * slack + 4.0 * std::sqrt(mean));
     constexpr uint32_t bb = 256;
     static const uint32_t kpts[] = {4, 8, 12, 17, 18, 24};
+    static const uint32_t kpts_keys[] = {4, 5, 9, 17, 24, 0};   // 64M keys: 1280-key tiles
     uint32_t small_cap = 0, small_kpt = 0;
-    for (uint32_t kpt : kpts)
-        if (!small_cap && want <= bb * kpt) { small_cap = bb * kpt; small_kpt = kpt; }
+    for (uint32_t kpt : keys ? kpts_keys : kpts)
+        if (kpt && !small_cap && want <= bb * kpt) { small_cap = bb * kpt; small_kpt = kpt; }
+    // keys only, buckets of up to ~1K keys (<= ~80M keys): one wave per bucket
+    // (k_bucket_sort_keys_wave, 64 x wave_kpt keys; RSORT_KBUCKET_WAVE=0 keeps the workgroup kernel)
+    static const bool wave_ok = [] { const char* e = getenv("RSORT_KBUCKET_WAVE"); return !e || strcmp(e, "0") != 0; }();
+    uint32_t wave_kpt = 0;
+    if (keys && wave_ok) {
+        for (uint32_t kpt : {10u, 18u})
+            if (!wave_kpt && want <= 64u * kpt) wave_kpt = kpt;
+        if (wave_kpt) small_cap = 64u * wave_kpt;
+    }
     p->timer.run(RS_KERNEL_SCAN, s, [&] {
         hipLaunchKernelGGL(rs::k_msd_plan<kLarge.tile>, dim3(1), dim3(1024), 0, s, (const uint32_t*)hist16,
                            (const uint32_t*)top_tot, base16, segtab, kBucketCap, small_cap, kMsdMaxTop, over,
@@ -766,8 +790,16 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
     const uint32_t* g_msd = gates + rs::kGateMsd;
     // MSD pass 0: input -> R1 records, partitioned by the top byte
     if (rs_status st = next_epoch(p, s)) return st;
+    static const bool keys_wide = [] { const char* e = getenv("RSORT_MSD_KEYS_CFG"); return e && strcmp(e, "0") == 0; }();
     p->timer.run(RS_KERNEL_SCATTER, s, [&] {
-        if (in_aos && kbase)
+        if (keys && keys_wide)
+            launch_msd_pass<K, K, 0>(p, sk, nullptr, r1, nullptr, n32, vbits - 8, ntiles, top_tot, p->tickets + 4,
+                                     g_msd, nullptr, nullptr, s);
+        else if (keys)
+            launch_msd_pass<K, K, 0, false, kLargeKeys.block, kLargeKeys.kpt>(
+                p, sk, nullptr, r1, nullptr, n32, vbits - 8, ntiles, top_tot, p->tickets + 4, g_msd, nullptr,
+                nullptr, s);
+        else if (in_aos && kbase)
             launch_msd_pass<A, A, 0, true>(p, sk, nullptr, r1, nullptr, n32, vbits - 8, ntiles, top_tot,
                                            p->tickets + 4, g_msd, nullptr, nullptr, s, kbase);
         else if (in_aos)
@@ -784,8 +816,16 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
     // MSD pass 1: R1 -> R2 records, by the next byte inside every top-byte segment
     if (rs_status st = next_epoch(p, s)) return st;
     p->timer.run(RS_KERNEL_SCATTER, s, [&] {
-        launch_msd_pass<A, A, 1>(p, r1, nullptr, r2, nullptr, n32, vbits - 16, ntiles + 257, nullptr,
-                                 p->tickets + 5, g_msd, segtab, base16, s);
+        if (keys && keys_wide)
+            launch_msd_pass<K, K, 1>(p, r1, nullptr, r2, nullptr, n32, vbits - 16, ntiles + 257, nullptr,
+                                     p->tickets + 5, g_msd, segtab, base16, s);
+        else if (keys)
+            launch_msd_pass<K, K, 1, false, kLargeKeys.block, kLargeKeys.kpt>(
+                p, r1, nullptr, r2, nullptr, n32, vbits - 16, ntiles + 257, nullptr, p->tickets + 5, g_msd,
+                segtab, base16, s);
+        else
+            launch_msd_pass<A, A, 1>(p, r1, nullptr, r2, nullptr, n32, vbits - 16, ntiles + 257, nullptr,
+                                     p->tickets + 5, g_msd, segtab, base16, s);
     });
     HIP_TRY(hipGetLastError());
     const bool ballot = p->rank_mode == rs::RANK_BALLOT;
@@ -795,6 +835,14 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
             hipLaunchKernelGGL(kern, dim3(65536), dim3(bb), 0, s, r2, hist16, base16, uk, uv, g_msd,
                                p->tickets + 16, 0u, (const uint32_t*)nullptr, kbase);
         };
+        // keys only: a persistent grid whose workgroups load their next bucket while sorting one
+        auto small_pf = [&](auto kern) {
+            static const uint32_t per_cu = resident_per_cu(kern, bb);
+            static const uint32_t mult = [] { const char* e = getenv("RSORT_KBUCKET_GRID"); return e ? (uint32_t)atoi(e) : 1u; }();
+            const uint32_t grid = std::min<uint32_t>(65536u, p->cus * per_cu * std::max(1u, mult));
+            hipLaunchKernelGGL(kern, dim3(grid), dim3(bb), 0, s, r2, hist16, base16, uk, uv, g_msd,
+                               p->tickets + 16, 0u, (const uint32_t*)nullptr, kbase);
+        };
         auto large = [&](auto kern) {
             hipLaunchKernelGGL(kern, dim3(256), dim3(kBucketBlock), 0, s, r2, hist16, base16, uk, uv, g_msd,
                                p->tickets + 16, small_cap, (const uint32_t*)over, kbase);
@@ -802,16 +850,46 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
         auto both = [&](auto lo) {
             constexpr int LO = decltype(lo)::value;
 #define RS_BK(KP) case KP: ballot ? small(rs::k_bucket_sort<bb, KP, B0, LO, (KP <= 18 ? 3 : 1)>) : small(rs::k_bucket_sort<bb, KP, A0, LO, (KP <= 18 ? 3 : 1)>); break;
-            switch (small_kpt) {
-                RS_BK(4) RS_BK(8) RS_BK(12) RS_BK(17) RS_BK(18) RS_BK(24)
-                default: break;   // every bucket goes to the listed large-tile launch
+            if constexpr (LO == K) {
+                if (wave_kpt) {
+                    constexpr int WPB = 4;
+                    auto wave = [&](auto kern) {
+                        hipLaunchKernelGGL(kern, dim3(65536 / WPB), dim3(64 * WPB), 0, s, uk, (const uint32_t*)hist16,
+                                           (const uint32_t*)base16, g_msd);
+                    };
+                    if (wave_kpt == 10)
+                        ballot ? wave(rs::k_bucket_sort_keys_wave<10, B0, WPB>) : wave(rs::k_bucket_sort_keys_wave<10, A0, WPB>);
+                    else
+                        ballot ? wave(rs::k_bucket_sort_keys_wave<18, B0, WPB>) : wave(rs::k_bucket_sort_keys_wave<18, A0, WPB>);
+                    small_kpt = 0;   // no workgroup-per-bucket launch
+                }
+                static const bool pf = [] { const char* e = getenv("RSORT_KBUCKET_PF"); return !e || strcmp(e, "0") != 0; }();
+#define RS_BKP(KP) case KP: ballot ? small_pf(rs::k_bucket_sort<bb, KP, B0, LO, 4, 1>) : small_pf(rs::k_bucket_sort<bb, KP, A0, LO, 4, 1>); break;
+                if (pf) {
+                    switch (small_kpt) {
+                        RS_BKP(4) RS_BKP(5) RS_BKP(9) RS_BKP(17) RS_BKP(24)
+                        default: break;
+                    }
+                } else {
+                    switch (small_kpt) {
+                        RS_BK(4) RS_BK(5) RS_BK(9) RS_BK(17) RS_BK(24)
+                        default: break;
+                    }
+                }
+#undef RS_BKP
+            } else {
+                switch (small_kpt) {
+                    RS_BK(4) RS_BK(8) RS_BK(12) RS_BK(17) RS_BK(18) RS_BK(24)
+                    default: break;   // every bucket goes to the listed large-tile launch
+                }
             }
 #undef RS_BK
             // the listed buckets (none for uniform keys): a small persistent grid over the list
             ballot ? large(rs::k_bucket_sort<kBucketBlock, kBucketKpt, B0, LO>)
                    : large(rs::k_bucket_sort<kBucketBlock, kBucketKpt, A0, LO>);
         };
-        if (out_aos) both(std::integral_constant<int, A>{});
+        if (keys) both(std::integral_constant<int, K>{});
+        else if (out_aos) both(std::integral_constant<int, A>{});
         else both(std::integral_constant<int, S>{});
     });
     HIP_TRY(hipGetLastError());
@@ -833,6 +911,17 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
                                (uint32_t*)nullptr, 0xFFFFFFFFu, 0x1u, g_lsd);
     });
     HIP_TRY(hipGetLastError());
+    if (keys) {
+        // keys only: four one-sweep passes input -> tmp_k -> uk -> tmp_k -> uk (5 gated launches;
+        // the keys-only LSD sort's histogram path would be 12)
+        p->scatter_kind = RS_KERNEL_FALLBACK;
+        rs_status st = RS_OK;
+        for (uint32_t i = 0; i < 4 && st == RS_OK; ++i)
+            st = run_pass(p, i == 0 ? sk : ((i & 1) ? p->tmp_k : uk), nullptr, (i & 1) ? uk : p->tmp_k, nullptr,
+                          n32, 8 * i, 8, layout_pair(K, K), g_lsd, (int)i, s, /*onesweep=*/true);
+        p->scatter_kind = RS_KERNEL_SCATTER;
+        return st;
+    }
     if (!out_aos) return enqueue_lsd_gated(p, sk, sv, in_aos, uk, uv, n32, g_lsd, s);
     // records in place: uk -> tmp_k -> uk -> tmp_k -> uk
     p->scatter_kind = RS_KERNEL_FALLBACK;

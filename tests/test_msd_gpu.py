@@ -73,7 +73,7 @@ def test_msd_uniform_matches_oracle(n):
 def test_msd_device_fallbacks(kind):
     t = _sort_and_check(1 << 24, kind)
     # the LSD fallback ran (its passes carry the time), the bucket pass was gated off
-    assert t["fallback"]["ms"] > 5 * t["bucket"]["ms"]
+    assert t["fallback"]["ms"] > 3 * t["bucket"]["ms"]   # a gated-off 65536-workgroup launch still costs ~0.1 ms
 
 
 @pytest.mark.parametrize("kind", ["dups", "few_big"])
@@ -139,7 +139,7 @@ def test_msd_records_uniform_matches_oracle(n):
 def test_msd_records_fallbacks_and_overflow(kind):
     t = _sort_tex_and_check((1 << 24) + 1, kind)
     if kind in ("top0", "low0"):
-        assert t["fallback"]["ms"] > 5 * t["bucket"]["ms"]
+        assert t["fallback"]["ms"] > 3 * t["bucket"]["ms"]   # a gated-off 65536-workgroup launch still costs ~0.1 ms
 
 
 def _records_sort(keys_u32, key_range=None, profile=False):
@@ -194,7 +194,7 @@ def test_msd_records_key_outside_range_falls_back(outside):
     keys = (np.uint32(lo) + (u & np.uint32(0x07FFFFFF))).astype(np.uint32)
     keys[12345] = lo - 1 if outside == "below" else hi + 1     # the hint is wrong for one key
     t = _records_sort(keys, key_range=(lo, hi))
-    assert t["fallback"]["ms"] > 5 * t["bucket"]["ms"]           # the 32-bit LSD passes ran
+    assert t["fallback"]["ms"] > 3 * t["bucket"]["ms"]   # the 32-bit LSD passes ran (a gated-off bucket launch costs ~0.1 ms)
 
 
 def test_msd_group_regions_use_key_range():
@@ -262,7 +262,7 @@ def test_msd_keys_uniform_matches_oracle(n):
 @pytest.mark.parametrize("kind", ["top0", "low0"])
 def test_msd_keys_device_fallbacks(kind):
     t = _sort_keys_and_check((1 << 24) + 4096, kind)
-    assert t["fallback"]["ms"] > 5 * t["bucket"]["ms"]
+    assert t["fallback"]["ms"] > 3 * t["bucket"]["ms"]   # a gated-off 65536-workgroup launch still costs ~0.1 ms
 
 
 @pytest.mark.parametrize("kind", ["dups", "few_big"])
@@ -285,7 +285,10 @@ def test_msd_keys_below_row_capacity_keeps_lsd(n):
     assert t["bucket"]["launches"] == 0 and t["fallback"]["launches"] == 0
 
 
-def test_msd_keys_wide_tile_config(monkeypatch):
-    monkeypatch.setenv("RSORT_MSD_KEYS_CFG", "0")   # 1024 x 16 pass tiles instead of 512 x 32
-    t = _sort_keys_and_check(1 << 25, "uniform")
+@pytest.mark.parametrize("cfg", ["0", "2"])
+def test_msd_keys_pass_tile_configs(monkeypatch, cfg):
+    # the other pass tiles: 1024 x 16 (16K keys) and 1024 x 32 (32K keys), instead of 512 x 32
+    monkeypatch.setenv("RSORT_MSD_KEYS_CFG", cfg)
+    t = _sort_keys_and_check((1 << 25) + 77, "uniform")
     assert t["scatter"]["launches"] == 2
+    _sort_keys_and_check((1 << 24) + 4096, "few_big")

@@ -1599,8 +1599,8 @@ __global__ __launch_bounds__(BLOCK, MW) void k_bucket_sort(const uint32_t* rec,
 // ~28 buckets in flight.  Two stable 8-bit passes (low byte, then the next), pads (kPadKey) after
 // every real key.  Buckets of more than 64 * KPT keys are listed by k_msd_plan for the large-tile
 // launch; empty and one-key buckets are skipped.
-template <int KPT, int RANK, int WPB>
-__global__ __launch_bounds__(64 * WPB) void k_bucket_sort_keys_wave(uint32_t* keys,
+template <int KPT, int RANK, int WPB, int MW = 1>
+__global__ __launch_bounds__(64 * WPB, MW) void k_bucket_sort_keys_wave(uint32_t* keys,
                                                                  const uint32_t* __restrict__ hist16,
                                                                  const uint32_t* __restrict__ base16,
                                                                  const uint32_t* gate) {

@@ -332,7 +332,7 @@ void launch_msd_pass(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint32_
                      uint32_t n, uint32_t shift, uint32_t ntiles, const uint32_t* dtot, uint32_t* ticket,
                      const uint32_t* gate, const uint32_t* segtab, const uint32_t* base16,
                      hipStream_t s, uint32_t kbase = 0) {
-    static_assert(BLOCK * KPT == kLarge.tile, "k_msd_plan lays out kLarge tiles");
+    static_assert(BLOCK * KPT == kLarge.tile || BLOCK * KPT == 2 * kLarge.tile, "k_msd_plan tile sizes");
     auto go = [&](auto kern) {
         static const uint32_t per_cu = resident_per_cu(kern, BLOCK);
         const uint32_t grid = std::min<uint32_t>(ntiles, p->cus * per_cu);
@@ -742,7 +742,11 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
     uint32_t* mtot = gates + 64;
     uint32_t* over = mtot + 1024;
     uint32_t* top_tot = mtot + 768;
-    const uint32_t ntiles = (uint32_t)((n + kLarge.tile - 1) / kLarge.tile);
+    // keys only, pass tile configuration (RSORT_MSD_KEYS_CFG): 0 = 1024 x 16, 1 = 512 x 32 (two
+    // workgroups per CU), 2 = 1024 x 32 (32K-key tiles: 512-B digit runs, as long as a 16K-record tile's)
+    static const int keys_cfg = [] { const char* e = getenv("RSORT_MSD_KEYS_CFG"); return e ? atoi(e) : 1; }();
+    const uint32_t tile = (keys && keys_cfg == 2) ? 2u * kLarge.tile : (uint32_t)kLarge.tile;
+    const uint32_t ntiles = (uint32_t)((n + tile - 1) / tile);
     HIP_TRY(hipMemsetAsync(p->ptot, 0, 4ull * (rs::kTotalsMax + 32), s));
     // one histogram row per CU in tmp_k (R1 is written only after the rows are added)
     uint32_t* range_bad = mtot;
@@ -782,19 +786,26 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
         if (wave_kpt) small_cap = 64u * wave_kpt;
     }
     p->timer.run(RS_KERNEL_SCAN, s, [&] {
-        hipLaunchKernelGGL(rs::k_msd_plan<kLarge.tile>, dim3(1), dim3(1024), 0, s, (const uint32_t*)hist16,
-                           (const uint32_t*)top_tot, base16, segtab, kBucketCap, small_cap, kMsdMaxTop, over,
-                           gates, (const uint32_t*)range_bad);
+        auto plan = [&](auto kern) {
+            hipLaunchKernelGGL(kern, dim3(1), dim3(1024), 0, s, (const uint32_t*)hist16, (const uint32_t*)top_tot,
+                               base16, segtab, kBucketCap, small_cap, kMsdMaxTop, over, gates,
+                               (const uint32_t*)range_bad);
+        };
+        if (tile == 2u * kLarge.tile) plan(rs::k_msd_plan<2 * kLarge.tile>);
+        else plan(rs::k_msd_plan<kLarge.tile>);
     });
     HIP_TRY(hipGetLastError());
     const uint32_t* g_msd = gates + rs::kGateMsd;
     // MSD pass 0: input -> R1 records, partitioned by the top byte
     if (rs_status st = next_epoch(p, s)) return st;
-    static const bool keys_wide = [] { const char* e = getenv("RSORT_MSD_KEYS_CFG"); return e && strcmp(e, "0") == 0; }();
+    const bool keys_wide = keys_cfg == 0;
     p->timer.run(RS_KERNEL_SCATTER, s, [&] {
         if (keys && keys_wide)
             launch_msd_pass<K, K, 0>(p, sk, nullptr, r1, nullptr, n32, vbits - 8, ntiles, top_tot, p->tickets + 4,
                                      g_msd, nullptr, nullptr, s);
+        else if (keys && keys_cfg == 2)
+            launch_msd_pass<K, K, 0, false, 1024, 32>(p, sk, nullptr, r1, nullptr, n32, vbits - 8, ntiles, top_tot,
+                                                      p->tickets + 4, g_msd, nullptr, nullptr, s);
         else if (keys)
             launch_msd_pass<K, K, 0, false, kLargeKeys.block, kLargeKeys.kpt>(
                 p, sk, nullptr, r1, nullptr, n32, vbits - 8, ntiles, top_tot, p->tickets + 4, g_msd, nullptr,
@@ -819,6 +830,9 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
         if (keys && keys_wide)
             launch_msd_pass<K, K, 1>(p, r1, nullptr, r2, nullptr, n32, vbits - 16, ntiles + 257, nullptr,
                                      p->tickets + 5, g_msd, segtab, base16, s);
+        else if (keys && keys_cfg == 2)
+            launch_msd_pass<K, K, 1, false, 1024, 32>(p, r1, nullptr, r2, nullptr, n32, vbits - 16, ntiles + 257,
+                                                      nullptr, p->tickets + 5, g_msd, segtab, base16, s);
         else if (keys)
             launch_msd_pass<K, K, 1, false, kLargeKeys.block, kLargeKeys.kpt>(
                 p, r1, nullptr, r2, nullptr, n32, vbits - 16, ntiles + 257, nullptr, p->tickets + 5, g_msd,
@@ -859,8 +873,16 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
                     };
                     if (wave_kpt == 10)
                         ballot ? wave(rs::k_bucket_sort_keys_wave<10, B0, WPB>) : wave(rs::k_bucket_sort_keys_wave<10, A0, WPB>);
-                    else
-                        ballot ? wave(rs::k_bucket_sort_keys_wave<18, B0, WPB>) : wave(rs::k_bucket_sort_keys_wave<18, A0, WPB>);
+                    else if (ballot)
+                        wave(rs::k_bucket_sort_keys_wave<18, B0, WPB>);
+                    else {
+                        // waves per SIMD the compiler must fit (VGPR budget): RSORT_KWAVE_MW sweeps
+                        static const int mw = [] { const char* e = getenv("RSORT_KWAVE_MW"); return e ? atoi(e) : 1; }();
+                        if (mw == 7) wave(rs::k_bucket_sort_keys_wave<18, A0, WPB, 7>);
+                        else if (mw == 6) wave(rs::k_bucket_sort_keys_wave<18, A0, WPB, 6>);
+                        else if (mw == 5) wave(rs::k_bucket_sort_keys_wave<18, A0, WPB, 5>);
+                        else wave(rs::k_bucket_sort_keys_wave<18, A0, WPB>);
+                    }
                     small_kpt = 0;   // no workgroup-per-bucket launch
                 }
                 static const bool pf = [] { const char* e = getenv("RSORT_KBUCKET_PF"); return !e || strcmp(e, "0") != 0; }();

@@ -9,7 +9,8 @@ A step = one full sort of one batch of synthetic input resident in HBM:
   local_shuffle=true, bit_count 32, one RadixSortKernel.dispatch() per step.  Every step sorts a
   different pre-generated batch (sorting already-sorted data would be a different workload).
   The library takes its hybrid MSD path here: `roofline` is the scatter kernel
-  (k_onesweep, 2 launches per sort), `bucket_pass` the in-LDS bucket kernel.
+  (k_onesweep, 2 launches per sort), `bucket_pass` the in-LDS bucket kernel.  `--workload
+  config2` (64M keys only) takes the keys-only form of the same path (one wave per 16-bit bucket).
 * N > 1 (torch.distributed.run, one process per GPU, RCCL): BASELINE configs[4] shape with
   2^28 keys+values per rank (2^31 at 8 GPUs): histogram all_gather -> stable top-byte partition
   into (key, value) records -> 4 rounds of batched RCCL point-to-point record messages over

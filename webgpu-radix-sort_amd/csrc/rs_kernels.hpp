@@ -1270,16 +1270,18 @@ __device__ __forceinline__ void set_gate(uint32_t* g, uint32_t v) {
 // outside [kbase, kbase + range] sets the workgroup's flag word (rows[gridDim.x * 65536 + block];
 // k_msd_plan then picks the LSD passes over the whole 32-bit keys).  Records load 8 bytes per lane
 // (a receive region is only 8-byte aligned), arrays 16.
-template <int L>
+// AOS_WIDE (records 16-byte aligned): two records per 16-byte load instead of one per 8-byte load.
+template <int L, bool AOS_WIDE = false>
 __global__ __launch_bounds__(1024) void k_hist16_in(const uint32_t* __restrict__ keys, uint32_t n,
                                                      uint32_t* __restrict__ rows, uint32_t kbase,
                                                      uint32_t range, uint32_t shift) {
     constexpr uint32_t B = 1024, W = 32768, PER = W / B;
-    constexpr uint32_t KPL = L == LAYOUT_AOS ? 1u : 4u;          // keys per load
+    constexpr bool NARROW = L == LAYOUT_AOS && !AOS_WIDE;
+    constexpr uint32_t KPL = NARROW ? 1u : (L == LAYOUT_AOS ? 2u : 4u);   // keys per load
     constexpr uint32_t STEPS = 61440u / (B * KPL);                // loads per thread per round
     constexpr uint32_t FLY = 5;                                    // loads in flight
     static_assert(STEPS % FLY == 0, "whole load groups per round");
-    using Vec = typename std::conditional<L == LAYOUT_AOS, uint2, uint4>::type;
+    using Vec = typename std::conditional<NARROW, uint2, uint4>::type;
     __shared__ uint32_t h[W];
     const uint32_t tid = threadIdx.x;
     uint32_t acc[2 * PER];
@@ -1320,7 +1322,8 @@ __global__ __launch_bounds__(1024) void k_hist16_in(const uint32_t* __restrict__
 #pragma unroll
             for (uint32_t u = 0; u < FLY; ++u) {
                 if (base + (uint64_t)(s0 + u) * B + tid < nv) {
-                    if constexpr (L == LAYOUT_AOS) { count(q[u].x); }
+                    if constexpr (NARROW) { count(q[u].x); }
+                    else if constexpr (L == LAYOUT_AOS) { count(q[u].x); count(q[u].z); }
                     else { count(q[u].x); count(q[u].y); count(q[u].z); count(q[u].w); }
                 }
             }

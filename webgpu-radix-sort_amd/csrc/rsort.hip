@@ -754,7 +754,12 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
     static const uint32_t hdiv = [] { const char* e = getenv("RSORT_HIST16_DIV"); return e ? std::max(1, atoi(e)) : 1; }();
     const uint32_t hrows = std::max(1u, p->cus / hdiv);
     p->timer.run(RS_KERNEL_HISTOGRAM, s, [&] {
-        if (in_aos)
+        // 16-byte aligned records: two per load (RSORT_HIST16_NARROW=1 keeps one per 8-byte load)
+        static const bool narrow = [] { const char* e = getenv("RSORT_HIST16_NARROW"); return e && strcmp(e, "1") == 0; }();
+        if (in_aos && !narrow && ((uintptr_t)sk & 15u) == 0)
+            hipLaunchKernelGGL((rs::k_hist16_in<A, true>), dim3(hrows), dim3(1024), 0, s, sk, n32, p->tmp_k, kbase,
+                               range, vbits - 16);
+        else if (in_aos)
             hipLaunchKernelGGL(rs::k_hist16_in<A>, dim3(hrows), dim3(1024), 0, s, sk, n32, p->tmp_k, kbase,
                                range, vbits - 16);
         else

@@ -862,15 +862,27 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
             hipLaunchKernelGGL(kern, dim3(grid), dim3(bb), 0, s, r2, hist16, base16, uk, uv, g_msd,
                                p->tickets + 16, 0u, (const uint32_t*)nullptr, kbase);
         };
+        // RSORT_OVER_GRID: workgroups of the listed-bucket launch (sweeps)
+        static const uint32_t over_grid = [] { const char* e = getenv("RSORT_OVER_GRID"); return e ? (uint32_t)atoi(e) : 256u; }();
         auto large = [&](auto kern) {
-            hipLaunchKernelGGL(kern, dim3(256), dim3(kBucketBlock), 0, s, r2, hist16, base16, uk, uv, g_msd,
-                               p->tickets + 16, small_cap, (const uint32_t*)over, kbase);
+            hipLaunchKernelGGL(kern, dim3(std::max(1u, over_grid)), dim3(kBucketBlock), 0, s, r2, hist16, base16, uk, uv,
+                               g_msd, p->tickets + 16, small_cap, (const uint32_t*)over, kbase);
         };
         auto both = [&](auto lo) {
             constexpr int LO = decltype(lo)::value;
 #define RS_BK(KP) case KP: ballot ? small(rs::k_bucket_sort<bb, KP, B0, LO, (KP <= 18 ? 3 : 1)>) : small(rs::k_bucket_sort<bb, KP, A0, LO, (KP <= 18 ? 3 : 1)>); break;
             if constexpr (LO == K) {
-                if (wave_kpt) {
+                static const int wpb = [] { const char* e = getenv("RSORT_KWAVE_WPB"); return e ? atoi(e) : 4; }();
+                if (wave_kpt && wave_kpt == 18 && !ballot && (wpb == 2 || wpb == 8)) {
+                    // sweep only: 2 or 8 waves (buckets) per workgroup
+                    auto wave = [&](auto kern, int w) {
+                        hipLaunchKernelGGL(kern, dim3(65536 / w), dim3(64 * w), 0, s, uk, (const uint32_t*)hist16,
+                                           (const uint32_t*)base16, g_msd);
+                    };
+                    if (wpb == 2) wave(rs::k_bucket_sort_keys_wave<18, A0, 2>, 2);
+                    else wave(rs::k_bucket_sort_keys_wave<18, A0, 8>, 8);
+                    small_kpt = 0;
+                } else if (wave_kpt) {
                     constexpr int WPB = 4;
                     auto wave = [&](auto kern) {
                         hipLaunchKernelGGL(kern, dim3(65536 / WPB), dim3(64 * WPB), 0, s, uk, (const uint32_t*)hist16,

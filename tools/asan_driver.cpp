@@ -251,6 +251,7 @@ int main() {
         sort_case(n, true, 0, ~0u);
         sort_case(n, false, 0, ~0u);
     }
+    sort_case(17000000, false, 0, ~0u);                            // keys-only hybrid MSD path
     sort_case(20000, true, RS_FLAG_CHECK_ORDER, 0xFFu);          // duplicate-heavy + check_order
     sort_case(13000000, true, RS_FLAG_CHECK_ORDER | RS_FLAG_LOCAL_SHUFFLE, ~0u);
     copy_and_records(70000);

@@ -1271,7 +1271,9 @@ __device__ __forceinline__ void set_gate(uint32_t* g, uint32_t v) {
 // k_msd_plan then picks the LSD passes over the whole 32-bit keys).  Records load 8 bytes per lane
 // (a receive region is only 8-byte aligned), arrays 16.
 // AOS_WIDE (records 16-byte aligned): two records per 16-byte load instead of one per 8-byte load.
-template <int L, bool AOS_WIDE = false>
+// FULL (kbase = 0, the whole 32-bit range, shift = 16): the bucket is key >> 16 and its counter
+// half bit 16, so a key costs ~3 VALU + 1 LDS atomic (the kernel is issue-bound, not HBM-bound).
+template <int L, bool AOS_WIDE = false, bool FULL = false>
 __global__ __launch_bounds__(1024) void k_hist16_in(const uint32_t* __restrict__ keys, uint32_t n,
                                                      uint32_t* __restrict__ rows, uint32_t kbase,
                                                      uint32_t range, uint32_t shift) {
@@ -1294,10 +1296,14 @@ __global__ __launch_bounds__(1024) void k_hist16_in(const uint32_t* __restrict__
     const Vec* v4 = reinterpret_cast<const Vec*>(keys + (L == LAYOUT_AOS ? 2 : 1) * lo);
     bool bad = false;
     auto count = [&](uint32_t key) {
-        const uint32_t rk = key - kbase;
-        bad |= rk > range;
-        const uint32_t b = (rk >> shift) & 0xFFFFu;
-        atomicAdd(&h[b >> 1], 1u << ((b & 1u) << 4));
+        if constexpr (FULL) {
+            atomicAdd(&h[key >> 17], 1u << ((key >> 12) & 16u));
+        } else {
+            const uint32_t rk = key - kbase;
+            bad |= rk > range;
+            const uint32_t b = (rk >> shift) & 0xFFFFu;
+            atomicAdd(&h[b >> 1], 1u << ((b & 1u) << 4));
+        }
     };
     auto flush = [&]() {
         __syncthreads();

@@ -756,15 +756,18 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
     p->timer.run(RS_KERNEL_HISTOGRAM, s, [&] {
         // 16-byte aligned records: two per load (RSORT_HIST16_NARROW=1 keeps one per 8-byte load)
         static const bool narrow = [] { const char* e = getenv("RSORT_HIST16_NARROW"); return e && strcmp(e, "1") == 0; }();
+        // the whole 32-bit range: the specialised counting (RSORT_HIST16_GENERIC=1 keeps the generic one)
+        static const bool generic = [] { const char* e = getenv("RSORT_HIST16_GENERIC"); return e && strcmp(e, "1") == 0; }();
+        const bool full = !generic && kbase == 0u && vbits == 32u;
+        auto go = [&](auto kern) {
+            hipLaunchKernelGGL(kern, dim3(hrows), dim3(1024), 0, s, sk, n32, p->tmp_k, kbase, range, vbits - 16);
+        };
         if (in_aos && !narrow && ((uintptr_t)sk & 15u) == 0)
-            hipLaunchKernelGGL((rs::k_hist16_in<A, true>), dim3(hrows), dim3(1024), 0, s, sk, n32, p->tmp_k, kbase,
-                               range, vbits - 16);
+            full ? go(rs::k_hist16_in<A, true, true>) : go(rs::k_hist16_in<A, true>);
         else if (in_aos)
-            hipLaunchKernelGGL(rs::k_hist16_in<A>, dim3(hrows), dim3(1024), 0, s, sk, n32, p->tmp_k, kbase,
-                               range, vbits - 16);
+            full ? go(rs::k_hist16_in<A, false, true>) : go(rs::k_hist16_in<A>);
         else
-            hipLaunchKernelGGL(rs::k_hist16_in<S>, dim3(hrows), dim3(1024), 0, s, sk, n32, p->tmp_k, kbase,
-                               range, vbits - 16);
+            full ? go(rs::k_hist16_in<S, false, true>) : go(rs::k_hist16_in<S>);
         hipLaunchKernelGGL(rs::k_hist16_reduce, dim3(256), dim3(1024), 0, s, (const uint32_t*)p->tmp_k,
                            hrows, hist16, top_tot, range_bad);
     });

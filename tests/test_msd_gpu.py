@@ -292,3 +292,15 @@ def test_msd_keys_pass_tile_configs(monkeypatch, cfg):
     t = _sort_keys_and_check((1 << 25) + 77, "uniform")
     assert t["scatter"]["launches"] == 2
     _sort_keys_and_check((1 << 24) + 4096, "few_big")
+
+
+@pytest.mark.parametrize("n,env", [((1 << 27) + 5, {}),                                  # 2K-key buckets
+                                   ((1 << 25) + 77, {"RSORT_KBUCKET_WAVE": "0"}),
+                                   ((1 << 25) + 77, {"RSORT_KBUCKET_WAVE": "0", "RSORT_KBUCKET_PF": "1"})])
+def test_msd_keys_workgroup_bucket_kernel(monkeypatch, n, env):
+    # buckets over the wave kernel's 64 x 18 keys (or the wave kernel off): one workgroup per
+    # bucket, in place (and its persistent prefetching variant)
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    t = _sort_keys_and_check(n, "uniform")
+    assert t["bucket"]["launches"] == 1 and t["scatter"]["launches"] == 2

@@ -198,6 +198,10 @@ struct rs_plan {
     uint32_t epoch = 0;            // tag of the last k_onesweep launch's status words
     uint32_t spin_max = 1u << 20;  // look-back wait bound in sleeps (RSORT_SPIN_MAX; tests force 0)
     int msd_mode = RS_MSD_DEFAULT;   // hybrid MSD path for values (RSORT_MSD=0/1)
+    // keys-only form of the hybrid MSD path, read per plan (tests switch them):
+    int msd_keys_cfg = 1;            // pass tiles (RSORT_MSD_KEYS_CFG): 0 1024x16, 1 512x32, 2 1024x32
+    bool kbucket_wave = true;        // one wave per 16-bit bucket (RSORT_KBUCKET_WAVE=0: workgroups)
+    bool kbucket_pf = false;         // workgroup kernel on a persistent prefetching grid (RSORT_KBUCKET_PF=1)
     uint32_t* msd = nullptr;         // its workspace: hist16 | base16 | segtab | gates | mtot
     int scatter_kind = RS_KERNEL_SCATTER;   // timer kind of the pass launches being enqueued
     uint32_t* host_err = nullptr;  // host-mapped error word: set by a timed-out look-back wait,
@@ -601,6 +605,9 @@ RS_EXPORT rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out) {
     if (const char* kc = getenv("RSORT_KV_CFG")) p->kv_cfg = atoi(kc);
     if (const char* fc = getenv("RSORT_FUSED_CHECK")) p->fused_check = strcmp(fc, "0") != 0;
     if (const char* ms = getenv("RSORT_MSD")) p->msd_mode = strcmp(ms, "0") != 0 ? 1 : 0;
+    if (const char* e = getenv("RSORT_MSD_KEYS_CFG")) p->msd_keys_cfg = atoi(e);
+    if (const char* e = getenv("RSORT_KBUCKET_WAVE")) p->kbucket_wave = strcmp(e, "0") != 0;
+    if (const char* e = getenv("RSORT_KBUCKET_PF")) p->kbucket_pf = strcmp(e, "1") == 0;
     if (const char* sm = getenv("RSORT_SPIN_MAX")) p->spin_max = (uint32_t)strtoul(sm, nullptr, 10);
     // Even number of passes so the result lands in the caller's buffers, like the reference's
     // bit_count/2 passes with ping-pong on bit % 4 (AbstractRadixSortKernel.ts:93-107).
@@ -744,7 +751,7 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
     uint32_t* top_tot = mtot + 768;
     // keys only, pass tile configuration (RSORT_MSD_KEYS_CFG): 0 = 1024 x 16, 1 = 512 x 32 (two
     // workgroups per CU), 2 = 1024 x 32 (32K-key tiles: 512-B digit runs, as long as a 16K-record tile's)
-    static const int keys_cfg = [] { const char* e = getenv("RSORT_MSD_KEYS_CFG"); return e ? atoi(e) : 1; }();
+    const int keys_cfg = p->msd_keys_cfg;
     const uint32_t tile = (keys && keys_cfg == 2) ? 2u * kLarge.tile : (uint32_t)kLarge.tile;
     const uint32_t ntiles = (uint32_t)((n + tile - 1) / tile);
     HIP_TRY(hipMemsetAsync(p->ptot, 0, 4ull * (rs::kTotalsMax + 32), s));
@@ -786,7 +793,7 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
         if (kpt && !small_cap && want <= bb * kpt) { small_cap = bb * kpt; small_kpt = kpt; }
     // keys only, buckets of up to ~1K keys (<= ~80M keys): one wave per bucket
     // (k_bucket_sort_keys_wave, 64 x wave_kpt keys; RSORT_KBUCKET_WAVE=0 keeps the workgroup kernel)
-    static const bool wave_ok = [] { const char* e = getenv("RSORT_KBUCKET_WAVE"); return !e || strcmp(e, "0") != 0; }();
+    const bool wave_ok = p->kbucket_wave;
     uint32_t wave_kpt = 0;
     if (keys && wave_ok) {
         for (uint32_t kpt : {10u, 18u})
@@ -905,7 +912,8 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
                     }
                     small_kpt = 0;   // no workgroup-per-bucket launch
                 }
-                static const bool pf = [] { const char* e = getenv("RSORT_KBUCKET_PF"); return !e || strcmp(e, "0") != 0; }();
+                // persistent grid + next-bucket prefetch (RSORT_KBUCKET_PF=1): measured slower, 0.265 vs 0.245 ms
+                const bool pf = p->kbucket_pf;
 #define RS_BKP(KP) case KP: ballot ? small_pf(rs::k_bucket_sort<bb, KP, B0, LO, 4, 1>) : small_pf(rs::k_bucket_sort<bb, KP, A0, LO, 4, 1>); break;
                 if (pf) {
                     switch (small_kpt) {

@@ -1010,7 +1010,7 @@ __global__ __launch_bounds__(BLOCK, pass_min_waves(BLOCK, KPT)) void k_onesweep(
         const bool full = tend - tile0 == (uint32_t)TILE;
         const uint32_t nvalid = tend - tile0;
         const bool first_tile = T == seg_first;   // publishes an inclusive prefix at once
-        if (SG && tid < (uint32_t)RADIX) s_dbase[tid] = base16[(seg << 8) | tid];
+        if (SG && tid < (uint32_t)RADIX) s_dbase[tid] = s_seg[257 + seg] + base16[(seg << 8) | tid];
         if (SR > 1 && L == LAYOUT_AOS && !full) {
             const uint64_t wb = (uint64_t)tile0 + w * WAVE_KEYS + lane_id();
 #pragma unroll
@@ -1276,7 +1276,10 @@ __device__ __forceinline__ void set_gate(uint32_t* g, uint32_t v) {
 template <int L, bool AOS_WIDE = false, bool FULL = false>
 __global__ __launch_bounds__(1024) void k_hist16_in(const uint32_t* __restrict__ keys, uint32_t n,
                                                      uint32_t* __restrict__ rows, uint32_t kbase,
-                                                     uint32_t range, uint32_t shift) {
+                                                     uint32_t range, uint32_t shift,
+                                                     uint32_t* __restrict__ z0, uint32_t* __restrict__ z1) {
+    // z0, z1: the reduction's overflow-bucket count and oversize flag (k_hist16_reduce adds to them)
+    if (blockIdx.x == 0 && threadIdx.x == 0) { *z0 = 0u; *z1 = 0u; }
     constexpr uint32_t B = 1024, W = 32768, PER = W / B;
     constexpr bool NARROW = L == LAYOUT_AOS && !AOS_WIDE;
     constexpr uint32_t KPL = NARROW ? 1u : (L == LAYOUT_AOS ? 2u : 4u);   // keys per load
@@ -1350,10 +1353,18 @@ __global__ __launch_bounds__(1024) void k_hist16_in(const uint32_t* __restrict__
 // hist16 = the sum of nrows rows of 65536 counts; top_tot[t] = the sum of hist16[t << 8 ..] (the
 // top-byte digit totals).  One workgroup per top byte: 64 columns of 4 buckets x 16 row groups
 // (nrows <= 1024).
+// Workgroup t also lays out its top byte's 256 buckets (the plan work that needs every bucket):
+// base16[b] = the bucket's start inside its top-byte segment (consumers add the segment start,
+// segtab[257 + (b >> 8)]), buckets over `small` appended to over[1..] (over[0] counts them, up to
+// kOverMax stored), *big |= a bucket over `cap`.
+constexpr uint32_t kOverMax = 4096;
 __global__ __launch_bounds__(1024) void k_hist16_reduce(const uint32_t* __restrict__ rows, uint32_t nrows,
                                                          uint32_t* __restrict__ hist16,
                                                          uint32_t* __restrict__ top_tot,
-                                                         uint32_t* __restrict__ range_bad) {
+                                                         uint32_t* __restrict__ range_bad,
+                                                         uint32_t* __restrict__ base16, uint32_t small,
+                                                         uint32_t cap, uint32_t* __restrict__ over,
+                                                         uint32_t* __restrict__ big) {
     __shared__ uint4 s_part[16][64];
     const uint32_t tid = threadIdx.x, c = tid & 63u, g = tid >> 6;
     if (blockIdx.x == 0) {   // any key outside the range (the rows' flag words)
@@ -1377,83 +1388,55 @@ __global__ __launch_bounds__(1024) void k_hist16_reduce(const uint32_t* __restri
 #pragma unroll
         for (int j = 1; j < 16; ++j) add(t, s_part[j][tid]);
         reinterpret_cast<uint4*>(hist16)[blockIdx.x * 64u + tid] = t;
-        uint32_t sum = t.x + t.y + t.z + t.w;
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) sum += __shfl_down(sum, off, 64);
-        if (tid == 0) top_tot[blockIdx.x] = sum;
-    }
-}
-
-// One workgroup: base16 = exclusive scan of hist16 (65536 buckets in key order), the segmented
-// tile table of MSD pass 1 (segment = top byte: [257] first tile + total, [256] start, [256]
-// end), and the path: MSD iff every 16-bit bucket fits the bucket tile (cap) and every top-byte
-// bucket holds at most max_top keys, else the LSD passes on the input.
-// Buckets larger than `small` (the population-sized bucket tile) are listed in over[1..]
-// (over[0] = their number; at most kOverMax, else the bucket pass is gated off too).
-constexpr uint32_t kOverMax = 4096;
-template <int TILE>
-__global__ __launch_bounds__(1024) void k_msd_plan(const uint32_t* __restrict__ hist16,
-                                                   const uint32_t* __restrict__ top_tot,
-                                                   uint32_t* __restrict__ base16,
-                                                   uint32_t* __restrict__ segtab, uint32_t cap,
-                                                   uint32_t small, uint32_t max_top,
-                                                   uint32_t* __restrict__ over, uint32_t* gates,
-                                                   const uint32_t* __restrict__ range_bad) {
-    constexpr int NW = 16;
-    __shared__ uint32_t s_scratch[NW];
-    __shared__ uint32_t s_big, s_nover;
-    const uint32_t tid = threadIdx.x;
-    if (tid == 0) { s_big = 0u; s_nover = 0u; }
-    // 64 consecutive buckets per thread, held in registers (16 loads of 16 bytes in flight)
-    uint4 c4[16];
-    const uint4* h4 = reinterpret_cast<const uint4*>(hist16) + tid * 16u;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) c4[j] = h4[j];
-    uint32_t sum = 0, mx = 0;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-        sum += c4[j].x + c4[j].y + c4[j].z + c4[j].w;
-        mx = max(mx, max(max(c4[j].x, c4[j].y), max(c4[j].z, c4[j].w)));
-    }
-    uint32_t total;
-    uint32_t run = block_excl_scan_n<NW>(sum, s_scratch, total);
-    uint4* b4 = reinterpret_cast<uint4*>(base16) + tid * 16u;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-        uint4 o;
-        o.x = run; run += c4[j].x;
-        o.y = run; run += c4[j].y;
-        o.z = run; run += c4[j].z;
-        o.w = run; run += c4[j].w;
-        b4[j] = o;
-    }
-    if (mx > small) {   // list the buckets the population-sized tile cannot take
-        for (uint32_t j = 0; j < 64u; ++j) {
-            const uint32_t c = hist16[tid * 64u + j];
-            if (c > small) {
-                const uint32_t slot = atomicAdd(&s_nover, 1u);
-                if (slot < kOverMax) over[1 + slot] = tid * 64u + j;
+        const uint32_t s4 = t.x + t.y + t.z + t.w;
+        const uint32_t inc = wave_incl_scan(s4);
+        const uint32_t ex = inc - s4;
+        reinterpret_cast<uint4*>(base16)[blockIdx.x * 64u + tid] =
+            make_uint4(ex, ex + t.x, ex + t.x + t.y, ex + t.x + t.y + t.z);
+        if (tid == 63) top_tot[blockIdx.x] = inc;
+        const uint32_t mx = max(max(t.x, t.y), max(t.z, t.w));
+        if (mx > cap) atomicOr(big, 1u);
+        if (mx > small) {
+            const uint32_t c4[4] = {t.x, t.y, t.z, t.w};
+            for (uint32_t j = 0; j < 4u; ++j) {
+                if (c4[j] > small) {
+                    const uint32_t slot = atomicAdd(&over[0], 1u);
+                    if (slot < kOverMax) over[1 + slot] = blockIdx.x * 256u + tid * 4u + j;
+                }
             }
         }
     }
-    if (mx > cap) atomicOr(&s_big, 1u);
-    // segments: tiles of TILE records per top-byte bucket
-    const uint32_t cnt = tid < 256u ? top_tot[tid] : 0u;
-    if (cnt > max_top) atomicOr(&s_big, 1u);
+}
+
+// One workgroup, after k_hist16_reduce: the segmented tile table of MSD pass 1 (segment = top
+// byte: [257] first tile + total, [256] start, [256] end; the starts are what the bucket bases of
+// k_hist16_reduce are relative to) and the path: MSD iff every 16-bit bucket fits the bucket tile
+// (*big == 0), at most kOverMax buckets need the large tile, every top-byte bucket holds at most
+// max_top keys and no key lies outside the range; else the LSD passes on the input.  over[0] is
+// clamped to the stored entries.
+template <int TILE>
+__global__ __launch_bounds__(256) void k_msd_plan(const uint32_t* __restrict__ top_tot,
+                                                  uint32_t* __restrict__ segtab, uint32_t max_top,
+                                                  uint32_t* over, const uint32_t* big, uint32_t* gates,
+                                                  const uint32_t* __restrict__ range_bad) {
+    constexpr int NW = 4;
+    __shared__ uint32_t s_scratch[NW];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t cnt = top_tot[tid];
+    const int any_big = __syncthreads_or(cnt > max_top ? 1 : 0);
     const uint32_t tiles = (cnt + TILE - 1) / TILE;
     uint32_t ttot;
     const uint32_t tbase = block_excl_scan_n<NW>(tiles, s_scratch, ttot);
     uint32_t stot;
     const uint32_t sbase = block_excl_scan_n<NW>(cnt, s_scratch, stot);
-    if (tid < 256u) {
-        segtab[tid] = tbase;
-        segtab[257 + tid] = sbase;
-        segtab[513 + tid] = sbase + cnt;
-    }
+    segtab[tid] = tbase;
+    segtab[257 + tid] = sbase;
+    segtab[513 + tid] = sbase + cnt;
     if (tid == 0) segtab[256] = ttot;
-    __syncthreads();
-    if (tid == 0) over[0] = s_nover < kOverMax ? s_nover : kOverMax;
-    const uint32_t ok = (s_big || s_nover > kOverMax || *range_bad) ? 0u : 1u;
+    const uint32_t nover = over[0];
+    __syncthreads();   // every thread has read over[0]
+    if (tid == 0) over[0] = nover < kOverMax ? nover : kOverMax;
+    const uint32_t ok = (any_big || *big || nover > kOverMax || *range_bad) ? 0u : 1u;
     set_gate(gates + kGateMsd, ok);
     set_gate(gates + kGateLsd, 1u - ok);
 }
@@ -1485,8 +1468,11 @@ __global__ __launch_bounds__(BLOCK, MW) void k_bucket_sort(const uint32_t* rec,
                                                        const uint32_t* gate, uint32_t* err,
                                                        uint32_t min_cnt,
                                                        const uint32_t* __restrict__ over = nullptr,
-                                                       uint32_t kbase = 0) {
+                                                       uint32_t kbase = 0,
+                                                       const uint32_t* __restrict__ sstart = nullptr) {
     constexpr int R = 8, RADIX = 256;
+    // bucket b's first record: its top-byte segment's start + its base inside the segment
+    auto bstart = [&](uint32_t b) { return sstart[b >> 8] + base16[b]; };
     constexpr int NW = BLOCK / 64;
     constexpr int TILE = BLOCK * KPT;
     constexpr int WAVE_KEYS = 64 * KPT;
@@ -1519,15 +1505,15 @@ __global__ __launch_bounds__(BLOCK, MW) void k_bucket_sort(const uint32_t* rec,
     if (it >= nb) return;
     uint32_t k[KPT], v[KV ? KPT : 1];
     uint32_t k2[PF ? KPT : 1], v2[PF && KV ? KPT : 1];
-    load_tile<KPT, LI>(rec + (KV ? 2ull : 1ull) * base16[over ? over[1 + it] : it], nullptr, wbase, cnt, false, k, v);
+    load_tile<KPT, LI>(rec + (KV ? 2ull : 1ull) * bstart(over ? over[1 + it] : it), nullptr, wbase, cnt, false, k, v);
     while (true) {
         const uint32_t b = over ? over[1 + it] : it;
-        const uint32_t base = base16[b];
+        const uint32_t base = bstart(b);
         uint32_t ncnt = 0;
         const uint32_t nit = next_valid(it + gridDim.x, ncnt);
         if constexpr (PF != 0) {
             if (nit < nb)
-                load_tile<KPT, LI>(rec + (KV ? 2ull : 1ull) * base16[over ? over[1 + nit] : nit], nullptr, wbase,
+                load_tile<KPT, LI>(rec + (KV ? 2ull : 1ull) * bstart(over ? over[1 + nit] : nit), nullptr, wbase,
                                    ncnt, false, k2, v2);
         }
         if (cnt > 1u) {
@@ -1596,7 +1582,7 @@ __global__ __launch_bounds__(BLOCK, MW) void k_bucket_sort(const uint32_t* rec,
                 if constexpr (KV) v[j] = v2[j];
             }
         } else {
-            load_tile<KPT, LI>(rec + (KV ? 2ull : 1ull) * base16[over ? over[1 + it] : it], nullptr, wbase, cnt, false, k, v);
+            load_tile<KPT, LI>(rec + (KV ? 2ull : 1ull) * bstart(over ? over[1 + it] : it), nullptr, wbase, cnt, false, k, v);
         }
     }
 }
@@ -1612,7 +1598,8 @@ template <int KPT, int RANK, int WPB, int MW = 1>
 __global__ __launch_bounds__(64 * WPB, MW) void k_bucket_sort_keys_wave(uint32_t* keys,
                                                                  const uint32_t* __restrict__ hist16,
                                                                  const uint32_t* __restrict__ base16,
-                                                                 const uint32_t* gate) {
+                                                                 const uint32_t* gate,
+                                                                 const uint32_t* __restrict__ sstart) {
     constexpr uint32_t CAP = 64u * KPT;
     __shared__ uint32_t s_h[WPB][256];
     __shared__ uint32_t s_k[WPB][CAP];
@@ -1624,7 +1611,7 @@ __global__ __launch_bounds__(64 * WPB, MW) void k_bucket_sort_keys_wave(uint32_t
     for (uint32_t b = blockIdx.x * WPB + w; b < 65536u; b += gridDim.x * WPB) {
         const uint32_t cnt = hist16[b];
         if (cnt <= 1u || cnt > CAP) continue;
-        uint32_t* src = keys + base16[b];
+        uint32_t* src = keys + sstart[b >> 8] + base16[b];
         uint32_t k[KPT];
 #pragma unroll
         for (int j = 0; j < KPT; ++j) {

@@ -749,36 +749,14 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
     uint32_t* mtot = gates + 64;
     uint32_t* over = mtot + 1024;
     uint32_t* top_tot = mtot + 768;
+    uint32_t* big = mtot + 1;          // a 16-bit bucket over the large bucket tile
+    uint32_t* sstart = segtab + 257;   // top-byte segment starts (bucket bases are relative to them)
     // keys only, pass tile configuration (RSORT_MSD_KEYS_CFG): 0 = 1024 x 16, 1 = 512 x 32 (two
     // workgroups per CU), 2 = 1024 x 32 (32K-key tiles: 512-B digit runs, as long as a 16K-record tile's)
     const int keys_cfg = p->msd_keys_cfg;
     const uint32_t tile = (keys && keys_cfg == 2) ? 2u * kLarge.tile : (uint32_t)kLarge.tile;
     const uint32_t ntiles = (uint32_t)((n + tile - 1) / tile);
     HIP_TRY(hipMemsetAsync(p->ptot, 0, 4ull * (rs::kTotalsMax + 32), s));
-    // one histogram row per CU in tmp_k (R1 is written only after the rows are added)
-    uint32_t* range_bad = mtot;
-    // RSORT_HIST16_DIV: one row per `div` CUs (fewer rows to write and add; sweeps)
-    static const uint32_t hdiv = [] { const char* e = getenv("RSORT_HIST16_DIV"); return e ? std::max(1, atoi(e)) : 1; }();
-    const uint32_t hrows = std::max(1u, p->cus / hdiv);
-    p->timer.run(RS_KERNEL_HISTOGRAM, s, [&] {
-        // 16-byte aligned records: two per load (RSORT_HIST16_NARROW=1 keeps one per 8-byte load)
-        static const bool narrow = [] { const char* e = getenv("RSORT_HIST16_NARROW"); return e && strcmp(e, "1") == 0; }();
-        // the whole 32-bit range: the specialised counting (RSORT_HIST16_GENERIC=1 keeps the generic one)
-        static const bool generic = [] { const char* e = getenv("RSORT_HIST16_GENERIC"); return e && strcmp(e, "1") == 0; }();
-        const bool full = !generic && kbase == 0u && vbits == 32u;
-        auto go = [&](auto kern) {
-            hipLaunchKernelGGL(kern, dim3(hrows), dim3(1024), 0, s, sk, n32, p->tmp_k, kbase, range, vbits - 16);
-        };
-        if (in_aos && !narrow && ((uintptr_t)sk & 15u) == 0)
-            full ? go(rs::k_hist16_in<A, true, true>) : go(rs::k_hist16_in<A, true>);
-        else if (in_aos)
-            full ? go(rs::k_hist16_in<A, false, true>) : go(rs::k_hist16_in<A>);
-        else
-            full ? go(rs::k_hist16_in<S, false, true>) : go(rs::k_hist16_in<S>);
-        hipLaunchKernelGGL(rs::k_hist16_reduce, dim3(256), dim3(1024), 0, s, (const uint32_t*)p->tmp_k,
-                           hrows, hist16, top_tot, range_bad);
-    });
-    HIP_TRY(hipGetLastError());
     // 16-bit buckets: a tile sized to the mean bucket + 4 sigma of a uniform population takes
     // every bucket that fits it (at 2^28 keys: 4352 records, ~2 buckets over it), the large tile
     // the listed rest
@@ -800,11 +778,37 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
             if (!wave_kpt && want <= 64u * kpt) wave_kpt = kpt;
         if (wave_kpt) small_cap = 64u * wave_kpt;
     }
+    // one histogram row per CU in tmp_k (R1 is written only after the rows are added)
+    uint32_t* range_bad = mtot;
+    // RSORT_HIST16_DIV: one row per `div` CUs (fewer rows to write and add; sweeps)
+    static const uint32_t hdiv = [] { const char* e = getenv("RSORT_HIST16_DIV"); return e ? std::max(1, atoi(e)) : 1; }();
+    const uint32_t hrows = std::max(1u, p->cus / hdiv);
+    p->timer.run(RS_KERNEL_HISTOGRAM, s, [&] {
+        // 16-byte aligned records: two per load (RSORT_HIST16_NARROW=1 keeps one per 8-byte load)
+        static const bool narrow = [] { const char* e = getenv("RSORT_HIST16_NARROW"); return e && strcmp(e, "1") == 0; }();
+        // the whole 32-bit range: the specialised counting (RSORT_HIST16_GENERIC=1 keeps the generic one)
+        static const bool generic = [] { const char* e = getenv("RSORT_HIST16_GENERIC"); return e && strcmp(e, "1") == 0; }();
+        const bool full = !generic && kbase == 0u && vbits == 32u;
+        auto go = [&](auto kern) {
+            hipLaunchKernelGGL(kern, dim3(hrows), dim3(1024), 0, s, sk, n32, p->tmp_k, kbase, range, vbits - 16,
+                               over, big);
+        };
+        if (in_aos && !narrow && ((uintptr_t)sk & 15u) == 0)
+            full ? go(rs::k_hist16_in<A, true, true>) : go(rs::k_hist16_in<A, true>);
+        else if (in_aos)
+            full ? go(rs::k_hist16_in<A, false, true>) : go(rs::k_hist16_in<A>);
+        else
+            full ? go(rs::k_hist16_in<S, false, true>) : go(rs::k_hist16_in<S>);
+        // the reduction also lays out every top byte's buckets (bases inside the segment, the
+        // overflow list, the oversize flag): the plan kernel is left with the 256 segments
+        hipLaunchKernelGGL(rs::k_hist16_reduce, dim3(256), dim3(1024), 0, s, (const uint32_t*)p->tmp_k,
+                           hrows, hist16, top_tot, range_bad, base16, small_cap, kBucketCap, over, big);
+    });
+    HIP_TRY(hipGetLastError());
     p->timer.run(RS_KERNEL_SCAN, s, [&] {
         auto plan = [&](auto kern) {
-            hipLaunchKernelGGL(kern, dim3(1), dim3(1024), 0, s, (const uint32_t*)hist16, (const uint32_t*)top_tot,
-                               base16, segtab, kBucketCap, small_cap, kMsdMaxTop, over, gates,
-                               (const uint32_t*)range_bad);
+            hipLaunchKernelGGL(kern, dim3(1), dim3(256), 0, s, (const uint32_t*)top_tot, segtab, kMsdMaxTop, over,
+                               (const uint32_t*)big, gates, (const uint32_t*)range_bad);
         };
         if (tile == 2u * kLarge.tile) plan(rs::k_msd_plan<2 * kLarge.tile>);
         else plan(rs::k_msd_plan<kLarge.tile>);
@@ -862,7 +866,7 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
     p->timer.run(RS_KERNEL_BUCKET, s, [&] {
         auto small = [&](auto kern) {
             hipLaunchKernelGGL(kern, dim3(65536), dim3(bb), 0, s, r2, hist16, base16, uk, uv, g_msd,
-                               p->tickets + 16, 0u, (const uint32_t*)nullptr, kbase);
+                               p->tickets + 16, 0u, (const uint32_t*)nullptr, kbase, (const uint32_t*)sstart);
         };
         // keys only: a persistent grid whose workgroups load their next bucket while sorting one
         auto small_pf = [&](auto kern) {
@@ -870,13 +874,13 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
             static const uint32_t mult = [] { const char* e = getenv("RSORT_KBUCKET_GRID"); return e ? (uint32_t)atoi(e) : 1u; }();
             const uint32_t grid = std::min<uint32_t>(65536u, p->cus * per_cu * std::max(1u, mult));
             hipLaunchKernelGGL(kern, dim3(grid), dim3(bb), 0, s, r2, hist16, base16, uk, uv, g_msd,
-                               p->tickets + 16, 0u, (const uint32_t*)nullptr, kbase);
+                               p->tickets + 16, 0u, (const uint32_t*)nullptr, kbase, (const uint32_t*)sstart);
         };
         // RSORT_OVER_GRID: workgroups of the listed-bucket launch (sweeps)
         static const uint32_t over_grid = [] { const char* e = getenv("RSORT_OVER_GRID"); return e ? (uint32_t)atoi(e) : 256u; }();
         auto large = [&](auto kern) {
             hipLaunchKernelGGL(kern, dim3(std::max(1u, over_grid)), dim3(kBucketBlock), 0, s, r2, hist16, base16, uk, uv,
-                               g_msd, p->tickets + 16, small_cap, (const uint32_t*)over, kbase);
+                               g_msd, p->tickets + 16, small_cap, (const uint32_t*)over, kbase, (const uint32_t*)sstart);
         };
         auto both = [&](auto lo) {
             constexpr int LO = decltype(lo)::value;
@@ -887,7 +891,7 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
                     // sweep only: 2 or 8 waves (buckets) per workgroup
                     auto wave = [&](auto kern, int w) {
                         hipLaunchKernelGGL(kern, dim3(65536 / w), dim3(64 * w), 0, s, uk, (const uint32_t*)hist16,
-                                           (const uint32_t*)base16, g_msd);
+                                           (const uint32_t*)base16, g_msd, (const uint32_t*)sstart);
                     };
                     if (wpb == 2) wave(rs::k_bucket_sort_keys_wave<18, A0, 2>, 2);
                     else wave(rs::k_bucket_sort_keys_wave<18, A0, 8>, 8);
@@ -896,7 +900,7 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
                     constexpr int WPB = 4;
                     auto wave = [&](auto kern) {
                         hipLaunchKernelGGL(kern, dim3(65536 / WPB), dim3(64 * WPB), 0, s, uk, (const uint32_t*)hist16,
-                                           (const uint32_t*)base16, g_msd);
+                                           (const uint32_t*)base16, g_msd, (const uint32_t*)sstart);
                     };
                     if (wave_kpt == 10)
                         ballot ? wave(rs::k_bucket_sort_keys_wave<10, B0, WPB>) : wave(rs::k_bucket_sort_keys_wave<10, A0, WPB>);

@@ -1364,7 +1364,11 @@ __global__ __launch_bounds__(1024) void k_hist16_reduce(const uint32_t* __restri
                                                          uint32_t* __restrict__ range_bad,
                                                          uint32_t* __restrict__ base16, uint32_t small,
                                                          uint32_t cap, uint32_t* __restrict__ over,
-                                                         uint32_t* __restrict__ big) {
+                                                         uint32_t* __restrict__ big,
+                                                         uint32_t* __restrict__ zero = nullptr, uint32_t nzero = 0) {
+    // zero[0..nzero): the sort's pass totals, tile tickets and device error word (no memset launch)
+    if (blockIdx.x == gridDim.x - 1)
+        for (uint32_t i = threadIdx.x; i < nzero; i += blockDim.x) zero[i] = 0u;
     __shared__ uint4 s_part[16][64];
     const uint32_t tid = threadIdx.x, c = tid & 63u, g = tid >> 6;
     if (blockIdx.x == 0) {   // any key outside the range (the rows' flag words)

@@ -756,7 +756,7 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
     const int keys_cfg = p->msd_keys_cfg;
     const uint32_t tile = (keys && keys_cfg == 2) ? 2u * kLarge.tile : (uint32_t)kLarge.tile;
     const uint32_t ntiles = (uint32_t)((n + tile - 1) / tile);
-    HIP_TRY(hipMemsetAsync(p->ptot, 0, 4ull * (rs::kTotalsMax + 32), s));
+    // the pass totals, tickets and error word are zeroed by k_hist16_reduce (nothing reads them before)
     // 16-bit buckets: a tile sized to the mean bucket + 4 sigma of a uniform population takes
     // every bucket that fits it (at 2^28 keys: 4352 records, ~2 buckets over it), the large tile
     // the listed rest
@@ -802,7 +802,8 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
         // the reduction also lays out every top byte's buckets (bases inside the segment, the
         // overflow list, the oversize flag): the plan kernel is left with the 256 segments
         hipLaunchKernelGGL(rs::k_hist16_reduce, dim3(256), dim3(1024), 0, s, (const uint32_t*)p->tmp_k,
-                           hrows, hist16, top_tot, range_bad, base16, small_cap, kBucketCap, over, big);
+                           hrows, hist16, top_tot, range_bad, base16, small_cap, kBucketCap, over, big,
+                           p->ptot, (uint32_t)(rs::kTotalsMax + 32));
     });
     HIP_TRY(hipGetLastError());
     p->timer.run(RS_KERNEL_SCAN, s, [&] {

@@ -232,6 +232,12 @@ def main() -> None:
                     help="PMC-derived HBM bytes per scatter launch (tools/pmc_traffic.py)")
     args = ap.parse_args()
 
+    # stdout carries exactly one JSON line: anything native code prints there (RCCL writes a
+    # version banner to stdout when a communicator is created) goes to stderr instead
+    sys.stdout.flush()
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+
     import torch
     import torch.distributed as dist
     from radix_sort_amd import RadixSortKernel, RadixSortTextureKernel, ops
@@ -447,7 +453,7 @@ def main() -> None:
                        f"{world} ranks, top-byte bucket exchange (RCCL point-to-point rounds)"},
             "roofline": roof, "cpu_baseline": cpu, **extra,
         }
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=json_out, flush=True)
     if use_dist:
         dist.destroy_process_group()
 

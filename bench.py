@@ -215,7 +215,55 @@ def verify_batch(torch, ops, wl, n, seed, batch, dev) -> None:
         raise SystemExit("bench: equal keys out of input order (not stable)")
 
 
+def launch_plan(gpus: int, env: dict, device_count: int, argv: list) -> tuple:
+    """How this invocation runs `--gpus N` (decided before anything touches the GPU).
+
+    -> ("run", None): this process is the bench (N = 1 alone, or one rank of a launcher whose
+       WORLD_SIZE equals N);
+       ("spawn", cmd): N > 1 without a launcher: start N rank processes under
+       torch.distributed.run (one per GPU, RCCL) as a child and exit with its status;
+       ("error", message): never silently measure fewer GPUs than asked for."""
+    if gpus < 1:
+        return "error", f"--gpus must be >= 1 (got {gpus})"
+    world = env.get("WORLD_SIZE")
+    if world is not None:
+        if int(world) != gpus:
+            return "error", (f"--gpus {gpus} but the launcher started WORLD_SIZE={world} ranks; "
+                             "they must agree")
+        if int(world) > device_count:
+            return "error", f"WORLD_SIZE={world} but only {device_count} GPU(s) are visible"
+        return "run", None
+    if gpus == 1:
+        return ("run", None) if device_count >= 1 else ("error", "no GPU visible")
+    if device_count < gpus:
+        return "error", f"--gpus {gpus} but only {device_count} GPU(s) are visible"
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+    return "spawn", cmd
+
+
+def _gpus_arg(argv: list) -> int:
+    ap = argparse.ArgumentParser(add_help=False)
+    ap.add_argument("--gpus", type=int, default=1)
+    return ap.parse_known_args(argv)[0].gpus
+
+
 def main() -> None:
+    # `--gpus N` must measure N GPUs however it is started: a plain `python bench.py --gpus N`
+    # starts N ranks itself (before any GPU call in this process); a launcher's WORLD_SIZE must
+    # match N; fewer visible GPUs than N is an error, never a 1-GPU line
+    import torch   # device_count() does not initialise the GPU
+    what, arg = launch_plan(_gpus_arg(sys.argv[1:]), dict(os.environ), torch.cuda.device_count(),
+                            sys.argv[1:])
+    if what == "error":
+        raise SystemExit(f"bench: {arg}")
+    if what == "spawn":
+        log("bench: starting " + " ".join(arg))
+        raise SystemExit(subprocess.run(arg).returncode)
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -246,8 +294,7 @@ def main() -> None:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    assert world == args.gpus, (world, args.gpus)   # launch_plan enforced it
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     use_dist = world > 1 or args.distributed
@@ -451,6 +498,7 @@ def main() -> None:
                        "radix_bits": args.radix_bits or 8,
                        "parallelism": "single GPU" if world == 1 else
                        f"{world} ranks, top-byte bucket exchange (RCCL point-to-point rounds)"},
+            "rccl_ranks": dist.get_world_size() if use_dist else 0,
             "roofline": roof, "cpu_baseline": cpu, **extra,
         }
         print(json.dumps(out), file=json_out, flush=True)

@@ -69,6 +69,28 @@ def _fingerprint(t):
     return h, int(s1), int(s2)
 
 
+def test_keys_only_default_at_max_count():
+    """The default route (no check_order) at the largest accepted count.  Round 2's hybrid-path
+    histogram computed its per-row chunk in 32 bits, which wraps for n > 2^32 - 256: every row
+    counted nothing, the plan saw all-zero buckets, picked the MSD passes and returned unsorted
+    keys with RS_OK.  The chunk is 64-bit now, the plan kernel refuses a histogram that does not
+    account for all n keys, and above 256 x 1.5M keys (where some top byte must exceed the MSD
+    path's limit) the host goes straight to the LSD passes."""
+    from radix_sort_amd import RadixSortKernel, ops
+    n = (1 << 32) - 1
+    kt = torch.empty(n, dtype=torch.int32, device=DEV)
+    ops.fill_random_u32(kt, 33)
+    fp_in = _fingerprint(kt)
+    k = RadixSortKernel(keys=kt, count=n)
+    k.dispatch()
+    k.check()
+    assert k.device_errors() == 0
+    k.destroy()
+    assert ops.is_sorted(kt, n)
+    fp_out = _fingerprint(kt)
+    assert torch.equal(fp_in[0], fp_out[0]) and fp_in[1:] == fp_out[1:]
+
+
 def test_keys_only_check_order_at_max_count():
     from radix_sort_amd import RadixSortKernel, ops
     n = (1 << 32) - 1

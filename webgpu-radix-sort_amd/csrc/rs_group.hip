@@ -406,36 +406,49 @@ RS_EXPORT rs_status rs_group_sort(rs_group* g, void* const* keys, void* const* v
         // 4: exchange rounds
         const bool rccl = g->desc.transport == RS_TRANSPORT_RCCL;
         for (uint32_t j = 0; j < G; ++j) {
-            if (rccl) G_NCCL(ncclGroupStart());
-            for (int src = 0; src < W; ++src) {
-                Rank& k = g->r[src];
-                Dev dev(k.device);
-                for (int dst = 0; dst < W; ++dst) {
-                    auto r = seg(src, cut(dst, j), cut(dst, j + 1));
-                    const uint64_t m = r.second - r.first;
-                    char* from = (char*)k.send + esz * r.first;
-                    char* to = (char*)g->r[dst].recv + esz * off[((size_t)dst * G + j) * W + src];
-                    if (dst == src || !rccl) {
-                        if (!m) continue;
-                        if (g->r[dst].device == k.device)
-                            G_HIP(hipMemcpyAsync(to, from, esz * m, hipMemcpyDeviceToDevice, k.comm_s));
-                        else
-                            G_HIP(hipMemcpyPeerAsync(to, g->r[dst].device, from, k.device, esz * m, k.comm_s));
-                    } else if (m) {
-                        G_NCCL(ncclSend(from, m, g->kv ? ncclUint64 : ncclUint32, dst, k.comm, k.comm_s));
-                    }
-                }
-                if (rccl)
-                    for (int s = 0; s < W; ++s) {
-                        if (s == src) continue;
-                        auto r = seg(s, cut(src, j), cut(src, j + 1));
+            // every send / receive of round j; inside an RCCL group a failure must not return
+            // before ncclGroupEnd (the group depth is per thread: the next round would nest in
+            // the open group), so the calls run in a lambda and the group is always closed
+            auto post = [&]() -> rs_status {
+                for (int src = 0; src < W; ++src) {
+                    Rank& k = g->r[src];
+                    Dev dev(k.device);
+                    for (int dst = 0; dst < W; ++dst) {
+                        auto r = seg(src, cut(dst, j), cut(dst, j + 1));
                         const uint64_t m = r.second - r.first;
-                        if (!m) continue;
-                        char* to = (char*)k.recv + esz * off[((size_t)src * G + j) * W + s];
-                        G_NCCL(ncclRecv(to, m, g->kv ? ncclUint64 : ncclUint32, s, k.comm, k.comm_s));
+                        char* from = (char*)k.send + esz * r.first;
+                        char* to = (char*)g->r[dst].recv + esz * off[((size_t)dst * G + j) * W + src];
+                        if (dst == src || !rccl) {
+                            if (!m) continue;
+                            if (g->r[dst].device == k.device)
+                                G_HIP(hipMemcpyAsync(to, from, esz * m, hipMemcpyDeviceToDevice, k.comm_s));
+                            else
+                                G_HIP(hipMemcpyPeerAsync(to, g->r[dst].device, from, k.device, esz * m, k.comm_s));
+                        } else if (m) {
+                            G_NCCL(ncclSend(from, m, g->kv ? ncclUint64 : ncclUint32, dst, k.comm, k.comm_s));
+                        }
                     }
+                    if (rccl)
+                        for (int s = 0; s < W; ++s) {
+                            if (s == src) continue;
+                            auto r = seg(s, cut(src, j), cut(src, j + 1));
+                            const uint64_t m = r.second - r.first;
+                            if (!m) continue;
+                            char* to = (char*)k.recv + esz * off[((size_t)src * G + j) * W + s];
+                            G_NCCL(ncclRecv(to, m, g->kv ? ncclUint64 : ncclUint32, s, k.comm, k.comm_s));
+                        }
+                }
+                return RS_OK;
+            };
+            if (rccl) G_NCCL(ncclGroupStart());
+            const rs_status posted = post();
+            if (rccl) {
+                const ncclResult_t ended = ncclGroupEnd();
+                G_TRY(posted);
+                if (ended != ncclSuccess)
+                    return gfail(RS_ERR_HIP, "ncclGroupEnd: %s (%s:%d)", ncclGetErrorString(ended), __FILE__, __LINE__);
             }
-            if (rccl) G_NCCL(ncclGroupEnd());
+            G_TRY(posted);
             for (int src = 0; src < W; ++src) {
                 Dev dev(g->r[src].device);
                 G_HIP(hipEventRecord(g->r[src].ev_round[j], g->r[src].comm_s));

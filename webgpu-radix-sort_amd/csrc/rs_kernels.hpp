@@ -1292,7 +1292,9 @@ __global__ __launch_bounds__(1024) void k_hist16_in(const uint32_t* __restrict__
     uint32_t acc[2 * PER];
 #pragma unroll
     for (uint32_t i = 0; i < PER; ++i) { h[tid + B * i] = 0u; acc[2 * i] = 0u; acc[2 * i + 1] = 0u; }
-    const uint32_t chunk = ((n + gridDim.x - 1) / gridDim.x + 3u) & ~3u;
+    // 64-bit: n + gridDim.x - 1 wraps in 32 bits for n > 2^32 - gridDim.x (chunk would be 0 and
+    // every row would count nothing)
+    const uint64_t chunk = (((uint64_t)n + gridDim.x - 1) / gridDim.x + 3u) & ~3ull;
     const uint64_t lo = (uint64_t)blockIdx.x * chunk;
     const uint64_t hi = lo + chunk < n ? lo + chunk : (lo < n ? n : lo);
     const uint64_t nv = (hi - lo) / KPL;                          // whole vectors
@@ -1418,11 +1420,13 @@ __global__ __launch_bounds__(1024) void k_hist16_reduce(const uint32_t* __restri
 // (*big == 0), at most kOverMax buckets need the large tile, every top-byte bucket holds at most
 // max_top keys and no key lies outside the range; else the LSD passes on the input.  over[0] is
 // clamped to the stored entries.
+// The histogram must account for every one of the n keys (a counting bug would otherwise send the
+// data through passes with wrong digit bases and return garbage): a mismatch picks the LSD passes.
 template <int TILE>
 __global__ __launch_bounds__(256) void k_msd_plan(const uint32_t* __restrict__ top_tot,
                                                   uint32_t* __restrict__ segtab, uint32_t max_top,
                                                   uint32_t* over, const uint32_t* big, uint32_t* gates,
-                                                  const uint32_t* __restrict__ range_bad) {
+                                                  const uint32_t* __restrict__ range_bad, uint32_t n) {
     constexpr int NW = 4;
     __shared__ uint32_t s_scratch[NW];
     const uint32_t tid = threadIdx.x;
@@ -1440,7 +1444,7 @@ __global__ __launch_bounds__(256) void k_msd_plan(const uint32_t* __restrict__ t
     const uint32_t nover = over[0];
     __syncthreads();   // every thread has read over[0]
     if (tid == 0) over[0] = nover < kOverMax ? nover : kOverMax;
-    const uint32_t ok = (any_big || *big || nover > kOverMax || *range_bad) ? 0u : 1u;
+    const uint32_t ok = (any_big || *big || nover > kOverMax || *range_bad || stot != n) ? 0u : 1u;
     set_gate(gates + kGateMsd, ok);
     set_gate(gates + kGateLsd, 1u - ok);
 }

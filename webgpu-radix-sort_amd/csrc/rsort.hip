@@ -490,6 +490,9 @@ bool use_msd(const rs_plan* p, uint64_t n) {
     if (!p->msd || p->msd_mode == 0 || p->check_order || p->bit_count != 32 || p->radix_bits != 8 ||
         use_small_tiles(n) || n < kMsdMin)
         return false;
+    // above 256 * kMsdMaxTop keys some top byte always holds more than kMsdMaxTop (pigeonhole):
+    // the device would always pick the fallback, so the histogram read would be wasted
+    if (n > 256ull * kMsdMaxTop) return false;
     // keys only: R1 = tmp_k (n words, which first holds the histogram rows), R2 = the caller's keys;
     // the one-sweep passes of this path are its own (the keys-only LSD sort keeps the histogram path)
     if (p->layout == rs::LAYOUT_KEYS)
@@ -809,7 +812,7 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
     p->timer.run(RS_KERNEL_SCAN, s, [&] {
         auto plan = [&](auto kern) {
             hipLaunchKernelGGL(kern, dim3(1), dim3(256), 0, s, (const uint32_t*)top_tot, segtab, kMsdMaxTop, over,
-                               (const uint32_t*)big, gates, (const uint32_t*)range_bad);
+                               (const uint32_t*)big, gates, (const uint32_t*)range_bad, n32);
         };
         if (tile == 2u * kLarge.tile) plan(rs::k_msd_plan<2 * kLarge.tile>);
         else plan(rs::k_msd_plan<kLarge.tile>);

@@ -1,9 +1,11 @@
 """GPU, large N: counts the C ABI accepts beyond BASELINE's 2^28 (README.md:100-102: N "not
 bound by the implementation itself"; SURVEY §7 hard part 5, 64-bit addressing).
 
-* 2^31 u32 keys + values on ONE GPU through rs_plan_sort (the single-GPU baseline of config 5),
-  verified as a stable permutation of the input (sizes too large for the CPU oracle: the
-  size-independent properties);
+* 2^29 and 2^31 u32 keys + values on ONE GPU through rs_plan_sort (2^31: the single-GPU baseline
+  of config 5), 2^29 keys only and as records in place - the hybrid path with the wide bucket
+  kernel - verified as the stable sorted permutation of the input (sizes too large for the CPU
+  oracle: sorted + a permutation with keys_out == keys_in[values_out] + equal keys in input order
+  determine the stable sort uniquely);
 * the largest accepted count, 2^32 - 1 keys, keys-only with check_order, and the top-byte
   histogram (k_pass_totals) at that count: every grid-stride loop near 2^32 terminates.
 Each run once; together ~100 GB of HBM at peak.
@@ -38,20 +40,64 @@ def _stable_kv_checks(keys_in, keys_out, vals_out):
         assert bool((v[1:][eq] > v[:-1][eq]).all())
 
 
-def test_kv_2pow31_single_gpu():
+def _hybrid_ran(times) -> bool:
+    """The hybrid MSD path sorted (its bucket pass carried the time), not its LSD fallback."""
+    return times["bucket"]["launches"] > 0 and times["fallback"]["ms"] < times["bucket"]["ms"]
+
+
+@pytest.mark.parametrize("n", [1 << 29, 1 << 31])
+def test_kv_large_single_gpu(n):
+    """2^29 and 2^31 KV on one GPU (2^31: the single-GPU baseline of config 5).  Their 16-bit
+    buckets hold ~8K / ~32K records, over every population-sized tile: the hybrid path sorts every
+    bucket with k_bucket_sort_wide (round 2 sent both sizes to the four LSD passes)."""
     from radix_sort_amd import RadixSortKernel, ops
-    n = 1 << 31
     kt = torch.empty(n, dtype=torch.int32, device=DEV)
     vt = torch.empty(n, dtype=torch.int32, device=DEV)
     ops.fill_random_u32(kt, 31)
     ops.fill_iota_u32(vt)
     kin = kt.clone()
     k = RadixSortKernel(keys=kt, values=vt, count=n)
+    k.set_profiling(True)
     k.dispatch()
     k.check()
     assert k.device_errors() == 0
+    assert _hybrid_ran(k.kernel_times())
     k.destroy()
     _stable_kv_checks(kin, kt, vt)
+
+
+def test_keys_only_and_records_2pow29():
+    """The wide bucket kernel's other layouts at a size where it takes every bucket: keys only (in
+    place) and (key, value) records in place (RadixSortTextureKernel)."""
+    from radix_sort_amd import RadixSortKernel, RadixSortTextureKernel, ops
+    n = 1 << 29
+    kt = torch.empty(n, dtype=torch.int32, device=DEV)
+    ops.fill_random_u32(kt, 29)
+    fp_in = _fingerprint(kt)
+    k = RadixSortKernel(keys=kt, count=n)
+    k.set_profiling(True)
+    k.dispatch()
+    k.check()
+    assert _hybrid_ran(k.kernel_times())
+    k.destroy()
+    assert ops.is_sorted(kt, n)
+    fp_out = _fingerprint(kt)
+    assert torch.equal(fp_in[0], fp_out[0]) and fp_in[1:] == fp_out[1:]
+    del kt
+    rec = torch.empty((n, 2), dtype=torch.int32, device=DEV)
+    kin = torch.empty(n, dtype=torch.int32, device=DEV)
+    ops.fill_random_u32(kin, 290)
+    rec[:, 0] = kin
+    rec[:, 1] = torch.arange(n, dtype=torch.int32, device=DEV)
+    k = RadixSortTextureKernel(texture=rec, count=n)
+    k.set_profiling(True)
+    k.dispatch()
+    k.check()
+    assert _hybrid_ran(k.kernel_times())
+    k.destroy()
+    ko, vo = rec[:, 0].contiguous(), rec[:, 1].contiguous()
+    del rec
+    _stable_kv_checks(kin, ko, vo)
 
 
 def _fingerprint(t):
@@ -74,8 +120,8 @@ def test_keys_only_default_at_max_count():
     histogram computed its per-row chunk in 32 bits, which wraps for n > 2^32 - 256: every row
     counted nothing, the plan saw all-zero buckets, picked the MSD passes and returned unsorted
     keys with RS_OK.  The chunk is 64-bit now, the plan kernel refuses a histogram that does not
-    account for all n keys, and above 256 x 1.5M keys (where some top byte must exceed the MSD
-    path's limit) the host goes straight to the LSD passes."""
+    account for all n keys, and above ~2.2G keys (where some 16-bit bucket all but certainly
+    exceeds the largest bucket tile) the host goes straight to the LSD passes."""
     from radix_sort_amd import RadixSortKernel, ops
     n = (1 << 32) - 1
     kt = torch.empty(n, dtype=torch.int32, device=DEV)

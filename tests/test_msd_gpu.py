@@ -30,6 +30,10 @@ def _keys(n, kind, seed):
     elif kind == "few_big":     # a few 16-bit buckets just over the population-sized tile
         k[:12000] = 0x12345678
         k[12000:21000] = 0x7FFF0000
+    elif kind == "wide":        # 2560 populated 16-bit buckets spread over every top byte (n / 2560
+        # records each: all over the population-sized tile, listed for k_bucket_sort_wide)
+        u = k.long() & 0xFFFFFFFF
+        k.copy_(((((u >> 16) % 2560) * 25) << 16 | (u & 0xFFFF)).to(torch.int32))
     return k
 
 
@@ -79,6 +83,23 @@ def test_msd_device_fallbacks(kind):
 @pytest.mark.parametrize("kind", ["dups", "few_big"])
 def test_msd_duplicates_and_overflow_buckets(kind):
     _sort_and_check(1 << 24, kind)
+
+
+@pytest.mark.parametrize("n", [(1 << 25) + 3, (1 << 26) - 5])
+def test_msd_wide_buckets_match_oracle(n, monkeypatch):
+    """16-bit buckets of 13K-26K records (over every population-sized tile, under the wide kernel's
+    34816): every populated bucket is listed and sorted by k_bucket_sort_wide (1024 threads, the
+    positions through LDS, the values gathered after), bit-exact against the oracle; separate arrays,
+    in place and out of place, both rank modes; and the texture layout (records in place)."""
+    t = _sort_and_check(n, "wide")
+    assert t["fallback"]["ms"] < t["bucket"]["ms"]      # the hybrid path ran, not the LSD fallback
+    _sort_and_check(n, "wide", copy=True)
+    _sort_and_check(n, "wide", rank="ballot", monkeypatch=monkeypatch)
+
+
+def test_msd_records_wide_buckets():
+    t = _sort_tex_and_check((1 << 25) + 9, "wide")
+    assert t["fallback"]["ms"] < t["bucket"]["ms"]
 
 
 def test_msd_out_of_place_and_ballot_ranking(monkeypatch):
@@ -295,11 +316,10 @@ def test_msd_keys_pass_tile_configs(monkeypatch, cfg):
 
 
 @pytest.mark.parametrize("n,env", [((1 << 27) + 5, {}),                                  # 2K-key buckets
-                                   ((1 << 25) + 77, {"RSORT_KBUCKET_WAVE": "0"}),
-                                   ((1 << 25) + 77, {"RSORT_KBUCKET_WAVE": "0", "RSORT_KBUCKET_PF": "1"})])
+                                   ((1 << 25) + 77, {"RSORT_KBUCKET_WAVE": "0"})])
 def test_msd_keys_workgroup_bucket_kernel(monkeypatch, n, env):
     # buckets over the wave kernel's 64 x 18 keys (or the wave kernel off): one workgroup per
-    # bucket, in place (and its persistent prefetching variant)
+    # bucket, in place
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     t = _sort_keys_and_check(n, "uniform")

@@ -423,15 +423,13 @@ def _dup_pattern(kind: str, n: int, seed: int) -> np.ndarray:
     raise ValueError(kind)
 
 
-@pytest.mark.parametrize("huge", ["0", "1"])
 @pytest.mark.parametrize("kind", ["runs2", "runs7", "runs16", "runs64", "runs100", "recurring",
                                   "sorted_repeats", "two_values"])
-def test_duplicate_heavy_keys_every_layout(monkeypatch, kind, huge):
+def test_duplicate_heavy_keys_every_layout(kind):
     """Run-counting ranks and counts give the oracle's stable order for duplicate-heavy inputs,
-    on both tile sizes of the one-sweep path (RSORT_HUGE), the histogram path (keys only) and
-    the small-tile path; values are a permutation so stability is checked word for word."""
+    on the one-sweep path, the histogram path (keys only) and the small-tile path; values are a
+    permutation so stability is checked word for word."""
     from radix_sort_amd import RadixSortKernel, RadixSortTextureKernel
-    monkeypatch.setenv("RSORT_HUGE", huge)
     for n in (3_000_017, 13_000_001):
         keys = _dup_pattern(kind, n, n + len(kind))
         vals = np.arange(n, dtype=np.uint32)

@@ -620,7 +620,10 @@ __device__ __forceinline__ void scatter_tile(const uint32_t* s_keys, const uint2
                                              const uint32_t* s_gdelta, uint32_t* __restrict__ out_k,
                                              uint32_t* __restrict__ out_v, uint32_t n,
                                              uint32_t nvalid, uint32_t tile0, uint32_t shift,
-                                             uint32_t mask, uint32_t pbase = 0) {
+                                             uint32_t mask, uint32_t pbase = 0,
+                                             uint32_t pmask = 0xFFFFFFFFu) {
+    // pmask: output positions taken modulo a power-of-two ring (the IC-resident R2 ring of the
+    // hybrid path's fused tail); all ones otherwise
 #pragma unroll 4
     for (uint32_t i = threadIdx.x; i < nvalid; i += BLOCK) {
         uint32_t key, val = 0;
@@ -638,12 +641,13 @@ __device__ __forceinline__ void scatter_tile(const uint32_t* s_keys, const uint2
         (void)tile0;
 #endif
         if (pos < n) {  // never false for consistent offsets; keeps a bug from faulting
+            const uint32_t q = pos & pmask;
             if (LO == LAYOUT_AOS) {
-                st_out(reinterpret_cast<unsigned long long*>(out_k) + pos,
+                st_out(reinterpret_cast<unsigned long long*>(out_k) + q,
                        (unsigned long long)key | ((unsigned long long)val << 32));
             } else {
-                st_out(out_k + pos, key);
-                if (HAS_VALUES) st_out(out_v + pos, val);
+                st_out(out_k + q, key);
+                if (HAS_VALUES) st_out(out_v + q, val);
             }
         }
     }
@@ -917,7 +921,7 @@ __global__ __launch_bounds__(BLOCK, pass_min_waves(BLOCK, KPT)) void k_onesweep(
     uint32_t nshift, uint32_t nmask, uint32_t epoch, const uint32_t* gate, int pass,
     uint32_t* chk, uint32_t fmask, uint32_t spin_max, uint32_t* host_err,
     const uint32_t* __restrict__ segtab = nullptr, const uint32_t* __restrict__ base16 = nullptr,
-    uint32_t kbase = 0) {
+    uint32_t kbase = 0, uint32_t pmask = 0xFFFFFFFFu) {
     // ntot (may be null): whole-array totals of the NEXT pass's digit (key >> nshift) & nmask,
     // counted here from the keys this workgroup stages, so only pass 0 needs k_pass_totals.
     // chk (may be null, check_order, pass > 0): the order check of this pass's input, fused:
@@ -1139,7 +1143,7 @@ __global__ __launch_bounds__(BLOCK, pass_min_waves(BLOCK, KPT)) void k_onesweep(
             if (lo < nvalid)
                 scatter_tile<BLOCK, HAS_VALUES, LO>(s_keys, s_kv, s_gdelta, out_k, out_v, n,
                                                     nvalid - lo < (uint32_t)STAGE ? nvalid - lo : (uint32_t)STAGE,
-                                                    tile0, shift, mask, lo);
+                                                    tile0, shift, mask, lo, pmask);
             __syncthreads();
         }
 #if RS_SCATTER_DEBUG == 2
@@ -1477,10 +1481,13 @@ __global__ __launch_bounds__(BLOCK, MW) void k_bucket_sort(const uint32_t* rec,
                                                        uint32_t min_cnt,
                                                        const uint32_t* __restrict__ over = nullptr,
                                                        uint32_t kbase = 0,
-                                                       const uint32_t* __restrict__ sstart = nullptr) {
+                                                       const uint32_t* __restrict__ sstart = nullptr,
+                                                       uint32_t rmask = 0xFFFFFFFFu) {
     constexpr int R = 8, RADIX = 256;
-    // bucket b's first record: its top-byte segment's start + its base inside the segment
+    // bucket b's first record in rec: its top-byte segment's start + its base inside the segment
+    // (modulo the ring of rmask + 1 records, sweep experiments), and in the output
     auto bstart = [&](uint32_t b) { return sstart[b >> 8] + base16[b]; };
+    auto rstart = [&](uint32_t b) { return bstart(b) & rmask; };
     constexpr int NW = BLOCK / 64;
     constexpr int TILE = BLOCK * KPT;
     constexpr int WAVE_KEYS = 64 * KPT;
@@ -1513,7 +1520,7 @@ __global__ __launch_bounds__(BLOCK, MW) void k_bucket_sort(const uint32_t* rec,
     if (it >= nb) return;
     uint32_t k[KPT], v[KV ? KPT : 1];
     uint32_t k2[PF ? KPT : 1], v2[PF && KV ? KPT : 1];
-    load_tile<KPT, LI>(rec + (KV ? 2ull : 1ull) * bstart(over ? over[1 + it] : it), nullptr, wbase, cnt, false, k, v);
+    load_tile<KPT, LI>(rec + (KV ? 2ull : 1ull) * rstart(over ? over[1 + it] : it), nullptr, wbase, cnt, false, k, v);
     while (true) {
         const uint32_t b = over ? over[1 + it] : it;
         const uint32_t base = bstart(b);
@@ -1521,7 +1528,7 @@ __global__ __launch_bounds__(BLOCK, MW) void k_bucket_sort(const uint32_t* rec,
         const uint32_t nit = next_valid(it + gridDim.x, ncnt);
         if constexpr (PF != 0) {
             if (nit < nb)
-                load_tile<KPT, LI>(rec + (KV ? 2ull : 1ull) * bstart(over ? over[1 + nit] : nit), nullptr, wbase,
+                load_tile<KPT, LI>(rec + (KV ? 2ull : 1ull) * rstart(over ? over[1 + nit] : nit), nullptr, wbase,
                                    ncnt, false, k2, v2);
         }
         if (cnt > 1u) {
@@ -1590,8 +1597,117 @@ __global__ __launch_bounds__(BLOCK, MW) void k_bucket_sort(const uint32_t* rec,
                 if constexpr (KV) v[j] = v2[j];
             }
         } else {
-            load_tile<KPT, LI>(rec + (KV ? 2ull : 1ull) * bstart(over ? over[1 + it] : it), nullptr, wbase, cnt, false, k, v);
+            load_tile<KPT, LI>(rec + (KV ? 2ull : 1ull) * rstart(over ? over[1 + it] : it), nullptr, wbase, cnt, false, k, v);
         }
+    }
+}
+
+// Wide buckets: up to 1024 x KPT records (KPT = 34: 34816, the 16-bit buckets of up to 2^31 uniform
+// keys, ~32K records each) sorted by one 1024-thread workgroup with 4 bytes of LDS per record, where
+// k_bucket_sort stages 8-byte records (16K at most).  The records stay in registers; what moves
+// through LDS is w = (low 16 bits of the key) << 16 | p, p = the record's position in the bucket
+// (< 65536), in two stable 8-bit passes (key bits 0-7, then 8-15); the values follow in one exchange
+// (s[p] = value, then value = s[w & 0xFFFF]).  The key is rebuilt from the bucket number and w:
+// (b << bshift) | (w >> 16), bshift = the bucket's low bit (16; the range form: vbits - 16, where
+// the bits w >> 16 shares with b << bshift agree).  Keys only: the keys themselves move (no p).
+// Pads (positions >= cnt) are w = kPadKey: digit 255 in both passes, after every real key.
+// One bucket per workgroup: a grid of 65536 (every bucket over min_cnt), or listed buckets (`over`).
+template <int KPT, int RANK, int LO>
+__global__ __launch_bounds__(1024, 1) void k_bucket_sort_wide(const uint32_t* rec,
+                                                              const uint32_t* __restrict__ hist16,
+                                                              const uint32_t* __restrict__ base16,
+                                                              uint32_t* out_k, uint32_t* __restrict__ out_v,
+                                                              const uint32_t* gate, uint32_t* err,
+                                                              uint32_t min_cnt,
+                                                              const uint32_t* __restrict__ over,
+                                                              uint32_t kbase,
+                                                              const uint32_t* __restrict__ sstart,
+                                                              uint32_t rmask, uint32_t bshift) {
+    constexpr int BLOCK = 1024, NW = BLOCK / 64, RADIX = 256;
+    constexpr int TILE = BLOCK * KPT;
+    constexpr int WAVE_KEYS = 64 * KPT;
+    constexpr bool KV = LO != LAYOUT_KEYS;
+    static_assert(TILE <= 65536, "16-bit record positions");
+    __shared__ uint32_t s_whist[NW][RADIX];
+    __shared__ uint32_t s_scratch[NW];
+    __shared__ uint32_t s_w[TILE];
+    if (gated_off(gate, 0)) return;
+    const uint32_t tid = threadIdx.x, w = tid >> 6, lane = lane_id();
+    const uint32_t wbase = w * WAVE_KEYS;
+    const uint32_t nb = over ? over[0] : 65536u;
+    for (uint32_t it = blockIdx.x; it < nb; it += gridDim.x) {
+        const uint32_t b = over ? over[1 + it] : it;
+        const uint32_t cnt = hist16[b];
+        if (cnt <= min_cnt || cnt <= 1u) continue;   // the smaller tile's launch took it (or trivial)
+        if (cnt > (uint32_t)TILE) {                   // never: k_hist16_reduce gates the path off
+            if (tid == 0) atomicOr(err, 8u);
+            continue;
+        }
+        const uint32_t base = sstart[b >> 8] + base16[b];
+        const uint32_t* src = rec + (KV ? 2ull : 1ull) * (base & rmask);
+        uint32_t x[KPT];
+        {
+            const int lim = (int)cnt - (int)(wbase + lane);
+            const uint2* sr = reinterpret_cast<const uint2*>(src) + wbase + lane;
+            const uint32_t* sk = src + wbase + lane;
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) {
+                if (KV) x[j] = j * 64 < lim ? ((sr[j * 64].x & 0xFFFFu) << 16) | (wbase + (uint32_t)j * 64u + lane) : kPadKey;
+                else x[j] = j * 64 < lim ? sk[j * 64] : kPadKey;
+            }
+        }
+        // KV: the key's low 16 bits sit in w's high half; keys only: the key itself
+        constexpr uint32_t S0 = KV ? 16u : 0u;
+#pragma unroll 1
+        for (uint32_t shift = S0; shift < S0 + 16u; shift += 8u) {
+            Slots<KPT, true> rank;
+            uint32_t c;
+            const uint32_t tstart = rank_tile<8, NW, KPT, RANK>(x, rank, s_whist, s_scratch, shift, 255u, 0u, c);
+            if (tid < (uint32_t)RADIX) set_wave_offsets<8, NW>(s_whist, tstart);
+            __syncthreads();
+            const uint32_t sh = opaque_u(shift);
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) s_w[s_whist[w][(x[j] >> sh) & 255u] + rank.get(j)] = x[j];
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) x[j] = s_w[wbase + (uint32_t)j * 64u + lane];
+            __syncthreads();
+        }
+        // the values to their sorted positions: the bucket's records are read again (this
+        // workgroup read them moments ago: Infinity Cache / L2) into LDS by position, then each
+        // sorted slot gathers its value by the position in w (holding the values in registers
+        // through the sort spilled)
+        if (KV) {
+            const int lim = (int)cnt - (int)(wbase + lane);
+            const uint2* sr = reinterpret_cast<const uint2*>(src) + wbase + lane;
+            uint32_t* sw = s_w + wbase + lane;
+#pragma unroll
+            for (int j = 0; j < KPT; ++j)
+                if (j * 64 < lim) sw[j * 64] = sr[j * 64].y;
+            __syncthreads();
+        }
+        const uint32_t hi = b << bshift;
+        // one base address per output array, constant per-slot offsets (per-slot 64-bit addresses
+        // spilled); slot j is real iff j * 64 < lim (pads sort last)
+        const size_t o0 = (size_t)base + wbase + lane;
+        const int lim = (int)cnt - (int)(wbase + lane);
+        uint2* oa = reinterpret_cast<uint2*>(out_k) + o0;
+        uint32_t* ok = out_k + o0;
+        uint32_t* ov = KV && LO != LAYOUT_AOS ? out_v + o0 : nullptr;
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) {
+            if (j * 64 < lim) {
+                const uint32_t key = (KV ? (hi | (x[j] >> 16)) : x[j]) + kbase;
+                const uint32_t val = KV ? s_w[x[j] & 0xFFFFu] : 0u;
+                if constexpr (LO == LAYOUT_AOS) {
+                    oa[j * 64] = make_uint2(key, val);
+                } else {
+                    ok[j * 64] = key;
+                    if constexpr (KV) ov[j * 64] = val;
+                }
+            }
+        }
+        __syncthreads();   // s_whist / s_w are reused by the next bucket
     }
 }
 

@@ -29,6 +29,24 @@
 
 #define RS_EXPORT extern "C" __attribute__((visibility("default")))
 
+// Tuning knobs.  The product library has none beyond the per-plan path choices read at plan
+// creation (rs_plan_create: RSORT_MSD / ONESWEEP / RANK / TILE / KEYS_CFG / MSD_KEYS_CFG /
+// KBUCKET_WAVE / SPIN_MAX, which the parity tests use to cover every path).  The sweep build
+// (`make variants`, tools/sweep.py: -DRS_SWEEP=1) adds the process-wide experiment knobs and the
+// alternative kernel instantiations they select; a product build compiles neither.
+#ifndef RS_SWEEP
+#define RS_SWEEP 0
+#endif
+#if RS_SWEEP
+static double sweep_knob(const char* name, double dflt) {
+    const char* e = getenv(name);
+    return e ? atof(e) : dflt;
+}
+#define RS_KNOB(name, dflt) sweep_knob(name, dflt)
+#else
+#define RS_KNOB(name, dflt) (dflt)
+#endif
+
 namespace {
 
 thread_local std::string g_err;
@@ -77,6 +95,7 @@ constexpr TileCfg kSmall{256, 16, 4096, 1024};
 #define RS_KEYS_KPT 32
 #endif
 constexpr TileCfg kLargeKeys{RS_KEYS_BLOCK, RS_KEYS_KPT, RS_KEYS_BLOCK * RS_KEYS_KPT, 512};
+#if RS_SWEEP
 // one-sweep passes that read a plan-owned records buffer (padded to whole tiles): 24K-record
 // tiles (1024 threads x 24 records, positions packed 16-bit) staged through LDS in two rounds of
 // 12K; longer digit runs per tile than 16K tiles (fewer lines shared by two tiles' runs)
@@ -91,19 +110,22 @@ constexpr TileCfg kKv512x16{512, 16, 8192, 1024};
 constexpr TileCfg kKv512x32{512, 32, 16384, 1024};
 constexpr TileCfg kKv256x32{256, 32, 8192, 2048};
 constexpr TileCfg kKv512x24{512, 24, 12288, 1024};
+#endif
 constexpr uint32_t kMinOnesweepTile = 8192;   // finest one-sweep tile (status words per plan)
 constexpr uint64_t kRecPad = 49152;           // records buffers: whole tiles of every config
 constexpr uint32_t kTinyMax = 1024 * 16;
-// Hybrid MSD path (enqueue_sort_msd): used for key/value arrays and records of >= kMsdMin keys when
-// no top-byte bucket exceeds kMsdMaxTop keys (decided on the device); 16-bit buckets of up to
-// kBucketCap records are sorted in LDS (k_bucket_sort<kBucketBlock, kBucketKpt>).
+// Hybrid MSD path (enqueue_sort_msd): used for key/value arrays and records of kMsdMin ... kMsdMax
+// keys when no 16-bit bucket exceeds kBucketCap records (decided on the device); buckets are sorted
+// in LDS by k_bucket_sort (tiles sized to the population) or, the largest, k_bucket_sort_wide.
 #ifndef RS_MSD_DEFAULT
 #define RS_MSD_DEFAULT 1
 #endif
 constexpr uint64_t kMsdMin = 12ull << 20;
-constexpr uint32_t kMsdMaxTop = 3u << 19;
-constexpr int kBucketBlock = 1024, kBucketKpt = 16;    // the large bucket tile (overflow launch)
-constexpr uint32_t kBucketCap = kBucketBlock * kBucketKpt;
+constexpr int kWideKpt = 34;                            // k_bucket_sort_wide: 1024 x 34 records
+constexpr uint32_t kBucketCap = 1024u * kWideKpt;       // the largest 16-bit bucket the path sorts
+// a uniform population's largest bucket (mean + ~5 sigma) still fits kBucketCap up to here (2^31
+// keys: mean 32768, sigma 181); above it the device would always pick the LSD fallback
+constexpr uint64_t kMsdMax = 65536ull * 33800;
 constexpr uint64_t kMsdWords = 65536ull * 2 + 1024 + 64 + 1024 + 1 + rs::kOverMax;   // hist16, base16,
                                                                     // segtab, gates, mtot, over
 constexpr uint32_t kHistGrid = 2048;
@@ -172,6 +194,7 @@ struct rs_plan {
     bool has_values = false, check_order = false, local_shuffle = false;
     int layout = rs::LAYOUT_KEYS;          // rs::Layout of the caller's data
     int rank_mode = rs::RANK_LDS_ATOMIC;   // RSORT_RANK=ballot selects the ballot-match ranking
+    int tile_mode = -1;                    // RSORT_TILE: -1 by size, 0 large tiles, 1 small tiles
     uint32_t passes = 0;
     uint32_t widths[16] = {};
     uint64_t capacity = 0;
@@ -182,14 +205,14 @@ struct rs_plan {
     uint32_t* flags = nullptr;     // [16] check_order results
     // one-sweep path (k_pass_totals + k_onesweep)
     int onesweep_mode = -1;                // -1 auto (use_onesweep), 0 off, 1 on (RSORT_ONESWEEP)
-    bool aos_tmp = true;                   // one-sweep KV: records as the ping-pong copy (RSORT_AOS_TMP)
-    uint32_t* tmp2 = nullptr;              // one-sweep KV: second records buffer (RSORT_RECS2=0: none)
+    bool aos_tmp = true;                   // one-sweep KV: records as the ping-pong copy (sweep: RSORT_AOS_TMP)
+    uint32_t* tmp2 = nullptr;              // one-sweep KV: second records buffer (sweep: RSORT_RECS2=0: none)
     bool keys_cfg = true;                  // keys-only 512x32 tiles (RSORT_KEYS_CFG=0: 1024x16)
-    int kv_cfg = 0;                        // one-sweep KV tile configuration (RSORT_KV_CFG)
-    int huge_tiles = 0;                    // one-sweep KV: 24K-record tiles (RSORT_HUGE=1: every
+    int kv_cfg = 0;                        // one-sweep KV tile configuration (sweep: RSORT_KV_CFG)
+    int huge_tiles = 0;                    // one-sweep KV: 24K-record tiles (sweep: RSORT_HUGE=1: every
                                            // pass; 2: the records -> arrays pass only)
     bool fused_check = true;               // one-sweep check_order: passes > 0 check their input
-                                           // in k_onesweep (RSORT_FUSED_CHECK=0: k_check)
+                                           // in k_onesweep (sweep: RSORT_FUSED_CHECK=0: k_check)
     unsigned long long* status = nullptr;  // [max_tiles][256] look-back status words
     uint64_t status_words = 0;
     uint32_t* ptot = nullptr;      // [kTotalsMax] whole-array digit totals of every pass
@@ -201,7 +224,7 @@ struct rs_plan {
     // keys-only form of the hybrid MSD path, read per plan (tests switch them):
     int msd_keys_cfg = 1;            // pass tiles (RSORT_MSD_KEYS_CFG): 0 1024x16, 1 512x32, 2 1024x32
     bool kbucket_wave = true;        // one wave per 16-bit bucket (RSORT_KBUCKET_WAVE=0: workgroups)
-    bool kbucket_pf = false;         // workgroup kernel on a persistent prefetching grid (RSORT_KBUCKET_PF=1)
+    bool kbucket_pf = false;         // workgroup kernel on a persistent prefetching grid (sweep: RSORT_KBUCKET_PF=1)
     uint32_t* msd = nullptr;         // its workspace: hist16 | base16 | segtab | gates | mtot
     int scatter_kind = RS_KERNEL_SCATTER;   // timer kind of the pass launches being enqueued
     uint32_t* host_err = nullptr;  // host-mapped error word: set by a timed-out look-back wait,
@@ -227,8 +250,8 @@ uint32_t pick_R(uint32_t w) { return w <= 2 ? 2 : (w <= 4 ? 4 : 8); }
 
 uint32_t full_mask(uint32_t bits) { return bits >= 32 ? 0xFFFFFFFFu : ((1u << bits) - 1u); }
 
-bool use_small_tiles(uint64_t n) {
-    if (const char* e = getenv("RSORT_TILE")) return strcmp(e, "small") == 0;
+bool use_small_tiles(const rs_plan* p, uint64_t n) {
+    if (p->tile_mode >= 0) return p->tile_mode == 1;
     return n < RS_SMALL_MAX;
 }
 
@@ -292,8 +315,9 @@ void launch_onesweep_t(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint3
                        const uint32_t* gate, int pass, hipStream_t s) {
     auto kern = rs::k_onesweep<R, BLOCK, KPT, L, RANK, LO, SR>;
     static const uint32_t per_cu = resident_per_cu(kern, BLOCK);   // per instantiation
-    // RSORT_OS_GRID caps the persistent grid (tiles come from tickets, so any grid >= 1 is correct)
-    static const uint32_t cap = [] { const char* g = getenv("RSORT_OS_GRID"); return g ? (uint32_t)atoi(g) : 0u; }();
+    // sweep: RSORT_OS_GRID caps the persistent grid (tiles come from tickets, so any grid >= 1 is
+    // correct)
+    const uint32_t cap = (uint32_t)RS_KNOB("RSORT_OS_GRID", 0);
     uint32_t grid = std::min<uint32_t>(ntiles, p->cus * per_cu);
     if (cap > 0 && cap < grid) grid = cap;
     const bool last = (uint32_t)pass + 1 >= p->passes;
@@ -306,7 +330,7 @@ void launch_onesweep_t(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint3
                        p->ptot + p->ptot_off[pass], p->status, p->tickets + pass,
                        p->tickets + 16, ntot, nshift, nmask, p->epoch, gate, pass, chk,
                        full_mask(p->bit_count), p->spin_max, p->host_err_dev,
-                       (const uint32_t*)nullptr, (const uint32_t*)nullptr, 0u);
+                       (const uint32_t*)nullptr, (const uint32_t*)nullptr, 0u, 0xFFFFFFFFu);
 }
 
 template <int R, int BLOCK, int KPT, int L, int LO, int SR>
@@ -335,14 +359,15 @@ template <int L, int LO, int SEG, bool KB = false, int BLOCK = kLarge.block, int
 void launch_msd_pass(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint32_t* ok, uint32_t* ov,
                      uint32_t n, uint32_t shift, uint32_t ntiles, const uint32_t* dtot, uint32_t* ticket,
                      const uint32_t* gate, const uint32_t* segtab, const uint32_t* base16,
-                     hipStream_t s, uint32_t kbase = 0) {
+                     hipStream_t s, uint32_t kbase = 0, uint32_t pmask = 0xFFFFFFFFu) {
     static_assert(BLOCK * KPT == kLarge.tile || BLOCK * KPT == 2 * kLarge.tile, "k_msd_plan tile sizes");
     auto go = [&](auto kern) {
         static const uint32_t per_cu = resident_per_cu(kern, BLOCK);
         const uint32_t grid = std::min<uint32_t>(ntiles, p->cus * per_cu);
         hipLaunchKernelGGL(kern, dim3(grid), dim3(BLOCK), 0, s, ik, iv, ok, ov, n, shift, 255u,
                            ntiles, dtot, p->status, ticket, p->tickets + 16, nullptr, 0u, 0u, p->epoch,
-                           gate, 0, nullptr, 0xFFFFFFFFu, p->spin_max, p->host_err_dev, segtab, base16, kbase);
+                           gate, 0, nullptr, 0xFFFFFFFFu, p->spin_max, p->host_err_dev, segtab, base16, kbase,
+                           pmask);
     };
     if (p->rank_mode == rs::RANK_BALLOT)
         go(rs::k_onesweep<8, BLOCK, KPT, L, rs::RANK_BALLOT, LO, 1, SEG, KB>);
@@ -418,13 +443,15 @@ rs_status run_pass(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint32_t*
                    uint32_t* ov, uint32_t n, uint32_t shift, uint32_t w, int LL,
                    const uint32_t* gate, int pass, hipStream_t s, bool onesweep = false) {
     const uint32_t R = pick_R(w);
-    if (use_small_tiles(n)) {
+    if (use_small_tiles(p, n)) {
         if (R == 2) return run_pass_cfg<2, kSmall.block, kSmall.kpt>(p, ik, iv, ok, ov, n, shift, w, LL, gate, pass, kSmall.max_grid, onesweep, s);
         if (R == 4) return run_pass_cfg<4, kSmall.block, kSmall.kpt>(p, ik, iv, ok, ov, n, shift, w, LL, gate, pass, kSmall.max_grid, onesweep, s);
         return run_pass_cfg<8, kSmall.block, kSmall.kpt>(p, ik, iv, ok, ov, n, shift, w, LL, gate, pass, kSmall.max_grid, onesweep, s);
     }
-    // with values; records only from a plan-owned buffer padded to whole kHuge tiles (the
-    // kernel loads whole record tiles without per-slot bounds, see k_onesweep's SR > 1)
+#if RS_SWEEP
+    // sweep only: 24K-record tiles with values (records only from a plan-owned buffer padded to
+    // whole kHuge tiles: the kernel loads whole record tiles without per-slot bounds, see
+    // k_onesweep's SR > 1), and the KV tile configurations with several workgroups per CU
     const int Lin = LL & 15;
     if (R == 8 && onesweep && p->huge_tiles &&
         (p->huge_tiles == 1 || LL == layout_pair(rs::LAYOUT_AOS, rs::LAYOUT_SOA)) &&
@@ -445,6 +472,7 @@ rs_status run_pass(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint32_t*
         }
         return run_pass_cfg<8, kKv512x16.block, kKv512x16.kpt>(p, ik, iv, ok, ov, n, shift, w, LL, gate, pass, kKv512x16.max_grid, onesweep, s);
     }
+#endif
     if (R == 8 && LL == layout_pair(rs::LAYOUT_KEYS, rs::LAYOUT_KEYS) && p->keys_cfg)
         return run_pass_cfg<8, kLargeKeys.block, kLargeKeys.kpt, true>(p, ik, iv, ok, ov, n, shift, w, LL, gate, pass, kLargeKeys.max_grid, onesweep, s);
     if (R == 2) return run_pass_cfg<2, kLarge.block, kLarge.kpt>(p, ik, iv, ok, ov, n, shift, w, LL, gate, pass, kLarge.max_grid, onesweep, s);
@@ -482,17 +510,18 @@ rs_status run_tiny(rs_plan* p, uint32_t* k, uint32_t* v, uint32_t n, hipStream_t
 // and on small tiles (thousands of tiles in flight at once make long look-back chains).
 bool use_onesweep(const rs_plan* p, uint64_t n) {
     if (p->onesweep_mode >= 0) return p->onesweep_mode == 1;
-    return p->layout != rs::LAYOUT_KEYS && !use_small_tiles(n);
+    return p->layout != rs::LAYOUT_KEYS && !use_small_tiles(p, n);
 }
 
 // The hybrid MSD path applies (the device still falls back to the LSD passes for skewed keys).
 bool use_msd(const rs_plan* p, uint64_t n) {
     if (!p->msd || p->msd_mode == 0 || p->check_order || p->bit_count != 32 || p->radix_bits != 8 ||
-        use_small_tiles(n) || n < kMsdMin)
+        use_small_tiles(p, n) || n < kMsdMin)
         return false;
-    // above 256 * kMsdMaxTop keys some top byte always holds more than kMsdMaxTop (pigeonhole):
-    // the device would always pick the fallback, so the histogram read would be wasted
-    if (n > 256ull * kMsdMaxTop) return false;
+    // above kMsdMax keys some 16-bit bucket is all but certain to exceed kBucketCap (and above
+    // 65536 * kBucketCap one must, pigeonhole): the device would pick the fallback, so the
+    // histogram read would be wasted
+    if (n > kMsdMax) return false;
     // keys only: R1 = tmp_k (n words, which first holds the histogram rows), R2 = the caller's keys;
     // the one-sweep passes of this path are its own (the keys-only LSD sort keeps the histogram path)
     if (p->layout == rs::LAYOUT_KEYS)
@@ -599,19 +628,23 @@ RS_EXPORT rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out) {
               : (p->has_values ? rs::LAYOUT_SOA : rs::LAYOUT_KEYS);
     p->check_order = d.flags & RS_FLAG_CHECK_ORDER;
     p->local_shuffle = d.flags & RS_FLAG_LOCAL_SHUFFLE;
+    // path choices (per plan; the parity tests switch them to cover every path)
     if (const char* os = getenv("RSORT_ONESWEEP")) p->onesweep_mode = strcmp(os, "0") != 0 ? 1 : 0;
-    if (const char* at = getenv("RSORT_AOS_TMP")) p->aos_tmp = strcmp(at, "0") != 0;
-    bool recs2 = true;
-    if (const char* r2 = getenv("RSORT_RECS2")) recs2 = strcmp(r2, "0") != 0;
+    if (const char* t = getenv("RSORT_TILE")) p->tile_mode = strcmp(t, "small") == 0 ? 1 : 0;
     if (const char* kc = getenv("RSORT_KEYS_CFG")) p->keys_cfg = strcmp(kc, "0") != 0;
-    if (const char* hg = getenv("RSORT_HUGE")) p->huge_tiles = atoi(hg);
-    if (const char* kc = getenv("RSORT_KV_CFG")) p->kv_cfg = atoi(kc);
-    if (const char* fc = getenv("RSORT_FUSED_CHECK")) p->fused_check = strcmp(fc, "0") != 0;
     if (const char* ms = getenv("RSORT_MSD")) p->msd_mode = strcmp(ms, "0") != 0 ? 1 : 0;
     if (const char* e = getenv("RSORT_MSD_KEYS_CFG")) p->msd_keys_cfg = atoi(e);
     if (const char* e = getenv("RSORT_KBUCKET_WAVE")) p->kbucket_wave = strcmp(e, "0") != 0;
-    if (const char* e = getenv("RSORT_KBUCKET_PF")) p->kbucket_pf = strcmp(e, "1") == 0;
     if (const char* sm = getenv("RSORT_SPIN_MAX")) p->spin_max = (uint32_t)strtoul(sm, nullptr, 10);
+    bool recs2 = true;
+#if RS_SWEEP
+    p->aos_tmp = RS_KNOB("RSORT_AOS_TMP", 1) != 0;
+    recs2 = RS_KNOB("RSORT_RECS2", 1) != 0;
+    p->huge_tiles = (int)RS_KNOB("RSORT_HUGE", 0);
+    p->kv_cfg = (int)RS_KNOB("RSORT_KV_CFG", 0);
+    p->fused_check = RS_KNOB("RSORT_FUSED_CHECK", 1) != 0;
+    p->kbucket_pf = RS_KNOB("RSORT_KBUCKET_PF", 0) == 1;
+#endif
     // Even number of passes so the result lands in the caller's buffers, like the reference's
     // bit_count/2 passes with ping-pong on bit % 4 (AbstractRadixSortKernel.ts:93-107).
     uint32_t P = (d.bit_count + rb - 1) / rb;
@@ -646,7 +679,9 @@ RS_EXPORT rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out) {
     const uint64_t max_tiles = std::max<uint64_t>(
         1, std::max<uint64_t>((d.count + kMinOnesweepTile - 1) / kMinOnesweepTile,
                               (std::min<uint64_t>(d.count, RS_SMALL_MAX) + kSmall.tile - 1) / kSmall.tile));
-    p->status_words = p->onesweep_mode != 0 ? max_tiles * 256 : 1;
+    // sized whatever RSORT_ONESWEEP says: the records / partition entry points and the hybrid
+    // path's passes are one-sweep passes on every plan
+    p->status_words = max_tiles * 256;
     hipError_t e;
     // with values the tmp copy is ONE 8n-byte buffer: (key, value) records for the one-sweep
     // path, or tmp_k / tmp_v halves (tmp_v = tmp_k + count) for the histogram path
@@ -764,7 +799,7 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
     // every bucket that fits it (at 2^28 keys: 4352 records, ~2 buckets over it), the large tile
     // the listed rest
     const double mean = (double)n / 65536.0;
-    static const double slack = [] { const char* e = getenv("RSORT_BUCKET_SLACK"); return e ? atof(e) : 1.0; }();
+    const double slack = RS_KNOB("RSORT_BUCKET_SLACK", 1.0);
     const uint32_t want = (uint32_t)(mean * slack + 4.0 * std::sqrt(mean));
     constexpr uint32_t bb = 256;
     static const uint32_t kpts[] = {4, 8, 12, 17, 18, 24};
@@ -781,16 +816,20 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
             if (!wave_kpt && want <= 64u * kpt) wave_kpt = kpt;
         if (wave_kpt) small_cap = 64u * wave_kpt;
     }
+    // buckets too large for every population-sized tile (~2^29 keys and more): the wide kernel
+    // takes every bucket, one workgroup each, and nothing is listed
+    const bool wide_all = small_cap == 0;
+    if (wide_all) small_cap = kBucketCap;
     // one histogram row per CU in tmp_k (R1 is written only after the rows are added)
     uint32_t* range_bad = mtot;
-    // RSORT_HIST16_DIV: one row per `div` CUs (fewer rows to write and add; sweeps)
-    static const uint32_t hdiv = [] { const char* e = getenv("RSORT_HIST16_DIV"); return e ? std::max(1, atoi(e)) : 1; }();
+    // sweep: RSORT_HIST16_DIV = one row per `div` CUs (fewer rows to write and add)
+    const uint32_t hdiv = std::max(1u, (uint32_t)RS_KNOB("RSORT_HIST16_DIV", 1));
     const uint32_t hrows = std::max(1u, p->cus / hdiv);
     p->timer.run(RS_KERNEL_HISTOGRAM, s, [&] {
-        // 16-byte aligned records: two per load (RSORT_HIST16_NARROW=1 keeps one per 8-byte load)
-        static const bool narrow = [] { const char* e = getenv("RSORT_HIST16_NARROW"); return e && strcmp(e, "1") == 0; }();
-        // the whole 32-bit range: the specialised counting (RSORT_HIST16_GENERIC=1 keeps the generic one)
-        static const bool generic = [] { const char* e = getenv("RSORT_HIST16_GENERIC"); return e && strcmp(e, "1") == 0; }();
+        // 16-byte aligned records: two per load (sweep: RSORT_HIST16_NARROW=1 keeps one per 8-byte load)
+        const bool narrow = RS_KNOB("RSORT_HIST16_NARROW", 0) == 1;
+        // the whole 32-bit range: the specialised counting (sweep: RSORT_HIST16_GENERIC=1 keeps the generic one)
+        const bool generic = RS_KNOB("RSORT_HIST16_GENERIC", 0) == 1;
         const bool full = !generic && kbase == 0u && vbits == 32u;
         auto go = [&](auto kern) {
             hipLaunchKernelGGL(kern, dim3(hrows), dim3(1024), 0, s, sk, n32, p->tmp_k, kbase, range, vbits - 16,
@@ -811,7 +850,7 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
     HIP_TRY(hipGetLastError());
     p->timer.run(RS_KERNEL_SCAN, s, [&] {
         auto plan = [&](auto kern) {
-            hipLaunchKernelGGL(kern, dim3(1), dim3(256), 0, s, (const uint32_t*)top_tot, segtab, kMsdMaxTop, over,
+            hipLaunchKernelGGL(kern, dim3(1), dim3(256), 0, s, (const uint32_t*)top_tot, segtab, 0xFFFFFFFFu, over,
                                (const uint32_t*)big, gates, (const uint32_t*)range_bad, n32);
         };
         if (tile == 2u * kLarge.tile) plan(rs::k_msd_plan<2 * kLarge.tile>);
@@ -819,6 +858,18 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
     });
     HIP_TRY(hipGetLastError());
     const uint32_t* g_msd = gates + rs::kGateMsd;
+    // R2 replaced by a power-of-two ring (sweep experiment RSORT_EXP_RING = log2 records; the
+    // results are then invalid: timing of an Infinity-Cache-resident R2 only)
+    uint32_t* ring = nullptr;
+    uint32_t rmask = 0xFFFFFFFFu;
+#if RS_SWEEP
+    if (const int rb = (int)RS_KNOB("RSORT_EXP_RING", 0); rb > 0 && !keys && !out_aos) {
+        static uint32_t* buf = nullptr;
+        if (!buf) HIP_TRY(hipMalloc((void**)&buf, 8ull * ((1ull << rb) + 65536)));
+        ring = buf;
+        rmask = (1u << rb) - 1u;
+    }
+#endif
     // MSD pass 0: input -> R1 records, partitioned by the top byte
     if (rs_status st = next_epoch(p, s)) return st;
     const bool keys_wide = keys_cfg == 0;
@@ -861,46 +912,62 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
                 p, r1, nullptr, r2, nullptr, n32, vbits - 16, ntiles + 257, nullptr, p->tickets + 5, g_msd,
                 segtab, base16, s);
         else
-            launch_msd_pass<A, A, 1>(p, r1, nullptr, r2, nullptr, n32, vbits - 16, ntiles + 257, nullptr,
-                                     p->tickets + 5, g_msd, segtab, base16, s);
+            launch_msd_pass<A, A, 1>(p, r1, nullptr, ring ? ring : r2, nullptr, n32, vbits - 16, ntiles + 257, nullptr,
+                                     p->tickets + 5, g_msd, segtab, base16, s, 0u, rmask);
     });
     HIP_TRY(hipGetLastError());
     const bool ballot = p->rank_mode == rs::RANK_BALLOT;
     constexpr int A0 = rs::RANK_LDS_ATOMIC, B0 = rs::RANK_BALLOT;
     p->timer.run(RS_KERNEL_BUCKET, s, [&] {
         auto small = [&](auto kern) {
-            hipLaunchKernelGGL(kern, dim3(65536), dim3(bb), 0, s, r2, hist16, base16, uk, uv, g_msd,
-                               p->tickets + 16, 0u, (const uint32_t*)nullptr, kbase, (const uint32_t*)sstart);
+            hipLaunchKernelGGL(kern, dim3(65536), dim3(bb), 0, s, ring ? ring : r2, hist16, base16, uk, uv, g_msd,
+                               p->tickets + 16, 0u, (const uint32_t*)nullptr, kbase, (const uint32_t*)sstart, rmask);
         };
-        // keys only: a persistent grid whose workgroups load their next bucket while sorting one
+#if RS_SWEEP
+        // sweep only, keys only: a persistent grid whose workgroups load their next bucket while
+        // sorting one (measured slower, 0.265 vs 0.245 ms)
         auto small_pf = [&](auto kern) {
             static const uint32_t per_cu = resident_per_cu(kern, bb);
-            static const uint32_t mult = [] { const char* e = getenv("RSORT_KBUCKET_GRID"); return e ? (uint32_t)atoi(e) : 1u; }();
-            const uint32_t grid = std::min<uint32_t>(65536u, p->cus * per_cu * std::max(1u, mult));
+            const uint32_t mult = std::max(1u, (uint32_t)RS_KNOB("RSORT_KBUCKET_GRID", 1));
+            const uint32_t grid = std::min<uint32_t>(65536u, p->cus * per_cu * mult);
             hipLaunchKernelGGL(kern, dim3(grid), dim3(bb), 0, s, r2, hist16, base16, uk, uv, g_msd,
-                               p->tickets + 16, 0u, (const uint32_t*)nullptr, kbase, (const uint32_t*)sstart);
+                               p->tickets + 16, 0u, (const uint32_t*)nullptr, kbase, (const uint32_t*)sstart,
+                               0xFFFFFFFFu);
         };
-        // RSORT_OVER_GRID: workgroups of the listed-bucket launch (sweeps)
-        static const uint32_t over_grid = [] { const char* e = getenv("RSORT_OVER_GRID"); return e ? (uint32_t)atoi(e) : 256u; }();
+#endif
+        // the wide kernel: every bucket (wide_all), or the listed buckets over the population-sized
+        // tile on a small persistent grid (sweep: RSORT_OVER_GRID workgroups)
+        const uint32_t over_grid = std::max(1u, (uint32_t)RS_KNOB("RSORT_OVER_GRID", 256));
         auto large = [&](auto kern) {
-            hipLaunchKernelGGL(kern, dim3(std::max(1u, over_grid)), dim3(kBucketBlock), 0, s, r2, hist16, base16, uk, uv,
-                               g_msd, p->tickets + 16, small_cap, (const uint32_t*)over, kbase, (const uint32_t*)sstart);
+            hipLaunchKernelGGL(kern, dim3(wide_all ? 65536u : over_grid), dim3(1024), 0, s, ring ? ring : r2,
+                               hist16, base16, uk, uv, g_msd, p->tickets + 16, wide_all ? 0u : small_cap,
+                               wide_all ? (const uint32_t*)nullptr : (const uint32_t*)over, kbase,
+                               (const uint32_t*)sstart, rmask, vbits - 16);
         };
         auto both = [&](auto lo) {
             constexpr int LO = decltype(lo)::value;
 #define RS_BK(KP) case KP: ballot ? small(rs::k_bucket_sort<bb, KP, B0, LO, (KP <= 18 ? 3 : 1)>) : small(rs::k_bucket_sort<bb, KP, A0, LO, (KP <= 18 ? 3 : 1)>); break;
             if constexpr (LO == K) {
-                static const int wpb = [] { const char* e = getenv("RSORT_KWAVE_WPB"); return e ? atoi(e) : 4; }();
-                if (wave_kpt && wave_kpt == 18 && !ballot && (wpb == 2 || wpb == 8)) {
-                    // sweep only: 2 or 8 waves (buckets) per workgroup
+                bool wave_done = false;
+#if RS_SWEEP
+                // sweep only: 2 or 8 waves (buckets) per workgroup (RSORT_KWAVE_WPB), or more waves
+                // per SIMD forced through the VGPR budget (RSORT_KWAVE_MW: spilled and was slower)
+                const int wpb = (int)RS_KNOB("RSORT_KWAVE_WPB", 4), mw = (int)RS_KNOB("RSORT_KWAVE_MW", 1);
+                if (wave_kpt == 18 && !ballot && (wpb == 2 || wpb == 8 || mw >= 5)) {
                     auto wave = [&](auto kern, int w) {
                         hipLaunchKernelGGL(kern, dim3(65536 / w), dim3(64 * w), 0, s, uk, (const uint32_t*)hist16,
                                            (const uint32_t*)base16, g_msd, (const uint32_t*)sstart);
                     };
                     if (wpb == 2) wave(rs::k_bucket_sort_keys_wave<18, A0, 2>, 2);
-                    else wave(rs::k_bucket_sort_keys_wave<18, A0, 8>, 8);
+                    else if (wpb == 8) wave(rs::k_bucket_sort_keys_wave<18, A0, 8>, 8);
+                    else if (mw == 7) wave(rs::k_bucket_sort_keys_wave<18, A0, 4, 7>, 4);
+                    else if (mw == 6) wave(rs::k_bucket_sort_keys_wave<18, A0, 4, 6>, 4);
+                    else wave(rs::k_bucket_sort_keys_wave<18, A0, 4, 5>, 4);
                     small_kpt = 0;
-                } else if (wave_kpt) {
+                    wave_done = true;
+                }
+#endif
+                if (wave_kpt && !wave_done) {
                     constexpr int WPB = 4;
                     auto wave = [&](auto kern) {
                         hipLaunchKernelGGL(kern, dim3(65536 / WPB), dim3(64 * WPB), 0, s, uk, (const uint32_t*)hist16,
@@ -908,33 +975,25 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
                     };
                     if (wave_kpt == 10)
                         ballot ? wave(rs::k_bucket_sort_keys_wave<10, B0, WPB>) : wave(rs::k_bucket_sort_keys_wave<10, A0, WPB>);
-                    else if (ballot)
-                        wave(rs::k_bucket_sort_keys_wave<18, B0, WPB>);
-                    else {
-                        // waves per SIMD the compiler must fit (VGPR budget): RSORT_KWAVE_MW sweeps
-                        static const int mw = [] { const char* e = getenv("RSORT_KWAVE_MW"); return e ? atoi(e) : 1; }();
-                        if (mw == 7) wave(rs::k_bucket_sort_keys_wave<18, A0, WPB, 7>);
-                        else if (mw == 6) wave(rs::k_bucket_sort_keys_wave<18, A0, WPB, 6>);
-                        else if (mw == 5) wave(rs::k_bucket_sort_keys_wave<18, A0, WPB, 5>);
-                        else wave(rs::k_bucket_sort_keys_wave<18, A0, WPB>);
-                    }
+                    else
+                        ballot ? wave(rs::k_bucket_sort_keys_wave<18, B0, WPB>) : wave(rs::k_bucket_sort_keys_wave<18, A0, WPB>);
                     small_kpt = 0;   // no workgroup-per-bucket launch
                 }
-                // persistent grid + next-bucket prefetch (RSORT_KBUCKET_PF=1): measured slower, 0.265 vs 0.245 ms
-                const bool pf = p->kbucket_pf;
+#if RS_SWEEP
 #define RS_BKP(KP) case KP: ballot ? small_pf(rs::k_bucket_sort<bb, KP, B0, LO, 4, 1>) : small_pf(rs::k_bucket_sort<bb, KP, A0, LO, 4, 1>); break;
-                if (pf) {
+                if (p->kbucket_pf) {
                     switch (small_kpt) {
                         RS_BKP(4) RS_BKP(5) RS_BKP(9) RS_BKP(17) RS_BKP(24)
                         default: break;
                     }
-                } else {
-                    switch (small_kpt) {
-                        RS_BK(4) RS_BK(5) RS_BK(9) RS_BK(17) RS_BK(24)
-                        default: break;
-                    }
+                    small_kpt = 0;
                 }
 #undef RS_BKP
+#endif
+                switch (small_kpt) {
+                    RS_BK(4) RS_BK(5) RS_BK(9) RS_BK(17) RS_BK(24)
+                    default: break;
+                }
             } else {
                 switch (small_kpt) {
                     RS_BK(4) RS_BK(8) RS_BK(12) RS_BK(17) RS_BK(18) RS_BK(24)
@@ -942,9 +1001,9 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
                 }
             }
 #undef RS_BK
-            // the listed buckets (none for uniform keys): a small persistent grid over the list
-            ballot ? large(rs::k_bucket_sort<kBucketBlock, kBucketKpt, B0, LO>)
-                   : large(rs::k_bucket_sort<kBucketBlock, kBucketKpt, A0, LO>);
+            // the listed buckets (none for uniform keys below ~2^29), or every bucket (wide_all)
+            ballot ? large(rs::k_bucket_sort_wide<kWideKpt, B0, LO>)
+                   : large(rs::k_bucket_sort_wide<kWideKpt, A0, LO>);
         };
         if (keys) both(std::integral_constant<int, K>{});
         else if (out_aos) both(std::integral_constant<int, A>{});
@@ -1386,7 +1445,7 @@ RS_EXPORT rs_status rs_plan_info_get(const rs_plan* p, rs_plan_info* info) {
     memset(info, 0, sizeof(*info));
     info->passes = p->passes;
     for (uint32_t i = 0; i < p->passes && i < 16; ++i) info->digit_bits[i] = p->widths[i];
-    const TileCfg& c = use_small_tiles(p->capacity) ? kSmall : kLarge;
+    const TileCfg& c = use_small_tiles(p, p->capacity) ? kSmall : kLarge;
     info->tile_keys = p->capacity <= kTinyMax ? kTinyMax : (uint32_t)c.tile;
     info->grid_blocks = p->capacity <= kTinyMax ? 1u
         : (uint32_t)std::min<uint64_t>((p->capacity + c.tile - 1) / c.tile, c.max_grid);

@@ -26,7 +26,7 @@ extern "C" {
 #endif
 
 #define RSORT_VERSION_MAJOR 0
-#define RSORT_VERSION_MINOR 4
+#define RSORT_VERSION_MINOR 5
 
 typedef enum rs_status {
     RS_OK = 0,
@@ -68,8 +68,13 @@ typedef struct rs_plan_desc {
     uint32_t radix_bits;    /* digit bits per HBM pass: 0 = auto (fused: 8-bit digits, four
                                4-way splits per pass); 2 = one 4-way split per pass, the
                                reference's pass structure (bit_count/2 passes); 4 or 8 */
-    uint32_t reserved;
+    uint32_t usage;         /* RS_USAGE_SORT (0): every entry point; RS_USAGE_PARTITION: only
+                               rs_plan_hist16 and the rs_plan_partition* passes (the multi-GPU
+                               sender side) - no ping-pong copy is allocated */
 } rs_plan_desc;
+
+#define RS_USAGE_SORT      0u
+#define RS_USAGE_PARTITION 1u
 
 typedef struct rs_plan rs_plan;
 
@@ -153,6 +158,24 @@ rs_status rs_plan_sort_records(rs_plan* plan, const void* records, void* keys_ou
 rs_status rs_plan_sort_records_range(rs_plan* plan, const void* records, void* keys_out,
                                      void* values_out, uint64_t n, uint32_t key_lo, uint32_t key_hi,
                                      void* stream);
+/* Multi-GPU bucket path (52 B/key per rank: the single-GPU hybrid sort's bytes, split across the
+ * exchange).  Sender: rs_plan_hist16 counts keys[0..n) (4-byte keys; records with
+ * RS_FLAG_INTERLEAVED) per 16-bit bucket key >> 16 in one read: d_hist16[0..65536) = the bucket
+ * counts, d_hist16[65536..65792) = the top-byte totals (their sums; what rs_plan_partition_records
+ * takes as d_totals).  The senders' tables are all-gathered: every receiver then knows the layout of
+ * what it will receive.  Receiver: rs_plan_sort_region sorts n records whose keys all have a top
+ * byte in [top_lo, top_hi) and that arrive grouped by top byte in increasing order (each group in
+ * global input order: the stable partition's output, source ranks in order) into separate arrays;
+ * d_hist16 (device, 65536 u32) = the region's count per 16-bit bucket, 0 outside
+ * [top_lo << 8, top_hi << 8).  The top-byte pass is the senders' partition, so the region takes
+ * only the next-byte pass (per top-byte segment) and the in-LDS bucket sort; a bucket larger than
+ * the bucket tile, or counts that do not add up to n, make the device sort the region with the
+ * LSD passes instead (the result is always the stable sort).  records[] is only read. */
+#define RS_HIST16_WORDS 65792u
+rs_status rs_plan_hist16(rs_plan* plan, const void* keys, uint64_t n, void* d_hist16, void* stream);
+rs_status rs_plan_sort_region(rs_plan* plan, const void* records, void* keys_out, void* values_out,
+                              uint64_t n, const void* d_hist16, uint32_t top_lo, uint32_t top_hi,
+                              void* stream);
 rs_status rs_plan_info_get(const rs_plan* plan, rs_plan_info* info);
 /* Kernel timing: when enabled, every launch of the plan is bracketed by HIP events on the
  * launch stream and per-kind durations are accumulated (read after synchronising). */

@@ -20,14 +20,14 @@ def test_library_exports_every_header_symbol():
 
 def test_version_and_status_strings():
     L = _lib.load()
-    assert L.rs_version() == (0 << 16) | 4
+    assert L.rs_version() == (0 << 16) | 5
     assert L.rs_status_string(_lib.RS_ERR_NOT_POW2).decode().startswith("workgroup")
     assert "device-side failure" in L.rs_status_string(_lib.RS_ERR_DEVICE).decode()
 
 
 def _create(**kw):
     d = dict(device=0, count=1000, bit_count=32, workgroup_x=16, workgroup_y=16, flags=0,
-             radix_bits=0, reserved=0)
+             radix_bits=0, usage=0)
     d.update(kw)
     desc = _lib.PlanDesc(**d)
     p = ctypes.c_void_p()
@@ -50,6 +50,8 @@ def test_plan_rejects_bad_bit_count(bits):
 
 def test_plan_rejects_bad_radix_bits_and_flags():
     assert _create(radix_bits=3)[0] == _lib.RS_ERR_INVALID_ARG
+    assert _create(usage=2)[0] == _lib.RS_ERR_INVALID_ARG
+    assert "usage" in _lib.load().rs_last_error().decode()
     assert _create(flags=0x100)[0] == _lib.RS_ERR_INVALID_ARG
     assert _create(count=1 << 33)[0] == _lib.RS_ERR_INVALID_ARG
 

@@ -24,10 +24,11 @@ class OracleLocalOps:
     def empty(self, n, like):
         return torch.empty(n, dtype=like.dtype)
 
-    def histogram(self, keys, shift, bits):
+    def hist16(self, keys):
         k = keys.numpy().view(np.uint32)
-        top = (k >> np.uint32(shift)) & np.uint32((1 << bits) - 1)
-        return torch.from_numpy(np.bincount(top, minlength=1 << bits).astype(np.int32))
+        h = np.bincount(k >> np.uint32(16), minlength=1 << 16).astype(np.int64)
+        top = h.reshape(256, 256).sum(axis=1)
+        return torch.from_numpy(np.concatenate([h, top]).astype(np.int32))
 
     def partition(self, keys, values, shift, bits, totals):
         k = keys.numpy().view(np.uint32)
@@ -40,12 +41,16 @@ class OracleLocalOps:
         rec = k[perm].astype(np.uint64) | (v.astype(np.uint64) << np.uint64(32))
         return torch.from_numpy(rec.view(np.int64))
 
-    def sort_records(self, records, keys_out, values_out, key_range=None):
+    def sort_region(self, records, keys_out, values_out, hist16, top_lo, top_hi):
         r = records.numpy().view(np.uint64)
         k = (r & np.uint64(0xFFFFFFFF)).astype(np.uint32)
         v = (r >> np.uint64(32)).astype(np.uint32)
-        if key_range is not None and k.size:   # the hint the exchange passes is exact
-            assert key_range[0] <= int(k.min()) and int(k.max()) <= key_range[1]
+        # the region contract the exchange must meet: grouped by top byte in [top_lo, top_hi),
+        # ascending, and the table = its 16-bit bucket counts (zero elsewhere)
+        top = k >> np.uint32(24)
+        assert (np.diff(top.astype(np.int64)) >= 0).all()
+        assert k.size == 0 or (top_lo <= int(top[0]) and int(top[-1]) < top_hi)
+        assert (np.bincount(k >> np.uint32(16), minlength=1 << 16) == hist16.numpy()).all()
         ok, ov = O.stable_sort_masked(k, v, 32)
         keys_out.numpy().view(np.uint32)[:] = ok
         values_out.numpy().view(np.uint32)[:] = ov
@@ -155,7 +160,7 @@ def test_bucket_owners_balanced_and_whole():
     assert sum(r0) + sum(r1) == 150 and (sum(r0) == 0 or sum(r1) == 0)
 
 
-def test_group_plan_rounds_are_contiguous_and_source_ordered():
+def test_group_plan_rounds_are_contiguous_and_byte_major():
     # world 2, 4 buckets, 2 rounds: rank 0 owns buckets [0, 2), rank 1 [2, 4)
     h = [[1, 2, 3, 4], [4, 3, 2, 1]]
     bounds = bucket_owners(h, 2)
@@ -163,10 +168,15 @@ def test_group_plan_rounds_are_contiguous_and_source_ordered():
     cuts = bucket_groups(h, bounds, 2)
     assert cuts == [[0, 1, 2], [2, 3, 4]]
     p = group_plan(h, cuts, 1, 2)
-    # rank 1's partitioned slice: bucket 0 at [0, 4), 1 at [4, 7), 2 at [7, 9), 3 at [9, 10)
-    assert p.send == [[(0, 4), (7, 9)], [(4, 7), (9, 10)]]
-    assert p.recv == [[3, 2], [4, 1]]                       # bucket 2, then bucket 3, per source
-    assert p.off == [[0, 3], [5, 9]] and p.base == [0, 5, 10]
+    # rank 1's partitioned slice: bucket 0 at [0, 4), 1 at [4, 7), 2 at [7, 9), 3 at [9, 10);
+    # one chunk per (peer, bucket)
+    assert p.send == [[(0, 0, 4), (1, 7, 9)], [(0, 4, 7), (1, 9, 10)]]
+    # round 0 = bucket 2: source 0's 3 records, then source 1's 2; round 1 = bucket 3: 4, then 1
+    assert p.recv == [[(0, 0, 3), (1, 3, 2)], [(0, 5, 4), (1, 9, 1)]]
+    assert p.base == [0, 5, 10] and p.cuts == [2, 3, 4]
+    # rank 0, two buckets in one round: byte-major, then source
+    p0 = group_plan(h, [[0, 2], [2, 4]], 0, 2)
+    assert p0.recv == [[(0, 0, 1), (1, 1, 4), (0, 5, 2), (1, 7, 3)]]
     # more rounds than buckets: empty rounds, still whole buckets in order
     c3 = bucket_groups(h, bounds, 4)
     assert all(len(c) == 5 and c == sorted(c) for c in c3)
@@ -204,6 +214,25 @@ def test_rccl_world1_hip_local_ops_round_trip(chunks):
         assert r2.n == n and (r2.keys.cpu().numpy().view(np.uint32) == ek).all()
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_rs_hist16_matches_bincount():
+    """The sender's 16-bit table (rs_plan_hist16): the bucket counts and the top-byte totals, on
+    a sort plan and on a partition-only plan, at sizes that use one row and many rows."""
+    from radix_sort_amd import _lib
+    from radix_sort_amd.ops import SortPlan
+    for n, usage in ((40_000, _lib.RS_USAGE_SORT), (3_000_017, _lib.RS_USAGE_PARTITION),
+                     (13_000_001, _lib.RS_USAGE_SORT)):
+        k = O.gen_u32(n, n)
+        kt = torch.from_numpy(k.view(np.int32)).cuda()
+        plan = SortPlan(0, n, True, usage=usage)
+        h = torch.empty(_lib.RS_HIST16_WORDS, dtype=torch.int32, device="cuda")
+        plan.hist16(kt, n, h)
+        exp = np.bincount(k >> np.uint32(16), minlength=1 << 16)
+        got = h.cpu().numpy()
+        assert (got[:65536] == exp).all() and (got[65536:] == exp.reshape(256, 256).sum(1)).all()
+        plan.destroy()
 
 
 @pytest.mark.gpu

@@ -5,18 +5,21 @@
 // (rsort.hip); the exchange is RCCL point-to-point (ncclCommInitAll + ncclGroupStart /
 // ncclSend / ncclRecv, the single-process multi-device pattern) or peer DMA copies.
 //
-// Per rank r (devices[r]), one sort:
-//   1. rs_histogram of the top digit of keys[r]            (sort stream; one key read)
-//   2. stable partition by the top digit into the send buffer (records with values), fed the
-//      step-1 counts (rs_plan_partition_records / _totals: one read of keys + values)
-//   3. the counts to the host (pinned copy, overlapped with 2), then the bucket plan on the host
-//      (rs_group_plan, identical to radix_sort_amd/distributed.py's bucket_owners/bucket_groups)
-//   4. `rounds` exchange rounds on the comm stream: round g sends rank q its round-g buckets (one
-//      contiguous range of the partitioned slice) and receives every source's round-g segment
-//      into [base_g + off_s, ...): source-major, so the region is the bucket range's keys in
-//      global input order; the own segment is a device copy
-//   5. the sort stream waits for round g only, then sorts region g (rs_plan_sort_records: records
-//      in, separate arrays out; keys only: rs_plan_sort_n in place) while later rounds move.
+// The exchange is the first pass of the single-GPU hybrid sort split across the ranks, so a rank
+// moves the bytes of one single-GPU sort of its share (52 B/key with values):
+//   1. rs_plan_hist16: the 16-bit bucket table of keys[r] (one key read, 4 B/key) -> pinned host
+//   2. the stable partition of keys[r] / values[r] by the top byte into the send buffer (records
+//      with values), fed the table's top-byte totals (16 B/key) = the hybrid sort's pass 0
+//   3. host: every rank's table; whole-top-byte ownership (~1/world of the keys per rank, equal keys
+//      never split) and `rounds` groups of top bytes per rank (rs_group_plan); every receiver's
+//      layout: round-major, then top byte, then source rank (so each top-byte segment of a round's
+//      region holds that byte's records in global input order), and its region tables (the 16-bit
+//      counts summed over the sources), uploaded to the receiver
+//   4. `rounds` exchange rounds on the comm stream: one message per (source, top byte) chunk, the
+//      own chunks device copies
+//   5. the sort stream waits for round g only, then sorts region g with rs_plan_sort_region (the
+//      segmented next-byte pass + the in-LDS bucket sort, 32 B/key; records in, separate arrays
+//      out) while later rounds move.  Keys only: the same exchange, rs_plan_sort_n per region.
 // At world size 1 nothing is exchanged: the slice is sorted straight from the input into the
 // output (rs_plan_sort_copy), no partition pass.
 #include <hip/hip_runtime.h>
@@ -110,14 +113,17 @@ struct Rank {
     hipEvent_t ev_in = nullptr, ev_part = nullptr, ev_hist = nullptr, ev_done = nullptr;
     hipEvent_t ev_round[kMaxRounds] = {};
     ncclComm_t comm = nullptr;
-    rs_plan* part = nullptr;        // partition pass (capacity = desc.capacity)
+    rs_plan* part = nullptr;        // 16-bit table + partition pass (RS_USAGE_PARTITION, capacity =
+                                    // desc.capacity)
     rs_plan* local = nullptr;       // local sorts (grows with the received regions)
     uint64_t local_cap = 0;
-    uint32_t* hist = nullptr;       // device [buckets]
-    uint32_t* hist_host = nullptr;  // pinned [buckets]
+    uint32_t* hist = nullptr;       // device [RS_HIST16_WORDS]: the slice's 16-bit table + top totals
+    uint32_t* hist_host = nullptr;  // pinned copy
+    uint32_t* reg = nullptr;        // device [rounds][65536]: this rank's region tables
+    uint32_t* reg_host = nullptr;   // pinned staging of them
     void* send = nullptr;           // partitioned slice (records or keys)
     uint64_t send_cap = 0;          // bytes
-    void* recv = nullptr;           // received regions, round-major then source-major
+    void* recv = nullptr;           // received regions: round-major, then top byte, then source
     uint64_t recv_cap = 0;
     uint32_t* out_k = nullptr;      // result with values: separate arrays
     uint32_t* out_v = nullptr;
@@ -177,6 +183,8 @@ RS_EXPORT void rs_group_destroy(rs_group* g) {
         if (k.local) rs_plan_destroy(k.local);
         (void)hipFree(k.hist);
         if (k.hist_host) (void)hipHostFree(k.hist_host);
+        (void)hipFree(k.reg);
+        if (k.reg_host) (void)hipHostFree(k.reg_host);
         (void)hipFree(k.send);
         (void)hipFree(k.recv);
         (void)hipFree(k.out_k);
@@ -204,7 +212,6 @@ static rs_status group_create(int32_t world, const int32_t* devices, const rs_gr
                     return gfail(RS_ERR_INVALID_ARG, "rs_group_create: device %d listed twice; RCCL needs one rank per device (RS_TRANSPORT_COPY allows virtual ranks)", devices[i]);
     }
     g->r.resize(world);
-    const uint32_t buckets = 1u << g->desc.top_bits;
     for (int i = 0; i < world; ++i) {
         Rank& k = g->r[i];
         k.device = devices[i];
@@ -215,14 +222,21 @@ static rs_status group_create(int32_t world, const int32_t* devices, const rs_gr
             G_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
         for (uint32_t j = 0; j < g->desc.rounds; ++j)
             G_HIP(hipEventCreateWithFlags(&k.ev_round[j], hipEventDisableTiming));
-        G_HIP(hipMalloc((void**)&k.hist, 4ull * buckets));
-        G_HIP(hipHostMalloc((void**)&k.hist_host, 4ull * buckets, hipHostMallocDefault));
         if (world > 1) {
+            G_HIP(hipMalloc((void**)&k.hist, 4ull * RS_HIST16_WORDS));
+            G_HIP(hipHostMalloc((void**)&k.hist_host, 4ull * RS_HIST16_WORDS, hipHostMallocDefault));
+            if (g->kv) {
+                G_HIP(hipMalloc((void**)&k.reg, 4ull * 65536 * g->desc.rounds));
+                G_HIP(hipHostMalloc((void**)&k.reg_host, 4ull * 65536 * g->desc.rounds, hipHostMallocDefault));
+            }
+            // the sender's plan: its 16-bit table and the partition pass only (no ping-pong copy;
+            // rs_plan_hist16 needs room for one histogram row: capacity >= 32768)
             rs_plan_desc pd{};
             pd.device = k.device;
-            pd.count = std::max<uint64_t>(g->desc.capacity, 1);
+            pd.count = std::max<uint64_t>(g->desc.capacity, 32768);
             pd.bit_count = 32;
             pd.flags = g->kv ? RS_FLAG_HAS_VALUES : 0u;
+            pd.usage = RS_USAGE_PARTITION;
             G_TRY(rs_plan_create(&pd, &k.part));
         }
         if (desc->transport == RS_TRANSPORT_COPY)
@@ -251,7 +265,9 @@ RS_EXPORT rs_status rs_group_create(int32_t world, const int32_t* devices, const
     rs_group_desc d = *desc;
     if (d.top_bits == 0) d.top_bits = 8;
     if (d.rounds == 0) d.rounds = 4;
-    if (d.top_bits > 8) return gfail(RS_ERR_INVALID_ARG, "rs_group_create: top_bits must be in [1, 8] (got %u)", d.top_bits);
+    if (d.top_bits != 8)
+        return gfail(RS_ERR_INVALID_ARG, "rs_group_create: top_bits must be 8 or 0 (got %u): the exchange digit is the top "
+                     "byte, the sort's first MSD pass", d.top_bits);
     if (d.rounds > kMaxRounds) return gfail(RS_ERR_INVALID_ARG, "rs_group_create: rounds must be in [1, %u] (got %u)", kMaxRounds, d.rounds);
     if (d.flags & ~RS_FLAG_HAS_VALUES) return gfail(RS_ERR_INVALID_ARG, "rs_group_create: flags may only hold RS_FLAG_HAS_VALUES (got 0x%x)", d.flags);
     if (d.transport != RS_TRANSPORT_RCCL && d.transport != RS_TRANSPORT_COPY)
@@ -336,53 +352,54 @@ RS_EXPORT rs_status rs_group_sort(rs_group* g, void* const* keys, void* const* v
     if (W == 1) {
         G_TRY(group_sort_world1(g, keys, values, counts[0]));
     } else {
-        // 1-2: top-digit counts, their copy to the host, then the partition (fed the counts)
+        // 1-2: the 16-bit table, its copy to the host, then the partition (fed the top totals)
         for (int i = 0; i < W; ++i) {
             Rank& k = g->r[i];
             Dev dev(k.device);
             const uint64_t n = counts[i];
             G_TRY(grow(&k.send, &k.send_cap, esz * n));
-            G_TRY(rs_histogram(keys[i], n, shift, bits, k.hist, k.sort_s));
-            G_HIP(hipMemcpyAsync(k.hist_host, k.hist, 4ull * B, hipMemcpyDeviceToHost, k.sort_s));
+            G_TRY(rs_plan_hist16(k.part, keys[i], n, k.hist, k.sort_s));
+            G_HIP(hipMemcpyAsync(k.hist_host, k.hist, 4ull * RS_HIST16_WORDS, hipMemcpyDeviceToHost, k.sort_s));
             G_HIP(hipEventRecord(k.ev_hist, k.sort_s));
             if (n) {
                 if (g->kv)
-                    G_TRY(rs_plan_partition_records(k.part, keys[i], values[i], k.send, n, shift, bits, k.hist, k.sort_s));
+                    G_TRY(rs_plan_partition_records(k.part, keys[i], values[i], k.send, n, shift, bits, k.hist + 65536,
+                                                    k.sort_s));
                 else
-                    G_TRY(rs_plan_partition_totals(k.part, keys[i], nullptr, k.send, nullptr, n, shift, bits, k.hist, k.sort_s));
+                    G_TRY(rs_plan_partition_totals(k.part, keys[i], nullptr, k.send, nullptr, n, shift, bits,
+                                                   k.hist + 65536, k.sort_s));
             }
             G_HIP(hipEventRecord(k.ev_part, k.sort_s));
         }
-        // 3: the bucket plan (host, from every rank's counts)
+        // 3: the bucket plan (host, from every rank's top-byte totals)
         g->hist_all.assign((size_t)W * B, 0);
         for (int i = 0; i < W; ++i) {
             Dev dev(g->r[i].device);
             G_HIP(hipEventSynchronize(g->r[i].ev_hist));
-            for (uint32_t b = 0; b < B; ++b) g->hist_all[(size_t)i * B + b] = g->r[i].hist_host[b];
+            for (uint32_t b = 0; b < B; ++b) g->hist_all[(size_t)i * B + b] = g->r[i].hist_host[65536 + b];
         }
         g->bounds.assign(W + 1, 0);
         g->cuts.assign((size_t)W * (G + 1), 0);
         G_TRY(rs_group_plan(W, B, G, g->hist_all.data(), g->bounds.data(), g->cuts.data()));
         auto cut = [&](int q, uint32_t j) { return g->cuts[(size_t)q * (G + 1) + j]; };
-        // start[r][b]: bucket b's offset in rank r's partitioned slice
+        auto cnt = [&](int src, uint32_t t) { return g->hist_all[(size_t)src * B + t]; };
+        // start[src][t]: top byte t's offset in rank src's partitioned slice
         std::vector<uint64_t> start((size_t)W * (B + 1), 0);
         for (int i = 0; i < W; ++i)
             for (uint32_t b = 0; b < B; ++b)
-                start[(size_t)i * (B + 1) + b + 1] = start[(size_t)i * (B + 1) + b] + g->hist_all[(size_t)i * B + b];
-        auto seg = [&](int src, uint32_t b0, uint32_t b1) {   // [begin, end) in src's slice
-            return std::make_pair(start[(size_t)src * (B + 1) + b0], start[(size_t)src * (B + 1) + b1]);
-        };
-        // receive layout of rank q: off[q][g][s], region bases base[q][g]
-        std::vector<uint64_t> off((size_t)W * G * W), base((size_t)W * (G + 1));
+                start[(size_t)i * (B + 1) + b + 1] = start[(size_t)i * (B + 1) + b] + cnt(i, b);
+        // receive layout: top byte t from source s lands at off[t * W + s] of its owner's buffer
+        // (round-major, then top byte, then source); region j of rank q = [base[q][j], base[q][j+1])
+        std::vector<uint64_t> off((size_t)B * W, 0), base((size_t)W * (G + 1), 0);
         for (int q = 0; q < W; ++q) {
             uint64_t pos = 0;
             for (uint32_t j = 0; j < G; ++j) {
                 base[(size_t)q * (G + 1) + j] = pos;
-                for (int s = 0; s < W; ++s) {
-                    off[((size_t)q * G + j) * W + s] = pos;
-                    auto r = seg(s, cut(q, j), cut(q, j + 1));
-                    pos += r.second - r.first;
-                }
+                for (uint32_t t = cut(q, j); t < cut(q, j + 1); ++t)
+                    for (int src = 0; src < W; ++src) {
+                        off[(size_t)t * W + src] = pos;
+                        pos += cnt(src, t);
+                    }
             }
             base[(size_t)q * (G + 1) + G] = pos;
             if (pos > 0xFFFFFFFFull)
@@ -399,11 +416,23 @@ RS_EXPORT rs_status rs_group_sort(rs_group* g, void* const* keys, void* const* v
             if (g->kv) {
                 G_TRY(grow((void**)&k.out_k, &k.out_k_cap, 4 * n_recv));
                 G_TRY(grow((void**)&k.out_v, &k.out_v_cap, 4 * n_recv));
+                // the region tables: round j's 16-bit counts summed over the sources, zero outside
+                // its top bytes; uploaded on the sort stream (ordered before the region sorts)
+                for (uint32_t j = 0; j < G; ++j) {
+                    uint32_t* t16 = k.reg_host + (size_t)j * 65536;
+                    memset(t16, 0, 4 * 65536);
+                    for (uint32_t b = cut(q, j) << 8; b < (cut(q, j + 1) << 8); ++b) {
+                        uint64_t c = 0;
+                        for (int src = 0; src < W; ++src) c += g->r[src].hist_host[b];
+                        t16[b] = (uint32_t)c;
+                    }
+                }
+                G_HIP(hipMemcpyAsync(k.reg, k.reg_host, 4ull * 65536 * G, hipMemcpyHostToDevice, k.sort_s));
             }
             G_TRY(ensure_local(g, k, biggest));
             G_HIP(hipStreamWaitEvent(k.comm_s, k.ev_part, 0));
         }
-        // 4: exchange rounds
+        // 4: exchange rounds, one message per (source, top byte) chunk
         const bool rccl = g->desc.transport == RS_TRANSPORT_RCCL;
         for (uint32_t j = 0; j < G; ++j) {
             // every send / receive of round j; inside an RCCL group a failure must not return
@@ -413,29 +442,30 @@ RS_EXPORT rs_status rs_group_sort(rs_group* g, void* const* keys, void* const* v
                 for (int src = 0; src < W; ++src) {
                     Rank& k = g->r[src];
                     Dev dev(k.device);
-                    for (int dst = 0; dst < W; ++dst) {
-                        auto r = seg(src, cut(dst, j), cut(dst, j + 1));
-                        const uint64_t m = r.second - r.first;
-                        char* from = (char*)k.send + esz * r.first;
-                        char* to = (char*)g->r[dst].recv + esz * off[((size_t)dst * G + j) * W + src];
-                        if (dst == src || !rccl) {
+                    for (int dst = 0; dst < W; ++dst)
+                        for (uint32_t t = cut(dst, j); t < cut(dst, j + 1); ++t) {
+                            const uint64_t m = cnt(src, t);
                             if (!m) continue;
-                            if (g->r[dst].device == k.device)
-                                G_HIP(hipMemcpyAsync(to, from, esz * m, hipMemcpyDeviceToDevice, k.comm_s));
-                            else
-                                G_HIP(hipMemcpyPeerAsync(to, g->r[dst].device, from, k.device, esz * m, k.comm_s));
-                        } else if (m) {
-                            G_NCCL(ncclSend(from, m, g->kv ? ncclUint64 : ncclUint32, dst, k.comm, k.comm_s));
+                            char* from = (char*)k.send + esz * start[(size_t)src * (B + 1) + t];
+                            char* to = (char*)g->r[dst].recv + esz * off[(size_t)t * W + src];
+                            if (dst == src || !rccl) {
+                                if (g->r[dst].device == k.device)
+                                    G_HIP(hipMemcpyAsync(to, from, esz * m, hipMemcpyDeviceToDevice, k.comm_s));
+                                else
+                                    G_HIP(hipMemcpyPeerAsync(to, g->r[dst].device, from, k.device, esz * m, k.comm_s));
+                            } else {
+                                G_NCCL(ncclSend(from, m, g->kv ? ncclUint64 : ncclUint32, dst, k.comm, k.comm_s));
+                            }
                         }
-                    }
-                    if (rccl)
+                    if (rccl)   // what src receives from every peer, in the peer's send order (t ascending)
                         for (int s = 0; s < W; ++s) {
                             if (s == src) continue;
-                            auto r = seg(s, cut(src, j), cut(src, j + 1));
-                            const uint64_t m = r.second - r.first;
-                            if (!m) continue;
-                            char* to = (char*)k.recv + esz * off[((size_t)src * G + j) * W + s];
-                            G_NCCL(ncclRecv(to, m, g->kv ? ncclUint64 : ncclUint32, s, k.comm, k.comm_s));
+                            for (uint32_t t = cut(src, j); t < cut(src, j + 1); ++t) {
+                                const uint64_t m = cnt(s, t);
+                                if (!m) continue;
+                                char* to = (char*)k.recv + esz * off[(size_t)t * W + s];
+                                G_NCCL(ncclRecv(to, m, g->kv ? ncclUint64 : ncclUint32, s, k.comm, k.comm_s));
+                            }
                         }
                 }
                 return RS_OK;
@@ -454,7 +484,7 @@ RS_EXPORT rs_status rs_group_sort(rs_group* g, void* const* keys, void* const* v
                 G_HIP(hipEventRecord(g->r[src].ev_round[j], g->r[src].comm_s));
             }
         }
-        // 5: region g sorted once round g has landed (RCCL: the receiver's own comm stream;
+        // 5: region j sorted once round j has landed (RCCL: the receiver's own comm stream;
         // copies: every sender's), later rounds still on the wire
         for (int q = 0; q < W; ++q) {
             Rank& k = g->r[q];
@@ -467,14 +497,9 @@ RS_EXPORT rs_status rs_group_sort(rs_group* g, void* const* keys, void* const* v
                 }
                 const uint64_t a = base[(size_t)q * (G + 1) + j], b = base[(size_t)q * (G + 1) + j + 1];
                 if (b <= a) continue;
-                // every key of round j lies in its buckets' range: the local sort may work on the
-                // range-relative bits (the hybrid MSD path over this rank's buckets)
-                const uint32_t ca = g->cuts[(size_t)q * (G + 1) + j], cb = g->cuts[(size_t)q * (G + 1) + j + 1];
-                const uint32_t klo = ca << (32 - bits);
-                const uint32_t khi = cb >= B ? 0xFFFFFFFFu : (cb << (32 - bits)) - 1u;
                 if (g->kv)
-                    G_TRY(rs_plan_sort_records_range(k.local, (char*)k.recv + 8 * a, k.out_k + a, k.out_v + a, b - a,
-                                                     klo, khi, k.sort_s));
+                    G_TRY(rs_plan_sort_region(k.local, (char*)k.recv + 8 * a, k.out_k + a, k.out_v + a, b - a,
+                                              k.reg + (size_t)j * 65536, cut(q, j), cut(q, j + 1), k.sort_s));
                 else
                     G_TRY(rs_plan_sort_n(k.local, (uint32_t*)k.recv + a, nullptr, b - a, k.sort_s));
             }

@@ -1418,6 +1418,30 @@ __global__ __launch_bounds__(1024) void k_hist16_reduce(const uint32_t* __restri
     }
 }
 
+// out[0..65536) = the sum of nrows rows of 65536 counts (k_hist16_in's rows), out[65536 + t] = the
+// sum of out[t << 8 ..]: the multi-GPU sender's table (rs_plan_hist16).  Workgroup t: top byte t.
+__global__ __launch_bounds__(256) void k_hist16_sum(const uint32_t* __restrict__ rows, uint32_t nrows,
+                                                    uint32_t* __restrict__ out) {
+    __shared__ uint32_t s_scratch[kWaves];
+    const uint32_t b = blockIdx.x * 256u + threadIdx.x;
+    uint32_t c = 0;
+    for (uint32_t r = 0; r < nrows; ++r) c += rows[(size_t)r * 65536u + b];
+    out[b] = c;
+    uint32_t tot;
+    block_excl_scan(c, s_scratch, tot);
+    if (threadIdx.x == 0) out[65536u + blockIdx.x] = tot;
+}
+
+// A multi-GPU receiver's region (rs_plan_sort_region): its 16-bit bucket counts arrive from the
+// senders' tables, so instead of k_hist16_in's rows there is one row, copied here, with a clear
+// range flag word; also clears the overflow count and the oversize flag (k_hist16_in's job).
+__global__ __launch_bounds__(256) void k_region_rows(const uint32_t* __restrict__ hist, uint32_t* __restrict__ row,
+                                                     uint32_t* z0, uint32_t* z1) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    row[i] = hist[i];
+    if (i == 0) { row[65536] = 0u; *z0 = 0u; *z1 = 0u; }
+}
+
 // One workgroup, after k_hist16_reduce: the segmented tile table of MSD pass 1 (segment = top
 // byte: [257] first tile + total, [256] start, [256] end; the starts are what the bucket bases of
 // k_hist16_reduce are relative to) and the path: MSD iff every 16-bit bucket fits the bucket tile
@@ -1622,7 +1646,9 @@ __global__ __launch_bounds__(1024, 1) void k_bucket_sort_wide(const uint32_t* re
                                                               const uint32_t* __restrict__ over,
                                                               uint32_t kbase,
                                                               const uint32_t* __restrict__ sstart,
-                                                              uint32_t rmask, uint32_t bshift) {
+                                                              uint32_t rmask, uint32_t bshift,
+                                                              uint32_t b_lo = 0, uint32_t b_cnt = 65536) {
+    // unlisted (over == null): buckets [b_lo, b_lo + b_cnt), e.g. a multi-GPU region's top bytes
     constexpr int BLOCK = 1024, NW = BLOCK / 64, RADIX = 256;
     constexpr int TILE = BLOCK * KPT;
     constexpr int WAVE_KEYS = 64 * KPT;
@@ -1634,9 +1660,9 @@ __global__ __launch_bounds__(1024, 1) void k_bucket_sort_wide(const uint32_t* re
     if (gated_off(gate, 0)) return;
     const uint32_t tid = threadIdx.x, w = tid >> 6, lane = lane_id();
     const uint32_t wbase = w * WAVE_KEYS;
-    const uint32_t nb = over ? over[0] : 65536u;
+    const uint32_t nb = over ? over[0] : b_cnt;
     for (uint32_t it = blockIdx.x; it < nb; it += gridDim.x) {
-        const uint32_t b = over ? over[1 + it] : it;
+        const uint32_t b = over ? over[1 + it] : b_lo + it;
         const uint32_t cnt = hist16[b];
         if (cnt <= min_cnt || cnt <= 1u) continue;   // the smaller tile's launch took it (or trivial)
         if (cnt > (uint32_t)TILE) {                   // never: k_hist16_reduce gates the path off

@@ -195,6 +195,8 @@ struct rs_plan {
     int layout = rs::LAYOUT_KEYS;          // rs::Layout of the caller's data
     int rank_mode = rs::RANK_LDS_ATOMIC;   // RSORT_RANK=ballot selects the ballot-match ranking
     int tile_mode = -1;                    // RSORT_TILE: -1 by size, 0 large tiles, 1 small tiles
+    uint32_t usage = RS_USAGE_SORT;        // RS_USAGE_PARTITION: hist16 + partition passes only
+    uint64_t rows_words = 0;               // words of tmp_k available to k_hist16_in's rows
     uint32_t passes = 0;
     uint32_t widths[16] = {};
     uint64_t capacity = 0;
@@ -392,6 +394,10 @@ rs_status run_pass_cfg(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint3
     const uint32_t grid = std::min<uint32_t>(ntiles, max_grid);
     const int L = LL & 15;
     if (onesweep) {
+        // the look-back status words of every tile of this launch must exist (never index past them)
+        if ((uint64_t)ntiles * 256u > p->status_words)
+            return fail(RS_ERR_INVALID_ARG, "internal: %u one-sweep tiles exceed the plan's %llu status words",
+                        ntiles, (unsigned long long)p->status_words);
         if (rs_status st = next_epoch(p, s)) return st;
         constexpr int K = rs::LAYOUT_KEYS, S = rs::LAYOUT_SOA, A = rs::LAYOUT_AOS;
         p->timer.run(p->scatter_kind, s, [&] {
@@ -574,6 +580,13 @@ rs_status take_device_error(rs_plan* p, const char* what) {
                 what, e);
 }
 
+// Sort entry points need the full workspace (a RS_USAGE_PARTITION plan has no ping-pong copy).
+rs_status need_sort_plan(const rs_plan* p, const char* what) {
+    if (p->usage == RS_USAGE_SORT) return RS_OK;
+    return fail(RS_ERR_INVALID_ARG, "%s: a RS_USAGE_PARTITION plan only runs rs_plan_hist16 and rs_plan_partition*",
+                what);
+}
+
 }  // namespace
 
 // ============================================================================================
@@ -617,6 +630,8 @@ RS_EXPORT rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out) {
     if (rb != 2 && rb != 4 && rb != 8)
         return fail(RS_ERR_INVALID_ARG, "radix_bits must be 0, 2, 4 or 8 (got %u)", d.radix_bits);
     if (d.flags & ~(uint32_t)0x1F) return fail(RS_ERR_INVALID_ARG, "unknown flag bits 0x%x", d.flags);
+    if (d.usage != RS_USAGE_SORT && d.usage != RS_USAGE_PARTITION)
+        return fail(RS_ERR_INVALID_ARG, "usage must be RS_USAGE_SORT or RS_USAGE_PARTITION (got %u)", d.usage);
 
     rs_plan* p = new (std::nothrow) rs_plan();
     if (!p) return fail(RS_ERR_OUT_OF_MEMORY, "host allocation failed");
@@ -626,6 +641,7 @@ RS_EXPORT rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out) {
     p->has_values = d.flags & (RS_FLAG_HAS_VALUES | RS_FLAG_INTERLEAVED);
     p->layout = (d.flags & RS_FLAG_INTERLEAVED) ? rs::LAYOUT_AOS
               : (p->has_values ? rs::LAYOUT_SOA : rs::LAYOUT_KEYS);
+    p->usage = d.usage;
     p->check_order = d.flags & RS_FLAG_CHECK_ORDER;
     p->local_shuffle = d.flags & RS_FLAG_LOCAL_SHUFFLE;
     // path choices (per plan; the parity tests switch them to cover every path)
@@ -676,9 +692,12 @@ RS_EXPORT rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out) {
             p->cus = (uint32_t)prop.multiProcessorCount;
     }
     // look-back status words: one per (tile, digit) of the finest tile configuration in use
+    // (the hybrid path's segmented pass: up to one partial tile per top-byte segment on top of
+    // the 16K-key tiles, which dominates below ~4M keys)
     const uint64_t max_tiles = std::max<uint64_t>(
-        1, std::max<uint64_t>((d.count + kMinOnesweepTile - 1) / kMinOnesweepTile,
-                              (std::min<uint64_t>(d.count, RS_SMALL_MAX) + kSmall.tile - 1) / kSmall.tile));
+        (d.count + kLarge.tile - 1) / kLarge.tile + 257,
+        std::max<uint64_t>((d.count + kMinOnesweepTile - 1) / kMinOnesweepTile,
+                           (std::min<uint64_t>(d.count, RS_SMALL_MAX) + kSmall.tile - 1) / kSmall.tile));
     // sized whatever RSORT_ONESWEEP says: the records / partition entry points and the hybrid
     // path's passes are one-sweep passes on every plan
     p->status_words = max_tiles * 256;
@@ -688,9 +707,14 @@ RS_EXPORT rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out) {
     // records buffers are padded to whole kHuge tiles (k_onesweep with staging rounds reads
     // whole tiles)
     const uint64_t padded = (d.count + kRecPad - 1) / kRecPad * kRecPad;
-    if ((p->layout == rs::LAYOUT_KEYS && (e = alloc(&p->tmp_k, 4 * d.count)) != hipSuccess) ||
-        (p->layout != rs::LAYOUT_KEYS && (e = alloc(&p->tmp_k, 8 * padded)) != hipSuccess) ||
-        (p->layout == rs::LAYOUT_SOA && p->onesweep_mode != 0 && p->aos_tmp && recs2 &&
+    // tmp_k: the ping-pong copy, which also holds k_hist16_in's rows (one per CU: 65536 counts, and
+    // a flag word each) before the passes use it; a partition plan keeps just the rows
+    const bool sorts = d.usage == RS_USAGE_SORT;
+    const uint64_t rows_bytes = 4ull * p->cus * 65537ull;
+    const uint64_t tmpk_bytes = !sorts ? rows_bytes : (p->layout == rs::LAYOUT_KEYS ? 4 * d.count : 8 * padded);
+    p->rows_words = tmpk_bytes / 4;
+    if ((e = alloc(&p->tmp_k, tmpk_bytes)) != hipSuccess ||
+        (sorts && p->layout == rs::LAYOUT_SOA && p->onesweep_mode != 0 && p->aos_tmp && recs2 &&
          d.count > kTinyMax && (e = alloc(&p->tmp2, 8 * padded)) != hipSuccess) ||
         (e = alloc(&p->counts, 4ull * 256 * std::max<uint64_t>(1, (d.count + kSmall.tile - 1) / kSmall.tile))) != hipSuccess ||
         (e = alloc(&p->totals, 4ull * 256)) != hipSuccess ||
@@ -699,7 +723,7 @@ RS_EXPORT rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out) {
         (e = alloc((uint32_t**)&p->status, 8ull * p->status_words)) != hipSuccess)
         return cleanup(fail(e == hipErrorOutOfMemory ? RS_ERR_OUT_OF_MEMORY : RS_ERR_HIP,
                             "rs_plan_create: hipMalloc failed: %s", hipGetErrorString(e)));
-    if (p->msd_mode != 0 && d.count >= kMsdMin &&
+    if (sorts && p->msd_mode != 0 && d.count > kTinyMax &&
         (p->layout == rs::LAYOUT_AOS || p->layout == rs::LAYOUT_KEYS ||
          (p->layout == rs::LAYOUT_SOA && p->tmp2)) &&
         (e = alloc(&p->msd, 4ull * kMsdWords)) != hipSuccess)
@@ -711,7 +735,7 @@ RS_EXPORT rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out) {
         (e = hipEventCreateWithFlags(&p->done, hipEventDisableTiming)) != hipSuccess)
         return cleanup(fail(RS_ERR_HIP, "rs_plan_create: host error word: %s", hipGetErrorString(e)));
     *p->host_err = 0u;
-    if (p->layout == rs::LAYOUT_SOA) p->tmp_v = p->tmp_k + d.count;
+    if (p->layout == rs::LAYOUT_SOA && sorts) p->tmp_v = p->tmp_k + d.count;
     if ((e = hipMemset(p->ptot, 0, 4ull * (rs::kTotalsMax + 32))) != hipSuccess ||
         (e = hipMemset(p->status, 0, 8ull * p->status_words)) != hipSuccess)
         return cleanup(fail(RS_ERR_HIP, "rs_plan_create: hipMemset failed: %s", hipGetErrorString(e)));
@@ -771,15 +795,23 @@ static rs_status enqueue_lsd_gated(rs_plan* p, const uint32_t* sk, const uint32_
 // Keys known to lie in [kbase, kbase + 2^vbits) (a group sort's received buckets) are sorted by
 // their vbits range-relative bits: digits of key - kbase at vbits - 8 and vbits - 16 (a key
 // outside the range sends the device to the 32-bit LSD passes).
+// Region form (region_hist != null; rs_plan_sort_region, records -> arrays): the input records are
+// already grouped by top byte (the senders' partition was pass 0) and region_hist holds their 16-bit
+// bucket counts (nbuckets of them populated): no histogram read, no pass 0; R1 = the input, R2 =
+// records in tmp_k.
 static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t* sv, bool in_aos,
                                   uint32_t* uk, uint32_t* uv, bool out_aos, uint64_t n, hipStream_t s,
-                                  uint32_t kbase = 0, uint32_t vbits = 32) {
+                                  uint32_t kbase = 0, uint32_t vbits = 32,
+                                  const uint32_t* region_hist = nullptr, uint32_t top_lo = 0, uint32_t top_hi = 256) {
+    // the populated 16-bit buckets: all, or a region's top bytes
+    const uint32_t b_lo = top_lo << 8, b_cnt = (top_hi - top_lo) << 8, nbuckets = b_cnt;
     constexpr int A = rs::LAYOUT_AOS, S = rs::LAYOUT_SOA, K = rs::LAYOUT_KEYS;
     const bool keys = p->layout == rs::LAYOUT_KEYS;   // keys only: R1 = tmp_k, R2 = the caller's keys
+    const bool region = region_hist != nullptr;
     const uint32_t n32 = (uint32_t)n;
     const uint32_t range = vbits >= 32 ? 0xFFFFFFFFu : (1u << vbits) - 1u;
-    uint32_t* r1 = p->tmp_k;
-    uint32_t* r2 = (out_aos || keys) ? uk : p->tmp2;
+    uint32_t* r1 = region ? const_cast<uint32_t*>(sk) : p->tmp_k;   // region: only read
+    uint32_t* r2 = region ? p->tmp_k : ((out_aos || keys) ? uk : p->tmp2);
     uint32_t* hist16 = p->msd;
     uint32_t* base16 = hist16 + 65536;
     uint32_t* segtab = base16 + 65536;
@@ -794,11 +826,15 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
     const int keys_cfg = p->msd_keys_cfg;
     const uint32_t tile = (keys && keys_cfg == 2) ? 2u * kLarge.tile : (uint32_t)kLarge.tile;
     const uint32_t ntiles = (uint32_t)((n + tile - 1) / tile);
+    // the segmented pass has up to ntiles + 256 tiles; each needs its look-back status words
+    if ((uint64_t)(ntiles + 257) * 256u > p->status_words)
+        return fail(RS_ERR_INVALID_ARG, "internal: %u segmented tiles exceed the plan's %llu status words",
+                    ntiles + 257, (unsigned long long)p->status_words);
     // the pass totals, tickets and error word are zeroed by k_hist16_reduce (nothing reads them before)
     // 16-bit buckets: a tile sized to the mean bucket + 4 sigma of a uniform population takes
     // every bucket that fits it (at 2^28 keys: 4352 records, ~2 buckets over it), the large tile
     // the listed rest
-    const double mean = (double)n / 65536.0;
+    const double mean = (double)n / std::max(1u, nbuckets);
     const double slack = RS_KNOB("RSORT_BUCKET_SLACK", 1.0);
     const uint32_t want = (uint32_t)(mean * slack + 4.0 * std::sqrt(mean));
     constexpr uint32_t bb = 256;
@@ -824,8 +860,15 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
     uint32_t* range_bad = mtot;
     // sweep: RSORT_HIST16_DIV = one row per `div` CUs (fewer rows to write and add)
     const uint32_t hdiv = std::max(1u, (uint32_t)RS_KNOB("RSORT_HIST16_DIV", 1));
-    const uint32_t hrows = std::max(1u, p->cus / hdiv);
+    const uint32_t hrows = region ? 1u : std::max(1u, p->cus / hdiv);
     p->timer.run(RS_KERNEL_HISTOGRAM, s, [&] {
+        if (region) {   // the senders counted: one row, their table
+            hipLaunchKernelGGL(rs::k_region_rows, dim3(256), dim3(256), 0, s, region_hist, p->tmp_k, over, big);
+            hipLaunchKernelGGL(rs::k_hist16_reduce, dim3(256), dim3(1024), 0, s, (const uint32_t*)p->tmp_k,
+                               1u, hist16, top_tot, range_bad, base16, small_cap, kBucketCap, over, big,
+                               p->ptot, (uint32_t)(rs::kTotalsMax + 32));
+            return;
+        }
         // 16-byte aligned records: two per load (sweep: RSORT_HIST16_NARROW=1 keeps one per 8-byte load)
         const bool narrow = RS_KNOB("RSORT_HIST16_NARROW", 0) == 1;
         // the whole 32-bit range: the specialised counting (sweep: RSORT_HIST16_GENERIC=1 keeps the generic one)
@@ -870,10 +913,10 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
         rmask = (1u << rb) - 1u;
     }
 #endif
-    // MSD pass 0: input -> R1 records, partitioned by the top byte
+    // MSD pass 0: input -> R1 records, partitioned by the top byte (region form: done by the senders)
     if (rs_status st = next_epoch(p, s)) return st;
     const bool keys_wide = keys_cfg == 0;
-    p->timer.run(RS_KERNEL_SCATTER, s, [&] {
+    if (!region) p->timer.run(RS_KERNEL_SCATTER, s, [&] {
         if (keys && keys_wide)
             launch_msd_pass<K, K, 0>(p, sk, nullptr, r1, nullptr, n32, vbits - 8, ntiles, top_tot, p->tickets + 4,
                                      g_msd, nullptr, nullptr, s);
@@ -939,10 +982,10 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
         // tile on a small persistent grid (sweep: RSORT_OVER_GRID workgroups)
         const uint32_t over_grid = std::max(1u, (uint32_t)RS_KNOB("RSORT_OVER_GRID", 256));
         auto large = [&](auto kern) {
-            hipLaunchKernelGGL(kern, dim3(wide_all ? 65536u : over_grid), dim3(1024), 0, s, ring ? ring : r2,
+            hipLaunchKernelGGL(kern, dim3(wide_all ? b_cnt : over_grid), dim3(1024), 0, s, ring ? ring : r2,
                                hist16, base16, uk, uv, g_msd, p->tickets + 16, wide_all ? 0u : small_cap,
                                wide_all ? (const uint32_t*)nullptr : (const uint32_t*)over, kbase,
-                               (const uint32_t*)sstart, rmask, vbits - 16);
+                               (const uint32_t*)sstart, rmask, vbits - 16, b_lo, b_cnt);
         };
         auto both = [&](auto lo) {
             constexpr int LO = decltype(lo)::value;
@@ -1152,6 +1195,7 @@ RS_EXPORT rs_status rs_plan_sort_n(rs_plan* p, void* keys, void* values, uint64_
     if (n > p->capacity)
         return fail(RS_ERR_CAPACITY, "count %llu exceeds plan capacity %llu",
                     (unsigned long long)n, (unsigned long long)p->capacity);
+    if (rs_status st = need_sort_plan(p, "rs_plan_sort")) return st;
     if (n <= 1) return RS_OK;
     if (!keys) return fail(RS_ERR_INVALID_ARG, "rs_plan_sort: keys is null");
     const int L = p->layout;
@@ -1185,6 +1229,7 @@ RS_EXPORT rs_status rs_plan_sort_copy(rs_plan* p, const void* in_k, const void* 
     if (n > p->capacity)
         return fail(RS_ERR_CAPACITY, "count %llu exceeds plan capacity %llu",
                     (unsigned long long)n, (unsigned long long)p->capacity);
+    if (rs_status st = need_sort_plan(p, "rs_plan_sort_copy")) return st;
     if (p->layout == rs::LAYOUT_AOS || p->check_order)
         return fail(RS_ERR_INVALID_ARG, "rs_plan_sort_copy: needs a plan with separate arrays (not interleaved) and no check_order");
     const bool kv = p->layout == rs::LAYOUT_SOA;
@@ -1376,6 +1421,7 @@ static rs_status enqueue_sort_records(rs_plan* p, const uint32_t* rec, uint32_t*
 static rs_status sort_records_impl(rs_plan* p, const void* records, void* keys_out, void* values_out,
                                    uint64_t n, uint32_t key_lo, uint32_t key_hi, void* stream) {
     if (!p) return fail(RS_ERR_INVALID_ARG, "rs_plan_sort_records: null plan");
+    if (rs_status st = need_sort_plan(p, "rs_plan_sort_records")) return st;
     if (p->layout != rs::LAYOUT_SOA)
         return fail(RS_ERR_INVALID_ARG, "rs_plan_sort_records: needs a plan with separate values (RS_FLAG_HAS_VALUES)");
     if (n > p->capacity)
@@ -1421,6 +1467,81 @@ RS_EXPORT rs_status rs_plan_sort_records_range(rs_plan* p, const void* records, 
                                                uint32_t key_hi, void* stream) {
     if (key_lo > key_hi) return fail(RS_ERR_INVALID_ARG, "rs_plan_sort_records_range: key_lo > key_hi");
     return sort_records_impl(p, records, keys_out, values_out, n, key_lo, key_hi, stream);
+}
+
+RS_EXPORT rs_status rs_plan_hist16(rs_plan* p, const void* keys, uint64_t n, void* d_hist16, void* stream) {
+    if (!p) return fail(RS_ERR_INVALID_ARG, "rs_plan_hist16: null plan");
+    if (!d_hist16 || (n && !keys)) return fail(RS_ERR_INVALID_ARG, "rs_plan_hist16: null pointer");
+    if (n > p->capacity)
+        return fail(RS_ERR_CAPACITY, "count %llu exceeds plan capacity %llu",
+                    (unsigned long long)n, (unsigned long long)p->capacity);
+    const bool aos = p->layout == rs::LAYOUT_AOS;
+    if (((uintptr_t)keys & 3) || (aos && ((uintptr_t)keys & 7)))
+        return fail(RS_ERR_INVALID_ARG, "rs_plan_hist16: keys must be 4-byte (records 8-byte) aligned");
+    DeviceGuard guard(p->desc.device);
+    hipStream_t s = (hipStream_t)stream;
+    // one row per CU where tmp_k holds them (k_hist16_in: 65536 counts per row, then a flag word
+    // per row); k_hist16_sum adds the rows and the top-byte totals
+    const uint32_t hrows = (uint32_t)std::min<uint64_t>(p->cus, p->rows_words / 65537ull);
+    if (hrows == 0)
+        return fail(RS_ERR_CAPACITY, "rs_plan_hist16: the plan's workspace holds no histogram row (capacity >= 32768 needed)");
+    p->timer.run(RS_KERNEL_HISTOGRAM, s, [&] {
+        // z0 / z1 (the MSD path's overflow words) point into the rows' flag area: unused here
+        uint32_t* z = p->tmp_k + (size_t)hrows * 65536u;
+        auto go = [&](auto kern) {
+            hipLaunchKernelGGL(kern, dim3(hrows), dim3(1024), 0, s, (const uint32_t*)keys, (uint32_t)n, p->tmp_k, 0u,
+                               0xFFFFFFFFu, 16u, z, z);
+        };
+        if (aos && ((uintptr_t)keys & 15u) == 0) go(rs::k_hist16_in<rs::LAYOUT_AOS, true, true>);
+        else if (aos) go(rs::k_hist16_in<rs::LAYOUT_AOS, false, true>);
+        else go(rs::k_hist16_in<rs::LAYOUT_SOA, false, true>);
+        hipLaunchKernelGGL(rs::k_hist16_sum, dim3(256), dim3(256), 0, s, (const uint32_t*)p->tmp_k, hrows,
+                           (uint32_t*)d_hist16);
+    });
+    HIP_TRY(hipGetLastError());
+    return RS_OK;
+}
+
+RS_EXPORT rs_status rs_plan_sort_region(rs_plan* p, const void* records, void* keys_out, void* values_out,
+                                        uint64_t n, const void* d_hist16, uint32_t top_lo, uint32_t top_hi,
+                                        void* stream) {
+    if (!p) return fail(RS_ERR_INVALID_ARG, "rs_plan_sort_region: null plan");
+    if (rs_status st = need_sort_plan(p, "rs_plan_sort_region")) return st;
+    if (p->layout != rs::LAYOUT_SOA)
+        return fail(RS_ERR_INVALID_ARG, "rs_plan_sort_region: needs a plan with separate values (RS_FLAG_HAS_VALUES)");
+    if (n > p->capacity)
+        return fail(RS_ERR_CAPACITY, "count %llu exceeds plan capacity %llu",
+                    (unsigned long long)n, (unsigned long long)p->capacity);
+    if (top_lo >= top_hi || top_hi > 256)
+        return fail(RS_ERR_INVALID_ARG, "rs_plan_sort_region: need top_lo < top_hi <= 256 (got %u, %u)", top_lo, top_hi);
+    if (n == 0) return RS_OK;
+    if (!records || !keys_out || !values_out || !d_hist16)
+        return fail(RS_ERR_INVALID_ARG, "rs_plan_sort_region: null buffer");
+    if (((uintptr_t)records & 7) || ((uintptr_t)keys_out & 3) || ((uintptr_t)values_out & 3) || ((uintptr_t)d_hist16 & 3))
+        return fail(RS_ERR_INVALID_ARG, "records must be 8-byte and arrays 4-byte aligned");
+    if (rs_status st = take_device_error(p, "rs_plan_sort_region")) return st;
+    DeviceGuard guard(p->desc.device);
+    hipStream_t s = (hipStream_t)stream;
+    uint32_t* uk = (uint32_t*)keys_out;
+    uint32_t* uv = (uint32_t*)values_out;
+    rs_status st;
+    if (n <= kTinyMax) {
+        hipLaunchKernelGGL(rs::k_split_records, dim3((uint32_t)((n + rs::kBlock - 1) / rs::kBlock)),
+                           dim3(rs::kBlock), 0, s, (const uint2*)records, uk, uv, n);
+        HIP_TRY(hipGetLastError());
+        st = n > 1 ? run_tiny(p, uk, uv, (uint32_t)n, s) : RS_OK;
+    } else if (p->msd && p->tmp2 && p->msd_mode != 0 && p->radix_bits == 8 && p->bit_count == 32 &&
+               !p->check_order && n <= kMsdMax) {
+        // the senders' partition was pass 0: the segmented next-byte pass and the bucket pass
+        st = enqueue_sort_msd(p, (const uint32_t*)records, nullptr, true, uk, uv, false, n, s, 0u, 32u,
+                              (const uint32_t*)d_hist16, top_lo, top_hi);
+    } else {
+        st = enqueue_sort_records(p, (const uint32_t*)records, uk, uv, n, s);
+    }
+    if (st != RS_OK) return st;
+    HIP_TRY(hipEventRecord(p->done, s));
+    p->done_recorded = true;
+    return RS_OK;
 }
 
 RS_EXPORT rs_status rs_plan_device_errors(rs_plan* p, uint32_t* errors) {

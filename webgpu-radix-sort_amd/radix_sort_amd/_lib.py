@@ -47,7 +47,12 @@ class PlanDesc(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int32), ("count", ctypes.c_uint64),
                 ("bit_count", ctypes.c_uint32), ("workgroup_x", ctypes.c_uint32),
                 ("workgroup_y", ctypes.c_uint32), ("flags", ctypes.c_uint32),
-                ("radix_bits", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+                ("radix_bits", ctypes.c_uint32), ("usage", ctypes.c_uint32)]
+
+
+RS_USAGE_SORT = 0
+RS_USAGE_PARTITION = 1
+RS_HIST16_WORDS = 65792
 
 
 class PlanInfo(ctypes.Structure):
@@ -86,6 +91,9 @@ _SIGS = {
     "rs_plan_sort_records": (ctypes.c_int, [_VP, _VP, _VP, _VP, ctypes.c_uint64, _VP]),
     "rs_plan_sort_records_range": (ctypes.c_int, [_VP, _VP, _VP, _VP, ctypes.c_uint64, ctypes.c_uint32,
                                                   ctypes.c_uint32, _VP]),
+    "rs_plan_hist16": (ctypes.c_int, [_VP, _VP, ctypes.c_uint64, _VP, _VP]),
+    "rs_plan_sort_region": (ctypes.c_int, [_VP, _VP, _VP, _VP, ctypes.c_uint64, _VP, ctypes.c_uint32,
+                                           ctypes.c_uint32, _VP]),
     "rs_plan_info_get": (ctypes.c_int, [_VP, ctypes.POINTER(PlanInfo)]),
     "rs_plan_set_profiling": (ctypes.c_int, [_VP, ctypes.c_int]),
     "rs_plan_kernel_times": (ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_double),

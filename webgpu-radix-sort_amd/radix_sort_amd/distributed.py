@@ -1,40 +1,43 @@
 """Multi-GPU sort: one process per GPU, one bucket exchange at the top digit.
 
 The reference has no multi-device path; this is the build's sharding of the
-same sort for inputs spread over the GPUs of one node (BASELINE config 5):
+same sort for inputs spread over the GPUs of one node (BASELINE config 5).  The exchange IS the
+first pass of the single-GPU hybrid sort (rsort.hip enqueue_sort_msd), split across the ranks, so
+a rank moves the bytes of one single-GPU sort of its share: 4 + 16 + 16 + 16 = 52 B/key with
+values (round 2 moved 76: an 8-bit histogram, the partition, and then a whole local sort of the
+received records with its own histogram read and its own top-byte pass).
 
 1. rank r holds a contiguous slice of the global input;
-2. the top-``bits`` digit histogram of the slice (``rs_histogram``, one read of the keys);
-3. ``all_gather`` of the histograms (RCCL over xGMI; a few KB) and one copy to the host, where
-   every rank computes the same bucket -> rank assignment on whole-bucket boundaries (equal
-   keys never split), and splits every rank's buckets into G consecutive groups of about equal
-   key counts (again whole buckets);
-4. a stable partition of the slice by the top digit (one scatter pass of the radix sort, the
-   one-sweep pass fed the step-2 counts: one key read), written as 8-byte (key, value) records
+2. its 16-bit bucket table (``rs_plan_hist16``: one read of the keys; 65536 counts + the 256
+   top-byte totals);
+3. ``all_gather`` of the tables (RCCL over xGMI; 263 KB per rank); the top-byte totals go to the
+   host, where every rank computes the same top byte -> rank ownership on whole-byte boundaries
+   (equal keys never split) and splits every rank's bytes into G consecutive rounds of about equal
+   key counts;
+4. a stable partition of the slice by the top byte (the sort's pass 0, the one-sweep pass fed the
+   table's top-byte totals: one read of keys + values), written as 8-byte (key, value) records
    (``rs_plan_partition_records``; keys only: ``rs_plan_partition_totals``), overlapped with the
-   host's wait for the counts: every (peer, group) send segment is now one contiguous range;
-5. G exchange rounds: round g is one batch of point-to-point messages (``batch_isend_irecv``;
-   RCCL sends to all peers at once, over all 7 xGMI links of a rank), one message per peer with
-   its group-g buckets' records.  The receiver lays round g out as [source 0's segment,
-   source 1's, ...] in its group-g region, which is therefore complete once round g lands: it
-   holds every key of those buckets, equal keys in (source rank, input position) order = global
-   input order;
-6. as soon as round g has landed, the group-g region is sorted locally (stable LSD, the same
-   plan; ``rs_plan_sort_records``: records in, separate key / value arrays out), while rounds
-   g+1.. are still on the wire: the local sort hides under the exchange,
-   and only the last group's sort is exposed.  Groups hold increasing buckets, so the regions
-   concatenated are rank r's part of the global stable order.
+   host's wait for the totals;
+5. G exchange rounds: round g is one batch of point-to-point messages (``batch_isend_irecv``; RCCL
+   sends to all peers at once, over all 7 xGMI links of a rank), one message per (source, top
+   byte) chunk.  The receiver lays round g out top byte by top byte, each byte's chunks in source
+   order: its group-g region is then grouped by top byte, every byte's records in global input
+   order - exactly what the hybrid sort's pass 0 would have produced;
+6. as soon as round g has landed, the group-g region is sorted locally
+   (``rs_plan_sort_region``: the segmented next-byte pass and the in-LDS bucket sort; its 16-bit
+   bucket counts are the gathered tables summed over the sources), while rounds g+1.. are still
+   on the wire: only the last group's sort is exposed.  Regions hold increasing top bytes, so
+   they concatenated are rank r's part of the global stable order.
 
-Stability: the partition is stable, segments are placed in source-rank order, the local sort
-is stable, and a bucket never spans two groups or two ranks.
+Stability: the partition is stable, chunks are placed in source-rank order, the local sort is
+stable, and a top byte never spans two groups or two ranks.
 
 The local compute is injected (`LocalOps`): the product uses :class:`HipLocalOps` (librsort);
 the CPU gloo tests inject an oracle-backed implementation.  The exchange itself
-(:func:`exchange_round`: point-to-point messages batched per round, the own segment copied
+(:func:`exchange_round`: point-to-point messages batched per round, the own chunks copied
 locally) is ONE code path for every backend, so the gloo world-2/3 tests run exactly what RCCL
 runs on the GPUs.  With values, a message is a run of 8-byte (key, value) records (the partition
-writes records, the local sort reads them and writes separate arrays): one message per peer per
-round instead of two.
+writes records, the local sort reads them and writes separate arrays).
 """
 from __future__ import annotations
 
@@ -42,18 +45,23 @@ from dataclasses import dataclass
 from typing import Protocol
 
 
+HIST16_WORDS = 65792     # 65536 bucket counts + 256 top-byte totals (RS_HIST16_WORDS)
+
+
 class LocalOps(Protocol):
-    def histogram(self, keys, shift: int, bits: int):
-        """-> hist[2^bits] int32 tensor on the keys' device (top-digit counts of keys)."""
+    def hist16(self, keys):
+        """-> int32 tensor [HIST16_WORDS] on the keys' device: counts per 16-bit bucket key >> 16,
+        then the 256 top-byte totals."""
 
     def partition(self, keys, values, shift: int, bits: int, totals):
         """Stable partition by (key >> shift) & (2^bits - 1) -> the send buffer: with values, one
         int64 (key, value) record per key (key | value << 32, the interleaved layout: one message
-        per peer carries both); keys only, the int32 keys.  totals: histogram() of the same keys."""
+        carries both); keys only, the int32 keys.  totals: the digit totals of the same keys."""
 
-    def sort_records(self, records, keys_out, values_out, key_range=None) -> None:
-        """Stable sort of the int64 records by their 32-bit key into keys_out / values_out.
-        key_range: (lo, hi), every key in [lo, hi] (the round's top-digit buckets), a hint."""
+    def sort_region(self, records, keys_out, values_out, hist16, top_lo: int, top_hi: int) -> None:
+        """Stable sort of the int64 records (grouped by top byte in [top_lo, top_hi), ascending;
+        each group in input order) by their 32-bit key into keys_out / values_out.  hist16: the
+        records' counts per 16-bit bucket (65536 int32, zero outside the region's top bytes)."""
 
     def sort(self, keys, n: int) -> None:
         """Stable in-place sort of keys[:n] (keys only) by the full 32-bit key."""
@@ -105,14 +113,6 @@ def bucket_groups(hist_all, bounds, groups: int):
     return [_split_whole(totals, bounds[q], bounds[q + 1], groups) for q in range(len(bounds) - 1)]
 
 
-def round_key_range(cuts_rank, g: int, bits: int):
-    """[lo, hi] of every key in round g's buckets [cuts_rank[g], cuts_rank[g + 1]) of the
-    top-`bits` digit (the hint the group sort passes to the local sort)."""
-    shift = 32 - bits
-    a, b = int(cuts_rank[g]), int(cuts_rank[g + 1])
-    return a << shift, min((b << shift) - 1, 0xFFFFFFFF)
-
-
 def split_sizes(hist_all, bounds, rank: int, world: int):
     """(send sizes of this rank to every peer, receive sizes from every peer)."""
     send = [sum(int(hist_all[rank][b]) for b in range(bounds[q], bounds[q + 1]))
@@ -124,37 +124,41 @@ def split_sizes(hist_all, bounds, rank: int, world: int):
 
 @dataclass
 class GroupPlan:
-    send: list   # send[g][q] = (begin, end) of the partitioned slice going to peer q in round g
-    recv: list   # recv[g][s] = keys arriving from source s in round g
-    off: list    # off[g][s] = where they land in the receive buffer
+    send: list   # send[g] = [(peer q, begin, end)]: this rank's chunks in round g, per peer by byte
+    recv: list   # recv[g] = [(source s, offset, count)]: where round g's chunks from s land
     base: list   # base[g] = start of round g's region; base[G] = total received
+    cuts: list   # cuts[g] = first top byte of this rank's round g; cuts[G] = end
 
 
 def group_plan(hist_all, cuts, rank: int, world: int) -> GroupPlan:
-    """Send ranges, receive sizes and receive offsets of every exchange round.
+    """Send chunks, receive offsets and regions of every exchange round.
 
-    hist_all: [world][B] top-digit counts; cuts: bucket_groups().  The partitioned slice holds
-    bucket b at [start[b], start[b + 1]) (start = exclusive scan of this rank's counts), so a
-    round's segment to one peer is one contiguous range.  The receive buffer is round-major,
-    then source-major: round g's region is complete when round g has landed."""
+    hist_all: [world][B] top-byte counts; cuts: bucket_groups().  The partitioned slice holds byte
+    t at [start[t], start[t + 1]) (start = exclusive scan of this rank's counts): one chunk per
+    (peer, byte).  The receive buffer is round-major, then byte, then source: round g's region is
+    complete when round g has landed, grouped by top byte, each byte in global input order."""
+    B = len(hist_all[0])
     mine = [int(x) for x in hist_all[rank]]
     start = [0]
     for c in mine:
         start.append(start[-1] + c)
     G = len(cuts[0]) - 1
-    send = [[(start[cuts[q][g]], start[cuts[q][g + 1]]) for q in range(world)] for g in range(G)]
-    recv = [[sum(int(x) for x in hist_all[s][cuts[rank][g]:cuts[rank][g + 1]]) for s in range(world)]
-            for g in range(G)]
-    off, base, pos = [], [], 0
+    send = [[(q, start[t], start[t + 1]) for q in range(world)
+             for t in range(cuts[q][g], cuts[q][g + 1]) if mine[t]] for g in range(G)]
+    recv, base, pos = [], [], 0
     for g in range(G):
         base.append(pos)
         row = []
-        for s in range(world):
-            row.append(pos)
-            pos += recv[g][s]
-        off.append(row)
+        for t in range(cuts[rank][g], cuts[rank][g + 1]):
+            for s in range(world):
+                c = int(hist_all[s][t])
+                if c:
+                    row.append((s, pos, c))
+                pos += c
+        recv.append(row)
     base.append(pos)
-    return GroupPlan(send, recv, off, base)
+    assert B >= 1
+    return GroupPlan(send, recv, base, list(cuts[rank]))
 
 
 @dataclass
@@ -203,26 +207,19 @@ def _side_stream(device):
 
 def exchange_round(send, recv, plan: GroupPlan, g: int, rank: int, world: int, group=None):
     """Round g of the bucket exchange, the same code on every backend (gloo on CPU, RCCL on the
-    GPUs): one point-to-point message per peer carrying that peer's round-g buckets (records or
-    keys), received into the peer's source slot of the round-g region; the rank's own segment is
-    a local copy (RCCL moves a self segment through a few channels at ~0.3 TB/s, measured).
-    Both sides skip empty messages (they compute the same sizes).  -> the round's works."""
+    GPUs): one point-to-point message per (peer, top byte) chunk, received into the byte's source
+    slot of the round-g region; the rank's own chunks are local copies (RCCL moves a self message
+    through a few channels at ~0.3 TB/s, measured).  A pair's messages are posted in the same
+    (byte) order on both sides, so they match.  Both sides skip empty chunks.  -> the round's works."""
     import torch.distributed as dist
-    a, b = plan.send[g][rank]
-    o = plan.off[g][rank]
-    if b > a and recv.data_ptr() != send.data_ptr():
-        recv[o:o + (b - a)].copy_(send[a:b])
-    p2p = []
-    for q in range(world):
-        if q == rank:
-            continue
-        a, b = plan.send[g][q]
-        if b > a:
-            p2p.append(dist.P2POp(dist.isend, send[a:b], q, group))
-        m = plan.recv[g][q]
-        if m:
-            o = plan.off[g][q]
-            p2p.append(dist.P2POp(dist.irecv, recv[o:o + m], q, group))
+    mine = [(o, m) for s, o, m in plan.recv[g] if s == rank]
+    own = [(a, b) for q, a, b in plan.send[g] if q == rank]
+    assert len(mine) == len(own)
+    if recv.data_ptr() != send.data_ptr():
+        for (o, m), (a, b) in zip(mine, own):
+            recv[o:o + m].copy_(send[a:b])
+    p2p = [dist.P2POp(dist.isend, send[a:b], q, group) for q, a, b in plan.send[g] if q != rank]
+    p2p += [dist.P2POp(dist.irecv, recv[o:o + m], s, group) for s, o, m in plan.recv[g] if s != rank]
     return dist.batch_isend_irecv(p2p) if p2p else []
 
 
@@ -230,6 +227,8 @@ def _distributed_sort(keys, values, ops, group, bits, chunks) -> ExchangeResult:
     import torch
     import torch.distributed as dist
 
+    if bits != 8:
+        raise ValueError("the exchange digit is the top byte (bits=8): the sort's first MSD pass")
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     n_local = keys.numel()
@@ -242,33 +241,37 @@ def _distributed_sort(keys, values, ops, group, bits, chunks) -> ExchangeResult:
         return ExchangeResult(out_k, out_v, n_local, [n_local], [n_local])
     G = max(1, int(chunks))
     shift = 32 - bits
-    hist = ops.histogram(keys, shift, bits)                     # [2^bits]
-    gathered = [torch.empty_like(hist) for _ in range(world)]
-    dist.all_gather(gathered, hist, group=group)
+    h16 = ops.hist16(keys)                                      # [HIST16_WORDS]
+    gathered = [torch.empty_like(h16) for _ in range(world)]
+    dist.all_gather(gathered, h16, group=group)
+    table = torch.stack(gathered)                               # [world, HIST16_WORDS]
+    tops = table[:, 65536:]
+    totals = h16[65536:]
     if keys.is_cuda:
-        # the counts travel to the host while the slice is partitioned (the partition needs no
-        # bucket ownership): copy, mark, enqueue the partition, then wait for the mark only
-        hcpu = torch.empty((world,) + tuple(hist.shape), dtype=hist.dtype, pin_memory=True)
-        hcpu.copy_(torch.stack(gathered), non_blocking=True)
+        # the top-byte totals travel to the host while the slice is partitioned (the partition
+        # needs no ownership): copy, mark, enqueue the partition, then wait for the mark only
+        hcpu = torch.empty(tuple(tops.shape), dtype=tops.dtype, pin_memory=True)
+        hcpu.copy_(tops, non_blocking=True)
         ready = torch.cuda.Event()
         ready.record()
-        send = ops.partition(keys, values, shift, bits, hist)
+        send = ops.partition(keys, values, shift, bits, totals)
         ready.synchronize()
         hist_all = hcpu.tolist()
     else:
-        hist_all = torch.stack(gathered).tolist()
-        send = ops.partition(keys, values, shift, bits, hist)
+        hist_all = tops.tolist()
+        send = ops.partition(keys, values, shift, bits, totals)
     bounds = bucket_owners(hist_all, world)
     cuts = bucket_groups(hist_all, bounds, G)
     plan = group_plan(hist_all, cuts, rank, world)
     n_recv = plan.base[G]
-    # one rank: the receive layout is the partitioned slice itself (no copy)
-    recv = send if world == 1 else ops.empty(n_recv, send)
+    recv = ops.empty(n_recv, send)
     rounds = [exchange_round(send, recv, plan, g, rank, world, group) for g in range(G)]
     if values is None:
-        out_k, out_v = recv, None
+        out_k, out_v, tot16 = recv, None, None
     else:
         out_k, out_v = ops.empty(n_recv, keys), ops.empty(n_recv, values)
+        # this rank's regions' 16-bit counts: the tables summed over the sources
+        tot16 = table[:, :65536].to(torch.int64).sum(dim=0).to(torch.int32)
     # round g's local sort waits for round g only (the stream waits, not the host); later rounds
     # keep moving meanwhile
     for g in range(G):
@@ -279,11 +282,12 @@ def _distributed_sort(keys, values, ops, group, bits, chunks) -> ExchangeResult:
             if values is None:
                 ops.sort(recv[a:b], b - a)
             else:
-                ops.sort_records(recv[a:b], out_k[a:b], out_v[a:b],
-                                 key_range=round_key_range(cuts[rank], g, bits))
-    return ExchangeResult(out_k, out_v, n_recv,
-                          [sum(b - a for a, b in (plan.send[g][q] for g in range(G))) for q in range(world)],
-                          [sum(plan.recv[g][s] for g in range(G)) for s in range(world)])
+                t0, t1 = plan.cuts[g], plan.cuts[g + 1]
+                reg = torch.zeros_like(tot16)
+                reg[t0 << 8:t1 << 8] = tot16[t0 << 8:t1 << 8]
+                ops.sort_region(recv[a:b], out_k[a:b], out_v[a:b], reg, t0, t1)
+    send_sizes, recv_sizes = split_sizes(hist_all, bounds, rank, world)
+    return ExchangeResult(out_k, out_v, n_recv, send_sizes, recv_sizes)
 
 
 class HipLocalOps:
@@ -294,35 +298,40 @@ class HipLocalOps:
         self.device = device
         self.has_values = has_values
         self.radix_bits = radix_bits
-        self.plan = SortPlan(device, capacity, has_values, 32, radix_bits)   # the local sort
-        self.part_plan = None     # partition passes (own plan: separate kernel timings)
+        self.plan = SortPlan(device, capacity, has_values, 32, radix_bits)   # the local sorts
+        self.part_plan = None     # the sender's table + partition (own plan, RS_USAGE_PARTITION)
         self.capacity = capacity
 
     def empty(self, n: int, like):
         import torch
         return torch.empty(n, dtype=like.dtype, device=like.device)
 
-    def histogram(self, keys, shift: int, bits: int):
+    def _part(self, n: int):
+        if self.part_plan is None or self.part_plan.capacity < n:
+            from . import _lib
+            from .ops import SortPlan
+            if self.part_plan is not None:
+                self.part_plan.destroy()
+            self.part_plan = SortPlan(self.device, max(n, 1 << 15), self.has_values, 32,
+                                      self.radix_bits, usage=_lib.RS_USAGE_PARTITION)
+        return self.part_plan
+
+    def hist16(self, keys):
         import torch
-        from .ops import histogram
-        h = torch.empty(1 << bits, dtype=torch.int32, device=keys.device)
-        histogram(keys, keys.numel(), shift, bits, h)
+        h = torch.empty(HIST16_WORDS, dtype=torch.int32, device=keys.device)
+        self._part(keys.numel()).hist16(keys, keys.numel(), h)
         return h
 
     def partition(self, keys, values, shift: int, bits: int, totals):
         import torch
         n = keys.numel()
-        if self.part_plan is None or self.part_plan.capacity < n:
-            from .ops import SortPlan
-            if self.part_plan is not None:
-                self.part_plan.destroy()
-            self.part_plan = SortPlan(self.device, max(n, 1), self.has_values, 32, self.radix_bits)
+        pp = self._part(n)
         if values is None:
             sk = torch.empty_like(keys)
-            self.part_plan.partition_totals(keys, None, sk, None, n, shift, bits, totals)
+            pp.partition_totals(keys, None, sk, None, n, shift, bits, totals)
             return sk
         rec = torch.empty(n, dtype=torch.int64, device=keys.device)
-        self.part_plan.partition_records(keys, values, rec, n, shift, bits, totals)
+        pp.partition_records(keys, values, rec, n, shift, bits, totals)
         return rec
 
     def _grow(self, n: int) -> None:
@@ -336,10 +345,10 @@ class HipLocalOps:
         self._grow(n)
         self.plan.sort(keys, None, n)
 
-    def sort_records(self, records, keys_out, values_out, key_range=None) -> None:
+    def sort_region(self, records, keys_out, values_out, hist16, top_lo: int, top_hi: int) -> None:
         n = records.numel()
         self._grow(n)
-        self.plan.sort_records(records, keys_out, values_out, n, key_range=key_range)
+        self.plan.sort_region(records, keys_out, values_out, n, hist16, top_lo, top_hi)
 
     def sort_copy(self, keys, values, keys_out, values_out) -> None:
         n = keys.numel()

@@ -47,10 +47,12 @@ class SortPlan:
     """A sort plan with a capacity; sorts any n <= capacity (multi-GPU receive buffers)."""
 
     def __init__(self, device: int, capacity: int, has_values: bool, bit_count: int = 32,
-                 radix_bits: int = 0, check_order: bool = False):
+                 radix_bits: int = 0, check_order: bool = False, usage: int = 0):
+        """usage: _lib.RS_USAGE_SORT (every entry point) or RS_USAGE_PARTITION (hist16() and the
+        partition passes only: the multi-GPU sender, no ping-pong copy)."""
         flags = (_lib.RS_FLAG_HAS_VALUES if has_values else 0) | \
                 (_lib.RS_FLAG_CHECK_ORDER if check_order else 0) | _lib.RS_FLAG_LOCAL_SHUFFLE
-        desc = _lib.PlanDesc(device, capacity, bit_count, 16, 16, flags, radix_bits, 0)
+        desc = _lib.PlanDesc(device, capacity, bit_count, 16, 16, flags, radix_bits, usage)
         p = ctypes.c_void_p()
         check(_lib.load().rs_plan_create(ctypes.byref(desc), ctypes.byref(p)), "SortPlan")
         self._plan = p
@@ -131,6 +133,21 @@ class SortPlan:
                                                values_out.data_ptr(), n, lo, hi,
                                                _stream(records, stream)),
                   "rs_plan_sort_records_range")
+
+    def hist16(self, keys, n: int, out, stream=None) -> None:
+        """out[0:65536] = counts of keys[:n] per 16-bit bucket key >> 16, out[65536:65792] = the
+        top-byte totals (out: RS_HIST16_WORDS int32 words on the keys' device)."""
+        check(_lib.load().rs_plan_hist16(self._plan, keys.data_ptr(), n, out.data_ptr(),
+                                         _stream(keys, stream)), "rs_plan_hist16")
+
+    def sort_region(self, records, keys_out, values_out, n: int, hist16, top_lo: int, top_hi: int,
+                    stream=None) -> None:
+        """Stable sort of n (key, value) records grouped by top byte in [top_lo, top_hi) (a
+        multi-GPU receiver's region) into key / value arrays; hist16 = the region's 16-bit bucket
+        counts (65536 int32, zero outside its top bytes)."""
+        check(_lib.load().rs_plan_sort_region(self._plan, records.data_ptr(), keys_out.data_ptr(),
+                                              values_out.data_ptr(), n, hist16.data_ptr(), top_lo,
+                                              top_hi, _stream(records, stream)), "rs_plan_sort_region")
 
     def destroy(self) -> None:
         if getattr(self, "_plan", None):

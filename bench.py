@@ -60,6 +60,14 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def _lib_sha16() -> str:
+    """First 16 hex digits of the sha256 of the librsort.so this run loads."""
+    import hashlib
+    lib = os.environ.get("RSORT_LIB", os.path.join(ROOT, "webgpu-radix-sort_amd", "lib", "librsort.so"))
+    with open(lib, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
 def _node_sort(keys) -> dict:
     with tempfile.TemporaryDirectory() as td:
         p = os.path.join(td, "keys.bin")
@@ -365,6 +373,7 @@ def main() -> None:
         info = kernels[0].info
         keys_per_step = n
         scatter_keys = n
+        bucket_keys = n
     else:
         keys, vals = make_input(torch, ops, wl, n, wl["seed"], rank * n, dev)
         # plans and receive buffers are created during the warmup steps (the local sort plan
@@ -377,6 +386,8 @@ def main() -> None:
         from radix_sort_amd import _lib
         import ctypes
         _lib.load().rs_plan_set_profiling(lo.plan._plan, 1)
+        if lo.part_plan is not None:     # the sender's plan: 16-bit table + partition
+            _lib.load().rs_plan_set_profiling(lo.part_plan._plan, 1)
         barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -391,6 +402,11 @@ def main() -> None:
         _lib.load().rs_plan_kernel_times(lo.plan._plan, ms, cnt)
         for i, name in enumerate(_lib.KERNEL_NAMES):
             kernel_ms[name] = {"ms": ms[i], "launches": int(cnt[i])}
+        if lo.part_plan is not None:
+            _lib.load().rs_plan_kernel_times(lo.part_plan._plan, ms, cnt)
+            extra["sender_kernel_ms_per_step"] = {
+                "hist16 (rs_plan_hist16: one key read)": round(ms[_lib.RS_KERNEL_HISTOGRAM] / max(K, 1), 4),
+                "partition (top-byte one-sweep pass -> records)": round(ms[_lib.RS_KERNEL_SCATTER] / max(K, 1), 4)}
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -398,6 +414,7 @@ def main() -> None:
             raise SystemExit(f"bench: rank {rank} output not sorted")
         info = {"passes": 4}
         keys_per_step = n * world
+        bucket_keys = r.n
         extra["recv_keys_rank0"] = r.n
         if world == 1:
             # one rank: nothing to exchange - the slice is sorted out of place in one sort
@@ -407,10 +424,13 @@ def main() -> None:
         else:
             # the local sort runs as `chunks` group sorts per step: a pass launch handles one group
             scatter_keys = r.n / EXCHANGE_ROUNDS
-            extra["partition"] = (f"top 8 bits, whole-bucket split; {EXCHANGE_ROUNDS} exchange rounds "
-                                  "of bucket groups, each sorted while the later rounds are on the wire")
-            extra["roofline_scope"] = ("local group sorts of the received keys (rank 0; a pass launch "
-                                       f"handles one of the {EXCHANGE_ROUNDS} bucket groups)")
+            extra["partition"] = (f"16-bit tables all-gathered; the top-byte partition is the sort's pass 0; "
+                                  f"whole top bytes per rank, {EXCHANGE_ROUNDS} exchange rounds of one "
+                                  "message per (source, byte) chunk, each round's region sorted (next-byte "
+                                  "pass + bucket sort) while the later rounds are on the wire; "
+                                  "52 B/key per rank")
+            extra["roofline_scope"] = ("the receiver's segmented next-byte pass (rank 0; a pass launch "
+                                       f"handles one of the {EXCHANGE_ROUNDS} regions)")
             extra["group_sorts_per_step"] = EXCHANGE_ROUNDS
 
     value = keys_per_step * K / elapsed / 1e9
@@ -436,18 +456,23 @@ def main() -> None:
         extra["bucket_pass"] = {
             "kernel": "k_bucket_sort (one workgroup per 16-bit bucket, 2 LDS passes, contiguous writes)",
             "ms_per_sort": round(bk["ms"] / max(K, 1), 4),
-            "achieved_GBs": round(scatter_keys * bytes_per_key / (bk["ms"] / max(K, 1) / 1e3) / 1e9, 1),
-            "frac": round(scatter_keys * bytes_per_key / (bk["ms"] / max(K, 1) / 1e3) / 1e9 / HBM_PEAK_GBS, 4)}
+            "achieved_GBs": round(bucket_keys * bytes_per_key / (bk["ms"] / max(K, 1) / 1e3) / 1e9, 1),
+            "frac": round(bucket_keys * bytes_per_key / (bk["ms"] / max(K, 1) / 1e3) / 1e9 / HBM_PEAK_GBS, 4)}
     elif bk["launches"]:
         extra["path"] = "LSD one-sweep passes (the hybrid MSD path's device-side fallback: skewed keys)"
     if sc["launches"]:
         avg_ms = sc["ms"] / sc["launches"]
         achieved = scatter_keys * bytes_per_key / (avg_ms / 1e3) / 1e9
-        traffic = None
+        # PMC traffic (tools/pmc_traffic.py, separate rocprofv3 passes): used only when it was
+        # measured on this very library (its sha) and the single-GPU launch shape
+        traffic, traffic_lib = None, None
+        lib_sha = _lib_sha16()
         try:
             with open(args.traffic_json) as f:
                 tj = json.load(f).get(args.workload)
-            if tj and not use_dist:   # measured for the single-GPU launch shape only
+            if tj:
+                traffic_lib = tj.get("lib_sha16")
+            if tj and not use_dist and traffic_lib == lib_sha:
                 traffic = tj.get("scatter_bytes_per_launch")
         except (OSError, ValueError):
             pass
@@ -456,7 +481,8 @@ def main() -> None:
                 "kernel": ("k_onesweep (rank + look-back + local shuffle + scatter)"
                            if onesweep else "k_scatter (rank + local shuffle + scatter)"),
                 "avg_launch_ms": round(avg_ms, 4),
-                "algorithmic_bytes_per_launch": scatter_keys * bytes_per_key}
+                "algorithmic_bytes_per_launch": scatter_keys * bytes_per_key,
+                "lib_sha16": lib_sha, "traffic_lib_sha16": traffic_lib}
     passes = info["passes"]
     # algorithmic HBM bytes of one sort per GPU: every pass reads and writes keys (+values);
     # the digit counts cost one key read per pass (histogram path) or one per sort (one-sweep

@@ -7,7 +7,7 @@ doubled.  Both corrections are re-checked in the same run on kernels with a know
 k_fill_random writes exactly n*4 bytes, k_histogram / k_pass_totals / k_hist16_in (the hybrid MSD
 path's 16-bit bucket count) read exactly n*4 bytes.
 
-    python3 tools/pmc_traffic.py [config3|config2] [out.json]
+    python3 tools/pmc_traffic.py [config3|config2|config4] [out.json]
 
 This script never touches the GPU itself: rocprofv3 runs tools/prof_driver.py as a child.
 """
@@ -19,8 +19,8 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-N = {"config3": 1 << 28, "config2": 1 << 26}
-KV = {"config3": True, "config2": False}
+N = {"config3": 1 << 28, "config2": 1 << 26, "config4": 1 << 28}
+KV = {"config3": True, "config2": False, "config4": True}
 
 
 def run_pass(counter: str, wl: str, outdir: str) -> dict:
@@ -74,6 +74,10 @@ def main():
         "histogram_bytes_per_launch": fetch["histogram"] * 2.0 + write.get("histogram", 0.0),
     }
     res["scatter_traffic_over_algorithmic"] = round(res["scatter_bytes_per_launch"] / alg, 4)
+    # the build these counters were taken on (bench.py uses the figure only for the same library)
+    import hashlib
+    lib = os.environ.get("RSORT_LIB", os.path.join(ROOT, "webgpu-radix-sort_amd", "lib", "librsort.so"))
+    res["lib_sha16"] = hashlib.sha256(open(lib, "rb").read()).hexdigest()[:16]
     if "bucket" in fetch and "bucket" in write:   # the hybrid MSD path's in-LDS bucket pass
         res["bucket_bytes_per_launch"] = fetch["bucket"] * 2.0 + write["bucket"]
         res["bucket_traffic_over_algorithmic"] = round(res["bucket_bytes_per_launch"] / alg, 4)

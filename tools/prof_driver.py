@@ -12,7 +12,8 @@ sys.path.insert(0, os.path.join(ROOT, "webgpu-radix-sort_amd"))
 import torch  # noqa: E402
 from radix_sort_amd import RadixSortKernel, ops  # noqa: E402
 
-WL = {"config3": (1 << 28, True, True), "config2": (1 << 26, False, False)}
+WL = {"config3": (1 << 28, True, True), "config2": (1 << 26, False, False),
+      "config4": (1 << 28, True, False)}   # f32 nearly sorted + check_order (bench.py's input)
 
 
 def main():
@@ -22,9 +23,18 @@ def main():
     n, kv, ls = WL[name]
     k = torch.empty(n, dtype=torch.int32, device="cuda")
     v = torch.empty(n, dtype=torch.int32, device="cuda") if kv else None
-    kern = RadixSortKernel(keys=k, values=v, count=n, local_shuffle=ls, radix_bits=radix_bits)
+    nearly = None
+    if name == "config4":
+        sys.path.insert(0, ROOT)
+        import bench
+        nearly = torch.from_numpy(bench.nearly_sorted_f32_bits(n, 4).view("int32"))
+    kern = RadixSortKernel(keys=k, values=v, count=n, local_shuffle=ls, radix_bits=radix_bits,
+                           check_order=nearly is not None)
     for r in range(reps):
-        ops.fill_random_u32(k, 1000 + r)
+        if nearly is not None:
+            k.copy_(nearly)
+        else:
+            ops.fill_random_u32(k, 1000 + r)
         if kv:
             ops.fill_iota_u32(v)
         kern.dispatch()

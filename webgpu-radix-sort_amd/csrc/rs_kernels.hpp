@@ -1506,7 +1506,9 @@ __global__ __launch_bounds__(BLOCK, MW) void k_bucket_sort(const uint32_t* rec,
                                                        const uint32_t* __restrict__ over = nullptr,
                                                        uint32_t kbase = 0,
                                                        const uint32_t* __restrict__ sstart = nullptr,
-                                                       uint32_t rmask = 0xFFFFFFFFu) {
+                                                       uint32_t rmask = 0xFFFFFFFFu,
+                                                       uint32_t b_lo = 0, uint32_t b_cnt = 65536) {
+    // unlisted (over == null): buckets [b_lo, b_lo + b_cnt) (a multi-GPU region's top bytes)
     constexpr int R = 8, RADIX = 256;
     // bucket b's first record in rec: its top-byte segment's start + its base inside the segment
     // (modulo the ring of rmask + 1 records, sweep experiments), and in the output
@@ -1526,10 +1528,11 @@ __global__ __launch_bounds__(BLOCK, MW) void k_bucket_sort(const uint32_t* rec,
     const uint32_t tid = threadIdx.x, w = tid >> 6, lane = lane_id();
     const uint32_t wbase = w * WAVE_KEYS;
     // workgroup i takes buckets (listed buckets with `over`) i, i + grid, ...
-    const uint32_t nb = over ? over[0] : 65536u;
+    const uint32_t nb = over ? over[0] : b_cnt;
+    auto bucket_of = [&](uint32_t it) { return over ? over[1 + it] : b_lo + it; };
     auto next_valid = [&](uint32_t it, uint32_t& cnt) {
         for (; it < nb; it += gridDim.x) {
-            cnt = hist16[over ? over[1 + it] : it];
+            cnt = hist16[bucket_of(it)];
             if (cnt == 0u || cnt <= min_cnt) continue;   // empty, or the smaller tile's launch took it
             if (cnt > (uint32_t)TILE) {                   // the large-tile launch's (or: never, gated)
                 if (over && tid == 0) atomicOr(err, 8u);
@@ -1544,36 +1547,24 @@ __global__ __launch_bounds__(BLOCK, MW) void k_bucket_sort(const uint32_t* rec,
     if (it >= nb) return;
     uint32_t k[KPT], v[KV ? KPT : 1];
     uint32_t k2[PF ? KPT : 1], v2[PF && KV ? KPT : 1];
-    load_tile<KPT, LI>(rec + (KV ? 2ull : 1ull) * rstart(over ? over[1 + it] : it), nullptr, wbase, cnt, false, k, v);
+    load_tile<KPT, LI>(rec + (KV ? 2ull : 1ull) * rstart(bucket_of(it)), nullptr, wbase, cnt, false, k, v);
     while (true) {
-        const uint32_t b = over ? over[1 + it] : it;
+        const uint32_t b = bucket_of(it);
         const uint32_t base = bstart(b);
         uint32_t ncnt = 0;
         const uint32_t nit = next_valid(it + gridDim.x, ncnt);
         if constexpr (PF != 0) {
             if (nit < nb)
-                load_tile<KPT, LI>(rec + (KV ? 2ull : 1ull) * rstart(over ? over[1 + nit] : nit), nullptr, wbase,
+                load_tile<KPT, LI>(rec + (KV ? 2ull : 1ull) * rstart(bucket_of(nit)), nullptr, wbase,
                                    ncnt, false, k2, v2);
         }
         if (cnt > 1u) {
             for (uint32_t p = 0, shift = 0; p < 2u; ++p, shift += 8u) {
                 const uint32_t mask = 255u;
-                for (uint32_t d = lane; d < (uint32_t)RADIX; d += 64) s_whist[w][d] = 0u;
                 Slots<KPT, false> rank;
-                rank_slots<R, KPT, RANK>(k, rank, s_whist[w], shift, mask);   // pads included
-                __syncthreads();
-                uint32_t c = 0, wc[NW];
-                if (tid < (uint32_t)RADIX) {
-#pragma unroll
-                    for (int q = 0; q < NW; ++q) { wc[q] = s_whist[q][tid]; c += wc[q]; }
-                }
-                uint32_t ttot;
-                const uint32_t tstart = block_excl_scan_n<NW>(c, s_scratch, ttot);
-                if (tid < (uint32_t)RADIX) {
-                    uint32_t o = tstart;
-#pragma unroll
-                    for (int q = 0; q < NW; ++q) { s_whist[q][tid] = o; o += wc[q]; }
-                }
+                uint32_t c;   // pads included (kPadKey: digit 255, after every real key)
+                const uint32_t tstart = rank_tile<R, NW, KPT, RANK>(k, rank, s_whist, s_scratch, shift, mask, 0u, c);
+                if (tid < (uint32_t)RADIX) set_wave_offsets<R, NW>(s_whist, tstart);
                 __syncthreads();
 #pragma unroll
                 for (int j = 0; j < KPT; ++j) {
@@ -1595,18 +1586,22 @@ __global__ __launch_bounds__(BLOCK, MW) void k_bucket_sort(const uint32_t* rec,
                 __syncthreads();
             }
         }
-        // slot j of lane l of wave w holds sorted position w * WAVE_KEYS + j * 64 + l
+        // slot j of lane l of wave w holds sorted position w * WAVE_KEYS + j * 64 + l; one base
+        // address per output array and constant per-slot offsets (per-slot addresses spilled)
+        {
+            const size_t o0 = (size_t)base + wbase + lane;
+            const int lim = (int)cnt - (int)(wbase + lane);
 #pragma unroll
-        for (int j = 0; j < KPT; ++j) {
-            const uint32_t p2 = wbase + j * 64 + lane;
-            if (p2 < cnt) {
-                if constexpr (LO == LAYOUT_AOS) {
-                    reinterpret_cast<uint2*>(out_k)[(size_t)base + p2] = make_uint2(k[j] + kbase, v[j]);
-                } else if constexpr (LO == LAYOUT_KEYS) {
-                    out_k[(size_t)base + p2] = k[j] + kbase;
-                } else {
-                    out_k[(size_t)base + p2] = k[j] + kbase;
-                    out_v[(size_t)base + p2] = v[j];
+            for (int j = 0; j < KPT; ++j) {
+                if (j * 64 < lim) {
+                    if constexpr (LO == LAYOUT_AOS) {
+                        (reinterpret_cast<uint2*>(out_k) + o0)[j * 64] = make_uint2(k[j] + kbase, v[j]);
+                    } else if constexpr (LO == LAYOUT_KEYS) {
+                        (out_k + o0)[j * 64] = k[j] + kbase;
+                    } else {
+                        (out_k + o0)[j * 64] = k[j] + kbase;
+                        (out_v + o0)[j * 64] = v[j];
+                    }
                 }
             }
         }
@@ -1621,7 +1616,7 @@ __global__ __launch_bounds__(BLOCK, MW) void k_bucket_sort(const uint32_t* rec,
                 if constexpr (KV) v[j] = v2[j];
             }
         } else {
-            load_tile<KPT, LI>(rec + (KV ? 2ull : 1ull) * rstart(over ? over[1 + it] : it), nullptr, wbase, cnt, false, k, v);
+            load_tile<KPT, LI>(rec + (KV ? 2ull : 1ull) * rstart(bucket_of(it)), nullptr, wbase, cnt, false, k, v);
         }
     }
 }
@@ -1636,8 +1631,12 @@ __global__ __launch_bounds__(BLOCK, MW) void k_bucket_sort(const uint32_t* rec,
 // the bits w >> 16 shares with b << bshift agree).  Keys only: the keys themselves move (no p).
 // Pads (positions >= cnt) are w = kPadKey: digit 255 in both passes, after every real key.
 // One bucket per workgroup: a grid of 65536 (every bucket over min_cnt), or listed buckets (`over`).
-template <int KPT, int RANK, int LO>
-__global__ __launch_bounds__(1024, 1) void k_bucket_sort_wide(const uint32_t* rec,
+// BLOCK x KPT per workgroup, MW waves per SIMD (the occupancy the register budget must allow:
+// 1024 x 34 = one workgroup per CU, 512 x 34 two, 512 x 18 three).  VREG: the values ride in
+// registers through the sort (else the bucket's records are read again, from L2 / Infinity Cache,
+// for the value exchange).
+template <int BLOCK, int KPT, int RANK, int LO, int MW = 4, bool VREG = false>
+__global__ __launch_bounds__(BLOCK, MW) void k_bucket_sort_wide(const uint32_t* rec,
                                                               const uint32_t* __restrict__ hist16,
                                                               const uint32_t* __restrict__ base16,
                                                               uint32_t* out_k, uint32_t* __restrict__ out_v,
@@ -1649,11 +1648,13 @@ __global__ __launch_bounds__(1024, 1) void k_bucket_sort_wide(const uint32_t* re
                                                               uint32_t rmask, uint32_t bshift,
                                                               uint32_t b_lo = 0, uint32_t b_cnt = 65536) {
     // unlisted (over == null): buckets [b_lo, b_lo + b_cnt), e.g. a multi-GPU region's top bytes
-    constexpr int BLOCK = 1024, NW = BLOCK / 64, RADIX = 256;
+    constexpr int NW = BLOCK / 64, RADIX = 256;
     constexpr int TILE = BLOCK * KPT;
     constexpr int WAVE_KEYS = 64 * KPT;
     constexpr bool KV = LO != LAYOUT_KEYS;
+    constexpr bool VR = KV && VREG;
     static_assert(TILE <= 65536, "16-bit record positions");
+    static_assert(BLOCK >= RADIX, "one digit per thread in the scan");
     __shared__ uint32_t s_whist[NW][RADIX];
     __shared__ uint32_t s_scratch[NW];
     __shared__ uint32_t s_w[TILE];
@@ -1672,14 +1673,22 @@ __global__ __launch_bounds__(1024, 1) void k_bucket_sort_wide(const uint32_t* re
         const uint32_t base = sstart[b >> 8] + base16[b];
         const uint32_t* src = rec + (KV ? 2ull : 1ull) * (base & rmask);
         uint32_t x[KPT];
+        uint32_t v[VR ? KPT : 1];
         {
             const int lim = (int)cnt - (int)(wbase + lane);
             const uint2* sr = reinterpret_cast<const uint2*>(src) + wbase + lane;
             const uint32_t* sk = src + wbase + lane;
 #pragma unroll
             for (int j = 0; j < KPT; ++j) {
-                if (KV) x[j] = j * 64 < lim ? ((sr[j * 64].x & 0xFFFFu) << 16) | (wbase + (uint32_t)j * 64u + lane) : kPadKey;
-                else x[j] = j * 64 < lim ? sk[j * 64] : kPadKey;
+                if (VR) {
+                    const uint2 r = j * 64 < lim ? sr[j * 64] : make_uint2(0u, 0u);
+                    x[j] = j * 64 < lim ? ((r.x & 0xFFFFu) << 16) | (wbase + (uint32_t)j * 64u + lane) : kPadKey;
+                    v[VR ? j : 0] = r.y;
+                } else if (KV) {
+                    x[j] = j * 64 < lim ? ((sr[j * 64].x & 0xFFFFu) << 16) | (wbase + (uint32_t)j * 64u + lane) : kPadKey;
+                } else {
+                    x[j] = j * 64 < lim ? sk[j * 64] : kPadKey;
+                }
             }
         }
         // KV: the key's low 16 bits sit in w's high half; keys only: the key itself
@@ -1709,7 +1718,7 @@ __global__ __launch_bounds__(1024, 1) void k_bucket_sort_wide(const uint32_t* re
             uint32_t* sw = s_w + wbase + lane;
 #pragma unroll
             for (int j = 0; j < KPT; ++j)
-                if (j * 64 < lim) sw[j * 64] = sr[j * 64].y;
+                if (j * 64 < lim) sw[j * 64] = VR ? v[VR ? j : 0] : sr[j * 64].y;
             __syncthreads();
         }
         const uint32_t hi = b << bshift;

@@ -23,6 +23,8 @@
 #include <string>
 #include <vector>
 
+#include <rocprofiler-sdk-roctx/roctx.h>
+
 #include "../../include/rsort.h"
 #include "rs_internal.h"
 #include "rs_kernels.hpp"
@@ -142,6 +144,14 @@ struct DeviceGuard {
     }
 };
 
+// Every launch group of a sort is a named roctx range on the host (rocprofv3 --marker-trace
+// attributes the kernels it encloses to histogram / MSD pass 0 / pass 1 / bucket / fallback / LSD
+// pass without relying on template names; SURVEY.md §5 "Tracing").
+struct RoctxRange {
+    explicit RoctxRange(const char* name) { roctxRangePushA(name); }
+    ~RoctxRange() { roctxRangePop(); }
+};
+
 struct KernelTimer {
     bool enabled = false;
     struct Rec { int kind; hipEvent_t a, b; };
@@ -156,9 +166,12 @@ struct KernelTimer {
         (void)hipEventCreate(&e);
         return e;
     }
-    // Records events around `launch` when enabled.
+    // Records events around `launch` when enabled; always a roctx range named `label`.
     template <class F>
-    void run(int kind, hipStream_t s, F&& launch) {
+    void run(int kind, hipStream_t s, F&& launch, const char* label = nullptr) {
+        static const char* const names[RS_KERNEL_KINDS] = {"rsort.histogram", "rsort.scan", "rsort.scatter",
+                                                           "rsort.check", "rsort.bucket", "rsort.fallback"};
+        RoctxRange range(label ? label : names[kind]);
         if (!enabled) { launch(); return; }
         Rec r{kind, get(), get()};
         (void)hipEventRecord(r.a, s);
@@ -412,7 +425,7 @@ rs_status run_pass_cfg(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint3
                     default: launch_onesweep_l<R, BLOCK, KPT, K, K, SR>(p, ik, iv, ok, ov, n, shift, mask, ntiles, gate, pass, s);
                 }
             }
-        });
+        }, p->scatter_kind == RS_KERNEL_FALLBACK ? "rsort.lsd.pass (fallback)" : "rsort.lsd.pass");
         HIP_TRY(hipGetLastError());
         return RS_OK;
     }
@@ -838,8 +851,9 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
     const double slack = RS_KNOB("RSORT_BUCKET_SLACK", 1.0);
     const uint32_t want = (uint32_t)(mean * slack + 4.0 * std::sqrt(mean));
     constexpr uint32_t bb = 256;
-    static const uint32_t kpts[] = {4, 8, 12, 17, 18, 24};
-    static const uint32_t kpts_keys[] = {4, 5, 9, 17, 24, 0};   // 64M keys: 1280-key tiles
+    // (KV 256 x 34 = 8704 records: 2^29 keys, two workgroups per CU)
+    static const uint32_t kpts[] = {4, 8, 12, 17, 18, 24, 34};
+    static const uint32_t kpts_keys[] = {4, 5, 9, 17, 24, 0, 0};   // 64M keys: 1280-key tiles
     uint32_t small_cap = 0, small_kpt = 0;
     for (uint32_t kpt : keys ? kpts_keys : kpts)
         if (kpt && !small_cap && want <= bb * kpt) { small_cap = bb * kpt; small_kpt = kpt; }
@@ -852,8 +866,13 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
             if (!wave_kpt && want <= 64u * kpt) wave_kpt = kpt;
         if (wave_kpt) small_cap = 64u * wave_kpt;
     }
-    // buckets too large for every population-sized tile (~2^29 keys and more): the wide kernel
-    // takes every bucket, one workgroup each, and nothing is listed
+    // with values, buckets of up to 17408 records (2^30 keys): 1024 x 17 records, 8-byte staging,
+    // one workgroup per CU (8-byte staging measured 1.7x faster than the wide kernel's 4-byte
+    // positions + value exchange at 2^29: 1.67 vs 2.87 ms, profiles/r03_wide_modes.jsonl)
+    const bool big_tile = !keys && !small_cap && want <= 1024u * 17u;
+    if (big_tile) small_cap = 1024u * 17u;
+    // buckets too large for every workgroup tile (~2^31 keys): the wide kernel takes every bucket,
+    // one workgroup each, and nothing is listed
     const bool wide_all = small_cap == 0;
     if (wide_all) small_cap = kBucketCap;
     // one histogram row per CU in tmp_k (R1 is written only after the rows are added)
@@ -889,7 +908,7 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
         hipLaunchKernelGGL(rs::k_hist16_reduce, dim3(256), dim3(1024), 0, s, (const uint32_t*)p->tmp_k,
                            hrows, hist16, top_tot, range_bad, base16, small_cap, kBucketCap, over, big,
                            p->ptot, (uint32_t)(rs::kTotalsMax + 32));
-    });
+    }, region ? "rsort.msd.region_table" : "rsort.msd.hist16");
     HIP_TRY(hipGetLastError());
     p->timer.run(RS_KERNEL_SCAN, s, [&] {
         auto plan = [&](auto kern) {
@@ -898,7 +917,7 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
         };
         if (tile == 2u * kLarge.tile) plan(rs::k_msd_plan<2 * kLarge.tile>);
         else plan(rs::k_msd_plan<kLarge.tile>);
-    });
+    }, "rsort.msd.plan");
     HIP_TRY(hipGetLastError());
     const uint32_t* g_msd = gates + rs::kGateMsd;
     // R2 replaced by a power-of-two ring (sweep experiment RSORT_EXP_RING = log2 records; the
@@ -939,7 +958,7 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
         else
             launch_msd_pass<S, A, 0>(p, sk, sv, r1, nullptr, n32, vbits - 8, ntiles, top_tot, p->tickets + 4,
                                      g_msd, nullptr, nullptr, s);
-    });
+    }, "rsort.msd.pass0");
     HIP_TRY(hipGetLastError());
     // MSD pass 1: R1 -> R2 records, by the next byte inside every top-byte segment
     if (rs_status st = next_epoch(p, s)) return st;
@@ -957,14 +976,20 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
         else
             launch_msd_pass<A, A, 1>(p, r1, nullptr, ring ? ring : r2, nullptr, n32, vbits - 16, ntiles + 257, nullptr,
                                      p->tickets + 5, g_msd, segtab, base16, s, 0u, rmask);
-    });
+    }, "rsort.msd.pass1");
     HIP_TRY(hipGetLastError());
     const bool ballot = p->rank_mode == rs::RANK_BALLOT;
     constexpr int A0 = rs::RANK_LDS_ATOMIC, B0 = rs::RANK_BALLOT;
     p->timer.run(RS_KERNEL_BUCKET, s, [&] {
         auto small = [&](auto kern) {
-            hipLaunchKernelGGL(kern, dim3(65536), dim3(bb), 0, s, ring ? ring : r2, hist16, base16, uk, uv, g_msd,
-                               p->tickets + 16, 0u, (const uint32_t*)nullptr, kbase, (const uint32_t*)sstart, rmask);
+            hipLaunchKernelGGL(kern, dim3(b_cnt), dim3(bb), 0, s, ring ? ring : r2, hist16, base16, uk, uv, g_msd,
+                               p->tickets + 16, 0u, (const uint32_t*)nullptr, kbase, (const uint32_t*)sstart, rmask,
+                               b_lo, b_cnt);
+        };
+        auto big = [&](auto kern) {   // the 1024 x 17 tile (big_tile), one bucket per workgroup
+            hipLaunchKernelGGL(kern, dim3(b_cnt), dim3(1024), 0, s, ring ? ring : r2, hist16, base16, uk, uv, g_msd,
+                               p->tickets + 16, 0u, (const uint32_t*)nullptr, kbase, (const uint32_t*)sstart, rmask,
+                               b_lo, b_cnt);
         };
 #if RS_SWEEP
         // sweep only, keys only: a persistent grid whose workgroups load their next bucket while
@@ -981,15 +1006,15 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
         // the wide kernel: every bucket (wide_all), or the listed buckets over the population-sized
         // tile on a small persistent grid (sweep: RSORT_OVER_GRID workgroups)
         const uint32_t over_grid = std::max(1u, (uint32_t)RS_KNOB("RSORT_OVER_GRID", 256));
-        auto large = [&](auto kern) {
-            hipLaunchKernelGGL(kern, dim3(wide_all ? b_cnt : over_grid), dim3(1024), 0, s, ring ? ring : r2,
+        auto large = [&](auto kern, uint32_t block) {
+            hipLaunchKernelGGL(kern, dim3(wide_all ? b_cnt : over_grid), dim3(block), 0, s, ring ? ring : r2,
                                hist16, base16, uk, uv, g_msd, p->tickets + 16, wide_all ? 0u : small_cap,
                                wide_all ? (const uint32_t*)nullptr : (const uint32_t*)over, kbase,
                                (const uint32_t*)sstart, rmask, vbits - 16, b_lo, b_cnt);
         };
         auto both = [&](auto lo) {
             constexpr int LO = decltype(lo)::value;
-#define RS_BK(KP) case KP: ballot ? small(rs::k_bucket_sort<bb, KP, B0, LO, (KP <= 18 ? 3 : 1)>) : small(rs::k_bucket_sort<bb, KP, A0, LO, (KP <= 18 ? 3 : 1)>); break;
+#define RS_BK(KP) case KP: ballot ? small(rs::k_bucket_sort<bb, KP, B0, LO, (KP <= 18 ? 3 : (KP == 34 ? 2 : 1))>) : small(rs::k_bucket_sort<bb, KP, A0, LO, (KP <= 18 ? 3 : (KP == 34 ? 2 : 1))>); break;
             if constexpr (LO == K) {
                 bool wave_done = false;
 #if RS_SWEEP
@@ -1039,19 +1064,31 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
                 }
             } else {
                 switch (small_kpt) {
-                    RS_BK(4) RS_BK(8) RS_BK(12) RS_BK(17) RS_BK(18) RS_BK(24)
+                    RS_BK(4) RS_BK(8) RS_BK(12) RS_BK(17) RS_BK(18) RS_BK(24) RS_BK(34)
                     default: break;   // every bucket goes to the listed large-tile launch
                 }
             }
 #undef RS_BK
-            // the listed buckets (none for uniform keys below ~2^29), or every bucket (wide_all)
-            ballot ? large(rs::k_bucket_sort_wide<kWideKpt, B0, LO>)
-                   : large(rs::k_bucket_sort_wide<kWideKpt, A0, LO>);
+            // the listed buckets (none for uniform keys below ~2^29): the largest wide tile; every
+            // bucket (wide_all): the smallest wide tile that holds the population's buckets (512 x 18:
+            // three workgroups per CU, 512 x 34: two, 1024 x 34: one)
+            if (big_tile)
+                ballot ? big(rs::k_bucket_sort<1024, 17, B0, LO, 4>) : big(rs::k_bucket_sort<1024, 17, A0, LO, 4>);
+            // the listed buckets over the primary tile (none for uniform keys), or every bucket
+            // (wide_all); keys only: the smallest wide tile that holds the population's buckets
+            // (512 x 18: three workgroups per CU, 512 x 34: two, 1024 x 34: one)
+            if (wide_all && LO == K && want <= 512u * 18u)
+                ballot ? large(rs::k_bucket_sort_wide<512, 18, B0, LO, 6>, 512) : large(rs::k_bucket_sort_wide<512, 18, A0, LO, 6>, 512);
+            else if (wide_all && LO == K && want <= 512u * 34u)
+                ballot ? large(rs::k_bucket_sort_wide<512, 34, B0, LO, 4>, 512) : large(rs::k_bucket_sort_wide<512, 34, A0, LO, 4>, 512);
+            else
+                ballot ? large(rs::k_bucket_sort_wide<1024, kWideKpt, B0, LO>, 1024)
+                       : large(rs::k_bucket_sort_wide<1024, kWideKpt, A0, LO>, 1024);
         };
         if (keys) both(std::integral_constant<int, K>{});
         else if (out_aos) both(std::integral_constant<int, A>{});
         else both(std::integral_constant<int, S>{});
-    });
+    }, "rsort.msd.bucket");
     HIP_TRY(hipGetLastError());
     // the fallback (gated off on the device unless taken): pass 0's byte-0 totals, then the four
     // LSD passes on the input
@@ -1069,7 +1106,7 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
         else
             hipLaunchKernelGGL(rs::k_pass_totals<1>, dim3(tgrid), dim3(RS_TOT_BLOCK), 0, s, sk, n32, pl, 0u, t0,
                                (uint32_t*)nullptr, 0xFFFFFFFFu, 0x1u, g_lsd);
-    });
+    }, "rsort.msd.fallback_totals");
     HIP_TRY(hipGetLastError());
     if (keys) {
         // keys only: four one-sweep passes input -> tmp_k -> uk -> tmp_k -> uk (5 gated launches;

@@ -49,6 +49,10 @@ WORKLOADS = {
     "config4": dict(n=1 << 28, values=True, local_shuffle=False, check_order=True,
                     kind="f32_nearly", seed=4,
                     desc="256M Float32 keys (nearly sorted) + Uint32 values, check_order=true"),
+    # config3 with check_order=true on unsorted input (the order check rides on the hybrid path's
+    # histogram read)
+    "config3_check_order": dict(n=1 << 28, values=True, local_shuffle=True, check_order=True, kind="u32",
+                                seed=3, desc="256M Uint32 keys + Uint32 values, check_order=true, unsorted"),
     # config3's data as one rg32uint texture of (key, value) texels (RadixSortTextureKernel)
     "config3_texture": dict(n=1 << 28, values=True, local_shuffle=False, check_order=False,
                             kind="u32", seed=3, layout="aos",

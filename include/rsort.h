@@ -223,11 +223,15 @@ void      rs_scan_plan_destroy(rs_scan_plan* plan);
  * process (the Node addon, a C/C++ host) the way ncclCommInitAll + ncclGroupStart/End drive
  * several devices from one thread.  Rank r's input is keys[r][0..counts[r]) (+ values[r]) on
  * devices[r]; after rs_group_sort, rank r holds slice r of the global stable ascending order by
- * the 32-bit key (rank-ordered concatenation = the sorted whole).  Steps: top-`top_bits`
- * histogram per rank -> counts to the host -> whole-bucket ownership (~1/world of the keys per
- * rank, equal keys never split) -> stable partition by the top digit (records with values) ->
- * `rounds` exchange rounds of point-to-point messages (one per peer per round) -> each round's
- * region sorted locally as soon as it has landed, while later rounds are on the wire. */
+ * the 32-bit key (rank-ordered concatenation = the sorted whole).  The exchange is the first
+ * MSD pass of the single-GPU hybrid sort split across the ranks (52 B/key per rank with values):
+ * rs_plan_hist16 per rank (16-bit bucket table + top-byte totals, one key read) -> tables to the
+ * host -> whole-top-byte ownership (~1/world of the keys per rank, equal keys never split) and
+ * `rounds` groups of top bytes per rank -> stable partition by the top byte (records with values;
+ * the hybrid sort's pass 0) -> `rounds` exchange rounds, one message per (source, top byte) chunk,
+ * laid out round-major, then top byte, then source -> each round's region sorted by
+ * rs_plan_sort_region (next-byte pass + in-LDS bucket sort) as soon as it has landed, while later
+ * rounds are on the wire.  Keys only: the same exchange, each region sorted by rs_plan_sort_n. */
 typedef struct rs_group rs_group;
 
 #define RS_TRANSPORT_RCCL 0u   /* ncclCommInitAll + ncclGroupStart / ncclSend / ncclRecv (xGMI) */
@@ -239,7 +243,7 @@ typedef struct rs_group_desc {
                                buffers and local sort plans grow on demand */
     uint32_t flags;         /* RS_FLAG_HAS_VALUES or 0 (keys only); nothing else */
     uint32_t transport;     /* RS_TRANSPORT_* */
-    uint32_t top_bits;      /* exchange digit width, 1..8; 0 -> 8 (256 buckets) */
+    uint32_t top_bits;      /* exchange digit width: 8 or 0 (-> 8, the top byte) */
     uint32_t rounds;        /* exchange rounds (bucket groups per rank), 1..16; 0 -> 4 */
 } rs_group_desc;
 

@@ -324,3 +324,69 @@ def test_msd_keys_workgroup_bucket_kernel(monkeypatch, n, env):
         monkeypatch.setenv(k, v)
     t = _sort_keys_and_check(n, "uniform")
     assert t["bucket"]["launches"] == 1 and t["scatter"]["launches"] == 2
+
+
+def _chk_keys(kind, n):
+    u = O.gen_u32(61, n)
+    if kind == "uniform":
+        return u
+    if kind == "sorted":
+        return np.sort(u)
+    if kind == "last_pair":            # sorted but the last pair (the reference's Q1 blind spot)
+        k = np.sort(u)
+        k[-2], k[-1] = k[-1], k[-2]
+        return k
+    if kind == "reverse":
+        return np.sort(u)[::-1].copy()
+    if kind == "f32_nearly":           # config 4's input shape: the LSD fallback, totals from the read
+        import bench
+        return bench.nearly_sorted_f32_bits(n, 4)
+    raise ValueError(kind)
+
+
+@pytest.mark.parametrize("kind", ["uniform", "sorted", "last_pair", "reverse", "f32_nearly"])
+def test_msd_check_order(kind):
+    """check_order on the hybrid path: the input's order check (and the LSD fallback's byte-0
+    totals) ride on the 16-bit histogram read; an input in order gates every later launch off (the
+    reference's early exit, CheckSort.ts:138-145) and comes back untouched; otherwise the hybrid
+    path (or, for skewed keys, the LSD fallback) sorts it - separate arrays, keys only, records."""
+    from radix_sort_amd import RadixSortTextureKernel
+    n = (1 << 25) + 3
+    keys = _chk_keys(kind, n)
+    vals = np.arange(n, dtype=np.uint32)
+    ek, ev = O.stable_sort_masked_c(keys, vals, 32)
+    kt = torch.from_numpy(keys.view(np.int32).copy()).to(DEV)
+    vt = torch.from_numpy(vals.view(np.int32).copy()).to(DEV)
+    kern = RadixSortKernel(keys=kt, values=vt, count=n, check_order=True)
+    kern.set_profiling(True)
+    kern.dispatch()
+    torch.cuda.synchronize()
+    kern.check()
+    t = kern.kernel_times()
+    assert np.array_equal(kt.cpu().numpy().view(np.uint32), ek)
+    assert np.array_equal(vt.cpu().numpy().view(np.uint32), ev)
+    assert t["bucket"]["launches"] >= 1 and t["check"]["launches"] == 0   # the hybrid path's launches
+    if kind == "uniform":
+        assert t["bucket"]["ms"] > t["fallback"]["ms"]
+    if kind == "f32_nearly":
+        assert t["fallback"]["ms"] > t["bucket"]["ms"]
+    if kind == "sorted":                  # everything after the read gated off
+        assert t["scatter"]["ms"] + t["bucket"]["ms"] + t["fallback"]["ms"] < t["histogram"]["ms"]
+    kern.destroy()
+    # keys only, in place
+    kt = torch.from_numpy(keys.view(np.int32).copy()).to(DEV)
+    kern = RadixSortKernel(keys=kt, count=n, check_order=True)
+    kern.dispatch()
+    torch.cuda.synchronize()
+    kern.check()
+    assert np.array_equal(kt.cpu().numpy().view(np.uint32), ek), "keys only"
+    kern.destroy()
+    # records in place (RadixSortTextureKernel)
+    rt = torch.from_numpy(np.stack([keys, vals], axis=-1).reshape(-1).view(np.int32).copy()).to(DEV).view(-1, 2)
+    kern = RadixSortTextureKernel(texture=rt, count=n, check_order=True)
+    kern.dispatch()
+    torch.cuda.synchronize()
+    kern.check()
+    out = rt.cpu().numpy().view(np.uint32).reshape(-1, 2)
+    assert np.array_equal(out[:, 0], ek) and np.array_equal(out[:, 1], ev), "records"
+    kern.destroy()

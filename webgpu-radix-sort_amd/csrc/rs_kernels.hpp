@@ -1277,25 +1277,38 @@ __device__ __forceinline__ void set_gate(uint32_t* g, uint32_t v) {
 // AOS_WIDE (records 16-byte aligned): two records per 16-byte load instead of one per 8-byte load.
 // FULL (kbase = 0, the whole 32-bit range, shift = 16): the bucket is key >> 16 and its counter
 // half bit 16, so a key costs ~3 VALU + 1 LDS atomic (the kernel is issue-bound, not HBM-bound).
-template <int L, bool AOS_WIDE = false, bool FULL = false>
+// CHECK (check_order on the hybrid path, FULL only): the same read also (a) checks the input's
+// order - *inv |= 1 if any adjacent pair is out of order (every pair, the reference's quirks Q1/Q2
+// fixed; CheckSort.ts:102-113) - and (b) counts the low byte of every key into b0rows[block][256]
+// (the LSD fallback's pass-0 totals: k_hist16_reduce adds them, so the fallback needs no read of
+// its own).
+template <int L, bool AOS_WIDE = false, bool FULL = false, bool CHECK = false>
 __global__ __launch_bounds__(1024) void k_hist16_in(const uint32_t* __restrict__ keys, uint32_t n,
                                                      uint32_t* __restrict__ rows, uint32_t kbase,
                                                      uint32_t range, uint32_t shift,
-                                                     uint32_t* __restrict__ z0, uint32_t* __restrict__ z1) {
+                                                     uint32_t* __restrict__ z0, uint32_t* __restrict__ z1,
+                                                     uint32_t* inv = nullptr, uint32_t* __restrict__ b0rows = nullptr) {
+    static_assert(!CHECK || FULL, "the order check rides on whole-range histograms only");
     // z0, z1: the reduction's overflow-bucket count and oversize flag (k_hist16_reduce adds to them)
     if (blockIdx.x == 0 && threadIdx.x == 0) { *z0 = 0u; *z1 = 0u; }
     constexpr uint32_t B = 1024, W = 32768, PER = W / B;
     constexpr bool NARROW = L == LAYOUT_AOS && !AOS_WIDE;
     constexpr uint32_t KPL = NARROW ? 1u : (L == LAYOUT_AOS ? 2u : 4u);   // keys per load
     constexpr uint32_t STEPS = 61440u / (B * KPL);                // loads per thread per round
-    constexpr uint32_t FLY = 5;                                    // loads in flight
+    // loads in flight (CHECK: 3, the order check's registers spilled at 5)
+    constexpr uint32_t FLY = CHECK ? 3 : 5;
     static_assert(STEPS % FLY == 0, "whole load groups per round");
     using Vec = typename std::conditional<NARROW, uint2, uint4>::type;
     __shared__ uint32_t h[W];
+    __shared__ uint32_t s_b0[CHECK ? 256 : 1];
     const uint32_t tid = threadIdx.x;
     uint32_t acc[2 * PER];
 #pragma unroll
     for (uint32_t i = 0; i < PER; ++i) { h[tid + B * i] = 0u; acc[2 * i] = 0u; acc[2 * i + 1] = 0u; }
+    if (CHECK && tid < 256u) s_b0[tid] = 0u;
+    constexpr uint32_t KS = L == LAYOUT_AOS ? 2u : 1u;   // words per key
+    bool inverted = false;
+    auto inv2 = [&](uint32_t a, uint32_t b) { inverted |= a > b; };
     // 64-bit: n + gridDim.x - 1 wraps in 32 bits for n > 2^32 - gridDim.x (chunk would be 0 and
     // every row would count nothing)
     const uint64_t chunk = (((uint64_t)n + gridDim.x - 1) / gridDim.x + 3u) & ~3ull;
@@ -1304,9 +1317,48 @@ __global__ __launch_bounds__(1024) void k_hist16_in(const uint32_t* __restrict__
     const uint64_t nv = (hi - lo) / KPL;                          // whole vectors
     const Vec* v4 = reinterpret_cast<const Vec*>(keys + (L == LAYOUT_AOS ? 2 : 1) * lo);
     bool bad = false;
+    // FULL, one load's keys (1, 2 or 4): sorted or duplicate-heavy input puts a whole wave's keys in
+    // one 16-bit bucket (and, check_order, one low byte: config 4's small floats have few mantissa
+    // bits, so a whole chunk has low byte 0), and 64 lanes adding to one LDS address serialise
+    // (config 4: the slowest chunks' workgroups set the kernel at 1.0 ms instead of 0.3), so lanes
+    // whose keys share a counter are grouped by counter, one add per group: up to two groups per
+    // wave (a sorted run, or a run crossing one counter edge, with a few displaced keys); random keys
+    // almost never share a counter within one load, and cost one ballot per counter array here
+    auto grouped = [&](uint32_t c, bool uni, uint32_t m, auto&& add) {
+        uint64_t left = __ballot(uni);
+        bool done = false;
+        for (int r = 0; r < 2 && left; ++r) {
+            const int lead = __builtin_ctzll(left);
+            const uint32_t cl = __builtin_amdgcn_readlane(c, lead);
+            const bool mine = uni && c == cl;
+            const uint64_t grp = __ballot(mine);
+            if (mine && mbcnt(grp) == 0) add(cl, m * (uint32_t)__popcll(grp));
+            done |= mine;
+            left &= ~grp;
+        }
+        if (!done && uni) add(c, m);
+        return done || uni;
+    };
+    auto add16 = [&](uint32_t b, uint32_t c) { atomicAdd(&h[b >> 1], c << ((b & 1u) << 4)); };
+    auto count_load = [&](const uint32_t (&ks)[4], int m) {
+        const uint32_t b = ks[0] >> 16;
+        bool uni = true;
+        for (int j = 1; j < m; ++j) uni &= (ks[j] >> 16) == b;
+        if (!grouped(b, uni, (uint32_t)m, add16))
+            for (int j = 0; j < m; ++j) add16(ks[j] >> 16, 1u);
+        if constexpr (CHECK) {
+            const uint32_t d = ks[0] & 255u;
+            bool uni0 = true;
+            for (int j = 1; j < m; ++j) uni0 &= (ks[j] & 255u) == d;
+            auto add0 = [&](uint32_t x, uint32_t c) { atomicAdd(&s_b0[x], c); };
+            if (!grouped(d, uni0, (uint32_t)m, add0))
+                for (int j = 0; j < m; ++j) add0(ks[j] & 255u, 1u);
+        }
+    };
     auto count = [&](uint32_t key) {
         if constexpr (FULL) {
             atomicAdd(&h[key >> 17], 1u << ((key >> 12) & 16u));
+            if constexpr (CHECK) atomicAdd(&s_b0[key & 255u], 1u);
         } else {
             const uint32_t rk = key - kbase;
             bad |= rk > range;
@@ -1332,14 +1384,37 @@ __global__ __launch_bounds__(1024) void k_hist16_in(const uint32_t* __restrict__
 #pragma unroll
             for (uint32_t u = 0; u < FLY; ++u) {
                 const uint64_t i = base + (uint64_t)(s0 + u) * B + tid;
+                if (CHECK) q[u] = Vec{};   // defined for the neighbour read of lanes past nv
                 if (i < nv) q[u] = v4[i];
             }
 #pragma unroll
             for (uint32_t u = 0; u < FLY; ++u) {
-                if (base + (uint64_t)(s0 + u) * B + tid < nv) {
-                    if constexpr (NARROW) { count(q[u].x); }
+                const uint64_t i = base + (uint64_t)(s0 + u) * B + tid;
+                uint32_t nxt = 0;
+                if constexpr (CHECK) {
+                    // the first key of vector i + 1: the next lane's (DPP wave_shl:1, in uniform
+                    // control flow), or loaded where that lane has none (lane 63, the chunk's last
+                    // vector: then the key after the vectors, which may be the next chunk's)
+                    nxt = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)q[u].x, 0x130, 0xf, 0xf, false);
+                    if (i < nv && (lane_id() == 63 || i + 1 >= nv)) {
+                        const uint64_t j = lo + KPL * (i + 1);
+                        nxt = j < n ? keys[KS * j] : 0xFFFFFFFFu;
+                    }
+                }
+                if (i < nv) {
+                    if constexpr (FULL) {
+                        if constexpr (NARROW) { const uint32_t ks[4] = {q[u].x, 0u, 0u, 0u}; count_load(ks, 1); }
+                        else if constexpr (L == LAYOUT_AOS) { const uint32_t ks[4] = {q[u].x, q[u].z, 0u, 0u}; count_load(ks, 2); }
+                        else { const uint32_t ks[4] = {q[u].x, q[u].y, q[u].z, q[u].w}; count_load(ks, 4); }
+                    }
+                    else if constexpr (NARROW) { count(q[u].x); }
                     else if constexpr (L == LAYOUT_AOS) { count(q[u].x); count(q[u].z); }
                     else { count(q[u].x); count(q[u].y); count(q[u].z); count(q[u].w); }
+                    if constexpr (CHECK) {
+                        if constexpr (NARROW) { inv2(q[u].x, nxt); }
+                        else if constexpr (L == LAYOUT_AOS) { inv2(q[u].x, q[u].z); inv2(q[u].z, nxt); }
+                        else { inv2(q[u].x, q[u].y); inv2(q[u].y, q[u].z); inv2(q[u].z, q[u].w); inv2(q[u].w, nxt); }
+                    }
                 }
             }
         }
@@ -1347,8 +1422,16 @@ __global__ __launch_bounds__(1024) void k_hist16_in(const uint32_t* __restrict__
     }
     // the last (hi - lo) % KPL keys of the chunk
     const uint64_t rest = lo + nv * KPL;
-    if (rest + tid < hi) count(keys[(L == LAYOUT_AOS ? 2 : 1) * (rest + tid)]);
+    if (rest + tid < hi) {
+        const uint32_t key = keys[KS * (rest + tid)];
+        count(key);
+        if (CHECK && rest + tid + 1 < n) inv2(key, keys[KS * (rest + tid + 1)]);
+    }
     flush();
+    if constexpr (CHECK) {
+        if (__ballot(inverted) != 0ull && lane_id() == 0) atomicOr(inv, 1u);
+        if (tid < 256u) b0rows[(size_t)blockIdx.x * 256u + tid] = s_b0[tid];   // flush()'s barriers passed
+    }
     uint2* row = reinterpret_cast<uint2*>(rows + (size_t)blockIdx.x * 65536u);
 #pragma unroll
     for (uint32_t i = 0; i < PER; ++i) row[tid + B * i] = make_uint2(acc[2 * i], acc[2 * i + 1]);
@@ -1371,10 +1454,18 @@ __global__ __launch_bounds__(1024) void k_hist16_reduce(const uint32_t* __restri
                                                          uint32_t* __restrict__ base16, uint32_t small,
                                                          uint32_t cap, uint32_t* __restrict__ over,
                                                          uint32_t* __restrict__ big,
-                                                         uint32_t* __restrict__ zero = nullptr, uint32_t nzero = 0) {
-    // zero[0..nzero): the sort's pass totals, tile tickets and device error word (no memset launch)
-    if (blockIdx.x == gridDim.x - 1)
+                                                         uint32_t* __restrict__ zero = nullptr, uint32_t nzero = 0,
+                                                         const uint32_t* __restrict__ b0rows = nullptr) {
+    // zero[0..nzero): the sort's pass totals, tile tickets and device error word (no memset launch);
+    // with b0rows (check_order): zero[0..256) = pass 0's byte-0 totals, the rows' sums
+    if (blockIdx.x == gridDim.x - 1) {
         for (uint32_t i = threadIdx.x; i < nzero; i += blockDim.x) zero[i] = 0u;
+        if (b0rows && threadIdx.x < 256u) {   // the same thread zeroed zero[threadIdx.x] above
+            uint32_t c = 0;
+            for (uint32_t r = 0; r < nrows; ++r) c += b0rows[(size_t)r * 256u + threadIdx.x];
+            zero[threadIdx.x] = c;
+        }
+    }
     __shared__ uint4 s_part[16][64];
     const uint32_t tid = threadIdx.x, c = tid & 63u, g = tid >> 6;
     if (blockIdx.x == 0) {   // any key outside the range (the rows' flag words)
@@ -1454,7 +1545,8 @@ template <int TILE>
 __global__ __launch_bounds__(256) void k_msd_plan(const uint32_t* __restrict__ top_tot,
                                                   uint32_t* __restrict__ segtab, uint32_t max_top,
                                                   uint32_t* over, const uint32_t* big, uint32_t* gates,
-                                                  const uint32_t* __restrict__ range_bad, uint32_t n) {
+                                                  const uint32_t* __restrict__ range_bad, uint32_t n,
+                                                  const uint32_t* inv = nullptr) {
     constexpr int NW = 4;
     __shared__ uint32_t s_scratch[NW];
     const uint32_t tid = threadIdx.x;
@@ -1473,8 +1565,11 @@ __global__ __launch_bounds__(256) void k_msd_plan(const uint32_t* __restrict__ t
     __syncthreads();   // every thread has read over[0]
     if (tid == 0) over[0] = nover < kOverMax ? nover : kOverMax;
     const uint32_t ok = (any_big || *big || nover > kOverMax || *range_bad || stot != n) ? 0u : 1u;
-    set_gate(gates + kGateMsd, ok);
-    set_gate(gates + kGateLsd, 1u - ok);
+    // check_order: an input already in order needs neither path (the reference's early exit,
+    // CheckSort.ts:138-145: every later dispatch zeroed)
+    const uint32_t run = (inv && *inv == 0u) ? 0u : 1u;
+    set_gate(gates + kGateMsd, ok & run);
+    set_gate(gates + kGateLsd, (1u - ok) & run);
 }
 
 // In-LDS sort of the 16-bit buckets: a workgroup takes a bucket's records (R2, contiguous, at most

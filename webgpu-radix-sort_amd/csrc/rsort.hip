@@ -532,9 +532,13 @@ bool use_onesweep(const rs_plan* p, uint64_t n) {
     return p->layout != rs::LAYOUT_KEYS && !use_small_tiles(p, n);
 }
 
+// Words of tmp_k per k_hist16_in row: 65536 counts and a flag word; with check_order also the
+// row's 256 byte-0 counts (the LSD fallback's pass-0 totals).
+uint64_t hist_row_words(const rs_plan* p) { return 65537ull + (p->check_order ? 256ull : 0ull); }
+
 // The hybrid MSD path applies (the device still falls back to the LSD passes for skewed keys).
 bool use_msd(const rs_plan* p, uint64_t n) {
-    if (!p->msd || p->msd_mode == 0 || p->check_order || p->bit_count != 32 || p->radix_bits != 8 ||
+    if (!p->msd || p->msd_mode == 0 || p->bit_count != 32 || p->radix_bits != 8 ||
         use_small_tiles(p, n) || n < kMsdMin)
         return false;
     // above kMsdMax keys some 16-bit bucket is all but certain to exceed kBucketCap (and above
@@ -544,9 +548,9 @@ bool use_msd(const rs_plan* p, uint64_t n) {
     // keys only: R1 = tmp_k (n words, which first holds the histogram rows), R2 = the caller's keys;
     // the one-sweep passes of this path are its own (the keys-only LSD sort keeps the histogram path)
     if (p->layout == rs::LAYOUT_KEYS)
-        return p->onesweep_mode != 0 && (uint64_t)p->cus * 65537ull <= n;   // rows + their flag words
+        return p->onesweep_mode != 0 && (uint64_t)p->cus * hist_row_words(p) <= n;   // rows + their flag words
     const bool bufs = (p->layout == rs::LAYOUT_AOS || (p->layout == rs::LAYOUT_SOA && p->tmp2 && p->aos_tmp)) &&
-                      (uint64_t)p->cus * 65536ull <= 2ull * n;   // the histogram rows fit in tmp_k
+                      (uint64_t)p->cus * hist_row_words(p) <= 2ull * n;   // the histogram rows fit in tmp_k
     return bufs && use_onesweep(p, n) && p->kv_cfg == 0 && !p->huge_tiles;
 }
 
@@ -880,6 +884,11 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
     // sweep: RSORT_HIST16_DIV = one row per `div` CUs (fewer rows to write and add)
     const uint32_t hdiv = std::max(1u, (uint32_t)RS_KNOB("RSORT_HIST16_DIV", 1));
     const uint32_t hrows = region ? 1u : std::max(1u, p->cus / hdiv);
+    // check_order (whole-range sorts; the region form never checks): the input's order check rides
+    // on the histogram read (p->flags[0]); the byte-0 rows follow the histogram rows and flags
+    const bool chk = p->check_order && !region && kbase == 0u && vbits == 32u;
+    uint32_t* b0rows = chk ? p->tmp_k + (size_t)hrows * 65537u : nullptr;
+    if (chk) HIP_TRY(hipMemsetAsync(p->flags, 0, 16 * 4, s));
     p->timer.run(RS_KERNEL_HISTOGRAM, s, [&] {
         if (region) {   // the senders counted: one row, their table
             hipLaunchKernelGGL(rs::k_region_rows, dim3(256), dim3(256), 0, s, region_hist, p->tmp_k, over, big);
@@ -895,25 +904,31 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
         const bool full = !generic && kbase == 0u && vbits == 32u;
         auto go = [&](auto kern) {
             hipLaunchKernelGGL(kern, dim3(hrows), dim3(1024), 0, s, sk, n32, p->tmp_k, kbase, range, vbits - 16,
-                               over, big);
+                               over, big, chk ? p->flags : (uint32_t*)nullptr, b0rows);
         };
-        if (in_aos && !narrow && ((uintptr_t)sk & 15u) == 0)
+        if (chk) {   // check_order: the order check and the fallback's byte-0 totals ride along
+            if (in_aos && !narrow && ((uintptr_t)sk & 15u) == 0) go(rs::k_hist16_in<A, true, true, true>);
+            else if (in_aos) go(rs::k_hist16_in<A, false, true, true>);
+            else go(rs::k_hist16_in<S, false, true, true>);
+        } else if (in_aos && !narrow && ((uintptr_t)sk & 15u) == 0) {
             full ? go(rs::k_hist16_in<A, true, true>) : go(rs::k_hist16_in<A, true>);
-        else if (in_aos)
+        } else if (in_aos) {
             full ? go(rs::k_hist16_in<A, false, true>) : go(rs::k_hist16_in<A>);
-        else
+        } else {
             full ? go(rs::k_hist16_in<S, false, true>) : go(rs::k_hist16_in<S>);
+        }
         // the reduction also lays out every top byte's buckets (bases inside the segment, the
         // overflow list, the oversize flag): the plan kernel is left with the 256 segments
         hipLaunchKernelGGL(rs::k_hist16_reduce, dim3(256), dim3(1024), 0, s, (const uint32_t*)p->tmp_k,
                            hrows, hist16, top_tot, range_bad, base16, small_cap, kBucketCap, over, big,
-                           p->ptot, (uint32_t)(rs::kTotalsMax + 32));
+                           p->ptot, (uint32_t)(rs::kTotalsMax + 32), (const uint32_t*)b0rows);
     }, region ? "rsort.msd.region_table" : "rsort.msd.hist16");
     HIP_TRY(hipGetLastError());
     p->timer.run(RS_KERNEL_SCAN, s, [&] {
         auto plan = [&](auto kern) {
             hipLaunchKernelGGL(kern, dim3(1), dim3(256), 0, s, (const uint32_t*)top_tot, segtab, 0xFFFFFFFFu, over,
-                               (const uint32_t*)big, gates, (const uint32_t*)range_bad, n32);
+                               (const uint32_t*)big, gates, (const uint32_t*)range_bad, n32,
+                               chk ? (const uint32_t*)p->flags : (const uint32_t*)nullptr);
         };
         if (tile == 2u * kLarge.tile) plan(rs::k_msd_plan<2 * kLarge.tile>);
         else plan(rs::k_msd_plan<kLarge.tile>);
@@ -1099,7 +1114,8 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
     pl.width[0] = 8;
     const uint32_t tgrid = (uint32_t)std::min<uint64_t>((uint64_t)RS_TOT_PER_CU * p->cus,
                                                         (n + 4ull * RS_TOT_BLOCK - 1) / (4ull * RS_TOT_BLOCK));
-    p->timer.run(RS_KERNEL_FALLBACK, s, [&] {
+    // (check_order: the totals came with the histogram read, see chk above)
+    if (!chk) p->timer.run(RS_KERNEL_FALLBACK, s, [&] {
         if (in_aos)
             hipLaunchKernelGGL(rs::k_pass_totals<2>, dim3(tgrid), dim3(RS_TOT_BLOCK), 0, s, sk, n32, pl, 0u, t0,
                                (uint32_t*)nullptr, 0xFFFFFFFFu, 0x1u, g_lsd);
@@ -1527,7 +1543,7 @@ RS_EXPORT rs_status rs_plan_hist16(rs_plan* p, const void* keys, uint64_t n, voi
         uint32_t* z = p->tmp_k + (size_t)hrows * 65536u;
         auto go = [&](auto kern) {
             hipLaunchKernelGGL(kern, dim3(hrows), dim3(1024), 0, s, (const uint32_t*)keys, (uint32_t)n, p->tmp_k, 0u,
-                               0xFFFFFFFFu, 16u, z, z);
+                               0xFFFFFFFFu, 16u, z, z, (uint32_t*)nullptr, (uint32_t*)nullptr);
         };
         if (aos && ((uintptr_t)keys & 15u) == 0) go(rs::k_hist16_in<rs::LAYOUT_AOS, true, true>);
         else if (aos) go(rs::k_hist16_in<rs::LAYOUT_AOS, false, true>);

@@ -154,6 +154,69 @@ static void range_and_texture(size_t n) {
     for (void* q : {rec, ok, ov}) OK(rs_free(q));
 }
 
+// the multi-GPU bucket path's entry points on one device: the sender's 16-bit table (a
+// partition-usage plan), its partition fed the table's top-byte totals, and region sorts of the
+// partitioned records (all 8 populated top bytes, then top bytes [2, 5) with their own table)
+static void hist16_and_region(size_t n) {
+    std::vector<uint32_t> hk(n), hv(n);
+    for (size_t i = 0; i < n; ++i) { hk[i] = mix(i + 4242) & 0x07FFFFFFu; hv[i] = (uint32_t)i; }
+    std::vector<uint32_t> ref(RS_HIST16_WORDS, 0);
+    for (uint32_t k : hk) { ++ref[k >> 16]; ++ref[65536 + (k >> 24)]; }
+    void *dk, *dv, *dh, *dr, *rec, *ok, *ov;
+    OK(rs_malloc(0, 4 * n, &dk));
+    OK(rs_malloc(0, 4 * n, &dv));
+    OK(rs_malloc(0, 4ull * RS_HIST16_WORDS, &dh));
+    OK(rs_malloc(0, 4ull * 65536, &dr));
+    OK(rs_malloc(0, 8 * n, &rec));
+    OK(rs_malloc(0, 4 * n, &ok));
+    OK(rs_malloc(0, 4 * n, &ov));
+    OK(rs_memcpy_h2d(dk, hk.data(), 4 * n, nullptr));
+    OK(rs_memcpy_h2d(dv, hv.data(), 4 * n, nullptr));
+    rs_plan_desc d{};
+    d.count = n;
+    d.flags = RS_FLAG_HAS_VALUES;
+    d.usage = RS_USAGE_PARTITION;
+    rs_plan *part = nullptr, *sp = nullptr;
+    OK(rs_plan_create(&d, &part));
+    d.usage = RS_USAGE_SORT;
+    OK(rs_plan_create(&d, &sp));
+    if (part && sp) {
+        CHECK(rs_plan_sort(part, dk, dv, nullptr) == RS_ERR_INVALID_ARG, "sort on a partition plan refused");
+        OK(rs_plan_hist16(part, dk, n, dh, nullptr));
+        std::vector<uint32_t> got(RS_HIST16_WORDS);
+        OK(rs_memcpy_d2h(got.data(), dh, 4ull * RS_HIST16_WORDS, nullptr));
+        CHECK(got == ref, "rs_plan_hist16 n=%zu", n);
+        OK(rs_plan_partition_records(part, dk, dv, rec, n, 24, 8, (const uint32_t*)dh + 65536, nullptr));
+        OK(rs_plan_sort_region(sp, rec, ok, ov, n, dh, 0, 8, nullptr));
+        OK(rs_plan_check(sp));
+        std::vector<uint32_t> gk(n), gv(n);
+        OK(rs_memcpy_d2h(gk.data(), ok, 4 * n, nullptr));
+        OK(rs_memcpy_d2h(gv.data(), ov, 4 * n, nullptr));
+        CHECK(verify(hk, gk, &gv, n), "sort_region [0, 8) n=%zu", n);
+        // top bytes [2, 5): the records of those bytes, their table, zero elsewhere
+        size_t a = 0, m = 0;
+        for (uint32_t t = 0; t < 2; ++t) a += ref[65536 + t];
+        for (uint32_t t = 2; t < 5; ++t) m += ref[65536 + t];
+        std::vector<uint32_t> reg(65536, 0), sk, sv;
+        for (uint32_t b = 2u << 8; b < (5u << 8); ++b) reg[b] = ref[b];
+        for (size_t i = 0; i < n; ++i)
+            if ((hk[i] >> 24) >= 2 && (hk[i] >> 24) < 5) { sk.push_back(hk[i]); sv.push_back((uint32_t)i); }
+        OK(rs_memcpy_h2d(dr, reg.data(), 4ull * 65536, nullptr));
+        OK(rs_plan_sort_region(sp, (const uint64_t*)rec + a, ok, ov, m, dr, 2, 5, nullptr));
+        OK(rs_plan_check(sp));
+        gk.assign(m, 0);
+        gv.assign(m, 0);
+        OK(rs_memcpy_d2h(gk.data(), ok, 4 * m, nullptr));
+        OK(rs_memcpy_d2h(gv.data(), ov, 4 * m, nullptr));
+        bool good = m == sk.size();
+        for (size_t i = 0; good && i < m; ++i) good = hk[gv[i]] == gk[i] && (i == 0 || gk[i - 1] < gk[i] || (gk[i - 1] == gk[i] && gv[i - 1] < gv[i]));
+        CHECK(good, "sort_region [2, 5) m=%zu", m);
+    }
+    if (part) rs_plan_destroy(part);
+    if (sp) rs_plan_destroy(sp);
+    for (void* q : {dk, dv, dh, dr, rec, ok, ov}) OK(rs_free(q));
+}
+
 static void scan_case(size_t n) {
     std::vector<uint32_t> h(n), out(n);
     for (size_t i = 0; i < n; ++i) h[i] = mix(i) & 0xFF;
@@ -257,11 +320,14 @@ int main() {
     copy_and_records(70000);
     copy_and_records(13000000);
     range_and_texture(13000001);
+    hist16_and_region(3000000);
+    hist16_and_region(20000003);
     scan_case(1000);
     scan_case(3000017);
     group_case(1, RS_TRANSPORT_RCCL, true, 200000);
     group_case(3, RS_TRANSPORT_COPY, true, 300000);
     group_case(2, RS_TRANSPORT_COPY, false, 13000000);
+    group_case(4, RS_TRANSPORT_COPY, true, 13000000);             // region sorts on the hybrid path
     printf("asan driver: %d failure(s)\n", g_fail);
     return g_fail ? 1 : 0;
 }

@@ -230,6 +230,9 @@ def verify_batch(torch, ops, wl, n, seed, batch, dev) -> None:
 def launch_plan(gpus: int, env: dict, device_count: int, argv: list) -> tuple:
     """How this invocation runs `--gpus N` (decided before anything touches the GPU).
 
+    `--share-gpu` (rehearsal only, never a measurement): every rank on GPU 0 over gloo, so one
+    visible GPU is enough.
+
     -> ("run", None): this process is the bench (N = 1 alone, or one rank of a launcher whose
        WORLD_SIZE equals N);
        ("spawn", cmd): N > 1 without a launcher: start N rank processes under
@@ -237,6 +240,8 @@ def launch_plan(gpus: int, env: dict, device_count: int, argv: list) -> tuple:
        ("error", message): never silently measure fewer GPUs than asked for."""
     if gpus < 1:
         return "error", f"--gpus must be >= 1 (got {gpus})"
+    if "--share-gpu" in argv:
+        device_count = gpus if device_count >= 1 else 0
     world = env.get("WORLD_SIZE")
     if world is not None:
         if int(world) != gpus:
@@ -281,11 +286,16 @@ def main() -> None:
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="config3", choices=sorted(WORKLOADS))
-    ap.add_argument("--n", type=int, default=0, help="override keys per GPU (testing only)")
+    # (not "--n": torch.distributed.run, which re-reads this command line when --gpus N spawns the
+    # ranks, rejects it as an ambiguous abbreviation of its own options)
+    ap.add_argument("--keys-per-gpu", type=int, default=0, help="override keys per GPU (testing only)")
     ap.add_argument("--radix-bits", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--distributed", action="store_true",
                     help="use the bucket-exchange path even at world size 1 (testing)")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="rehearsal of the N-rank path on one GPU: every rank on GPU 0, gloo moves "
+                         "the exchange through host copies (the line is marked; not a measurement)")
     ap.add_argument("--cpu-log2", default="20,22,24",
                     help="CPU baseline sample sizes (log2, comma-separated; 2^20 mandatory)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
@@ -307,9 +317,12 @@ def main() -> None:
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     assert world == args.gpus, (world, args.gpus)   # launch_plan enforced it
+    if args.share_gpu:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    use_dist = world > 1 or args.distributed
+    use_dist = world > 1 or args.distributed or args.share_gpu
+    backend = "gloo" if args.share_gpu else "nccl"
     wl = dict(WORKLOADS[args.workload])
     if use_dist and wl.get("layout") == "aos":
         raise SystemExit("bench: the multi-GPU path sorts separate key/value arrays; "
@@ -322,8 +335,11 @@ def main() -> None:
         os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
                           MASTER_PORT=str(port))
     if use_dist:
-        dist.init_process_group("nccl", device_id=dev)
-    n = args.n or wl["n"]
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+    n = args.keys_per_gpu or wl["n"]
     K, W = args.steps, args.warmup
 
     def barrier():
@@ -411,7 +427,7 @@ def main() -> None:
             extra["sender_kernel_ms_per_step"] = {
                 "hist16 (rs_plan_hist16: one key read)": round(ms[_lib.RS_KERNEL_HISTOGRAM] / max(K, 1), 4),
                 "partition (top-byte one-sweep pass -> records)": round(ms[_lib.RS_KERNEL_SCATTER] / max(K, 1), 4)}
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
         if not ops.is_sorted(r.keys, r.n):
@@ -528,9 +544,12 @@ def main() -> None:
                        "radix_bits": args.radix_bits or 8,
                        "parallelism": "single GPU" if world == 1 else
                        f"{world} ranks, top-byte bucket exchange (RCCL point-to-point rounds)"},
-            "rccl_ranks": dist.get_world_size() if use_dist else 0,
+            "rccl_ranks": dist.get_world_size() if use_dist and backend == "nccl" else 0,
             "roofline": roof, "cpu_baseline": cpu, **extra,
         }
+        if args.share_gpu:
+            out["rehearsal"] = (f"{world} gloo ranks sharing GPU 0, exchange through host copies: "
+                                "tests the N-rank code path, NOT a measurement")
         print(json.dumps(out), file=json_out, flush=True)
     if use_dist:
         dist.destroy_process_group()

@@ -216,6 +216,75 @@ def test_rccl_world1_hip_local_ops_round_trip(chunks):
         dist.destroy_process_group()
 
 
+def _gpu_worker(rank, world, port, n_per_rank, kind, q, chunks, kv):
+    """One rank of the product path (HipLocalOps: rs_plan_hist16, rs_plan_partition_records,
+    rs_plan_sort_region) at world > 1, every rank on cuda:0; the exchange over gloo moves the
+    device buffers through host copies (RCCL would send them directly)."""
+    from radix_sort_amd.distributed import HipLocalOps
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        k = _keys(kind, n_per_rank, rank * n_per_rank)
+        v = np.arange(rank * n_per_rank, (rank + 1) * n_per_rank, dtype=np.uint32)
+        kt = torch.from_numpy(k.view(np.int32).copy()).cuda()
+        vt = torch.from_numpy(v.view(np.int32).copy()).cuda() if kv else None
+        ops = HipLocalOps(0, int(n_per_rank * 1.25), kv)
+        for _ in range(2):          # the second sort reuses the plans and the side stream
+            r = distributed_sort(kt, vt, ops, chunks=chunks)
+        torch.cuda.synchronize()
+        ops.check()
+        q.put((rank, r.keys[: r.n].cpu().numpy().view(np.uint32).copy(),
+               r.values[: r.n].cpu().numpy().view(np.uint32).copy() if kv else None,
+               r.send_sizes, r.recv_sizes))
+        ops.destroy()
+    except BaseException as e:       # report instead of leaving the parent waiting on the queue
+        q.put((rank, repr(e), None, None, None))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,world,chunks,kv,n", [
+    ("uniform", 2, 4, True, 16 << 20), ("few", 2, 2, True, 3_000_017),
+    ("skewed", 3, 4, True, 5_000_000), ("uniform", 3, 3, False, 6_000_011),
+    ("one_bucket", 2, 4, True, 4_000_000)])
+def test_hip_local_ops_multi_rank_on_one_gpu(kind, world, chunks, kv, n):
+    """The multi-GPU host (distributed_sort + HipLocalOps) with world > 1 on real kernels: 16-bit
+    tables gathered, top-byte partition into records, per-(source, byte) chunks, region sorts of
+    the received records; output = the global stable sort (oracle)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gpu_worker, args=(r, world, port, n, kind, q, chunks, kv))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        outs = sorted([q.get(timeout=180) for _ in range(world)], key=lambda x: x[0])
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.exitcode is None:
+                p.kill()
+    for o in outs:
+        assert not isinstance(o[1], str), f"rank {o[0]}: {o[1]}"
+    for p in procs:
+        assert p.exitcode == 0
+    keys = np.concatenate([o[1] for o in outs])
+    all_k = np.concatenate([_keys(kind, n, r * n) for r in range(world)])
+    ek, ev = O.stable_sort_masked(all_k, np.arange(world * n, dtype=np.uint32), 32)
+    assert (keys == ek).all()
+    if kv:
+        assert (np.concatenate([o[2] for o in outs]) == ev).all()
+    for r in range(world):
+        assert sum(outs[r][3]) == n
+        for s_ in range(world):
+            assert outs[r][4][s_] == outs[s_][3][r]
+
+
 @pytest.mark.gpu
 def test_rs_hist16_matches_bincount():
     """The sender's 16-bit table (rs_plan_hist16): the bucket counts and the top-byte totals, on

@@ -1,0 +1,60 @@
+"""rs_plan_sort_region (a multi-GPU receiver's local sort) at bucket populations that pick each
+large-bucket kernel: ~7K records per 16-bit bucket (256 x 34 tiles), ~12K (1024 x 17) and ~20K
+(the wide kernel over every bucket), with and without the persistent prefetching grids
+(RSORT_BUCKET_PF, read at plan creation).  Every region also holds an empty bucket, one-record and
+two-record buckets and one bucket near the largest tile, compared word for word with the oracle's
+stable sort."""
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+from radix_sort_amd.ops import SortPlan
+
+WIDE_CAP = 1024 * 34
+
+
+def _region(mean: int, top_lo: int, ntop: int, seed: int):
+    rng = np.random.default_rng(seed)
+    nb = ntop * 256
+    counts = rng.integers(int(mean * 0.9), int(mean * 1.1) + 1, size=nb)
+    counts[3], counts[4], counts[5] = 1, 0, 2
+    counts[7] = WIDE_CAP - 17            # one bucket over every population-sized tile
+    counts[nb - 1] = 1                   # the region's last bucket: one record
+    buckets = (top_lo << 8) + np.repeat(np.arange(nb, dtype=np.uint32), counts)
+    low = rng.integers(0, 1 << 16, size=buckets.size, dtype=np.uint32)
+    low[: buckets.size // 3] &= np.uint32(0x00FF)   # many duplicates: stability matters
+    keys = (buckets.astype(np.uint32) << np.uint32(16)) | low
+    # grouped by top byte (ascending), each top byte's records in arbitrary (input) order
+    order = np.lexsort((rng.random(keys.size), keys >> np.uint32(24)))
+    keys = keys[order]
+    vals = rng.permutation(keys.size).astype(np.uint32)
+    hist = np.zeros(65536, dtype=np.int32)
+    np.add.at(hist, keys >> np.uint32(16), 1)
+    return keys, vals, hist
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pf", ["1", "0"])
+@pytest.mark.parametrize("mean,top_lo,ntop", [(20000, 0x42, 1), (12000, 0x10, 1), (7000, 0xF0, 2)])
+def test_region_large_buckets_with_tiny_ones(pf, mean, top_lo, ntop, monkeypatch):
+    monkeypatch.setenv("RSORT_BUCKET_PF", pf)
+    keys, vals, hist = _region(mean, top_lo, ntop, seed=mean + ntop)
+    n = keys.size
+    rec = keys.astype(np.uint64) | (vals.astype(np.uint64) << np.uint64(32))
+    rt = torch.from_numpy(rec.view(np.int64)).cuda()
+    ht = torch.from_numpy(hist).cuda()
+    ok = torch.empty(n, dtype=torch.int32, device="cuda")
+    ov = torch.empty(n, dtype=torch.int32, device="cuda")
+    plan = SortPlan(0, max(n, 13 << 20), True)
+    try:
+        plan.set_profiling(True)
+        plan.sort_region(rt, ok, ov, n, ht, top_lo, top_lo + ntop)
+        plan.check()
+        times = plan.kernel_times()
+        assert times["bucket"]["launches"] > 0 and times["bucket"]["ms"] > times["fallback"]["ms"]
+    finally:
+        plan.destroy()
+    ek, ev = O.stable_sort_masked(keys, vals, 32)
+    assert (ok.cpu().numpy().view(np.uint32) == ek).all()
+    assert (ov.cpu().numpy().view(np.uint32) == ev).all()

@@ -1730,7 +1730,7 @@ __global__ __launch_bounds__(BLOCK, MW) void k_bucket_sort(const uint32_t* rec,
 // 1024 x 34 = one workgroup per CU, 512 x 34 two, 512 x 18 three).  VREG: the values ride in
 // registers through the sort (else the bucket's records are read again, from L2 / Infinity Cache,
 // for the value exchange).
-template <int BLOCK, int KPT, int RANK, int LO, int MW = 4, bool VREG = false>
+template <int BLOCK, int KPT, int RANK, int LO, int MW = 4, bool VREG = false, int PF = 0>
 __global__ __launch_bounds__(BLOCK, MW) void k_bucket_sort_wide(const uint32_t* rec,
                                                               const uint32_t* __restrict__ hist16,
                                                               const uint32_t* __restrict__ base16,
@@ -1743,11 +1743,16 @@ __global__ __launch_bounds__(BLOCK, MW) void k_bucket_sort_wide(const uint32_t* 
                                                               uint32_t rmask, uint32_t bshift,
                                                               uint32_t b_lo = 0, uint32_t b_cnt = 65536) {
     // unlisted (over == null): buckets [b_lo, b_lo + b_cnt), e.g. a multi-GPU region's top bytes
+    // PF = 1 (a persistent grid, one workgroup per CU): the next bucket's words are loaded before
+    // the current bucket is sorted, so the load of bucket i + 1 and the stores of bucket i overlap
+    // the LDS passes instead of alternating with them (one workgroup per CU has nothing else to
+    // hide them behind)
     constexpr int NW = BLOCK / 64, RADIX = 256;
     constexpr int TILE = BLOCK * KPT;
     constexpr int WAVE_KEYS = 64 * KPT;
     constexpr bool KV = LO != LAYOUT_KEYS;
     constexpr bool VR = KV && VREG;
+    static_assert(!(VR && PF), "values in registers leave no room for the prefetch");
     static_assert(TILE <= 65536, "16-bit record positions");
     static_assert(BLOCK >= RADIX, "one digit per thread in the scan");
     __shared__ uint32_t s_whist[NW][RADIX];
@@ -1757,34 +1762,55 @@ __global__ __launch_bounds__(BLOCK, MW) void k_bucket_sort_wide(const uint32_t* 
     const uint32_t tid = threadIdx.x, w = tid >> 6, lane = lane_id();
     const uint32_t wbase = w * WAVE_KEYS;
     const uint32_t nb = over ? over[0] : b_cnt;
-    for (uint32_t it = blockIdx.x; it < nb; it += gridDim.x) {
-        const uint32_t b = over ? over[1 + it] : b_lo + it;
-        const uint32_t cnt = hist16[b];
-        if (cnt <= min_cnt || cnt <= 1u) continue;   // the smaller tile's launch took it (or trivial)
-        if (cnt > (uint32_t)TILE) {                   // never: k_hist16_reduce gates the path off
-            if (tid == 0) atomicOr(err, 8u);
-            continue;
+    auto bucket_of = [&](uint32_t it) { return over ? over[1 + it] : b_lo + it; };
+    // the next bucket at or after `it` (stride gridDim.x) this launch sorts.  A one-record bucket
+    // is sorted too: the output is not R2 (with values), so every record must be written.
+    auto next_valid = [&](uint32_t it, uint32_t& cnt) {
+        for (; it < nb; it += gridDim.x) {
+            cnt = hist16[bucket_of(it)];
+            if (cnt == 0u || cnt <= min_cnt) continue;   // empty, or the smaller tile's launch took it
+            if (cnt > (uint32_t)TILE) {                   // never: k_hist16_reduce gates the path off
+                if (tid == 0) atomicOr(err, 8u);
+                continue;
+            }
+            break;
         }
+        return it;
+    };
+    auto src_of = [&](uint32_t b) { return rec + (KV ? 2ull : 1ull) * ((sstart[b >> 8] + base16[b]) & rmask); };
+    // w = (low 16 bits of the key) << 16 | position (KV), or the key (keys only); pads kPadKey
+    auto load_words = [&](const uint32_t* src, uint32_t cnt, uint32_t (&xx)[KPT], uint32_t (&vv)[VR ? KPT : 1]) {
+        const int lim = (int)cnt - (int)(wbase + lane);
+        const uint2* sr = reinterpret_cast<const uint2*>(src) + wbase + lane;
+        const uint32_t* sk = src + wbase + lane;
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) {
+            if (VR) {
+                const uint2 r = j * 64 < lim ? sr[j * 64] : make_uint2(0u, 0u);
+                xx[j] = j * 64 < lim ? ((r.x & 0xFFFFu) << 16) | (wbase + (uint32_t)j * 64u + lane) : kPadKey;
+                vv[VR ? j : 0] = r.y;
+            } else if (KV) {
+                xx[j] = j * 64 < lim ? ((sr[j * 64].x & 0xFFFFu) << 16) | (wbase + (uint32_t)j * 64u + lane) : kPadKey;
+            } else {
+                xx[j] = j * 64 < lim ? sk[j * 64] : kPadKey;
+            }
+        }
+    };
+    uint32_t cnt = 0;
+    uint32_t it = next_valid(blockIdx.x, cnt);
+    if (it >= nb) return;
+    uint32_t x[KPT];
+    uint32_t v[VR ? KPT : 1];
+    uint32_t x2[PF ? KPT : 1];
+    load_words(src_of(bucket_of(it)), cnt, x, v);
+    while (true) {
+        const uint32_t b = bucket_of(it);
         const uint32_t base = sstart[b >> 8] + base16[b];
         const uint32_t* src = rec + (KV ? 2ull : 1ull) * (base & rmask);
-        uint32_t x[KPT];
-        uint32_t v[VR ? KPT : 1];
-        {
-            const int lim = (int)cnt - (int)(wbase + lane);
-            const uint2* sr = reinterpret_cast<const uint2*>(src) + wbase + lane;
-            const uint32_t* sk = src + wbase + lane;
-#pragma unroll
-            for (int j = 0; j < KPT; ++j) {
-                if (VR) {
-                    const uint2 r = j * 64 < lim ? sr[j * 64] : make_uint2(0u, 0u);
-                    x[j] = j * 64 < lim ? ((r.x & 0xFFFFu) << 16) | (wbase + (uint32_t)j * 64u + lane) : kPadKey;
-                    v[VR ? j : 0] = r.y;
-                } else if (KV) {
-                    x[j] = j * 64 < lim ? ((sr[j * 64].x & 0xFFFFu) << 16) | (wbase + (uint32_t)j * 64u + lane) : kPadKey;
-                } else {
-                    x[j] = j * 64 < lim ? sk[j * 64] : kPadKey;
-                }
-            }
+        uint32_t ncnt = 0;
+        const uint32_t nit = PF ? next_valid(it + gridDim.x, ncnt) : it;
+        if constexpr (PF != 0) {
+            if (nit < nb) load_words(src_of(bucket_of(nit)), ncnt, x2, v);
         }
         // KV: the key's low 16 bits sit in w's high half; keys only: the key itself
         constexpr uint32_t S0 = KV ? 16u : 0u;
@@ -1819,25 +1845,38 @@ __global__ __launch_bounds__(BLOCK, MW) void k_bucket_sort_wide(const uint32_t* 
         const uint32_t hi = b << bshift;
         // one base address per output array, constant per-slot offsets (per-slot 64-bit addresses
         // spilled); slot j is real iff j * 64 < lim (pads sort last)
-        const size_t o0 = (size_t)base + wbase + lane;
-        const int lim = (int)cnt - (int)(wbase + lane);
-        uint2* oa = reinterpret_cast<uint2*>(out_k) + o0;
-        uint32_t* ok = out_k + o0;
-        uint32_t* ov = KV && LO != LAYOUT_AOS ? out_v + o0 : nullptr;
+        {
+            const size_t o0 = (size_t)base + wbase + lane;
+            const int lim = (int)cnt - (int)(wbase + lane);
+            uint2* oa = reinterpret_cast<uint2*>(out_k) + o0;
+            uint32_t* ok = out_k + o0;
+            uint32_t* ov = KV && LO != LAYOUT_AOS ? out_v + o0 : nullptr;
 #pragma unroll
-        for (int j = 0; j < KPT; ++j) {
-            if (j * 64 < lim) {
-                const uint32_t key = (KV ? (hi | (x[j] >> 16)) : x[j]) + kbase;
-                const uint32_t val = KV ? s_w[x[j] & 0xFFFFu] : 0u;
-                if constexpr (LO == LAYOUT_AOS) {
-                    oa[j * 64] = make_uint2(key, val);
-                } else {
-                    ok[j * 64] = key;
-                    if constexpr (KV) ov[j * 64] = val;
+            for (int j = 0; j < KPT; ++j) {
+                if (j * 64 < lim) {
+                    const uint32_t key = (KV ? (hi | (x[j] >> 16)) : x[j]) + kbase;
+                    const uint32_t val = KV ? s_w[x[j] & 0xFFFFu] : 0u;
+                    if constexpr (LO == LAYOUT_AOS) {
+                        oa[j * 64] = make_uint2(key, val);
+                    } else {
+                        ok[j * 64] = key;
+                        if constexpr (KV) ov[j * 64] = val;
+                    }
                 }
             }
         }
         __syncthreads();   // s_whist / s_w are reused by the next bucket
+        if constexpr (PF != 0) {
+            if (nit >= nb) break;
+            it = nit;
+            cnt = ncnt;
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) x[j] = x2[j];
+        } else {
+            it = next_valid(it + gridDim.x, cnt);
+            if (it >= nb) break;
+            load_words(src_of(bucket_of(it)), cnt, x, v);
+        }
     }
 }
 

@@ -205,12 +205,37 @@ def _side_stream(device):
     return _SIDE[device]
 
 
+def _host_staged(t, group) -> bool:
+    """gloo moves host memory only: device tensors on a gloo group travel through host copies
+    (the GPU tests run the product's HipLocalOps at world > 1 with every rank on one GPU this
+    way; RCCL sends device memory directly)."""
+    import torch.distributed as dist
+    return t.is_cuda and dist.get_backend(group) == "gloo"
+
+
+def all_gather_tables(h16, world: int, group=None):
+    """[world, HIST16_WORDS] = every rank's 16-bit table (all_gather; host-staged on gloo)."""
+    import torch
+    import torch.distributed as dist
+    if _host_staged(h16, group):
+        hc = h16.cpu()
+        out = [torch.empty_like(hc) for _ in range(world)]
+        dist.all_gather(out, hc, group=group)
+        return torch.stack(out).to(h16.device)
+    out = [torch.empty_like(h16) for _ in range(world)]
+    dist.all_gather(out, h16, group=group)
+    return torch.stack(out)
+
+
 def exchange_round(send, recv, plan: GroupPlan, g: int, rank: int, world: int, group=None):
     """Round g of the bucket exchange, the same code on every backend (gloo on CPU, RCCL on the
     GPUs): one point-to-point message per (peer, top byte) chunk, received into the byte's source
     slot of the round-g region; the rank's own chunks are local copies (RCCL moves a self message
     through a few channels at ~0.3 TB/s, measured).  A pair's messages are posted in the same
-    (byte) order on both sides, so they match.  Both sides skip empty chunks.  -> the round's works."""
+    (byte) order on both sides, so they match.  Both sides skip empty chunks.  -> the round's works.
+
+    Device tensors on a gloo group (tests: several ranks on one GPU) are staged through host
+    copies and the round completes before returning (no works)."""
     import torch.distributed as dist
     mine = [(o, m) for s, o, m in plan.recv[g] if s == rank]
     own = [(a, b) for q, a, b in plan.send[g] if q == rank]
@@ -218,6 +243,16 @@ def exchange_round(send, recv, plan: GroupPlan, g: int, rank: int, world: int, g
     if recv.data_ptr() != send.data_ptr():
         for (o, m), (a, b) in zip(mine, own):
             recv[o:o + m].copy_(send[a:b])
+    if _host_staged(send, group):
+        sends = [(q, send[a:b].cpu()) for q, a, b in plan.send[g] if q != rank]
+        recvs = [(s, o, m, recv.new_empty(m, device="cpu")) for s, o, m in plan.recv[g] if s != rank]
+        p2p = [dist.P2POp(dist.isend, t, q, group) for q, t in sends]
+        p2p += [dist.P2POp(dist.irecv, t, s, group) for s, _, _, t in recvs]
+        for w in (dist.batch_isend_irecv(p2p) if p2p else []):
+            w.wait()
+        for _, o, m, t in recvs:
+            recv[o:o + m].copy_(t)
+        return []
     p2p = [dist.P2POp(dist.isend, send[a:b], q, group) for q, a, b in plan.send[g] if q != rank]
     p2p += [dist.P2POp(dist.irecv, recv[o:o + m], s, group) for s, o, m in plan.recv[g] if s != rank]
     return dist.batch_isend_irecv(p2p) if p2p else []
@@ -242,9 +277,7 @@ def _distributed_sort(keys, values, ops, group, bits, chunks) -> ExchangeResult:
     G = max(1, int(chunks))
     shift = 32 - bits
     h16 = ops.hist16(keys)                                      # [HIST16_WORDS]
-    gathered = [torch.empty_like(h16) for _ in range(world)]
-    dist.all_gather(gathered, h16, group=group)
-    table = torch.stack(gathered)                               # [world, HIST16_WORDS]
+    table = all_gather_tables(h16, world, group)                # [world, HIST16_WORDS]
     tops = table[:, 65536:]
     totals = h16[65536:]
     if keys.is_cuda:

@@ -1,7 +1,6 @@
 """rs_plan_sort_region (a multi-GPU receiver's local sort) at bucket populations that pick each
 large-bucket kernel: ~7K records per 16-bit bucket (256 x 34 tiles), ~12K (1024 x 17) and ~20K
-(the wide kernel over every bucket), with and without the persistent prefetching grids
-(RSORT_BUCKET_PF, read at plan creation).  Every region also holds an empty bucket, one-record and
+(the wide kernel over every bucket).  Every region also holds an empty bucket, one-record and
 two-record buckets and one bucket near the largest tile, compared word for word with the oracle's
 stable sort."""
 import numpy as np
@@ -35,10 +34,8 @@ def _region(mean: int, top_lo: int, ntop: int, seed: int):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("pf", ["1", "0"])
 @pytest.mark.parametrize("mean,top_lo,ntop", [(20000, 0x42, 1), (12000, 0x10, 1), (7000, 0xF0, 2)])
-def test_region_large_buckets_with_tiny_ones(pf, mean, top_lo, ntop, monkeypatch):
-    monkeypatch.setenv("RSORT_BUCKET_PF", pf)
+def test_region_large_buckets_with_tiny_ones(mean, top_lo, ntop):
     keys, vals, hist = _region(mean, top_lo, ntop, seed=mean + ntop)
     n = keys.size
     rec = keys.astype(np.uint64) | (vals.astype(np.uint64) << np.uint64(32))

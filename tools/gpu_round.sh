@@ -20,4 +20,7 @@ step 7 && bench 7 config3_check_order --no-cpu-baseline
 step 8 && { timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_bench -o b --output-format csv -- python3 bench.py --no-cpu-baseline > gpurun_out/bench_prof.json 2> gpurun_out/bench_prof.err || exit 18; }
 step 9 && { for w in config3 config2 config4; do timeout -k 10 600 python3 tools/pmc_traffic.py $w gpurun_out/traffic_$w.json > gpurun_out/pmc_$w.log 2>&1 || exit 19; done; }
 step 10 && { timeout -k 10 600 python3 -u tools/rank_model.py > gpurun_out/rank_model.json 2> gpurun_out/rank_model.err || exit 20; }
+# the driver's N-GPU bench path (plain --gpus N -> torch.distributed.run -> N ranks) rehearsed with
+# 2 ranks sharing GPU 0 over gloo (host-staged exchange: not a measurement)
+step 11 && { timeout -k 10 400 python3 bench.py --gpus 2 --share-gpu --keys-per-gpu 67108864 --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/bench_rehearsal_2ranks.json 2> gpurun_out/bench_rehearsal_2ranks.err || exit 21; }
 exit 0

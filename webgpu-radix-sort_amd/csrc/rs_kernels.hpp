@@ -1730,7 +1730,7 @@ __global__ __launch_bounds__(BLOCK, MW) void k_bucket_sort(const uint32_t* rec,
 // 1024 x 34 = one workgroup per CU, 512 x 34 two, 512 x 18 three).  VREG: the values ride in
 // registers through the sort (else the bucket's records are read again, from L2 / Infinity Cache,
 // for the value exchange).
-template <int BLOCK, int KPT, int RANK, int LO, int MW = 4, bool VREG = false, int PF = 0>
+template <int BLOCK, int KPT, int RANK, int LO, int MW = 4, bool VREG = false>
 __global__ __launch_bounds__(BLOCK, MW) void k_bucket_sort_wide(const uint32_t* rec,
                                                               const uint32_t* __restrict__ hist16,
                                                               const uint32_t* __restrict__ base16,
@@ -1743,16 +1743,13 @@ __global__ __launch_bounds__(BLOCK, MW) void k_bucket_sort_wide(const uint32_t* 
                                                               uint32_t rmask, uint32_t bshift,
                                                               uint32_t b_lo = 0, uint32_t b_cnt = 65536) {
     // unlisted (over == null): buckets [b_lo, b_lo + b_cnt), e.g. a multi-GPU region's top bytes
-    // PF = 1 (a persistent grid, one workgroup per CU): the next bucket's words are loaded before
-    // the current bucket is sorted, so the load of bucket i + 1 and the stores of bucket i overlap
-    // the LDS passes instead of alternating with them (one workgroup per CU has nothing else to
-    // hide them behind)
+    // (a persistent grid loading the next bucket while sorting one was measured slower: the
+    // prefetch registers spill at one workgroup per CU, profiles/r03_bucket_prefetch_ab.json)
     constexpr int NW = BLOCK / 64, RADIX = 256;
     constexpr int TILE = BLOCK * KPT;
     constexpr int WAVE_KEYS = 64 * KPT;
     constexpr bool KV = LO != LAYOUT_KEYS;
     constexpr bool VR = KV && VREG;
-    static_assert(!(VR && PF), "values in registers leave no room for the prefetch");
     static_assert(TILE <= 65536, "16-bit record positions");
     static_assert(BLOCK >= RADIX, "one digit per thread in the scan");
     __shared__ uint32_t s_whist[NW][RADIX];
@@ -1801,17 +1798,11 @@ __global__ __launch_bounds__(BLOCK, MW) void k_bucket_sort_wide(const uint32_t* 
     if (it >= nb) return;
     uint32_t x[KPT];
     uint32_t v[VR ? KPT : 1];
-    uint32_t x2[PF ? KPT : 1];
     load_words(src_of(bucket_of(it)), cnt, x, v);
     while (true) {
         const uint32_t b = bucket_of(it);
         const uint32_t base = sstart[b >> 8] + base16[b];
         const uint32_t* src = rec + (KV ? 2ull : 1ull) * (base & rmask);
-        uint32_t ncnt = 0;
-        const uint32_t nit = PF ? next_valid(it + gridDim.x, ncnt) : it;
-        if constexpr (PF != 0) {
-            if (nit < nb) load_words(src_of(bucket_of(nit)), ncnt, x2, v);
-        }
         // KV: the key's low 16 bits sit in w's high half; keys only: the key itself
         constexpr uint32_t S0 = KV ? 16u : 0u;
 #pragma unroll 1
@@ -1866,17 +1857,9 @@ __global__ __launch_bounds__(BLOCK, MW) void k_bucket_sort_wide(const uint32_t* 
             }
         }
         __syncthreads();   // s_whist / s_w are reused by the next bucket
-        if constexpr (PF != 0) {
-            if (nit >= nb) break;
-            it = nit;
-            cnt = ncnt;
-#pragma unroll
-            for (int j = 0; j < KPT; ++j) x[j] = x2[j];
-        } else {
-            it = next_valid(it + gridDim.x, cnt);
-            if (it >= nb) break;
-            load_words(src_of(bucket_of(it)), cnt, x, v);
-        }
+        it = next_valid(it + gridDim.x, cnt);
+        if (it >= nb) break;
+        load_words(src_of(bucket_of(it)), cnt, x, v);
     }
 }
 

@@ -240,9 +240,6 @@ struct rs_plan {
     int msd_keys_cfg = 1;            // pass tiles (RSORT_MSD_KEYS_CFG): 0 1024x16, 1 512x32, 2 1024x32
     bool kbucket_wave = true;        // one wave per 16-bit bucket (RSORT_KBUCKET_WAVE=0: workgroups)
     bool kbucket_pf = false;         // workgroup kernel on a persistent prefetching grid (sweep: RSORT_KBUCKET_PF=1)
-    // buckets of >= 8K records (>= 2^29 keys, multi-GPU receivers): persistent grids whose
-    // workgroups load their next bucket while sorting one (RSORT_BUCKET_PF=0: a workgroup per bucket)
-    bool bucket_pf = true;
     uint32_t* msd = nullptr;         // its workspace: hist16 | base16 | segtab | gates | mtot
     int scatter_kind = RS_KERNEL_SCATTER;   // timer kind of the pass launches being enqueued
     uint32_t* host_err = nullptr;  // host-mapped error word: set by a timed-out look-back wait,
@@ -671,7 +668,6 @@ RS_EXPORT rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out) {
     if (const char* ms = getenv("RSORT_MSD")) p->msd_mode = strcmp(ms, "0") != 0 ? 1 : 0;
     if (const char* e = getenv("RSORT_MSD_KEYS_CFG")) p->msd_keys_cfg = atoi(e);
     if (const char* e = getenv("RSORT_KBUCKET_WAVE")) p->kbucket_wave = strcmp(e, "0") != 0;
-    if (const char* e = getenv("RSORT_BUCKET_PF")) p->bucket_pf = strcmp(e, "0") != 0;
     if (const char* sm = getenv("RSORT_SPIN_MAX")) p->spin_max = (uint32_t)strtoul(sm, nullptr, 10);
     bool recs2 = true;
 #if RS_SWEEP
@@ -1010,16 +1006,7 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
                                p->tickets + 16, 0u, (const uint32_t*)nullptr, kbase, (const uint32_t*)sstart, rmask,
                                b_lo, b_cnt);
         };
-        // bucket_pf: the same tiles on a persistent grid (as many workgroups as are resident), each
-        // loading its next bucket before sorting the current one
-        auto persistent = [&](auto kern, uint32_t block) {
-            static const uint32_t per_cu = resident_per_cu(kern, (int)block);
-            const uint32_t grid = std::min<uint32_t>(b_cnt, p->cus * per_cu);
-            hipLaunchKernelGGL(kern, dim3(grid), dim3(block), 0, s, ring ? ring : r2, hist16, base16, uk, uv, g_msd,
-                               p->tickets + 16, 0u, (const uint32_t*)nullptr, kbase, (const uint32_t*)sstart, rmask,
-                               b_lo, b_cnt);
-        };
-        const bool pf = p->bucket_pf;
+
 #if RS_SWEEP
         // sweep only, keys only: a persistent grid whose workgroups load their next bucket while
         // sorting one (measured slower, 0.265 vs 0.245 ms)
@@ -1036,12 +1023,7 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
         // tile on a small persistent grid (sweep: RSORT_OVER_GRID workgroups)
         const uint32_t over_grid = std::max(1u, (uint32_t)RS_KNOB("RSORT_OVER_GRID", 256));
         auto large = [&](auto kern, uint32_t block) {
-            uint32_t grid = wide_all ? b_cnt : over_grid;
-            if (pf && wide_all) {   // the prefetching instantiations: a persistent grid
-                static const uint32_t per_cu = resident_per_cu(kern, (int)block);
-                grid = std::min<uint32_t>(b_cnt, p->cus * per_cu);
-            }
-            hipLaunchKernelGGL(kern, dim3(grid), dim3(block), 0, s, ring ? ring : r2,
+            hipLaunchKernelGGL(kern, dim3(wide_all ? b_cnt : over_grid), dim3(block), 0, s, ring ? ring : r2,
                                hist16, base16, uk, uv, g_msd, p->tickets + 16, wide_all ? 0u : small_cap,
                                wide_all ? (const uint32_t*)nullptr : (const uint32_t*)over, kbase,
                                (const uint32_t*)sstart, rmask, vbits - 16, b_lo, b_cnt);
@@ -1097,11 +1079,6 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
                     default: break;
                 }
             } else {
-                if (pf && small_kpt == 34) {   // ~8K-record buckets (2^29 keys): two per CU, prefetching
-                    ballot ? persistent(rs::k_bucket_sort<bb, 34, B0, LO, 2, 1>, bb)
-                           : persistent(rs::k_bucket_sort<bb, 34, A0, LO, 2, 1>, bb);
-                    small_kpt = 0;
-                }
                 switch (small_kpt) {
                     RS_BK(4) RS_BK(8) RS_BK(12) RS_BK(17) RS_BK(18) RS_BK(24) RS_BK(34)
                     default: break;   // every bucket goes to the listed large-tile launch
@@ -1111,10 +1088,7 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
             // the listed buckets (none for uniform keys below ~2^29): the largest wide tile; every
             // bucket (wide_all): the smallest wide tile that holds the population's buckets (512 x 18:
             // three workgroups per CU, 512 x 34: two, 1024 x 34: one)
-            if (big_tile && pf)
-                ballot ? persistent(rs::k_bucket_sort<1024, 17, B0, LO, 4, 1>, 1024)
-                       : persistent(rs::k_bucket_sort<1024, 17, A0, LO, 4, 1>, 1024);
-            else if (big_tile)
+            if (big_tile)
                 ballot ? big(rs::k_bucket_sort<1024, 17, B0, LO, 4>) : big(rs::k_bucket_sort<1024, 17, A0, LO, 4>);
             // the listed buckets over the primary tile (none for uniform keys), or every bucket
             // (wide_all); keys only: the smallest wide tile that holds the population's buckets
@@ -1123,9 +1097,6 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
                 ballot ? large(rs::k_bucket_sort_wide<512, 18, B0, LO, 6>, 512) : large(rs::k_bucket_sort_wide<512, 18, A0, LO, 6>, 512);
             else if (wide_all && LO == K && want <= 512u * 34u)
                 ballot ? large(rs::k_bucket_sort_wide<512, 34, B0, LO, 4>, 512) : large(rs::k_bucket_sort_wide<512, 34, A0, LO, 4>, 512);
-            else if (wide_all && pf)
-                ballot ? large(rs::k_bucket_sort_wide<1024, kWideKpt, B0, LO, 4, false, 1>, 1024)
-                       : large(rs::k_bucket_sort_wide<1024, kWideKpt, A0, LO, 4, false, 1>, 1024);
             else
                 ballot ? large(rs::k_bucket_sort_wide<1024, kWideKpt, B0, LO>, 1024)
                        : large(rs::k_bucket_sort_wide<1024, kWideKpt, A0, LO>, 1024);

@@ -371,8 +371,11 @@ def main() -> None:
                 del wk2, wv2
             kern.dispatch()
         torch.cuda.synchronize()
+        # inside the timed region HIP events bracket only the pass launches (the roofline's kernel:
+        # the scatter passes, or the LSD passes of the device's fallback); every other launch group
+        # runs back to back, as it does unprofiled
         for k in kernels:
-            k.set_profiling(True)
+            k.set_profiling(True, kinds=("scatter", "fallback"))
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for i in range(K):
@@ -380,10 +383,30 @@ def main() -> None:
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
         for k in kernels:
-            for name, v in k.kernel_times().items():
+            for name, v in k.kernel_times(reset=True).items():
                 acc = kernel_ms.setdefault(name, {"ms": 0.0, "launches": 0})
                 acc["ms"] += v["ms"]
                 acc["launches"] += v["launches"]
+            k.set_profiling(False)
+        # the per-kind breakdown (and which path the device took): a few more sorts of fresh
+        # unsorted batches after the timed region, every launch group bracketed
+        nbd = 3
+        kern.set_profiling(True)
+        for j in range(nbd):
+            fk, fv = make_input(torch, ops, wl, n, wl["seed"] + 424242 + j, 0, dev)
+            wk.copy_(fk)
+            if wv is not None:
+                wv.copy_(fv)
+            del fk, fv
+            kern.dispatch()
+        torch.cuda.synchronize()
+        for name, v in kern.kernel_times(reset=True).items():
+            if name not in ("scatter", "fallback"):
+                # per-sort times of the untimed runs, scaled to K sorts (reported per step below)
+                kernel_ms[name] = {"ms": v["ms"] / nbd * K, "launches": round(v["launches"] / nbd * K)}
+        kern.set_profiling(False)
+        extra["breakdown_from"] = (f"{nbd} profiled sorts after the timed region (the timed region "
+                                   "brackets only the pass launches with HIP events)")
         # outside the timed region: no sort failed on the device (a timed-out look-back wait
         # would make its output invalid), and the last batch is a stable sorted permutation
         for k in kernels:
@@ -391,6 +414,7 @@ def main() -> None:
         last = (K - 1) % nb
         verify_batch(torch, ops, wl, n, wl["seed"] + 7919 * last, batches[last], dev)
         info = kernels[0].info
+        device_path = kernels[last].last_path()
         keys_per_step = n
         scatter_keys = n
         bucket_keys = n
@@ -417,6 +441,7 @@ def main() -> None:
         barrier()
         elapsed = time.perf_counter() - t0
         lo.check()      # no local sort or partition failed on the device
+        device_path = lo.plan.last_path()
         ms = (ctypes.c_double * _lib.RS_KERNEL_KINDS)()
         cnt = (ctypes.c_uint64 * _lib.RS_KERNEL_KINDS)()
         _lib.load().rs_plan_kernel_times(lo.plan._plan, ms, cnt)
@@ -461,8 +486,10 @@ def main() -> None:
     # the hybrid MSD path (separate arrays >= 12M keys): two one-sweep passes (top byte, next byte
     # within top-byte segments) and the in-LDS 16-bit bucket pass; its LSD fallbacks are enqueued
     # too and gated off on the device unless the keys are too skewed (then they carry the time)
-    msd = bk["launches"] > 0 and bk["ms"] > fb["ms"]
-    if bk["launches"] and not msd:
+    # the path the device chose (rs_plan_last_path: the hybrid path's gate words, read back)
+    msd = device_path == "hybrid"
+    extra["device_path"] = device_path
+    if device_path == "hybrid_fallback":
         sc = fb        # the device took the LSD fallback: its passes are the pass launches
     # one-sweep path: one digit-count launch per sort instead of one per pass
     onesweep = msd or 0 < hist_launches < sc["launches"]
@@ -520,7 +547,11 @@ def main() -> None:
                                                   + 4 * hist_reads)
     extra["digit_count_reads_per_sort"] = hist_reads
     extra["whole_sort_hbm_GBs_per_gpu"] = round(sort_bytes / (elapsed / K) / 1e9, 1)
-    extra["kernel_ms_per_step"] = {k: round(v["ms"] / max(K, 1), 4) for k, v in kernel_ms.items()}
+    extra["kernel_ms_per_step"] = {k: round(v["ms"] / max(K, 1), 4) for k, v in kernel_ms.items()
+                                   if not (msd and k == "fallback")}
+    if msd:
+        extra["fallback"] = ("LSD fallback launches gated off on the device; they run on a side stream "
+                             "beside the MSD passes (their event spans there are not kernel time)")
     extra["passes"] = passes
 
     cpu = None

@@ -177,9 +177,23 @@ rs_status rs_plan_sort_region(rs_plan* plan, const void* records, void* keys_out
                               uint64_t n, const void* d_hist16, uint32_t top_lo, uint32_t top_hi,
                               void* stream);
 rs_status rs_plan_info_get(const rs_plan* plan, rs_plan_info* info);
+/* Which path the plan's last sort took (waits for it): the hybrid MSD path's choice is made on
+ * the device (k_msd_plan's gate words), so this reads it back.  Diagnostics and tests; the result
+ * never depends on it. */
+enum {
+    RS_PATH_NONE = 0,             /* no sort yet */
+    RS_PATH_LSD = 1,              /* the LSD passes directly (small n, keys-only < 16M, radix_bits != 8 ...) */
+    RS_PATH_HYBRID = 2,           /* hybrid MSD: top-byte pass, next-byte pass, in-LDS bucket sort */
+    RS_PATH_HYBRID_FALLBACK = 3,  /* the hybrid path's LSD fallback (a bucket too large, skewed keys) */
+    RS_PATH_IN_ORDER = 4          /* check_order found the input sorted: nothing moved */
+};
+rs_status rs_plan_last_path(rs_plan* plan, uint32_t* path);
 /* Kernel timing: when enabled, every launch of the plan is bracketed by HIP events on the
  * launch stream and per-kind durations are accumulated (read after synchronising). */
 rs_status rs_plan_set_profiling(rs_plan* plan, int enable);
+/* Events around the launches of the kinds in kind_mask only (bit k = RS_KERNEL_k; 0 disables):
+ * a timed run brackets just the kernel it reports, the other launch groups run back to back. */
+rs_status rs_plan_set_profiling_kinds(rs_plan* plan, uint32_t kind_mask);
 rs_status rs_plan_kernel_times(rs_plan* plan, double ms[RS_KERNEL_KINDS],
                                uint64_t launches[RS_KERNEL_KINDS]);
 rs_status rs_plan_reset_kernel_times(rs_plan* plan);

@@ -48,8 +48,8 @@ def test_region_large_buckets_with_tiny_ones(mean, top_lo, ntop):
         plan.set_profiling(True)
         plan.sort_region(rt, ok, ov, n, ht, top_lo, top_lo + ntop)
         plan.check()
-        times = plan.kernel_times()
-        assert times["bucket"]["launches"] > 0 and times["bucket"]["ms"] > times["fallback"]["ms"]
+        assert plan.kernel_times()["bucket"]["launches"] > 0
+        assert plan.last_path() == "hybrid"
     finally:
         plan.destroy()
     ek, ev = O.stable_sort_masked(keys, vals, 32)

@@ -154,6 +154,7 @@ struct RoctxRange {
 
 struct KernelTimer {
     bool enabled = false;
+    uint32_t mask = ~0u;     // kinds bracketed by events (rs_plan_set_profiling_kinds)
     struct Rec { int kind; hipEvent_t a, b; };
     std::vector<Rec> pending;
     std::vector<hipEvent_t> pool;
@@ -172,7 +173,7 @@ struct KernelTimer {
         static const char* const names[RS_KERNEL_KINDS] = {"rsort.histogram", "rsort.scan", "rsort.scatter",
                                                            "rsort.check", "rsort.bucket", "rsort.fallback"};
         RoctxRange range(label ? label : names[kind]);
-        if (!enabled) { launch(); return; }
+        if (!enabled || !((mask >> kind) & 1u)) { launch(); return; }
         Rec r{kind, get(), get()};
         (void)hipEventRecord(r.a, s);
         launch();
@@ -241,6 +242,13 @@ struct rs_plan {
     bool kbucket_wave = true;        // one wave per 16-bit bucket (RSORT_KBUCKET_WAVE=0: workgroups)
     bool kbucket_pf = false;         // workgroup kernel on a persistent prefetching grid (sweep: RSORT_KBUCKET_PF=1)
     uint32_t* msd = nullptr;         // its workspace: hist16 | base16 | segtab | gates | mtot
+    // the hybrid path's LSD fallback runs on a low-priority side stream forked after the plan
+    // kernel: its launches (gated off unless the device chose them) overlap the MSD passes instead
+    // of trailing the bucket pass (RSORT_FALLBACK_SIDE=0: on the sort's own stream)
+    bool fallback_side = true;
+    bool last_hybrid = false;        // the last sort enqueued the hybrid path (rs_plan_last_path)
+    hipStream_t side = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     int scatter_kind = RS_KERNEL_SCATTER;   // timer kind of the pass launches being enqueued
     uint32_t* host_err = nullptr;  // host-mapped error word: set by a timed-out look-back wait,
     uint32_t* host_err_dev = nullptr;   // read + cleared by rs_plan_check / the next rs_plan_sort
@@ -668,6 +676,7 @@ RS_EXPORT rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out) {
     if (const char* ms = getenv("RSORT_MSD")) p->msd_mode = strcmp(ms, "0") != 0 ? 1 : 0;
     if (const char* e = getenv("RSORT_MSD_KEYS_CFG")) p->msd_keys_cfg = atoi(e);
     if (const char* e = getenv("RSORT_KBUCKET_WAVE")) p->kbucket_wave = strcmp(e, "0") != 0;
+    if (const char* e = getenv("RSORT_FALLBACK_SIDE")) p->fallback_side = strcmp(e, "0") != 0;
     if (const char* sm = getenv("RSORT_SPIN_MAX")) p->spin_max = (uint32_t)strtoul(sm, nullptr, 10);
     bool recs2 = true;
 #if RS_SWEEP
@@ -747,6 +756,14 @@ RS_EXPORT rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out) {
         return cleanup(fail(e == hipErrorOutOfMemory ? RS_ERR_OUT_OF_MEMORY : RS_ERR_HIP,
                             "rs_plan_create: hipMalloc failed: %s", hipGetErrorString(e)));
     p->tickets = p->ptot + rs::kTotalsMax;   // [16] tickets, [16] error word
+    if (p->msd && p->fallback_side) {
+        int least = 0, greatest = 0;
+        (void)hipDeviceGetStreamPriorityRange(&least, &greatest);
+        if ((e = hipStreamCreateWithPriority(&p->side, hipStreamNonBlocking, least)) != hipSuccess ||
+            (e = hipEventCreateWithFlags(&p->ev_fork, hipEventDisableTiming)) != hipSuccess ||
+            (e = hipEventCreateWithFlags(&p->ev_join, hipEventDisableTiming)) != hipSuccess)
+            return cleanup(fail(RS_ERR_HIP, "rs_plan_create: side stream: %s", hipGetErrorString(e)));
+    }
     if ((e = hipHostMalloc((void**)&p->host_err, 4, hipHostMallocMapped)) != hipSuccess ||
         (e = hipHostGetDevicePointer((void**)&p->host_err_dev, p->host_err, 0)) != hipSuccess ||
         (e = hipEventCreateWithFlags(&p->done, hipEventDisableTiming)) != hipSuccess)
@@ -774,6 +791,12 @@ RS_EXPORT void rs_plan_destroy(rs_plan* p) {
     (void)hipFree(p->msd);
     if (p->host_err) (void)hipHostFree(p->host_err);
     if (p->done) (void)hipEventDestroy(p->done);
+    if (p->side) {
+        (void)hipStreamSynchronize(p->side);
+        (void)hipStreamDestroy(p->side);
+    }
+    if (p->ev_fork) (void)hipEventDestroy(p->ev_fork);
+    if (p->ev_join) (void)hipEventDestroy(p->ev_join);
     delete p;
 }
 
@@ -847,6 +870,13 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
     if ((uint64_t)(ntiles + 257) * 256u > p->status_words)
         return fail(RS_ERR_INVALID_ARG, "internal: %u segmented tiles exceed the plan's %llu status words",
                     ntiles + 257, (unsigned long long)p->status_words);
+    p->last_hybrid = true;
+    // every pass of this sort (MSD passes on s, fallback passes on the side stream) takes its epoch
+    // without a wrap: a wrap's clearing memset must not run beside a pass using the words
+    if (p->epoch + 16u >= (1u << 30)) {
+        HIP_TRY(hipMemsetAsync(p->status, 0, 8ull * p->status_words, s));
+        p->epoch = 1;
+    }
     // the pass totals, tickets and error word are zeroed by k_hist16_reduce (nothing reads them before)
     // 16-bit buckets: a tile sized to the mean bucket + 4 sigma of a uniform population takes
     // every bucket that fits it (at 2^28 keys: 4352 records, ~2 buckets over it), the large tile
@@ -934,6 +964,13 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
         else plan(rs::k_msd_plan<kLarge.tile>);
     }, "rsort.msd.plan");
     HIP_TRY(hipGetLastError());
+    // fork: the fallback's launches wait for the plan kernel's gates only
+    hipStream_t fs = s;
+    if (p->side) {
+        HIP_TRY(hipEventRecord(p->ev_fork, s));
+        HIP_TRY(hipStreamWaitEvent(p->side, p->ev_fork, 0));
+        fs = p->side;
+    }
     const uint32_t* g_msd = gates + rs::kGateMsd;
     // R2 replaced by a power-of-two ring (sweep experiment RSORT_EXP_RING = log2 records; the
     // results are then invalid: timing of an Infinity-Cache-resident R2 only)
@@ -1116,34 +1153,40 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
     const uint32_t tgrid = (uint32_t)std::min<uint64_t>((uint64_t)RS_TOT_PER_CU * p->cus,
                                                         (n + 4ull * RS_TOT_BLOCK - 1) / (4ull * RS_TOT_BLOCK));
     // (check_order: the totals came with the histogram read, see chk above)
-    if (!chk) p->timer.run(RS_KERNEL_FALLBACK, s, [&] {
+    if (!chk) p->timer.run(RS_KERNEL_FALLBACK, fs, [&] {
         if (in_aos)
-            hipLaunchKernelGGL(rs::k_pass_totals<2>, dim3(tgrid), dim3(RS_TOT_BLOCK), 0, s, sk, n32, pl, 0u, t0,
+            hipLaunchKernelGGL(rs::k_pass_totals<2>, dim3(tgrid), dim3(RS_TOT_BLOCK), 0, fs, sk, n32, pl, 0u, t0,
                                (uint32_t*)nullptr, 0xFFFFFFFFu, 0x1u, g_lsd);
         else
-            hipLaunchKernelGGL(rs::k_pass_totals<1>, dim3(tgrid), dim3(RS_TOT_BLOCK), 0, s, sk, n32, pl, 0u, t0,
+            hipLaunchKernelGGL(rs::k_pass_totals<1>, dim3(tgrid), dim3(RS_TOT_BLOCK), 0, fs, sk, n32, pl, 0u, t0,
                                (uint32_t*)nullptr, 0xFFFFFFFFu, 0x1u, g_lsd);
     }, "rsort.msd.fallback_totals");
     HIP_TRY(hipGetLastError());
+    rs_status st = RS_OK;
     if (keys) {
         // keys only: four one-sweep passes input -> tmp_k -> uk -> tmp_k -> uk (5 gated launches;
         // the keys-only LSD sort's histogram path would be 12)
         p->scatter_kind = RS_KERNEL_FALLBACK;
-        rs_status st = RS_OK;
         for (uint32_t i = 0; i < 4 && st == RS_OK; ++i)
             st = run_pass(p, i == 0 ? sk : ((i & 1) ? p->tmp_k : uk), nullptr, (i & 1) ? uk : p->tmp_k, nullptr,
-                          n32, 8 * i, 8, layout_pair(K, K), g_lsd, (int)i, s, /*onesweep=*/true);
+                          n32, 8 * i, 8, layout_pair(K, K), g_lsd, (int)i, fs, /*onesweep=*/true);
         p->scatter_kind = RS_KERNEL_SCATTER;
-        return st;
+    } else if (!out_aos) {
+        st = enqueue_lsd_gated(p, sk, sv, in_aos, uk, uv, n32, g_lsd, fs);
+    } else {
+        // records in place: uk -> tmp_k -> uk -> tmp_k -> uk
+        p->scatter_kind = RS_KERNEL_FALLBACK;
+        for (uint32_t i = 0; i < 4 && st == RS_OK; ++i)
+            st = run_pass(p, (i & 1) ? p->tmp_k : uk, nullptr, (i & 1) ? uk : p->tmp_k, nullptr, n32, 8 * i, 8,
+                          layout_pair(A, A), g_lsd, (int)i, fs, /*onesweep=*/true);
+        p->scatter_kind = RS_KERNEL_SCATTER;
     }
-    if (!out_aos) return enqueue_lsd_gated(p, sk, sv, in_aos, uk, uv, n32, g_lsd, s);
-    // records in place: uk -> tmp_k -> uk -> tmp_k -> uk
-    p->scatter_kind = RS_KERNEL_FALLBACK;
-    rs_status st = RS_OK;
-    for (uint32_t i = 0; i < 4 && st == RS_OK; ++i)
-        st = run_pass(p, (i & 1) ? p->tmp_k : uk, nullptr, (i & 1) ? uk : p->tmp_k, nullptr, n32, 8 * i, 8,
-                      layout_pair(A, A), g_lsd, (int)i, s, /*onesweep=*/true);
-    p->scatter_kind = RS_KERNEL_SCATTER;
+    // join: the sort is done on s once the side stream's launches are (also on an error, so the
+    // side stream never runs ahead of a later sort on this plan)
+    if (p->side) {
+        HIP_TRY(hipEventRecord(p->ev_join, p->side));
+        HIP_TRY(hipStreamWaitEvent(s, p->ev_join, 0));
+    }
     return st;
 }
 
@@ -1267,6 +1310,7 @@ RS_EXPORT rs_status rs_plan_sort_n(rs_plan* p, void* keys, void* values, uint64_
     uint32_t* uk = (uint32_t*)keys;
     uint32_t* uv = L == rs::LAYOUT_SOA ? (uint32_t*)values : nullptr;
     if (rs_status st = take_device_error(p, "rs_plan_sort")) return st;
+    p->last_hybrid = false;
     const rs_status st = n <= kTinyMax ? run_tiny(p, uk, uv, n32, s)   // one launch; check_order moot
                                        : enqueue_sort(p, uk, uv, n, s);
     if (st != RS_OK) return st;
@@ -1293,6 +1337,7 @@ RS_EXPORT rs_status rs_plan_sort_copy(rs_plan* p, const void* in_k, const void* 
     if (((uintptr_t)in_k | (uintptr_t)out_k | (kv ? ((uintptr_t)in_v | (uintptr_t)out_v) : 0)) & 3)
         return fail(RS_ERR_INVALID_ARG, "keys/values must be 4-byte aligned");
     if (rs_status st = take_device_error(p, "rs_plan_sort_copy")) return st;
+    p->last_hybrid = false;
     DeviceGuard guard(p->desc.device);
     hipStream_t s = (hipStream_t)stream;
     uint32_t* uk = (uint32_t*)out_k;
@@ -1308,6 +1353,25 @@ RS_EXPORT rs_status rs_plan_sort_copy(rs_plan* p, const void* in_k, const void* 
     if (st != RS_OK) return st;
     HIP_TRY(hipEventRecord(p->done, s));
     p->done_recorded = true;
+    return RS_OK;
+}
+
+RS_EXPORT rs_status rs_plan_last_path(rs_plan* p, uint32_t* path) {
+    if (!p || !path) return fail(RS_ERR_INVALID_ARG, "rs_plan_last_path: null argument");
+    DeviceGuard guard(p->desc.device);
+    *path = RS_PATH_NONE;
+    if (!p->done_recorded) return RS_OK;
+    HIP_TRY(hipEventSynchronize(p->done));
+    if (!p->last_hybrid) {
+        *path = RS_PATH_LSD;
+        return RS_OK;
+    }
+    // the plan kernel's gate words (first word of each gate block)
+    const uint32_t* gates = p->msd + 65536 * 2 + 1024;
+    uint32_t g[2] = {0u, 0u};
+    HIP_TRY(hipMemcpy(&g[0], gates + rs::kGateMsd, 4, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(&g[1], gates + rs::kGateLsd, 4, hipMemcpyDeviceToHost));
+    *path = g[0] ? RS_PATH_HYBRID : g[1] ? RS_PATH_HYBRID_FALLBACK : RS_PATH_IN_ORDER;
     return RS_OK;
 }
 
@@ -1487,6 +1551,7 @@ static rs_status sort_records_impl(rs_plan* p, const void* records, void* keys_o
     if (((uintptr_t)records & 7) || ((uintptr_t)keys_out & 3) || ((uintptr_t)values_out & 3))
         return fail(RS_ERR_INVALID_ARG, "records must be 8-byte and arrays 4-byte aligned");
     if (rs_status st = take_device_error(p, "rs_plan_sort_records")) return st;
+    p->last_hybrid = false;
     DeviceGuard guard(p->desc.device);
     hipStream_t s = (hipStream_t)stream;
     uint32_t* uk = (uint32_t*)keys_out;
@@ -1574,6 +1639,7 @@ RS_EXPORT rs_status rs_plan_sort_region(rs_plan* p, const void* records, void* k
     if (((uintptr_t)records & 7) || ((uintptr_t)keys_out & 3) || ((uintptr_t)values_out & 3) || ((uintptr_t)d_hist16 & 3))
         return fail(RS_ERR_INVALID_ARG, "records must be 8-byte and arrays 4-byte aligned");
     if (rs_status st = take_device_error(p, "rs_plan_sort_region")) return st;
+    p->last_hybrid = false;
     DeviceGuard guard(p->desc.device);
     hipStream_t s = (hipStream_t)stream;
     uint32_t* uk = (uint32_t*)keys_out;
@@ -1639,6 +1705,17 @@ RS_EXPORT rs_status rs_plan_set_wait_limit(rs_plan* p, uint32_t sleeps) {
 RS_EXPORT rs_status rs_plan_set_profiling(rs_plan* p, int enable) {
     if (!p) return fail(RS_ERR_INVALID_ARG, "null plan");
     p->timer.enabled = enable != 0;
+    p->timer.mask = ~0u;
+    return RS_OK;
+}
+
+RS_EXPORT rs_status rs_plan_set_profiling_kinds(rs_plan* p, uint32_t kind_mask) {
+    if (!p) return fail(RS_ERR_INVALID_ARG, "null plan");
+    if (kind_mask >> RS_KERNEL_KINDS)
+        return fail(RS_ERR_INVALID_ARG, "rs_plan_set_profiling_kinds: mask 0x%x has bits beyond the %d kinds",
+                    kind_mask, RS_KERNEL_KINDS);
+    p->timer.enabled = kind_mask != 0;
+    p->timer.mask = kind_mask;
     return RS_OK;
 }
 

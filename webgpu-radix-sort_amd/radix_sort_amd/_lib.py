@@ -33,6 +33,8 @@ RS_FLAG_INTERLEAVED = 0x10
  RS_KERNEL_FALLBACK) = range(6)
 RS_KERNEL_KINDS = 6
 KERNEL_NAMES = ("histogram", "scan", "scatter", "check", "bucket", "fallback")
+# rs_plan_last_path
+PATH_NAMES = ("none", "lsd", "hybrid", "hybrid_fallback", "in_order")
 
 
 class RadixSortError(RuntimeError):
@@ -96,6 +98,8 @@ _SIGS = {
                                            ctypes.c_uint32, _VP]),
     "rs_plan_info_get": (ctypes.c_int, [_VP, ctypes.POINTER(PlanInfo)]),
     "rs_plan_set_profiling": (ctypes.c_int, [_VP, ctypes.c_int]),
+    "rs_plan_set_profiling_kinds": (ctypes.c_int, [_VP, ctypes.c_uint32]),
+    "rs_plan_last_path": (ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_uint32)]),
     "rs_plan_kernel_times": (ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_double),
                                             ctypes.POINTER(ctypes.c_uint64)]),
     "rs_plan_reset_kernel_times": (ctypes.c_int, [_VP]),

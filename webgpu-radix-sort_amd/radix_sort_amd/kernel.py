@@ -245,8 +245,25 @@ class RadixSortKernel:
         look-back wait: that sort's output is invalid).  Reported once."""
         check(_lib.load().rs_plan_check(self._plan), "check")
 
-    def set_profiling(self, enable: bool) -> None:
-        check(_lib.load().rs_plan_set_profiling(self._plan, 1 if enable else 0), "profiling")
+    def set_profiling(self, enable: bool, kinds=None) -> None:
+        """HIP events around every launch group (kinds=None) or only around the launches of the
+        named kinds (e.g. ("scatter", "fallback"): the others run back to back)."""
+        L = _lib.load()
+        if kinds is None or not enable:
+            check(L.rs_plan_set_profiling(self._plan, 1 if enable else 0), "profiling")
+        else:
+            mask = 0
+            for k in kinds:
+                mask |= 1 << _lib.KERNEL_NAMES.index(k)
+            check(L.rs_plan_set_profiling_kinds(self._plan, mask), "profiling")
+
+    def last_path(self) -> str:
+        """Which path the last dispatch took (waits for it): "lsd", "hybrid", "hybrid_fallback"
+        (the device chose the LSD passes: skewed keys), "in_order" (check_order: nothing moved) or
+        "none" (rs_plan_last_path)."""
+        v = ctypes.c_uint32()
+        check(_lib.load().rs_plan_last_path(self._plan, ctypes.byref(v)), "last_path")
+        return _lib.PATH_NAMES[v.value]
 
     def kernel_times(self, reset: bool = False) -> dict:
         ms = (ctypes.c_double * _lib.RS_KERNEL_KINDS)()

@@ -82,6 +82,12 @@ class SortPlan:
     def set_profiling(self, enable: bool) -> None:
         check(_lib.load().rs_plan_set_profiling(self._plan, 1 if enable else 0), "profiling")
 
+    def last_path(self) -> str:
+        """Which path the plan's last sort took (rs_plan_last_path; waits for it)."""
+        v = ctypes.c_uint32()
+        check(_lib.load().rs_plan_last_path(self._plan, ctypes.byref(v)), "last_path")
+        return _lib.PATH_NAMES[v.value]
+
     def kernel_times(self) -> dict:
         """Accumulated per-kind kernel times of the plan's launches (after set_profiling)."""
         ms = (ctypes.c_double * _lib.RS_KERNEL_KINDS)()

@@ -550,8 +550,8 @@ def main() -> None:
     extra["kernel_ms_per_step"] = {k: round(v["ms"] / max(K, 1), 4) for k, v in kernel_ms.items()
                                    if not (msd and k == "fallback")}
     if msd:
-        extra["fallback"] = ("LSD fallback launches gated off on the device; they run on a side stream "
-                             "beside the MSD passes (their event spans there are not kernel time)")
+        extra["fallback_ms_per_step"] = round(fb["ms"] / max(K, 1), 4)
+        extra["fallback"] = "LSD fallback launches enqueued behind the MSD passes, gated off on the device"
     extra["passes"] = passes
 
     cpu = None

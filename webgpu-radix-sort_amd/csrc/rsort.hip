@@ -242,13 +242,7 @@ struct rs_plan {
     bool kbucket_wave = true;        // one wave per 16-bit bucket (RSORT_KBUCKET_WAVE=0: workgroups)
     bool kbucket_pf = false;         // workgroup kernel on a persistent prefetching grid (sweep: RSORT_KBUCKET_PF=1)
     uint32_t* msd = nullptr;         // its workspace: hist16 | base16 | segtab | gates | mtot
-    // the hybrid path's LSD fallback runs on a low-priority side stream forked after the plan
-    // kernel: its launches (gated off unless the device chose them) overlap the MSD passes instead
-    // of trailing the bucket pass (RSORT_FALLBACK_SIDE=0: on the sort's own stream)
-    bool fallback_side = true;
     bool last_hybrid = false;        // the last sort enqueued the hybrid path (rs_plan_last_path)
-    hipStream_t side = nullptr;
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     int scatter_kind = RS_KERNEL_SCATTER;   // timer kind of the pass launches being enqueued
     uint32_t* host_err = nullptr;  // host-mapped error word: set by a timed-out look-back wait,
     uint32_t* host_err_dev = nullptr;   // read + cleared by rs_plan_check / the next rs_plan_sort
@@ -676,7 +670,6 @@ RS_EXPORT rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out) {
     if (const char* ms = getenv("RSORT_MSD")) p->msd_mode = strcmp(ms, "0") != 0 ? 1 : 0;
     if (const char* e = getenv("RSORT_MSD_KEYS_CFG")) p->msd_keys_cfg = atoi(e);
     if (const char* e = getenv("RSORT_KBUCKET_WAVE")) p->kbucket_wave = strcmp(e, "0") != 0;
-    if (const char* e = getenv("RSORT_FALLBACK_SIDE")) p->fallback_side = strcmp(e, "0") != 0;
     if (const char* sm = getenv("RSORT_SPIN_MAX")) p->spin_max = (uint32_t)strtoul(sm, nullptr, 10);
     bool recs2 = true;
 #if RS_SWEEP
@@ -756,14 +749,7 @@ RS_EXPORT rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out) {
         return cleanup(fail(e == hipErrorOutOfMemory ? RS_ERR_OUT_OF_MEMORY : RS_ERR_HIP,
                             "rs_plan_create: hipMalloc failed: %s", hipGetErrorString(e)));
     p->tickets = p->ptot + rs::kTotalsMax;   // [16] tickets, [16] error word
-    if (p->msd && p->fallback_side) {
-        int least = 0, greatest = 0;
-        (void)hipDeviceGetStreamPriorityRange(&least, &greatest);
-        if ((e = hipStreamCreateWithPriority(&p->side, hipStreamNonBlocking, least)) != hipSuccess ||
-            (e = hipEventCreateWithFlags(&p->ev_fork, hipEventDisableTiming)) != hipSuccess ||
-            (e = hipEventCreateWithFlags(&p->ev_join, hipEventDisableTiming)) != hipSuccess)
-            return cleanup(fail(RS_ERR_HIP, "rs_plan_create: side stream: %s", hipGetErrorString(e)));
-    }
+
     if ((e = hipHostMalloc((void**)&p->host_err, 4, hipHostMallocMapped)) != hipSuccess ||
         (e = hipHostGetDevicePointer((void**)&p->host_err_dev, p->host_err, 0)) != hipSuccess ||
         (e = hipEventCreateWithFlags(&p->done, hipEventDisableTiming)) != hipSuccess)
@@ -791,12 +777,6 @@ RS_EXPORT void rs_plan_destroy(rs_plan* p) {
     (void)hipFree(p->msd);
     if (p->host_err) (void)hipHostFree(p->host_err);
     if (p->done) (void)hipEventDestroy(p->done);
-    if (p->side) {
-        (void)hipStreamSynchronize(p->side);
-        (void)hipStreamDestroy(p->side);
-    }
-    if (p->ev_fork) (void)hipEventDestroy(p->ev_fork);
-    if (p->ev_join) (void)hipEventDestroy(p->ev_join);
     delete p;
 }
 
@@ -871,12 +851,6 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
         return fail(RS_ERR_INVALID_ARG, "internal: %u segmented tiles exceed the plan's %llu status words",
                     ntiles + 257, (unsigned long long)p->status_words);
     p->last_hybrid = true;
-    // every pass of this sort (MSD passes on s, fallback passes on the side stream) takes its epoch
-    // without a wrap: a wrap's clearing memset must not run beside a pass using the words
-    if (p->epoch + 16u >= (1u << 30)) {
-        HIP_TRY(hipMemsetAsync(p->status, 0, 8ull * p->status_words, s));
-        p->epoch = 1;
-    }
     // the pass totals, tickets and error word are zeroed by k_hist16_reduce (nothing reads them before)
     // 16-bit buckets: a tile sized to the mean bucket + 4 sigma of a uniform population takes
     // every bucket that fits it (at 2^28 keys: 4352 records, ~2 buckets over it), the large tile
@@ -964,13 +938,10 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
         else plan(rs::k_msd_plan<kLarge.tile>);
     }, "rsort.msd.plan");
     HIP_TRY(hipGetLastError());
-    // fork: the fallback's launches wait for the plan kernel's gates only
+    // (the fallback's launches on a low-priority side stream forked here, so that their gated-off
+    // launches overlap the MSD passes, measured slower: the scatter passes lost 5-25 % beside
+    // them, profiles/r03_side_stream_nogo/)
     hipStream_t fs = s;
-    if (p->side) {
-        HIP_TRY(hipEventRecord(p->ev_fork, s));
-        HIP_TRY(hipStreamWaitEvent(p->side, p->ev_fork, 0));
-        fs = p->side;
-    }
     const uint32_t* g_msd = gates + rs::kGateMsd;
     // R2 replaced by a power-of-two ring (sweep experiment RSORT_EXP_RING = log2 records; the
     // results are then invalid: timing of an Infinity-Cache-resident R2 only)
@@ -1180,12 +1151,6 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
             st = run_pass(p, (i & 1) ? p->tmp_k : uk, nullptr, (i & 1) ? uk : p->tmp_k, nullptr, n32, 8 * i, 8,
                           layout_pair(A, A), g_lsd, (int)i, fs, /*onesweep=*/true);
         p->scatter_kind = RS_KERNEL_SCATTER;
-    }
-    // join: the sort is done on s once the side stream's launches are (also on an error, so the
-    // side stream never runs ahead of a later sort on this plan)
-    if (p->side) {
-        HIP_TRY(hipEventRecord(p->ev_join, p->side));
-        HIP_TRY(hipStreamWaitEvent(s, p->ev_join, 0));
     }
     return st;
 }

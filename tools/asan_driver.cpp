@@ -60,8 +60,22 @@ static void sort_case(size_t n, bool kv, uint32_t flags_extra, uint32_t key_mask
     rs_plan* p = nullptr;
     OK(rs_plan_create(&d, &p));
     if (p) {
+        uint32_t path = 99;
+        OK(rs_plan_last_path(p, &path));
+        CHECK(path == RS_PATH_NONE, "last_path before any sort: %u", path);
+        // events around the pass launches only (the bench's timed region)
+        OK(rs_plan_set_profiling_kinds(p, (1u << RS_KERNEL_SCATTER) | (1u << RS_KERNEL_FALLBACK)));
+        CHECK(rs_plan_set_profiling_kinds(p, 1u << RS_KERNEL_KINDS) == RS_ERR_INVALID_ARG, "bad kind mask accepted");
         OK(rs_plan_sort(p, dk, kv ? dv : nullptr, nullptr));
         OK(rs_plan_check(p));
+        OK(rs_plan_last_path(p, &path));
+        CHECK(path >= RS_PATH_LSD && path <= RS_PATH_IN_ORDER, "last_path after a sort: %u", path);
+        double ms[RS_KERNEL_KINDS];
+        uint64_t launches[RS_KERNEL_KINDS];
+        OK(rs_plan_kernel_times(p, ms, launches));
+        CHECK(launches[RS_KERNEL_HISTOGRAM] == 0 && launches[RS_KERNEL_BUCKET] == 0,
+              "only the pass kinds are bracketed");
+        OK(rs_plan_set_profiling(p, 0));
         std::vector<uint32_t> ok(n), ov(n);
         OK(rs_memcpy_d2h(ok.data(), dk, 4 * n, nullptr));
         OK(rs_memcpy_d2h(ov.data(), dv, 4 * n, nullptr));

@@ -23,4 +23,8 @@ step 10 && { timeout -k 10 600 python3 -u tools/rank_model.py > gpurun_out/rank_
 # the driver's N-GPU bench path (plain --gpus N -> torch.distributed.run -> N ranks) rehearsed with
 # 2 ranks sharing GPU 0 over gloo (host-staged exchange: not a measurement)
 step 11 && { timeout -k 10 400 python3 bench.py --gpus 2 --share-gpu --keys-per-gpu 67108864 --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/bench_rehearsal_2ranks.json 2> gpurun_out/bench_rehearsal_2ranks.err || exit 21; }
+# host ASan/UBSan/LSan driver over every C-ABI entry point (built here: make -C
+# webgpu-radix-sort_amd/csrc asan; the binary and the asan library must not be gpurun-ignored
+# for this step)
+step 12 && { ASAN_OPTIONS=halt_on_error=1 LSAN_OPTIONS=suppressions=tools/lsan.supp:print_suppressions=1 UBSAN_OPTIONS=halt_on_error=1:print_stacktrace=1 timeout -k 10 400 ./tools/asan_driver > gpurun_out/asan_driver.log 2>&1 || exit 22; }
 exit 0

@@ -238,8 +238,8 @@ struct rs_plan {
     uint32_t spin_max = 1u << 20;  // look-back wait bound in sleeps (RSORT_SPIN_MAX; tests force 0)
     int msd_mode = RS_MSD_DEFAULT;   // hybrid MSD path for values (RSORT_MSD=0/1)
     // keys-only form of the hybrid MSD path, read per plan (tests switch them):
-    int msd_keys_cfg = 1;            // pass tiles (RSORT_MSD_KEYS_CFG): 0 1024x16, 1 512x32, 2 1024x32,
-                                     // 3 pass 0 1024x32 (512-B digit runs), pass 1 512x32
+    int msd_keys_cfg = 1;            // pass tiles (RSORT_MSD_KEYS_CFG): 0 1024x16, 1 512x32, 2 1024x32
+                                     // (32K-key tiles for pass 0 only: no faster, r03_keys_pass0_tiles_ab)
     bool kbucket_wave = true;        // one wave per 16-bit bucket (RSORT_KBUCKET_WAVE=0: workgroups)
     bool kbucket_pf = false;         // workgroup kernel on a persistent prefetching grid (sweep: RSORT_KBUCKET_PF=1)
     uint32_t* msd = nullptr;         // its workspace: hist16 | base16 | segtab | gates | mtot
@@ -966,10 +966,6 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
         else if (keys && keys_cfg == 2)
             launch_msd_pass<K, K, 0, false, 1024, 32>(p, sk, nullptr, r1, nullptr, n32, vbits - 8, ntiles, top_tot,
                                                       p->tickets + 4, g_msd, nullptr, nullptr, s);
-        else if (keys && keys_cfg == 3)   // 32K-key tiles for pass 0 only (pass 1 keeps the plan's 16K)
-            launch_msd_pass<K, K, 0, false, 1024, 32>(p, sk, nullptr, r1, nullptr, n32, vbits - 8,
-                                                      (uint32_t)((n + 2u * kLarge.tile - 1) / (2u * kLarge.tile)),
-                                                      top_tot, p->tickets + 4, g_msd, nullptr, nullptr, s);
         else if (keys)
             launch_msd_pass<K, K, 0, false, kLargeKeys.block, kLargeKeys.kpt>(
                 p, sk, nullptr, r1, nullptr, n32, vbits - 8, ntiles, top_tot, p->tickets + 4, g_msd, nullptr,

@@ -1296,7 +1296,10 @@ __global__ __launch_bounds__(1024) void k_hist16_in(const uint32_t* __restrict__
     constexpr uint32_t KPL = NARROW ? 1u : (L == LAYOUT_AOS ? 2u : 4u);   // keys per load
     constexpr uint32_t STEPS = 61440u / (B * KPL);                // loads per thread per round
     // loads in flight (CHECK: 3, the order check's registers spilled at 5)
-    constexpr uint32_t FLY = CHECK ? 3 : 5;
+#ifndef RS_H16_FLY
+#define RS_H16_FLY 5
+#endif
+    constexpr uint32_t FLY = CHECK ? 3 : RS_H16_FLY;
     static_assert(STEPS % FLY == 0, "whole load groups per round");
     using Vec = typename std::conditional<NARROW, uint2, uint4>::type;
     __shared__ uint32_t h[W];

@@ -311,7 +311,8 @@ def main() -> None:
     import torch
     import torch.distributed as dist
     from radix_sort_amd import RadixSortKernel, RadixSortTextureKernel, ops
-    from radix_sort_amd.distributed import HipLocalOps, distributed_sort
+    from radix_sort_amd.distributed import (HipLocalOps, StepTimeline, distributed_sort,
+                                            summarize_timelines, timeline_record)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -457,6 +458,42 @@ def main() -> None:
         elapsed = float(t.item())
         if not ops.is_sorted(r.keys, r.n):
             raise SystemExit(f"bench: rank {rank} output not sorted")
+        if world > 1:
+            # after the timed region: where a step's time goes on every rank (one step with GPU
+            # event marks, one with the exchange rounds alone), gathered to rank 0 as the line's
+            # multi_gpu breakdown (E, xGMI GB/s, the slowest rank's local terms, rank edges)
+            my_kernel_ms = [kernel_ms[nm]["ms"] / max(K, 1) for nm in _lib.KERNEL_NAMES]
+            if lo.part_plan is not None:
+                my_kernel_ms += [ms[_lib.RS_KERNEL_HISTOGRAM] / max(K, 1), ms[_lib.RS_KERNEL_SCATTER] / max(K, 1)]
+            else:
+                my_kernel_ms += [0.0, 0.0]
+            _lib.load().rs_plan_set_profiling(lo.plan._plan, 0)
+            if lo.part_plan is not None:
+                _lib.load().rs_plan_set_profiling(lo.part_plan._plan, 0)
+            barrier()
+            tl = StepTimeline()
+            r = distributed_sort(keys, vals, lo, chunks=EXCHANGE_ROUNDS, timeline=tl)
+            torch.cuda.synchronize()
+            barrier()
+            tle = StepTimeline(exchange_only=True)
+            distributed_sort(keys, vals, lo, chunks=EXCHANGE_ROUNDS, timeline=tle)
+            torch.cuda.synchronize()
+            me = tle.ms()
+            eo_ms = me.get(f"landed{EXCHANGE_ROUNDS - 1}", 0.0) - me.get("partition", 0.0)
+            lo.check()
+            if not ops.is_sorted(r.keys, r.n):
+                raise SystemExit(f"bench: rank {rank} output not sorted (timeline step)")
+            fk = int(r.keys[0].item()) & 0xFFFFFFFF if r.n else -1
+            lk = int(r.keys[r.n - 1].item()) & 0xFFFFFFFF if r.n else -1
+            row = timeline_record(tl, EXCHANGE_ROUNDS, fk, lk, r.n, my_kernel_ms, eo_ms)
+            mine = torch.tensor(row, dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+            rows = [torch.empty_like(mine) for _ in range(world)]
+            dist.all_gather(rows, mine)
+            names = list(_lib.KERNEL_NAMES) + ["sender_hist16", "sender_partition"]
+            extra["multi_gpu"] = summarize_timelines([x.cpu().tolist() for x in rows], EXCHANGE_ROUNDS, names)
+            extra["multi_gpu"]["from"] = ("one step with GPU event marks after the timed region (every rank), "
+                                          "one step with the exchange rounds alone; kernel_ms = the timed "
+                                          "steps' per-kind launch times")
         info = {"passes": 4}
         keys_per_step = n * world
         bucket_keys = r.n

@@ -205,9 +205,26 @@ rs_status rs_plan_device_errors(rs_plan* plan, uint32_t* errors);
  * synchronising points (mapAsync / Python check()). */
 rs_status rs_plan_check(rs_plan* plan);
 /* Bound of every inter-workgroup wait of the one-sweep pass, in s_sleep(1) periods (default
- * 2^20, ~ms; env RSORT_SPIN_MAX at plan creation).  0 makes any wait on a not-yet-published
- * predecessor time out at once: the failure path's test (rs_plan_check must then report it). */
+ * 2^20, ~ms).  0 makes any wait on a not-yet-published predecessor time out at once: the
+ * failure path's test (rs_plan_check must then report it). */
 rs_status rs_plan_set_wait_limit(rs_plan* plan, uint32_t sleeps);
+/* Test / diagnostics only: force the plan onto one of the paths it would otherwise pick by size
+ * (so parity tests can cover every kernel).  Never changes a result, only which kernels run.  The
+ * library reads no environment variables: a caller's environment cannot change the path.  Each
+ * field: -1 = keep the plan's own choice.  Call before the plan's first sort (it only selects
+ * among the resources rs_plan_create allocated; a path whose workspace is absent stays off). */
+typedef struct rs_plan_debug {
+    int32_t rank;           /* 0 lane-ordered LDS-atomic ranking, 1 ballot-match ranking */
+    int32_t tile;           /* 0 large tiles (16K keys), 1 small tiles (4K keys) at every size */
+    int32_t onesweep;       /* 0 histogram / scan / scatter passes, 1 one-sweep passes */
+    int32_t msd;            /* 0 the hybrid MSD path off (LSD passes only), 1 on where it applies */
+    int32_t keys_cfg;       /* keys-only LSD tiles: 0 1024 x 16, 1 512 x 32 */
+    int32_t msd_keys_cfg;   /* keys-only hybrid pass tiles: 0 1024 x 16, 1 512 x 32, 2 1024 x 32 */
+    int32_t kbucket_wave;   /* keys-only bucket pass: 0 a workgroup per bucket, 1 a wave per bucket */
+    int32_t selftest_fail;  /* 1: treat the lane-order self-test as failed (ballot ranking,
+                               rs_plan_info.lane_order_selftest = 0) */
+} rs_plan_debug;
+rs_status rs_plan_set_debug(rs_plan* plan, const rs_plan_debug* debug);
 void      rs_plan_destroy(rs_plan* plan);     /* frees the workspace (reference quirk Q9) */
 
 /* ---- prefix sum (PrefixSumKernel) ------------------------------------------------------- */
@@ -279,6 +296,25 @@ rs_status rs_group_result(const rs_group* g, int32_t rank, void** keys, void** v
 /* Wait for the last sort on every rank; RS_ERR_DEVICE if any of its kernels failed on the
  * device (rs_plan_check of every rank's plans). */
 rs_status rs_group_synchronize(rs_group* g);
+/* Per-rank timing of the group sorts (diagnostics; what an N-GPU run needs to explain itself:
+ * where the step's time goes, the exchange time and its xGMI rate).  rs_group_set_profiling(g, 1)
+ * records timing events on every rank's streams from the next rs_group_sort on (a few per round);
+ * rs_group_times_get waits for the last sort and reads rank r's: ms since the sort's start on the
+ * rank's sort stream.  round_done_ms[j]: the rank's comm stream finished round j (RCCL: its sends
+ * and receives of round j; peer copies: the copies it sent).  bytes_*: the rank's off-rank
+ * exchange bytes (its own chunks are device copies). */
+typedef struct rs_group_times {
+    uint32_t rounds;              /* rounds of the last sort (0: world size 1, nothing exchanged) */
+    float    hist16_ms;           /* the 16-bit table read */
+    float    partition_ms;        /* the top-byte partition (the sort's first MSD pass) */
+    float    round_done_ms[16];
+    float    region_sorted_ms[16];/* region j's local sort done */
+    float    done_ms;             /* the rank's whole sort */
+    uint64_t bytes_sent;
+    uint64_t bytes_recv;
+} rs_group_times;
+rs_status rs_group_set_profiling(rs_group* g, int enable);
+rs_status rs_group_times_get(rs_group* g, int32_t rank, rs_group_times* out);
 void      rs_group_destroy(rs_group* g);
 /* The host-side bucket plan, a pure function (identical on every rank; no device needed):
  * hist_all[r * buckets + b] = rank r's count of bucket b.  Writes bounds[0..world] (rank q owns

@@ -28,6 +28,22 @@ def golden():
     return manifest, arrays
 
 
+@pytest.fixture
+def plan_debug():
+    """Path overrides (rs_plan_set_debug) for every plan the test creates through the Python
+    wrappers: plan_debug(rank="ballot", tile="small", onesweep=0, ...); reset after the test."""
+    from radix_sort_amd import _lib
+    saved = dict(_lib._DEBUG)
+
+    def set_(**fields):
+        _lib.plan_debug(**fields)          # validates the field names
+        _lib._DEBUG.update(fields)
+
+    yield set_
+    _lib._DEBUG.clear()
+    _lib._DEBUG.update(saved)
+
+
 def case_arrays(arrays, case):
     keys = arrays[case["name"] + "_keys"]
     exp_k = arrays[case["name"] + "_exp_keys"]

@@ -315,3 +315,36 @@ def test_rs_histogram_matches_bincount():
         ops.histogram(kt[1:], n - 1, shift, bits, h)
         exp = np.bincount((k[1:] >> np.uint32(shift)) & np.uint32((1 << bits) - 1), minlength=1 << bits)
         assert (h.cpu().numpy() == exp).all(), (shift, bits)
+
+
+def test_multi_gpu_breakdown_fields():
+    """The N-rank bench line's multi_gpu breakdown (bench.py, distributed.summarize_timelines):
+    the layout every rank gathers (timeline_record) and the fields rank 0 derives from it - the
+    exchange time E and xGMI GB/s per rank, the slowest rank's local terms, rank edges."""
+    from radix_sort_amd.distributed import StepTimeline, summarize_timelines, timeline_record
+    G = 4
+    names = ["histogram", "scan", "scatter", "check", "bucket", "fallback", "sender_hist16", "sender_partition"]
+    tl = StepTimeline()
+    tl.bytes_sent, tl.bytes_recv = 7 * 10**8, 7 * 10**8
+    empty = timeline_record(tl, G, 10, 20, 1000, [0.0] * len(names), 1.5)   # no GPU marks: zeros
+    assert len(empty) == 3 + 2 * G + 6 + len(names)
+
+    def row(t_off, k0, k1, n):
+        return ([0.3, 0.35, 1.4] + [1.4 + 0.6 * (g + 1) + t_off for g in range(G)]
+                + [2.5 + 0.6 * (g + 1) + t_off for g in range(G)]
+                + [7e8, 7e8, k0, k1, n, 2.2] + [0.3, 0.0, 2.0, 0.0, 2.06, 0.0, 0.3, 1.05])
+
+    s = summarize_timelines([row(0.0, 5, 100, 10), row(0.5, 100, 300, 12), row(0.0, 0, 0, 0)], G, names)
+    assert s["ranks"] == 3
+    assert s["exchange"]["rounds"] == G
+    assert abs(s["exchange"]["E_ms_max"] - 2.9) < 1e-9             # last round landed - partition
+    assert len(s["exchange"]["landed_ms_after_partition_max"]) == G
+    assert s["exchange"]["xgmi_GBs_per_rank_min"] > 0 and s["exchange"]["exchange_only_ms_max"] == 2.2
+    assert s["exchange"]["bytes_off_gpu_per_rank_max"] == 14 * 10**8
+    assert set(s["local_ms_max_over_ranks"]) == {"hist16", "table_all_gather", "partition",
+                                                 "after_last_round_landed"}
+    assert s["kernel_ms_max_over_ranks"]["bucket"] == 2.06
+    assert s["recv_keys_min_max"] == [0, 12]
+    assert s["rank_edges_sorted"] is True                           # the empty rank is skipped
+    s2 = summarize_timelines([row(0.0, 5, 150, 10), row(0.0, 100, 300, 12)], G, names)
+    assert s2["rank_edges_sorted"] is False

@@ -170,3 +170,46 @@ def test_config5_shape_eight_virtual_ranks():
         assert bool((vi[1:][eq] > vi[:-1][eq]).all())
         del vi
     assert bool(seen.all())
+
+
+def test_group_times_explain_the_step():
+    """rs_group_set_profiling / rs_group_times_get: every rank's step breakdown (16-bit table,
+    partition, each round's comm-stream completion, each region's sort, done) is ordered in time,
+    and the off-rank bytes match what the ranks actually exchanged (virtual ranks over copies)."""
+    from radix_sort_amd import ops
+    W, n, G = 3, 3 << 20, 4
+    dev = torch.device("cuda", 0)
+    kt, vt = [], []
+    for r in range(W):
+        k = torch.empty(n, dtype=torch.int32, device=dev)
+        ops.fill_random_u32(k, 21, r * n)
+        v = torch.empty(n, dtype=torch.int32, device=dev)
+        ops.fill_iota_u32(v, r * n)
+        kt.append(k)
+        vt.append(v)
+    g = RadixSortGroup([0] * W, capacity=n, has_values=True, transport="copy", rounds=G)
+    try:
+        with pytest.raises(RadixSortError):
+            g.times(0)                       # no profiled sort yet
+        g.set_profiling(True)
+        out = g.sort(kt, vt)
+        total_sent = total_recv = 0
+        for r in range(W):
+            t = g.times(r)
+            assert t["rounds"] == G
+            assert 0 < t["hist16_ms"] <= t["partition_ms"] <= t["region_sorted_ms"][0]
+            assert all(a <= b for a, b in zip(t["region_sorted_ms"], t["region_sorted_ms"][1:]))
+            assert t["region_sorted_ms"][-1] <= t["done_ms"]
+            assert all(x >= t["partition_ms"] for x in t["round_done_ms"])
+            total_sent += t["bytes_sent"]
+            total_recv += t["bytes_recv"]
+            # what rank r received from the others: its records minus its own keys in its top bytes
+            lo_top = (int(out[r][0][0]) & 0xFFFFFFFF) >> 24
+            hi_top = (int(out[r][0][-1]) & 0xFFFFFFFF) >> 24
+            top = (kt[r].long() & 0xFFFFFFFF) >> 24
+            own = int(((top >= lo_top) & (top <= hi_top)).sum())
+            assert t["bytes_recv"] == 8 * (out[r][0].numel() - own)
+        assert total_sent == total_recv > 0
+        assert sum(o[0].numel() for o in out) == W * n
+    finally:
+        g.destroy()

@@ -37,9 +37,9 @@ def _keys(n, kind, seed):
     return k
 
 
-def _sort_and_check(n, kind, seed=5, copy=False, rank=None, monkeypatch=None):
-    if rank and monkeypatch is not None:
-        monkeypatch.setenv("RSORT_RANK", rank)
+def _sort_and_check(n, kind, seed=5, copy=False, rank=None, plan_debug=None):
+    if rank and plan_debug is not None:
+        plan_debug(rank=rank)
     k = _keys(n, kind, seed)
     v = torch.arange(n, dtype=torch.int32, device=DEV)
     kin = k.clone()
@@ -89,7 +89,7 @@ def test_msd_duplicates_and_overflow_buckets(kind):
 
 
 @pytest.mark.parametrize("n", [(1 << 25) + 3, (1 << 26) - 5])
-def test_msd_wide_buckets_match_oracle(n, monkeypatch):
+def test_msd_wide_buckets_match_oracle(n, plan_debug):
     """16-bit buckets of 13K-26K records (over every population-sized tile, under the wide kernel's
     34816): every populated bucket is listed and sorted by k_bucket_sort_wide (1024 threads, the
     positions through LDS, the values gathered after), bit-exact against the oracle; separate arrays,
@@ -97,7 +97,7 @@ def test_msd_wide_buckets_match_oracle(n, monkeypatch):
     t = _sort_and_check(n, "wide")
     assert t["path"] == "hybrid"      # the hybrid path ran, not the LSD fallback
     _sort_and_check(n, "wide", copy=True)
-    _sort_and_check(n, "wide", rank="ballot", monkeypatch=monkeypatch)
+    _sort_and_check(n, "wide", rank="ballot", plan_debug=plan_debug)
 
 
 def test_msd_records_wide_buckets():
@@ -105,13 +105,13 @@ def test_msd_records_wide_buckets():
     assert t["path"] == "hybrid"
 
 
-def test_msd_out_of_place_and_ballot_ranking(monkeypatch):
+def test_msd_out_of_place_and_ballot_ranking(plan_debug):
     _sort_and_check((1 << 24) + 3, "uniform", copy=True)
-    _sort_and_check(1 << 24, "dups", rank="ballot", monkeypatch=monkeypatch)
+    _sort_and_check(1 << 24, "dups", rank="ballot", plan_debug=plan_debug)
 
 
-def test_msd_path_off_by_env(monkeypatch):
-    monkeypatch.setenv("RSORT_MSD", "0")
+def test_msd_path_off_by_debug(plan_debug):
+    plan_debug(msd=0)
     t = _sort_and_check(1 << 24, "uniform")
     assert t["bucket"]["launches"] == 0 and t["fallback"]["launches"] == 0
 
@@ -299,10 +299,10 @@ def test_msd_keys_duplicates_and_overflow_buckets(kind):
     _sort_keys_and_check((1 << 24) + 4096, kind)
 
 
-def test_msd_keys_out_of_place_partial_count_and_ballot(monkeypatch):
+def test_msd_keys_out_of_place_partial_count_and_ballot(plan_debug):
     _sort_keys_and_check((1 << 24) + 4099, "uniform", copy=True)
     _sort_keys_and_check((1 << 25) + 3, "uniform", count=(1 << 24) + 5000)
-    monkeypatch.setenv("RSORT_RANK", "ballot")
+    plan_debug(rank="ballot")
     _sort_keys_and_check((1 << 24) + 4096, "dups")
 
 
@@ -315,21 +315,20 @@ def test_msd_keys_below_row_capacity_keeps_lsd(n):
 
 
 @pytest.mark.parametrize("cfg", ["0", "2"])
-def test_msd_keys_pass_tile_configs(monkeypatch, cfg):
+def test_msd_keys_pass_tile_configs(plan_debug, cfg):
     # the other pass tiles: 1024 x 16 (16K keys) and 1024 x 32 (32K keys), instead of 512 x 32
-    monkeypatch.setenv("RSORT_MSD_KEYS_CFG", cfg)
+    plan_debug(msd_keys_cfg=int(cfg))
     t = _sort_keys_and_check((1 << 25) + 77, "uniform")
     assert t["scatter"]["launches"] == 2
     _sort_keys_and_check((1 << 24) + 4096, "few_big")
 
 
-@pytest.mark.parametrize("n,env", [((1 << 27) + 5, {}),                                  # 2K-key buckets
-                                   ((1 << 25) + 77, {"RSORT_KBUCKET_WAVE": "0"})])
-def test_msd_keys_workgroup_bucket_kernel(monkeypatch, n, env):
+@pytest.mark.parametrize("n,dbg", [((1 << 27) + 5, {}),                                  # 2K-key buckets
+                                   ((1 << 25) + 77, {"kbucket_wave": 0})])
+def test_msd_keys_workgroup_bucket_kernel(plan_debug, n, dbg):
     # buckets over the wave kernel's 64 x 18 keys (or the wave kernel off): one workgroup per
     # bucket, in place
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
+    plan_debug(**dbg)
     t = _sort_keys_and_check(n, "uniform")
     assert t["bucket"]["launches"] == 1 and t["scatter"]["launches"] == 2
 

@@ -64,3 +64,24 @@ def test_partition_records_matches_oracle(n, given_totals):
     assert ((r & np.uint64(0xFFFFFFFF)).astype(np.uint32) == keys[perm]).all()
     assert ((r >> np.uint64(32)).astype(np.uint32) == vals[perm]).all()
     plan.destroy()
+
+
+@pytest.mark.parametrize("n", [1_000_003, 13_000_001])
+def test_sorted_records_to_arrays_with_check_order(n):
+    """A check_order plan sorting records that are ALREADY in order into separate arrays: the
+    order check must not skip the passes (the output arrays are not the input) -
+    the arrays get the records' keys and values, path "hybrid" at >= 12M keys."""
+    from radix_sort_amd.ops import SortPlan
+    keys = np.sort(O.gen_u32(n + 5, n))
+    vals = np.arange(n, dtype=np.uint32)
+    rec = torch.from_numpy((keys.astype(np.uint64) | (vals.astype(np.uint64) << np.uint64(32)))
+                           .view(np.int64)).to(DEV)
+    ko = torch.zeros(n, dtype=torch.int32, device=DEV)
+    vo = torch.zeros(n, dtype=torch.int32, device=DEV)
+    plan = SortPlan(0, n, True, check_order=True)
+    plan.sort_records(rec, ko, vo, n)
+    plan.check()
+    assert (_np(ko) == keys).all() and (_np(vo) == vals).all()
+    if n >= 12 << 20:
+        assert plan.last_path() == "hybrid"
+    plan.destroy()

@@ -94,9 +94,9 @@ def test_lane_order_selftest_passes_and_default_ranking():
     assert info["rank_mode"] == "lds_atomic"
 
 
-def test_selftest_failure_falls_back_to_ballot_ranking(monkeypatch):
+def test_selftest_failure_falls_back_to_ballot_ranking(plan_debug):
     from radix_sort_amd import RadixSortKernel
-    monkeypatch.setenv("RSORT_SELFTEST", "fail")
+    plan_debug(selftest_fail=1)
     for n in (5_000, 1_000_003, 13_000_001):
         keys = O.gen_u32(n, n) % np.uint32(1000)          # duplicates: stability is visible
         vals = np.arange(n, dtype=np.uint32)

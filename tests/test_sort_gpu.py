@@ -277,13 +277,11 @@ def test_config4_256M_nearly_sorted_f32_check_order():
 
 @pytest.mark.parametrize("rank", ["atomic", "ballot"])
 @pytest.mark.parametrize("tile", ["small", "large", "large_keys1024"])
-def test_rank_modes_and_tile_configs(monkeypatch, golden, rank, tile):
+def test_rank_modes_and_tile_configs(plan_debug, golden, rank, tile):
     """Both in-wave ranking implementations and both tile configurations give the oracle's
-    result (RSORT_RANK / RSORT_TILE are read at plan creation)."""
-    monkeypatch.setenv("RSORT_RANK", rank)
-    monkeypatch.setenv("RSORT_TILE", tile.split("_")[0])
-    # keys-only large tiles: 512 x 32 by default, 1024 x 16 with RSORT_KEYS_CFG=0
-    monkeypatch.setenv("RSORT_KEYS_CFG", "0" if tile.endswith("1024") else "1")
+    result (selected per plan with rs_plan_set_debug)."""
+    # keys-only large tiles: 512 x 32 by default, 1024 x 16 with keys_cfg=0
+    plan_debug(rank=rank, tile=tile.split("_")[0], keys_cfg=0 if tile.endswith("1024") else 1)
     for n, bits, kind in ((20_000, 32, "u32"), (300_001, 32, "few"), (1_000_003, 24, "u32"),
                           (70_001, 12, "u32")):
         keys = O.gen_u32(n + bits, n)
@@ -307,12 +305,11 @@ def test_rank_modes_and_tile_configs(monkeypatch, golden, rank, tile):
 
 @pytest.mark.parametrize("onesweep", ["1", "0"])
 @pytest.mark.parametrize("tile", ["small", "large"])
-def test_onesweep_and_three_kernel_paths(monkeypatch, onesweep, tile):
+def test_onesweep_and_three_kernel_paths(plan_debug, onesweep, tile):
     """The one-sweep pass (whole-array totals + decoupled look-back) and the histogram / scan /
     scatter pass give the oracle's result for every layout; no bounded wait times out."""
     from radix_sort_amd import RadixSortKernel, RadixSortTextureKernel
-    monkeypatch.setenv("RSORT_ONESWEEP", onesweep)
-    monkeypatch.setenv("RSORT_TILE", tile)
+    plan_debug(onesweep=int(onesweep), tile=tile)
     for n, bits, kind in ((16_385, 32, "u32"), (100_003, 32, "few"), (2_500_000, 32, "u32"),
                           (5_000_001, 20, "u32"), (40_000, 8, "sorted"), (300_000, 12, "u32")):
         keys = O.gen_u32(n * 3 + bits, n)
@@ -344,14 +341,13 @@ def test_onesweep_and_three_kernel_paths(monkeypatch, onesweep, tile):
 
 
 @pytest.mark.parametrize("tile", ["small", "large"])
-def test_onesweep_check_order_exits_and_narrow_digits(monkeypatch, tile):
+def test_onesweep_check_order_exits_and_narrow_digits(plan_debug, tile):
     """One-sweep path: check_order early exits (an exit after pass 0 or 1 leaves the data as
     (key, value) records in one of the two records buffers: k_finalize<SOA, AOS>), and 2-/4-bit
     digits.  The order checks are fused into k_pass_totals / k_onesweep here, on all three
     layouts."""
     from radix_sort_amd import RadixSortKernel, RadixSortTextureKernel
-    monkeypatch.setenv("RSORT_ONESWEEP", "1")
-    monkeypatch.setenv("RSORT_TILE", tile)
+    plan_debug(onesweep=1, tile=tile)
     n = 1_500_001
     u = O.gen_u32(77, n)
     vals = O.gen_u32(78, n)

@@ -93,9 +93,8 @@ def test_texture_check_order(kind):
 
 @pytest.mark.parametrize("rank", ["atomic", "ballot"])
 @pytest.mark.parametrize("tile", ["small", "large"])
-def test_texture_rank_modes_and_tiles(monkeypatch, rank, tile):
-    monkeypatch.setenv("RSORT_RANK", rank)
-    monkeypatch.setenv("RSORT_TILE", tile)
+def test_texture_rank_modes_and_tiles(plan_debug, rank, tile):
+    plan_debug(rank=rank, tile=tile)
     for n, bits in ((40_000, 32), (1_000_003, 24), (5_000, 8)):
         keys = O.gen_u32(n + bits, n)
         vals = np.arange(n, dtype=np.uint32)

@@ -9,6 +9,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <vector>
+#include <algorithm>
 
 #include "../include/rsort.h"
 
@@ -84,6 +85,29 @@ static void sort_case(size_t n, bool kv, uint32_t flags_extra, uint32_t key_mask
         CHECK(verify(hk, ok, kv ? &ov : nullptr, n), "sort n=%zu kv=%d flags=%x", n, kv, flags_extra);
         rs_plan_info info;
         OK(rs_plan_info_get(p, &info));
+        // a 1-key sort after a real one reports no path (nothing moved)
+        if (n >= 2) {
+            OK(rs_plan_sort_n(p, dk, kv ? dv : nullptr, 1, nullptr));
+            OK(rs_plan_last_path(p, &path));
+            CHECK(path == RS_PATH_NONE, "last_path after a 1-key sort: %u", path);
+        }
+        // the test-only path overrides: a bad field is refused, a valid set sorts the same
+        rs_plan_debug dbg;
+        memset(&dbg, 0xFF, sizeof(dbg));   // every field -1: keep
+        dbg.tile = 3;
+        CHECK(rs_plan_set_debug(p, &dbg) == RS_ERR_INVALID_ARG, "bad debug field accepted");
+        CHECK(rs_plan_set_debug(p, nullptr) == RS_ERR_INVALID_ARG, "null debug accepted");
+        dbg.tile = -1;
+        dbg.rank = 1;
+        dbg.msd = 0;
+        OK(rs_plan_set_debug(p, &dbg));
+        OK(rs_memcpy_h2d(dk, hk.data(), 4 * n, nullptr));
+        OK(rs_memcpy_h2d(dv, hv.data(), 4 * n, nullptr));
+        OK(rs_plan_sort(p, dk, kv ? dv : nullptr, nullptr));
+        OK(rs_plan_check(p));
+        OK(rs_memcpy_d2h(ok.data(), dk, 4 * n, nullptr));
+        OK(rs_memcpy_d2h(ov.data(), dv, 4 * n, nullptr));
+        CHECK(verify(hk, ok, kv ? &ov : nullptr, n), "debug sort n=%zu kv=%d flags=%x", n, kv, flags_extra);
         rs_plan_destroy(p);
     }
     OK(rs_free(dk));
@@ -119,6 +143,24 @@ static void copy_and_records(size_t n) {
         OK(rs_memcpy_d2h(gk.data(), ok, 4 * n, nullptr));
         OK(rs_memcpy_d2h(gv.data(), ov, 4 * n, nullptr));
         CHECK(verify(hk, gk, &gv, n), "partition+sort_records n=%zu", n);
+        rs_plan_destroy(p);
+    }
+    // records already in order, through a check_order plan: the arrays are still written
+    d.flags = RS_FLAG_HAS_VALUES | RS_FLAG_CHECK_ORDER;
+    p = nullptr;
+    OK(rs_plan_create(&d, &p));
+    if (p) {
+        std::vector<uint32_t> sk(hk), sr(2 * n);
+        std::sort(sk.begin(), sk.end());
+        for (size_t i = 0; i < n; ++i) { sr[2 * i] = sk[i]; sr[2 * i + 1] = (uint32_t)i; }
+        OK(rs_memcpy_h2d(rec, sr.data(), 8 * n, nullptr));
+        std::vector<uint32_t> zero(n, 0u);
+        OK(rs_memcpy_h2d(ok, zero.data(), 4 * n, nullptr));
+        OK(rs_plan_sort_records(p, rec, ok, ov, n, nullptr));
+        OK(rs_plan_check(p));
+        OK(rs_memcpy_d2h(gk.data(), ok, 4 * n, nullptr));
+        OK(rs_memcpy_d2h(gv.data(), ov, 4 * n, nullptr));
+        CHECK(verify(sk, gk, &gv, n), "sorted records -> arrays with check_order n=%zu", n);
         rs_plan_destroy(p);
     }
     for (void* q : {ik, iv, ok, ov, rec}) OK(rs_free(q));

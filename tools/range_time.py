@@ -10,7 +10,7 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "webgpu-radix-sort_amd"))
-from radix_sort_amd import ops  # noqa: E402
+from radix_sort_amd import _lib, ops  # noqa: E402
 from radix_sort_amd.ops import SortPlan  # noqa: E402
 
 dev = torch.device("cuda", 0)
@@ -31,8 +31,8 @@ for G in (1, 4):
     rec = rec.view(torch.int64).view(-1)
     ok_, ov_ = torch.empty(N, dtype=torch.int32, device=dev), torch.empty(N, dtype=torch.int32, device=dev)
     for mode in ("lsd", "range"):
-        os.environ["RSORT_MSD"] = "0" if mode == "lsd" else "1"
-        plan = SortPlan(0, max(counts), True)
+        with _lib.plan_debug(msd=0 if mode == "lsd" else 1):
+            plan = SortPlan(0, max(counts), True)
 
         def step():
             a = 0

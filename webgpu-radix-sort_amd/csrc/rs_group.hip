@@ -132,6 +132,13 @@ struct Rank {
     void* res_k = nullptr;
     void* res_v = nullptr;
     uint64_t res_n = 0;
+    // rs_group_set_profiling: timing events of the last sort (start, hist16, partition, per round
+    // the comm stream's completion and the region sort's, done) and its off-rank exchange bytes
+    hipEvent_t t_start = nullptr, t_hist = nullptr, t_part = nullptr, t_done = nullptr;
+    hipEvent_t t_round[kMaxRounds] = {}, t_sorted[kMaxRounds] = {};
+    uint32_t t_rounds = 0;
+    bool t_valid = false;
+    uint64_t bytes_sent = 0, bytes_recv = 0;
 };
 
 rs_status grow(void** ptr, uint64_t* cap, uint64_t need) {
@@ -151,6 +158,7 @@ struct rs_group {
     int world = 0;
     rs_group_desc desc{};
     bool kv = false;
+    bool profiling = false;
     std::vector<Rank> r;
     std::vector<uint64_t> hist_all;   // [world][buckets]
     std::vector<uint32_t> bounds, cuts;
@@ -193,6 +201,12 @@ RS_EXPORT void rs_group_destroy(rs_group* g) {
             if (e) (void)hipEventDestroy(e);
         for (hipEvent_t e : k.ev_round)
             if (e) (void)hipEventDestroy(e);
+        for (hipEvent_t e : {k.t_start, k.t_hist, k.t_part, k.t_done})
+            if (e) (void)hipEventDestroy(e);
+        for (uint32_t j = 0; j < kMaxRounds; ++j) {
+            if (k.t_round[j]) (void)hipEventDestroy(k.t_round[j]);
+            if (k.t_sorted[j]) (void)hipEventDestroy(k.t_sorted[j]);
+        }
         if (k.sort_s) (void)hipStreamDestroy(k.sort_s);
         if (k.comm_s) (void)hipStreamDestroy(k.comm_s);
     }
@@ -349,6 +363,19 @@ RS_EXPORT rs_status rs_group_sort(rs_group* g, void* const* keys, void* const* v
             G_HIP(hipStreamWaitEvent(k.sort_s, k.ev_in, 0));
         }
     }
+    const bool prof = g->profiling;
+    auto mark = [&](Rank& k, hipEvent_t e, hipStream_t s) -> rs_status {
+        if (prof) G_HIP(hipEventRecord(e, s));
+        return RS_OK;
+    };
+    for (int i = 0; i < W; ++i) {
+        Rank& k = g->r[i];
+        Dev dev(k.device);
+        k.t_valid = prof;
+        k.t_rounds = W == 1 ? 0u : G;
+        k.bytes_sent = k.bytes_recv = 0;
+        G_TRY(mark(k, k.t_start, k.sort_s));
+    }
     if (W == 1) {
         G_TRY(group_sort_world1(g, keys, values, counts[0]));
     } else {
@@ -361,6 +388,7 @@ RS_EXPORT rs_status rs_group_sort(rs_group* g, void* const* keys, void* const* v
             G_TRY(rs_plan_hist16(k.part, keys[i], n, k.hist, k.sort_s));
             G_HIP(hipMemcpyAsync(k.hist_host, k.hist, 4ull * RS_HIST16_WORDS, hipMemcpyDeviceToHost, k.sort_s));
             G_HIP(hipEventRecord(k.ev_hist, k.sort_s));
+            G_TRY(mark(k, k.t_hist, k.sort_s));
             if (n) {
                 if (g->kv)
                     G_TRY(rs_plan_partition_records(k.part, keys[i], values[i], k.send, n, shift, bits, k.hist + 65536,
@@ -370,6 +398,7 @@ RS_EXPORT rs_status rs_group_sort(rs_group* g, void* const* keys, void* const* v
                                                    k.hist + 65536, k.sort_s));
             }
             G_HIP(hipEventRecord(k.ev_part, k.sort_s));
+            G_TRY(mark(k, k.t_part, k.sort_s));
         }
         // 3: the bucket plan (host, from every rank's top-byte totals)
         g->hist_all.assign((size_t)W * B, 0);
@@ -431,6 +460,13 @@ RS_EXPORT rs_status rs_group_sort(rs_group* g, void* const* keys, void* const* v
             }
             G_TRY(ensure_local(g, k, biggest));
             G_HIP(hipStreamWaitEvent(k.comm_s, k.ev_part, 0));
+            // off-rank exchange bytes: what q sends to every other rank and receives from them
+            for (uint32_t j = 0; j < G; ++j)
+                for (int o = 0; o < W; ++o) {
+                    if (o == q) continue;
+                    for (uint32_t t = cut(o, j); t < cut(o, j + 1); ++t) k.bytes_sent += esz * cnt(q, t);
+                    for (uint32_t t = cut(q, j); t < cut(q, j + 1); ++t) k.bytes_recv += esz * cnt(o, t);
+                }
         }
         // 4: exchange rounds, one message per (source, top byte) chunk
         const bool rccl = g->desc.transport == RS_TRANSPORT_RCCL;
@@ -482,6 +518,7 @@ RS_EXPORT rs_status rs_group_sort(rs_group* g, void* const* keys, void* const* v
             for (int src = 0; src < W; ++src) {
                 Dev dev(g->r[src].device);
                 G_HIP(hipEventRecord(g->r[src].ev_round[j], g->r[src].comm_s));
+                G_TRY(mark(g->r[src], g->r[src].t_round[j], g->r[src].comm_s));
             }
         }
         // 5: region j sorted once round j has landed (RCCL: the receiver's own comm stream;
@@ -496,12 +533,14 @@ RS_EXPORT rs_status rs_group_sort(rs_group* g, void* const* keys, void* const* v
                     for (int s = 0; s < W; ++s) G_HIP(hipStreamWaitEvent(k.sort_s, g->r[s].ev_round[j], 0));
                 }
                 const uint64_t a = base[(size_t)q * (G + 1) + j], b = base[(size_t)q * (G + 1) + j + 1];
-                if (b <= a) continue;
-                if (g->kv)
-                    G_TRY(rs_plan_sort_region(k.local, (char*)k.recv + 8 * a, k.out_k + a, k.out_v + a, b - a,
-                                              k.reg + (size_t)j * 65536, cut(q, j), cut(q, j + 1), k.sort_s));
-                else
-                    G_TRY(rs_plan_sort_n(k.local, (uint32_t*)k.recv + a, nullptr, b - a, k.sort_s));
+                if (b > a) {
+                    if (g->kv)
+                        G_TRY(rs_plan_sort_region(k.local, (char*)k.recv + 8 * a, k.out_k + a, k.out_v + a, b - a,
+                                                  k.reg + (size_t)j * 65536, cut(q, j), cut(q, j + 1), k.sort_s));
+                    else
+                        G_TRY(rs_plan_sort_n(k.local, (uint32_t*)k.recv + a, nullptr, b - a, k.sort_s));
+                }
+                G_TRY(mark(k, k.t_sorted[j], k.sort_s));
             }
             k.res_k = g->kv ? (void*)k.out_k : k.recv;
             k.res_v = g->kv ? (void*)k.out_v : nullptr;
@@ -511,6 +550,7 @@ RS_EXPORT rs_status rs_group_sort(rs_group* g, void* const* keys, void* const* v
     for (int i = 0; i < W; ++i) {
         Rank& k = g->r[i];
         Dev dev(k.device);
+        G_TRY(mark(k, k.t_done, k.sort_s));
         G_HIP(hipEventRecord(k.ev_done, k.sort_s));
         if (streams && streams[i]) G_HIP(hipStreamWaitEvent((hipStream_t)streams[i], k.ev_done, 0));
     }
@@ -525,6 +565,50 @@ RS_EXPORT rs_status rs_group_result(const rs_group* g, int32_t rank, void** keys
     if (keys) *keys = k.res_k;
     if (values) *values = k.res_v;
     if (count) *count = k.res_n;
+    return RS_OK;
+}
+
+RS_EXPORT rs_status rs_group_set_profiling(rs_group* g, int enable) {
+    if (!g) return gfail(RS_ERR_INVALID_ARG, "rs_group_set_profiling: null group");
+    if (enable)
+        for (auto& k : g->r) {
+            Dev dev(k.device);
+            for (hipEvent_t* e : {&k.t_start, &k.t_hist, &k.t_part, &k.t_done})
+                if (!*e) G_HIP(hipEventCreate(e));
+            for (uint32_t j = 0; j < g->desc.rounds; ++j) {
+                if (!k.t_round[j]) G_HIP(hipEventCreate(&k.t_round[j]));
+                if (!k.t_sorted[j]) G_HIP(hipEventCreate(&k.t_sorted[j]));
+            }
+        }
+    g->profiling = enable != 0;
+    return RS_OK;
+}
+
+RS_EXPORT rs_status rs_group_times_get(rs_group* g, int32_t rank, rs_group_times* out) {
+    if (!g || !out || rank < 0 || rank >= g->world)
+        return gfail(RS_ERR_INVALID_ARG, "rs_group_times_get: null argument or rank out of range");
+    memset(out, 0, sizeof(*out));
+    Rank& k = g->r[rank];
+    if (!k.t_valid) return gfail(RS_ERR_INVALID_ARG, "rs_group_times_get: the last sort ran without rs_group_set_profiling");
+    Dev dev(k.device);
+    G_HIP(hipEventSynchronize(k.t_done));
+    for (uint32_t j = 0; j < k.t_rounds; ++j) G_HIP(hipEventSynchronize(k.t_round[j]));
+    auto since = [&](hipEvent_t e, float* ms) -> rs_status {
+        G_HIP(hipEventElapsedTime(ms, k.t_start, e));
+        return RS_OK;
+    };
+    out->rounds = k.t_rounds;
+    if (k.t_rounds) {
+        G_TRY(since(k.t_hist, &out->hist16_ms));
+        G_TRY(since(k.t_part, &out->partition_ms));
+        for (uint32_t j = 0; j < k.t_rounds; ++j) {
+            G_TRY(since(k.t_round[j], &out->round_done_ms[j]));
+            G_TRY(since(k.t_sorted[j], &out->region_sorted_ms[j]));
+        }
+    }
+    G_TRY(since(k.t_done, &out->done_ms));
+    out->bytes_sent = k.bytes_sent;
+    out->bytes_recv = k.bytes_recv;
     return RS_OK;
 }
 

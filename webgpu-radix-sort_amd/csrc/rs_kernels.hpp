@@ -1167,6 +1167,87 @@ __global__ __launch_bounds__(BLOCK, pass_min_waves(BLOCK, KPT)) void k_onesweep(
     if (chk && tid == 0 && s_inv) atomicOr(chk + pass, 1u);
 }
 
+// ---- one MSD pass over a static split: no look-back, no tickets -----------------------------
+// The hybrid path reads a 16-bit histogram of the input before its passes (k_hist16_in: one row per
+// contiguous input chunk), so the output start of every digit of every work unit is known before
+// the pass begins - the reduce-then-scan form of the pass, with the reduce done by that read:
+//   SEG = 0 (the top-byte pass): unit u = input chunk u (k_hist16_in's chunk of row u: the same
+//           formula, the same grid); digit d of unit u starts at segment d's start + cbase[u][d];
+//   SEG = 1 (the next-byte pass): unit u = top-byte segment u of R1; digit d of it starts at
+//           the segment's start + base16[u << 8 | d] (k_hist16_reduce).
+// A workgroup takes its unit's tiles in order and keeps each digit's running output position in
+// LDS, so a tile's scatter waits for nothing but its own ranking.  (k_onesweep's decoupled look-back
+// waits on status words whose loads queue behind the workgroup's own 128 KB tile prefetch in the
+// CU's memory pipeline.)  Rank, local shuffle and scatter are k_onesweep's (the same helpers), so the
+// output is the same stable partition.  KB: range-relative keys as in k_onesweep.
+template <int BLOCK, int KPT, int L, int RANK, int LO, int SEG, bool KB = false>
+__global__ __launch_bounds__(BLOCK, pass_min_waves(BLOCK, KPT)) void k_static_pass(
+    const uint32_t* __restrict__ in_k, const uint32_t* __restrict__ in_v,
+    uint32_t* __restrict__ out_k, uint32_t* __restrict__ out_v, uint32_t n, uint32_t shift,
+    const uint32_t* gate, const uint32_t* __restrict__ segtab,
+    const uint32_t* __restrict__ base16, const uint32_t* __restrict__ cbase, uint32_t kbase) {
+    constexpr bool HAS_VALUES = L != LAYOUT_KEYS;
+    static_assert((L == LAYOUT_KEYS) == (LO == LAYOUT_KEYS), "values in and out");
+    constexpr int R = 8, RADIX = 256;
+    constexpr int NW = BLOCK / 64;
+    constexpr int TILE = BLOCK * KPT;
+    constexpr int WAVE_KEYS = 64 * KPT;
+    constexpr uint32_t mask = 255u;
+    __shared__ uint32_t s_whist[NW][RADIX];
+    __shared__ uint32_t s_gdelta[RADIX];
+    __shared__ uint32_t s_scratch[NW];
+    __shared__ uint32_t s_keys[HAS_VALUES ? 1 : TILE];
+    __shared__ uint2 s_kv[HAS_VALUES ? TILE : 1];
+    if (gated_off(gate, 0)) return;
+    const uint32_t u = blockIdx.x, tid = threadIdx.x, w = tid >> 6;
+    uint64_t lo, hi;
+    if (SEG) {
+        lo = segtab[257 + u];
+        hi = segtab[513 + u];
+    } else {   // k_hist16_in's chunk of row u
+        const uint64_t chunk = (((uint64_t)n + gridDim.x - 1) / gridDim.x + 3u) & ~3ull;
+        lo = (uint64_t)u * chunk < n ? (uint64_t)u * chunk : n;
+        hi = lo + chunk < n ? lo + chunk : n;
+    }
+    if (lo >= hi) return;
+    // running output position of digit `tid` (thread tid < 256 owns it for the whole unit)
+    uint32_t run = 0;
+    if (tid < (uint32_t)RADIX)
+        run = SEG ? segtab[257 + u] + base16[(u << 8) | tid] : segtab[257 + tid] + cbase[(size_t)u * 256u + tid];
+    uint32_t k[KPT];
+    uint32_t v[HAS_VALUES ? KPT : 1];
+    auto load = [&](uint64_t t0) {
+        load_tile<KPT, L>(in_k, in_v, t0 + w * WAVE_KEYS, (uint32_t)hi, t0 + TILE <= hi, k, v);
+    };
+    load(lo);
+    for (uint64_t t0 = lo; t0 < hi; t0 += TILE) {
+        const uint32_t nvalid = (uint32_t)(hi - t0 < (uint64_t)TILE ? hi - t0 : (uint64_t)TILE);
+        if (KB) {   // range-relative keys (the pads past nvalid stay kPadKey)
+            const uint32_t wb = w * WAVE_KEYS + lane_id();
+#pragma unroll
+            for (int j = 0; j < KPT; ++j)
+                if (wb + j * 64 < nvalid) k[j] -= kbase;
+        }
+        Slots<KPT, false> rank;
+        uint32_t c;
+        const uint32_t tstart = rank_tile<R, NW, KPT, RANK>(k, rank, s_whist, s_scratch, shift, mask,
+                                                            (uint32_t)TILE - nvalid, c);
+        if (tid < (uint32_t)RADIX) {
+            set_wave_offsets<R, NW>(s_whist, tstart);
+            s_gdelta[tid] = run - tstart;
+            run += c;
+        }
+        __syncthreads();
+        stage_tile<KPT, HAS_VALUES, TILE>(k, v, rank, s_whist[w], s_keys, s_kv, shift, mask, nullptr, 0u, 0u);
+        __syncthreads();
+        // the next tile's loads into the (now free) registers: in flight during this scatter
+        if (t0 + TILE < hi) load(t0 + TILE);
+        scatter_tile<BLOCK, HAS_VALUES, LO>(s_keys, s_kv, s_gdelta, out_k, out_v, n, nvalid,
+                                            (uint32_t)t0, shift, mask);
+        __syncthreads();
+    }
+}
+
 // ---- whole sort of a small array in one workgroup ------------------------------------------
 // n <= BLOCK*KPT: keys (+values) stay in registers between passes; every pass ranks, stages the
 // tile sorted by its digit in LDS, and reloads the registers from LDS.  One launch, one HBM read
@@ -1449,7 +1530,17 @@ __global__ __launch_bounds__(1024) void k_hist16_in(const uint32_t* __restrict__
 // base16[b] = the bucket's start inside its top-byte segment (consumers add the segment start,
 // segtab[257 + (b >> 8)]), buckets over `small` appended to over[1..] (over[0] counts them, up to
 // kOverMax stored), *big |= a bucket over `cap`.
+// cbase (may be null): cbase[r * 256 + t] = the keys with top byte t in the chunks of the rows
+// before row r (an exclusive scan over the rows of each top byte's row sums): where chunk r's
+// top-byte-t keys start inside segment t.  The static first MSD pass (k_static_pass) takes its
+// per-digit output bases from it, so it needs no look-back.
 constexpr uint32_t kOverMax = 4096;
+constexpr uint32_t kMaxRows = 1024;
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
 __global__ __launch_bounds__(1024) void k_hist16_reduce(const uint32_t* __restrict__ rows, uint32_t nrows,
                                                          uint32_t* __restrict__ hist16,
                                                          uint32_t* __restrict__ top_tot,
@@ -1458,7 +1549,8 @@ __global__ __launch_bounds__(1024) void k_hist16_reduce(const uint32_t* __restri
                                                          uint32_t cap, uint32_t* __restrict__ over,
                                                          uint32_t* __restrict__ big,
                                                          uint32_t* __restrict__ zero = nullptr, uint32_t nzero = 0,
-                                                         const uint32_t* __restrict__ b0rows = nullptr) {
+                                                         const uint32_t* __restrict__ b0rows = nullptr,
+                                                         uint32_t* __restrict__ cbase = nullptr) {
     // zero[0..nzero): the sort's pass totals, tile tickets and device error word (no memset launch);
     // with b0rows (check_order): zero[0..256) = pass 0's byte-0 totals, the rows' sums
     if (blockIdx.x == gridDim.x - 1) {
@@ -1470,6 +1562,8 @@ __global__ __launch_bounds__(1024) void k_hist16_reduce(const uint32_t* __restri
         }
     }
     __shared__ uint4 s_part[16][64];
+    __shared__ uint32_t s_rowsum[kMaxRows];
+    __shared__ uint32_t s_scan[16];
     const uint32_t tid = threadIdx.x, c = tid & 63u, g = tid >> 6;
     if (blockIdx.x == 0) {   // any key outside the range (the rows' flag words)
         const int bad = __syncthreads_or(tid < nrows && rows[(size_t)nrows * 65536u + tid] != 0u);
@@ -1479,14 +1573,32 @@ __global__ __launch_bounds__(1024) void k_hist16_reduce(const uint32_t* __restri
     constexpr size_t RS = 65536 / 4;    // row stride in 16-byte words
     uint4 a = make_uint4(0u, 0u, 0u, 0u);
     auto add = [](uint4& x, const uint4 y) { x.x += y.x; x.y += y.y; x.z += y.z; x.w += y.w; };
+    // wave g holds one row's 256 buckets of this top byte at a time: their sum is the row's
+    // (chunk's) count of the top byte
+    auto rowsum = [&](uint32_t row, const uint4 q) {
+        if (cbase) {
+            const uint32_t s = wave_sum(q.x + q.y + q.z + q.w);
+            if (c == 0) s_rowsum[row] = s;
+        }
+    };
     uint32_t r = g;
     for (; r + 48u < nrows; r += 64u) {
         const uint4 q0 = r4[r * RS], q1 = r4[(r + 16u) * RS], q2 = r4[(r + 32u) * RS], q3 = r4[(r + 48u) * RS];
         add(a, q0); add(a, q1); add(a, q2); add(a, q3);
+        rowsum(r, q0); rowsum(r + 16u, q1); rowsum(r + 32u, q2); rowsum(r + 48u, q3);
     }
-    for (; r < nrows; r += 16u) add(a, r4[r * RS]);
+    for (; r < nrows; r += 16u) {
+        const uint4 q = r4[r * RS];
+        add(a, q);
+        rowsum(r, q);
+    }
     s_part[g][c] = a;
     __syncthreads();
+    if (cbase) {   // exclusive scan of the row sums (uniform branch: every thread takes part)
+        uint32_t tot;
+        const uint32_t ex = block_excl_scan_n<16>(tid < nrows ? s_rowsum[tid] : 0u, s_scan, tot);
+        if (tid < nrows) cbase[(size_t)tid * 256u + blockIdx.x] = ex;
+    }
     if (tid < 64u) {
         uint4 t = s_part[0][tid];
 #pragma unroll
@@ -1544,17 +1656,26 @@ __global__ __launch_bounds__(256) void k_region_rows(const uint32_t* __restrict_
 // clamped to the stored entries.
 // The histogram must account for every one of the n keys (a counting bug would otherwise send the
 // data through passes with wrong digit bases and return garbage): a mismatch picks the LSD passes.
+// The second MSD pass runs over a static split (k_static_pass: one workgroup per top-byte segment,
+// no look-back) when the segments are balanced - none over the mean by more than 1/16 plus a tile
+// - else with the look-back (k_onesweep SEG): gates g[32..47] / g[48..63], each ANDed with the MSD
+// choice.  The populated buckets must lie in the top bytes [top_lo, top_hi) (a region's
+// table; counts outside them would never be sorted): otherwise the LSD passes run.
+constexpr uint32_t kGateSegStatic = 32, kGateSegLookback = 48;
 template <int TILE>
 __global__ __launch_bounds__(256) void k_msd_plan(const uint32_t* __restrict__ top_tot,
                                                   uint32_t* __restrict__ segtab, uint32_t max_top,
                                                   uint32_t* over, const uint32_t* big, uint32_t* gates,
                                                   const uint32_t* __restrict__ range_bad, uint32_t n,
-                                                  const uint32_t* inv = nullptr) {
+                                                  const uint32_t* inv = nullptr, uint32_t top_lo = 0,
+                                                  uint32_t top_hi = 256) {
     constexpr int NW = 4;
     __shared__ uint32_t s_scratch[NW];
     const uint32_t tid = threadIdx.x;
     const uint32_t cnt = top_tot[tid];
-    const int any_big = __syncthreads_or(cnt > max_top ? 1 : 0);
+    const int any_big = __syncthreads_or((cnt > max_top || (cnt != 0u && (tid < top_lo || tid >= top_hi))) ? 1 : 0);
+    const uint32_t seg_cap = n / 256u + n / 4096u + (uint32_t)TILE;
+    const int unbalanced = __syncthreads_or(cnt > seg_cap ? 1 : 0);
     const uint32_t tiles = (cnt + TILE - 1) / TILE;
     uint32_t ttot;
     const uint32_t tbase = block_excl_scan_n<NW>(tiles, s_scratch, ttot);
@@ -1573,6 +1694,8 @@ __global__ __launch_bounds__(256) void k_msd_plan(const uint32_t* __restrict__ t
     const uint32_t run = (inv && *inv == 0u) ? 0u : 1u;
     set_gate(gates + kGateMsd, ok & run);
     set_gate(gates + kGateLsd, (1u - ok) & run);
+    set_gate(gates + kGateSegStatic, ok & run & (unbalanced ? 0u : 1u));
+    set_gate(gates + kGateSegLookback, ok & run & (unbalanced ? 1u : 0u));
 }
 
 // In-LDS sort of the 16-bit buckets: a workgroup takes a bucket's records (R2, contiguous, at most

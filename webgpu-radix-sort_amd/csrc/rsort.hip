@@ -23,7 +23,7 @@
 #include <string>
 #include <vector>
 
-#include <rocprofiler-sdk-roctx/roctx.h>
+#include <dlfcn.h>
 
 #include "../../include/rsort.h"
 #include "rs_internal.h"
@@ -31,11 +31,11 @@
 
 #define RS_EXPORT extern "C" __attribute__((visibility("default")))
 
-// Tuning knobs.  The product library has none beyond the per-plan path choices read at plan
-// creation (rs_plan_create: RSORT_MSD / ONESWEEP / RANK / TILE / KEYS_CFG / MSD_KEYS_CFG /
-// KBUCKET_WAVE / SPIN_MAX, which the parity tests use to cover every path).  The sweep build
-// (`make variants`, tools/sweep.py: -DRS_SWEEP=1) adds the process-wide experiment knobs and the
-// alternative kernel instantiations they select; a product build compiles neither.
+// Tuning knobs.  The product library reads no environment variables: the per-plan path choices
+// the parity tests use to cover every kernel are set through rs_plan_set_debug.  The sweep build
+// (`make variants`, tools/sweep.py: -DRS_SWEEP=1) adds the process-wide experiment knobs (RSORT_*
+// environment variables) and the alternative kernel instantiations they select; a product build
+// compiles neither.
 #ifndef RS_SWEEP
 #define RS_SWEEP 0
 #endif
@@ -128,8 +128,8 @@ constexpr uint32_t kBucketCap = 1024u * kWideKpt;       // the largest 16-bit bu
 // a uniform population's largest bucket (mean + ~5 sigma) still fits kBucketCap up to here (2^31
 // keys: mean 32768, sigma 181); above it the device would always pick the LSD fallback
 constexpr uint64_t kMsdMax = 65536ull * 33800;
-constexpr uint64_t kMsdWords = 65536ull * 2 + 1024 + 64 + 1024 + 1 + rs::kOverMax;   // hist16, base16,
-                                                                    // segtab, gates, mtot, over
+constexpr uint64_t kMsdWords = 65536ull * 2 + 1024 + 64 + 1024 + 1 + rs::kOverMax +   // hist16, base16,
+                                 256ull * rs::kMaxRows;             // segtab, gates, mtot, over, cbase
 constexpr uint32_t kHistGrid = 2048;
 constexpr int kCheckGrid = 2048;
 
@@ -146,10 +146,37 @@ struct DeviceGuard {
 
 // Every launch group of a sort is a named roctx range on the host (rocprofv3 --marker-trace
 // attributes the kernels it encloses to histogram / MSD pass 0 / pass 1 / bucket / fallback / LSD
-// pass without relying on template names; SURVEY.md §5 "Tracing").
+// pass without relying on template names; SURVEY.md §5 "Tracing").  roctx is bound lazily with
+// dlopen: librsort.so has no link-time dependency on rocprofiler-sdk, and without it the ranges
+// are no-ops.
+struct Roctx {
+    using Push = int (*)(const char*);
+    using Pop = int (*)();
+    Push push = nullptr;
+    Pop pop = nullptr;
+    Roctx() {
+        void* h = dlopen("librocprofiler-sdk-roctx.so", RTLD_NOW | RTLD_LOCAL | RTLD_NOLOAD);
+        if (!h) h = dlopen("librocprofiler-sdk-roctx.so", RTLD_NOW | RTLD_LOCAL);
+        if (!h) h = dlopen("/opt/rocm/lib/librocprofiler-sdk-roctx.so", RTLD_NOW | RTLD_LOCAL);
+        if (h) {
+            push = reinterpret_cast<Push>(dlsym(h, "roctxRangePushA"));
+            pop = reinterpret_cast<Pop>(dlsym(h, "roctxRangePop"));
+            if (!push || !pop) push = nullptr, pop = nullptr;
+        }
+    }
+    static const Roctx& get() {
+        static const Roctx r;
+        return r;
+    }
+};
 struct RoctxRange {
-    explicit RoctxRange(const char* name) { roctxRangePushA(name); }
-    ~RoctxRange() { roctxRangePop(); }
+    bool on;
+    explicit RoctxRange(const char* name) : on(Roctx::get().push != nullptr) {
+        if (on) Roctx::get().push(name);
+    }
+    ~RoctxRange() {
+        if (on) Roctx::get().pop();
+    }
 };
 
 struct KernelTimer {
@@ -242,8 +269,11 @@ struct rs_plan {
                                      // (32K-key tiles for pass 0 only: no faster, r03_keys_pass0_tiles_ab)
     bool kbucket_wave = true;        // one wave per 16-bit bucket (RSORT_KBUCKET_WAVE=0: workgroups)
     bool kbucket_pf = false;         // workgroup kernel on a persistent prefetching grid (sweep: RSORT_KBUCKET_PF=1)
+    bool static_passes = false;      // hybrid MSD passes over static splits (sweep only, RSORT_STATIC=1: measured
+                                     // slower than the look-back passes)
     uint32_t* msd = nullptr;         // its workspace: hist16 | base16 | segtab | gates | mtot
     bool last_hybrid = false;        // the last sort enqueued the hybrid path (rs_plan_last_path)
+    bool path_none = false;          // the last sort moved nothing (n <= 1): rs_plan_last_path NONE
     int scatter_kind = RS_KERNEL_SCATTER;   // timer kind of the pass launches being enqueued
     uint32_t* host_err = nullptr;  // host-mapped error word: set by a timed-out look-back wait,
     uint32_t* host_err_dev = nullptr;   // read + cleared by rs_plan_check / the next rs_plan_sort
@@ -392,6 +422,41 @@ void launch_msd_pass(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint32_
     else
         go(rs::k_onesweep<8, BLOCK, KPT, L, rs::RANK_LDS_ATOMIC, LO, 1, SEG, KB>);
 }
+
+// The hybrid path's passes over a static split (k_static_pass; 16K-record tiles, one 1024-thread
+// workgroup per unit).  Pass 0: one workgroup per k_hist16_in row (input chunk), input arrays or
+// records -> R1 records; pass 1: one workgroup per top-byte segment, R1 -> R2 records.
+#if RS_SWEEP
+void launch_static_pass0(rs_plan* p, const uint32_t* ik, const uint32_t* iv, bool in_aos, bool kb, uint32_t* r1,
+                         uint32_t n, uint32_t shift, uint32_t rows, const uint32_t* gate, const uint32_t* segtab,
+                         const uint32_t* cbase, uint32_t kbase, hipStream_t s) {
+    constexpr int A = rs::LAYOUT_AOS, S = rs::LAYOUT_SOA, B = kLarge.block, K = kLarge.kpt;
+    auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3(rows), dim3(B), 0, s, ik, iv, r1, (uint32_t*)nullptr, n, shift, gate, segtab,
+                           (const uint32_t*)nullptr, cbase, kbase);
+    };
+    const bool ballot = p->rank_mode == rs::RANK_BALLOT;
+    constexpr int RA = rs::RANK_LDS_ATOMIC, RB = rs::RANK_BALLOT;
+    if (in_aos) {
+        if (kb) ballot ? go(rs::k_static_pass<B, K, A, RB, A, 0, true>) : go(rs::k_static_pass<B, K, A, RA, A, 0, true>);
+        else ballot ? go(rs::k_static_pass<B, K, A, RB, A, 0>) : go(rs::k_static_pass<B, K, A, RA, A, 0>);
+    } else {
+        if (kb) ballot ? go(rs::k_static_pass<B, K, S, RB, A, 0, true>) : go(rs::k_static_pass<B, K, S, RA, A, 0, true>);
+        else ballot ? go(rs::k_static_pass<B, K, S, RB, A, 0>) : go(rs::k_static_pass<B, K, S, RA, A, 0>);
+    }
+}
+
+void launch_static_pass1(rs_plan* p, const uint32_t* r1, uint32_t* r2, uint32_t n, uint32_t shift,
+                         const uint32_t* gate, const uint32_t* segtab, const uint32_t* base16, hipStream_t s) {
+    constexpr int A = rs::LAYOUT_AOS, B = kLarge.block, K = kLarge.kpt;
+    auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3(256), dim3(B), 0, s, r1, (const uint32_t*)nullptr, r2, (uint32_t*)nullptr, n,
+                           shift, gate, segtab, base16, (const uint32_t*)nullptr, 0u);
+    };
+    if (p->rank_mode == rs::RANK_BALLOT) go(rs::k_static_pass<B, K, A, rs::RANK_BALLOT, A, 1>);
+    else go(rs::k_static_pass<B, K, A, rs::RANK_LDS_ATOMIC, A, 1>);
+}
+#endif
 
 // Layout pair of one pass: input layout | output layout << 4 (they differ only on the one-sweep
 // separate-values path, which stages its ping-pong copy as (key, value) records).
@@ -559,13 +624,10 @@ bool use_msd(const rs_plan* p, uint64_t n) {
 
 // Lane-order self-test of the device's LDS atomics (k_lane_order_selftest), once per device
 // per process: 1 passed, 0 failed (plans then rank with RANK_BALLOT), -1 could not run.
-// RSORT_SELFTEST=fail simulates a failure (tests), RSORT_SELFTEST=0 skips it (counts as passed).
+// rs_plan_set_debug(selftest_fail = 1) simulates a failure (tests).
 int lane_order_selftest(int dev) {
     static std::mutex mu;
     static std::map<int, int> done;
-    const char* env = getenv("RSORT_SELFTEST");
-    if (env && strcmp(env, "fail") == 0) return 0;
-    if (env && strcmp(env, "0") == 0) return 1;
     std::lock_guard<std::mutex> lock(mu);
     auto it = done.find(dev);
     if (it != done.end()) return it->second;
@@ -664,14 +726,7 @@ RS_EXPORT rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out) {
     p->usage = d.usage;
     p->check_order = d.flags & RS_FLAG_CHECK_ORDER;
     p->local_shuffle = d.flags & RS_FLAG_LOCAL_SHUFFLE;
-    // path choices (per plan; the parity tests switch them to cover every path)
-    if (const char* os = getenv("RSORT_ONESWEEP")) p->onesweep_mode = strcmp(os, "0") != 0 ? 1 : 0;
-    if (const char* t = getenv("RSORT_TILE")) p->tile_mode = strcmp(t, "small") == 0 ? 1 : 0;
-    if (const char* kc = getenv("RSORT_KEYS_CFG")) p->keys_cfg = strcmp(kc, "0") != 0;
-    if (const char* ms = getenv("RSORT_MSD")) p->msd_mode = strcmp(ms, "0") != 0 ? 1 : 0;
-    if (const char* e = getenv("RSORT_MSD_KEYS_CFG")) p->msd_keys_cfg = atoi(e);
-    if (const char* e = getenv("RSORT_KBUCKET_WAVE")) p->kbucket_wave = strcmp(e, "0") != 0;
-    if (const char* sm = getenv("RSORT_SPIN_MAX")) p->spin_max = (uint32_t)strtoul(sm, nullptr, 10);
+    // path choices: by size; the parity tests switch them with rs_plan_set_debug
     bool recs2 = true;
 #if RS_SWEEP
     p->aos_tmp = RS_KNOB("RSORT_AOS_TMP", 1) != 0;
@@ -680,6 +735,7 @@ RS_EXPORT rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out) {
     p->kv_cfg = (int)RS_KNOB("RSORT_KV_CFG", 0);
     p->fused_check = RS_KNOB("RSORT_FUSED_CHECK", 1) != 0;
     p->kbucket_pf = RS_KNOB("RSORT_KBUCKET_PF", 0) == 1;
+    p->static_passes = RS_KNOB("RSORT_STATIC", 0) != 0;
 #endif
     // Even number of passes so the result lands in the caller's buffers, like the reference's
     // bit_count/2 passes with ping-pong on bit % 4 (AbstractRadixSortKernel.ts:93-107).
@@ -696,11 +752,9 @@ RS_EXPORT rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out) {
     DeviceGuard guard(d.device);
     auto cleanup = [&](rs_status s) { rs_plan_destroy(p); return s; };
     // stable ranking: lane-ordered LDS atomics where the device passes the self-test, else the
-    // architecture-guaranteed ballot ranking; RSORT_RANK=ballot|atomic overrides
+    // architecture-guaranteed ballot ranking (rs_plan_set_debug overrides)
     p->selftest = lane_order_selftest(d.device);
     p->rank_mode = p->selftest == 1 ? rs::RANK_LDS_ATOMIC : rs::RANK_BALLOT;
-    if (const char* rk = getenv("RSORT_RANK"))
-        p->rank_mode = (strcmp(rk, "ballot") == 0) ? rs::RANK_BALLOT : rs::RANK_LDS_ATOMIC;
     auto alloc = [&](uint32_t** ptr, uint64_t bytes) -> hipError_t {
         if (bytes == 0) bytes = 4;
         p->workspace += bytes;
@@ -839,6 +893,7 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
     uint32_t* gates = segtab + 1024;
     uint32_t* mtot = gates + 64;
     uint32_t* over = mtot + 1024;
+    uint32_t* cbase = over + 1 + rs::kOverMax;   // [row][top byte]: chunk starts inside the segments
     uint32_t* top_tot = mtot + 768;
     uint32_t* big = mtot + 1;          // a 16-bit bucket over the large bucket tile
     uint32_t* sstart = segtab + 257;   // top-byte segment starts (bucket bases are relative to them)
@@ -891,7 +946,17 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
     const uint32_t hrows = region ? 1u : std::max(1u, p->cus / hdiv);
     // check_order (whole-range sorts; the region form never checks): the input's order check rides
     // on the histogram read (p->flags[0]); the byte-0 rows follow the histogram rows and flags
-    const bool chk = p->check_order && !region && kbase == 0u && vbits == 32u;
+    // check_order rides on the histogram read only for in-place sorts: a sorted input then needs
+    // nothing moved, which is right only when the output IS the input (records -> arrays and
+    // out-of-place sorts always run their passes)
+    const bool in_place = sk == uk && in_aos == out_aos && (in_aos || sv == uv);
+    const bool chk = p->check_order && !region && kbase == 0u && vbits == 32u && in_place;
+    // static work splits (k_static_pass, no look-back) for the passes with values: pass 0 over the
+    // histogram's input chunks, pass 1 over the top-byte segments when they are balanced (the
+    // device picks; else the look-back pass).  Keys only keeps the look-back passes (two 512-thread
+    // workgroups per CU).
+    const bool static_p0 = !region && !keys && p->static_passes && hrows <= rs::kMaxRows;
+    const bool static_p1 = !keys && p->static_passes;
     uint32_t* b0rows = chk ? p->tmp_k + (size_t)hrows * 65537u : nullptr;
     if (chk) HIP_TRY(hipMemsetAsync(p->flags, 0, 16 * 4, s));
     p->timer.run(RS_KERNEL_HISTOGRAM, s, [&] {
@@ -926,14 +991,15 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
         // overflow list, the oversize flag): the plan kernel is left with the 256 segments
         hipLaunchKernelGGL(rs::k_hist16_reduce, dim3(256), dim3(1024), 0, s, (const uint32_t*)p->tmp_k,
                            hrows, hist16, top_tot, range_bad, base16, small_cap, kBucketCap, over, big,
-                           p->ptot, (uint32_t)(rs::kTotalsMax + 32), (const uint32_t*)b0rows);
+                           p->ptot, (uint32_t)(rs::kTotalsMax + 32), (const uint32_t*)b0rows,
+                           static_p0 ? cbase : (uint32_t*)nullptr);
     }, region ? "rsort.msd.region_table" : "rsort.msd.hist16");
     HIP_TRY(hipGetLastError());
     p->timer.run(RS_KERNEL_SCAN, s, [&] {
         auto plan = [&](auto kern) {
             hipLaunchKernelGGL(kern, dim3(1), dim3(256), 0, s, (const uint32_t*)top_tot, segtab, 0xFFFFFFFFu, over,
                                (const uint32_t*)big, gates, (const uint32_t*)range_bad, n32,
-                               chk ? (const uint32_t*)p->flags : (const uint32_t*)nullptr);
+                               chk ? (const uint32_t*)p->flags : (const uint32_t*)nullptr, top_lo, top_hi);
         };
         if (tile == 2u * kLarge.tile) plan(rs::k_msd_plan<2 * kLarge.tile>);
         else plan(rs::k_msd_plan<kLarge.tile>);
@@ -970,6 +1036,10 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
             launch_msd_pass<K, K, 0, false, kLargeKeys.block, kLargeKeys.kpt>(
                 p, sk, nullptr, r1, nullptr, n32, vbits - 8, ntiles, top_tot, p->tickets + 4, g_msd, nullptr,
                 nullptr, s);
+#if RS_SWEEP
+        else if (static_p0)
+            launch_static_pass0(p, sk, sv, in_aos, kbase != 0u, r1, n32, vbits - 8, hrows, g_msd, segtab, cbase, kbase, s);
+#endif
         else if (in_aos && kbase)
             launch_msd_pass<A, A, 0, true>(p, sk, nullptr, r1, nullptr, n32, vbits - 8, ntiles, top_tot,
                                            p->tickets + 4, g_msd, nullptr, nullptr, s, kbase);
@@ -997,9 +1067,17 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
             launch_msd_pass<K, K, 1, false, kLargeKeys.block, kLargeKeys.kpt>(
                 p, r1, nullptr, r2, nullptr, n32, vbits - 16, ntiles + 257, nullptr, p->tickets + 5, g_msd,
                 segtab, base16, s);
-        else
+        else {
+            // the static split when the device found the segments balanced, else the look-back pass
+            // (each launch exits at once unless its gate is set)
+#if RS_SWEEP
+            if (static_p1 && !ring)
+                launch_static_pass1(p, r1, r2, n32, vbits - 16, gates + rs::kGateSegStatic, segtab, base16, s);
+#endif
             launch_msd_pass<A, A, 1>(p, r1, nullptr, ring ? ring : r2, nullptr, n32, vbits - 16, ntiles + 257, nullptr,
-                                     p->tickets + 5, g_msd, segtab, base16, s, 0u, rmask);
+                                     p->tickets + 5, (static_p1 && !ring) ? gates + rs::kGateSegLookback : g_msd,
+                                     segtab, base16, s, 0u, rmask);
+        }
     }, "rsort.msd.pass1");
     HIP_TRY(hipGetLastError());
     const bool ballot = p->rank_mode == rs::RANK_BALLOT;
@@ -1025,7 +1103,7 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
             const uint32_t grid = std::min<uint32_t>(65536u, p->cus * per_cu * mult);
             hipLaunchKernelGGL(kern, dim3(grid), dim3(bb), 0, s, r2, hist16, base16, uk, uv, g_msd,
                                p->tickets + 16, 0u, (const uint32_t*)nullptr, kbase, (const uint32_t*)sstart,
-                               0xFFFFFFFFu);
+                               0xFFFFFFFFu, 0u, 65536u);
         };
 #endif
         // the wide kernel: every bucket (wide_all), or the listed buckets over the population-sized
@@ -1259,7 +1337,11 @@ RS_EXPORT rs_status rs_plan_sort_n(rs_plan* p, void* keys, void* values, uint64_
         return fail(RS_ERR_CAPACITY, "count %llu exceeds plan capacity %llu",
                     (unsigned long long)n, (unsigned long long)p->capacity);
     if (rs_status st = need_sort_plan(p, "rs_plan_sort")) return st;
-    if (n <= 1) return RS_OK;
+    if (n <= 1) {   // nothing to move: no path taken
+        p->last_hybrid = false;
+        p->path_none = true;
+        return RS_OK;
+    }
     if (!keys) return fail(RS_ERR_INVALID_ARG, "rs_plan_sort: keys is null");
     const int L = p->layout;
     if (L == rs::LAYOUT_SOA && !values)
@@ -1282,6 +1364,7 @@ RS_EXPORT rs_status rs_plan_sort_n(rs_plan* p, void* keys, void* values, uint64_
     if (st != RS_OK) return st;
     HIP_TRY(hipEventRecord(p->done, s));
     p->done_recorded = true;
+    p->path_none = false;
     return RS_OK;
 }
 
@@ -1297,7 +1380,11 @@ RS_EXPORT rs_status rs_plan_sort_copy(rs_plan* p, const void* in_k, const void* 
     if (p->layout == rs::LAYOUT_AOS || p->check_order)
         return fail(RS_ERR_INVALID_ARG, "rs_plan_sort_copy: needs a plan with separate arrays (not interleaved) and no check_order");
     const bool kv = p->layout == rs::LAYOUT_SOA;
-    if (n == 0) return RS_OK;
+    if (n == 0) {
+        p->last_hybrid = false;
+        p->path_none = true;
+        return RS_OK;
+    }
     if (!in_k || !out_k || (kv && (!in_v || !out_v)))
         return fail(RS_ERR_INVALID_ARG, "rs_plan_sort_copy: null buffer");
     if (((uintptr_t)in_k | (uintptr_t)out_k | (kv ? ((uintptr_t)in_v | (uintptr_t)out_v) : 0)) & 3)
@@ -1319,6 +1406,7 @@ RS_EXPORT rs_status rs_plan_sort_copy(rs_plan* p, const void* in_k, const void* 
     if (st != RS_OK) return st;
     HIP_TRY(hipEventRecord(p->done, s));
     p->done_recorded = true;
+    p->path_none = false;
     return RS_OK;
 }
 
@@ -1326,7 +1414,7 @@ RS_EXPORT rs_status rs_plan_last_path(rs_plan* p, uint32_t* path) {
     if (!p || !path) return fail(RS_ERR_INVALID_ARG, "rs_plan_last_path: null argument");
     DeviceGuard guard(p->desc.device);
     *path = RS_PATH_NONE;
-    if (!p->done_recorded) return RS_OK;
+    if (!p->done_recorded || p->path_none) return RS_OK;
     HIP_TRY(hipEventSynchronize(p->done));
     if (!p->last_hybrid) {
         *path = RS_PATH_LSD;
@@ -1511,7 +1599,11 @@ static rs_status sort_records_impl(rs_plan* p, const void* records, void* keys_o
     if (n > p->capacity)
         return fail(RS_ERR_CAPACITY, "count %llu exceeds plan capacity %llu",
                     (unsigned long long)n, (unsigned long long)p->capacity);
-    if (n == 0) return RS_OK;
+    if (n == 0) {
+        p->last_hybrid = false;
+        p->path_none = true;
+        return RS_OK;
+    }
     if (!records || !keys_out || !values_out)
         return fail(RS_ERR_INVALID_ARG, "rs_plan_sort_records: null buffer");
     if (((uintptr_t)records & 7) || ((uintptr_t)keys_out & 3) || ((uintptr_t)values_out & 3))
@@ -1539,6 +1631,7 @@ static rs_status sort_records_impl(rs_plan* p, const void* records, void* keys_o
     if (st != RS_OK) return st;
     HIP_TRY(hipEventRecord(p->done, s));
     p->done_recorded = true;
+    p->path_none = false;
     return RS_OK;
 }
 
@@ -1569,7 +1662,8 @@ RS_EXPORT rs_status rs_plan_hist16(rs_plan* p, const void* keys, uint64_t n, voi
     // per row); k_hist16_sum adds the rows and the top-byte totals
     const uint32_t hrows = (uint32_t)std::min<uint64_t>(p->cus, p->rows_words / 65537ull);
     if (hrows == 0)
-        return fail(RS_ERR_CAPACITY, "rs_plan_hist16: the plan's workspace holds no histogram row (capacity >= 32768 needed)");
+        return fail(RS_ERR_CAPACITY, "rs_plan_hist16: the plan's workspace holds no histogram row (a keys-only "
+                    "sort plan needs capacity >= 65537; plans with values and RS_USAGE_PARTITION plans always hold one)");
     p->timer.run(RS_KERNEL_HISTOGRAM, s, [&] {
         // z0 / z1 (the MSD path's overflow words) point into the rows' flag area: unused here
         uint32_t* z = p->tmp_k + (size_t)hrows * 65536u;
@@ -1599,7 +1693,11 @@ RS_EXPORT rs_status rs_plan_sort_region(rs_plan* p, const void* records, void* k
                     (unsigned long long)n, (unsigned long long)p->capacity);
     if (top_lo >= top_hi || top_hi > 256)
         return fail(RS_ERR_INVALID_ARG, "rs_plan_sort_region: need top_lo < top_hi <= 256 (got %u, %u)", top_lo, top_hi);
-    if (n == 0) return RS_OK;
+    if (n == 0) {
+        p->last_hybrid = false;
+        p->path_none = true;
+        return RS_OK;
+    }
     if (!records || !keys_out || !values_out || !d_hist16)
         return fail(RS_ERR_INVALID_ARG, "rs_plan_sort_region: null buffer");
     if (((uintptr_t)records & 7) || ((uintptr_t)keys_out & 3) || ((uintptr_t)values_out & 3) || ((uintptr_t)d_hist16 & 3))
@@ -1627,6 +1725,7 @@ RS_EXPORT rs_status rs_plan_sort_region(rs_plan* p, const void* records, void* k
     if (st != RS_OK) return st;
     HIP_TRY(hipEventRecord(p->done, s));
     p->done_recorded = true;
+    p->path_none = false;
     return RS_OK;
 }
 
@@ -1665,6 +1764,27 @@ RS_EXPORT rs_status rs_plan_info_get(const rs_plan* p, rs_plan_info* info) {
 RS_EXPORT rs_status rs_plan_set_wait_limit(rs_plan* p, uint32_t sleeps) {
     if (!p) return fail(RS_ERR_INVALID_ARG, "rs_plan_set_wait_limit: null plan");
     p->spin_max = sleeps;
+    return RS_OK;
+}
+
+RS_EXPORT rs_status rs_plan_set_debug(rs_plan* p, const rs_plan_debug* d) {
+    if (!p || !d) return fail(RS_ERR_INVALID_ARG, "rs_plan_set_debug: null argument");
+    auto tri = [](int32_t v, int hi) { return v >= -1 && v <= hi; };
+    if (!tri(d->rank, 1) || !tri(d->tile, 1) || !tri(d->onesweep, 1) || !tri(d->msd, 1) ||
+        !tri(d->keys_cfg, 1) || !tri(d->msd_keys_cfg, 2) || !tri(d->kbucket_wave, 1) ||
+        !tri(d->selftest_fail, 1))
+        return fail(RS_ERR_INVALID_ARG, "rs_plan_set_debug: every field must be -1 or a listed choice");
+    if (d->selftest_fail == 1) {
+        p->selftest = 0;
+        p->rank_mode = rs::RANK_BALLOT;
+    }
+    if (d->rank >= 0) p->rank_mode = d->rank == 1 ? rs::RANK_BALLOT : rs::RANK_LDS_ATOMIC;
+    if (d->tile >= 0) p->tile_mode = d->tile;
+    if (d->onesweep >= 0) p->onesweep_mode = d->onesweep;
+    if (d->msd >= 0) p->msd_mode = d->msd;
+    if (d->keys_cfg >= 0) p->keys_cfg = d->keys_cfg == 1;
+    if (d->msd_keys_cfg >= 0) p->msd_keys_cfg = d->msd_keys_cfg;
+    if (d->kbucket_wave >= 0) p->kbucket_wave = d->kbucket_wave == 1;
     return RS_OK;
 }
 

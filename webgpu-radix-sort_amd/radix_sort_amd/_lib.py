@@ -52,6 +52,55 @@ class PlanDesc(ctypes.Structure):
                 ("radix_bits", ctypes.c_uint32), ("usage", ctypes.c_uint32)]
 
 
+class PlanDebug(ctypes.Structure):
+    """rs_plan_debug (test / diagnostics only): force a plan onto one of its paths; -1 = keep."""
+    _fields_ = [("rank", ctypes.c_int32), ("tile", ctypes.c_int32), ("onesweep", ctypes.c_int32),
+                ("msd", ctypes.c_int32), ("keys_cfg", ctypes.c_int32), ("msd_keys_cfg", ctypes.c_int32),
+                ("kbucket_wave", ctypes.c_int32), ("selftest_fail", ctypes.c_int32)]
+
+
+# Path overrides applied to every plan the Python wrappers create (tests select kernels with
+# plan_debug(); the library itself reads no environment variables).  Values: the rs_plan_debug
+# field choices, with names for the common ones ("ballot" / "atomic", "small" / "large").
+_DEBUG: dict = {}
+_DEBUG_NAMES = {"rank": {"atomic": 0, "lds_atomic": 0, "ballot": 1},
+                "tile": {"large": 0, "small": 1}}
+
+
+class plan_debug:
+    """Context manager: ``with plan_debug(rank="ballot", tile="small"): ...`` - every plan created
+    inside it gets rs_plan_set_debug with these fields."""
+
+    def __init__(self, **fields):
+        for k in fields:
+            if k not in dict(PlanDebug._fields_):
+                raise ValueError(f"unknown rs_plan_debug field {k!r}")
+        self.fields = fields
+        self.saved = None
+
+    def __enter__(self):
+        self.saved = dict(_DEBUG)
+        _DEBUG.update(self.fields)
+        return self
+
+    def __exit__(self, *exc):
+        _DEBUG.clear()
+        _DEBUG.update(self.saved)
+        return False
+
+
+def apply_debug(plan) -> None:
+    """rs_plan_set_debug(plan, the active plan_debug overrides) - a no-op when none are active."""
+    if not _DEBUG:
+        return
+    d = PlanDebug(*([-1] * len(PlanDebug._fields_)))
+    for k, v in _DEBUG.items():
+        if isinstance(v, str):
+            v = _DEBUG_NAMES[k][v]
+        setattr(d, k, int(v))
+    check(load().rs_plan_set_debug(plan, ctypes.byref(d)), "rs_plan_set_debug")
+
+
 RS_USAGE_SORT = 0
 RS_USAGE_PARTITION = 1
 RS_HIST16_WORDS = 65792
@@ -68,6 +117,13 @@ class GroupDesc(ctypes.Structure):
     _fields_ = [("capacity", ctypes.c_uint64), ("flags", ctypes.c_uint32),
                 ("transport", ctypes.c_uint32), ("top_bits", ctypes.c_uint32),
                 ("rounds", ctypes.c_uint32)]
+
+
+class GroupTimes(ctypes.Structure):
+    _fields_ = [("rounds", ctypes.c_uint32), ("hist16_ms", ctypes.c_float),
+                ("partition_ms", ctypes.c_float), ("round_done_ms", ctypes.c_float * 16),
+                ("region_sorted_ms", ctypes.c_float * 16), ("done_ms", ctypes.c_float),
+                ("bytes_sent", ctypes.c_uint64), ("bytes_recv", ctypes.c_uint64)]
 
 
 RS_TRANSPORT_RCCL = 0
@@ -106,6 +162,7 @@ _SIGS = {
     "rs_plan_device_errors": (ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_uint32)]),
     "rs_plan_check": (ctypes.c_int, [_VP]),
     "rs_plan_set_wait_limit": (ctypes.c_int, [_VP, ctypes.c_uint32]),
+    "rs_plan_set_debug": (ctypes.c_int, [_VP, ctypes.POINTER(PlanDebug)]),
     "rs_plan_destroy": (None, [_VP]),
     "rs_scan_plan_create": (ctypes.c_int, [ctypes.c_int32, ctypes.c_uint64, ctypes.c_uint32,
                                            ctypes.c_uint32, ctypes.c_uint32,
@@ -122,6 +179,8 @@ _SIGS = {
     "rs_group_result": (ctypes.c_int, [_VP, ctypes.c_int32, ctypes.POINTER(_VP),
                                        ctypes.POINTER(_VP), ctypes.POINTER(ctypes.c_uint64)]),
     "rs_group_synchronize": (ctypes.c_int, [_VP]),
+    "rs_group_set_profiling": (ctypes.c_int, [_VP, ctypes.c_int]),
+    "rs_group_times_get": (ctypes.c_int, [_VP, ctypes.c_int32, ctypes.POINTER(GroupTimes)]),
     "rs_group_destroy": (None, [_VP]),
     "rs_group_plan": (ctypes.c_int, [ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint32,
                                      ctypes.POINTER(ctypes.c_uint64),

@@ -170,11 +170,120 @@ class ExchangeResult:
     recv_sizes: list
 
 
+class StepTimeline:
+    """Where one multi-GPU step's time goes on this rank (GPU events; the diagnostics of the N-rank
+    bench line): marks after the 16-bit table, the table all_gather and the
+    partition, the moment each exchange round has landed (an event on a watch stream that waits
+    for that round's messages only) and the end of each round's region sort; the off-GPU bytes
+    this rank sent and received.  `exchange_only`: post the rounds with no region sorts (the
+    exchange's own time E, nothing competing)."""
+
+    def __init__(self, exchange_only: bool = False):
+        self.exchange_only = exchange_only
+        self.marks = []          # (name, torch.cuda.Event)
+        self.bytes_sent = 0      # off-rank message bytes (own chunks are local copies)
+        self.bytes_recv = 0
+        self._watch = None
+
+    def mark(self, name: str, stream=None) -> None:
+        import torch
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record(stream)
+        self.marks.append((name, ev))
+
+    def landed(self, g: int, works, device) -> None:
+        """Event when round g's messages have arrived (waits for those works only)."""
+        import torch
+        if self._watch is None:
+            self._watch = torch.cuda.Stream(device)
+        self._watch.wait_stream(torch.cuda.current_stream(device))
+        with torch.cuda.stream(self._watch):
+            for w in works:
+                w.wait()
+            self.mark(f"landed{g}", self._watch)
+
+    def ms(self) -> dict:
+        """{mark: ms since the step's first mark} (synchronises)."""
+        if not self.marks:
+            return {}
+        t0 = self.marks[0][1]
+        t0.synchronize()
+        out = {}
+        for name, ev in self.marks:
+            ev.synchronize()
+            out[name] = t0.elapsed_time(ev)
+        return out
+
+
+# the per-rank record gathered to rank 0: a fixed layout of floats (all_gather of one tensor)
+def timeline_record(tl: StepTimeline, rounds: int, first_key: int, last_key: int, n_recv: int,
+                    kernel_ms: list, exchange_only_ms: float) -> list:
+    m = tl.ms()
+    row = [m.get("hist16", 0.0), m.get("gather", 0.0), m.get("partition", 0.0)]
+    row += [m.get(f"landed{g}", 0.0) for g in range(rounds)]
+    row += [m.get(f"sorted{g}", 0.0) for g in range(rounds)]
+    row += [float(tl.bytes_sent), float(tl.bytes_recv), float(first_key), float(last_key), float(n_recv),
+            float(exchange_only_ms)]
+    row += [float(x) for x in kernel_ms]
+    return row
+
+
+def summarize_timelines(rows: list, rounds: int, kernel_names) -> dict:
+    """The N-rank bench line's breakdown from every rank's timeline_record (pure: CPU-tested).
+    Times are ms since each rank's step start; the step's time is its slowest rank's."""
+    G = rounds
+    per = []
+    for r in rows:
+        d = {"hist16": r[0], "gather": r[1], "partition": r[2],
+             "landed": list(r[3:3 + G]), "sorted": list(r[3 + G:3 + 2 * G])}
+        (d["bytes_sent"], d["bytes_recv"], d["first_key"], d["last_key"], d["n_recv"],
+         d["exchange_only_ms"]) = r[3 + 2 * G:9 + 2 * G]
+        d["kernel_ms"] = dict(zip(kernel_names, r[9 + 2 * G:]))
+        per.append(d)
+
+    def mx(f):
+        return round(max(f(d) for d in per), 4)
+
+    E = [d["landed"][-1] - d["partition"] for d in per]
+    xg = [(d["bytes_sent"] + d["bytes_recv"]) / (e / 1e3) / 1e9 if e > 0 else 0.0 for d, e in zip(per, E)]
+    eo = [d["exchange_only_ms"] for d in per]
+    xo = [(d["bytes_sent"] + d["bytes_recv"]) / (e / 1e3) / 1e9 if e > 0 else 0.0 for d, e in zip(per, eo)]
+    # rank edges of the global order: the last key of every non-empty rank <= the first key of the
+    # next non-empty one (keys are the u32 bit patterns, gathered as floats: exact below 2^53)
+    nonempty = [d for d in per if d["n_recv"] > 0]
+    edges_ok = all(a["last_key"] <= b["first_key"] for a, b in zip(nonempty, nonempty[1:]))
+    return {
+        "ranks": len(per),
+        "step_ms_max_over_ranks": mx(lambda d: d["sorted"][-1] if G else d["partition"]),
+        "local_ms_max_over_ranks": {
+            "hist16": mx(lambda d: d["hist16"]),
+            "table_all_gather": mx(lambda d: d["gather"] - d["hist16"]),
+            "partition": mx(lambda d: d["partition"] - d["gather"]),
+            "after_last_round_landed": mx(lambda d: d["sorted"][-1] - d["landed"][-1]),
+        },
+        "exchange": {
+            "rounds": G,
+            "landed_ms_after_partition_max": [round(max(d["landed"][g] - d["partition"] for d in per), 4)
+                                              for g in range(G)],
+            "E_ms_max": round(max(E), 4),
+            "xgmi_GBs_per_rank_min": round(min(xg), 1),
+            "xgmi_GBs_per_rank_max": round(max(xg), 1),
+            "exchange_only_ms_max": round(max(eo), 4),
+            "exchange_only_xgmi_GBs_per_rank_min": round(min(xo), 1),
+            "bytes_off_gpu_per_rank_max": int(max(d["bytes_sent"] + d["bytes_recv"] for d in per)),
+        },
+        "kernel_ms_max_over_ranks": {k: round(max(d["kernel_ms"][k] for d in per), 4) for k in kernel_names},
+        "recv_keys_min_max": [int(min(d["n_recv"] for d in per)), int(max(d["n_recv"] for d in per))],
+        "rank_edges_sorted": bool(edges_ok),
+    }
+
+
 def distributed_sort(keys, values, ops: LocalOps, group=None, bits: int = 8,
-                     chunks: int = 4) -> ExchangeResult:
+                     chunks: int = 4, timeline: StepTimeline | None = None) -> ExchangeResult:
     """Sort the global array whose slice on this rank is (keys, values); returns this rank's
     slice of the global stable sorted order (rank-ordered concatenation).  `chunks` = exchange
     rounds (bucket groups per rank), each sorted while the next ones are on the wire.
+    `timeline` (GPU only): record where the step's time goes (StepTimeline).
 
     On the GPU the work runs on a side stream (ordered after the caller's current stream, and
     the caller's stream after it): the legacy default stream would serialise every local sort
@@ -186,7 +295,7 @@ def distributed_sort(keys, values, ops: LocalOps, group=None, bits: int = 8,
         side = _side_stream(keys.device)
         side.wait_stream(caller)
         with torch.cuda.stream(side):
-            r = _distributed_sort(keys, values, ops, group, bits, chunks)
+            r = _distributed_sort(keys, values, ops, group, bits, chunks, timeline)
         caller.wait_stream(side)
         for t in (r.keys, r.values):
             if t is not None:
@@ -258,9 +367,13 @@ def exchange_round(send, recv, plan: GroupPlan, g: int, rank: int, world: int, g
     return dist.batch_isend_irecv(p2p) if p2p else []
 
 
-def _distributed_sort(keys, values, ops, group, bits, chunks) -> ExchangeResult:
+def _distributed_sort(keys, values, ops, group, bits, chunks, timeline=None) -> ExchangeResult:
     import torch
     import torch.distributed as dist
+
+    tl = timeline if (timeline is not None and keys.is_cuda) else None
+    if tl is not None:
+        tl.mark("start")
 
     if bits != 8:
         raise ValueError("the exchange digit is the top byte (bits=8): the sort's first MSD pass")
@@ -277,7 +390,11 @@ def _distributed_sort(keys, values, ops, group, bits, chunks) -> ExchangeResult:
     G = max(1, int(chunks))
     shift = 32 - bits
     h16 = ops.hist16(keys)                                      # [HIST16_WORDS]
+    if tl is not None:
+        tl.mark("hist16")
     table = all_gather_tables(h16, world, group)                # [world, HIST16_WORDS]
+    if tl is not None:
+        tl.mark("gather")
     tops = table[:, 65536:]
     totals = h16[65536:]
     if keys.is_cuda:
@@ -288,6 +405,8 @@ def _distributed_sort(keys, values, ops, group, bits, chunks) -> ExchangeResult:
         ready = torch.cuda.Event()
         ready.record()
         send = ops.partition(keys, values, shift, bits, totals)
+        if tl is not None:
+            tl.mark("partition")
         ready.synchronize()
         hist_all = hcpu.tolist()
     else:
@@ -299,6 +418,18 @@ def _distributed_sort(keys, values, ops, group, bits, chunks) -> ExchangeResult:
     n_recv = plan.base[G]
     recv = ops.empty(n_recv, send)
     rounds = [exchange_round(send, recv, plan, g, rank, world, group) for g in range(G)]
+    if tl is not None:
+        rec = send.element_size()
+        tl.bytes_sent = rec * sum(b - a for g in range(G) for q, a, b in plan.send[g] if q != rank)
+        tl.bytes_recv = rec * sum(m for g in range(G) for s, _, m in plan.recv[g] if s != rank)
+        for g in range(G):
+            tl.landed(g, rounds[g], keys.device)
+        if tl.exchange_only:
+            for g in range(G):
+                for w in rounds[g]:
+                    w.wait()
+            send_sizes, recv_sizes = split_sizes(hist_all, bounds, rank, world)
+            return ExchangeResult(recv, None, n_recv, send_sizes, recv_sizes)
     if values is None:
         out_k, out_v, tot16 = recv, None, None
     else:
@@ -319,6 +450,8 @@ def _distributed_sort(keys, values, ops, group, bits, chunks) -> ExchangeResult:
                 reg = torch.zeros_like(tot16)
                 reg[t0 << 8:t1 << 8] = tot16[t0 << 8:t1 << 8]
                 ops.sort_region(recv[a:b], out_k[a:b], out_v[a:b], reg, t0, t1)
+        if tl is not None:
+            tl.mark(f"sorted{g}")
     send_sizes, recv_sizes = split_sizes(hist_all, bounds, rank, world)
     return ExchangeResult(out_k, out_v, n_recv, send_sizes, recv_sizes)
 

@@ -75,6 +75,20 @@ class RadixSortGroup:
     def synchronize(self) -> None:
         check(_lib.load().rs_group_synchronize(self._g), "rs_group_synchronize")
 
+    def set_profiling(self, enable: bool) -> None:
+        """Timing events on every rank from the next sort on (rs_group_set_profiling)."""
+        check(_lib.load().rs_group_set_profiling(self._g, 1 if enable else 0), "rs_group_set_profiling")
+
+    def times(self, rank: int) -> dict:
+        """Where rank's last sort spent its time (rs_group_times_get; waits for it): ms since the
+        sort's start, and the rank's off-rank exchange bytes."""
+        t = _lib.GroupTimes()
+        check(_lib.load().rs_group_times_get(self._g, rank, ctypes.byref(t)), "rs_group_times_get")
+        G = t.rounds
+        return {"rounds": G, "hist16_ms": t.hist16_ms, "partition_ms": t.partition_ms,
+                "round_done_ms": list(t.round_done_ms[:G]), "region_sorted_ms": list(t.region_sorted_ms[:G]),
+                "done_ms": t.done_ms, "bytes_sent": t.bytes_sent, "bytes_recv": t.bytes_recv}
+
     def sort(self, keys, values=None, counts=None):
         """Sort and return [(keys_r, values_r or None)] as new int32 tensors on devices[r]
         (copied out of the group's buffers)."""

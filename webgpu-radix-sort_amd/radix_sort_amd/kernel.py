@@ -204,6 +204,7 @@ class RadixSortKernel:
         plan = ctypes.c_void_p()
         check(L.rs_plan_create(ctypes.byref(desc), ctypes.byref(plan)), "RadixSortKernel")
         self._plan = plan
+        _lib.apply_debug(plan)
 
     # -- reference surface --------------------------------------------------------------------
     def dispatch(self, pass_=None) -> None:
@@ -333,6 +334,7 @@ class RadixSortTextureKernel(RadixSortKernel):
         check(_lib.load().rs_plan_create(ctypes.byref(desc), ctypes.byref(plan)),
               "RadixSortTextureKernel")
         self._plan = plan
+        _lib.apply_debug(plan)
 
 
 class PrefixSumKernel:

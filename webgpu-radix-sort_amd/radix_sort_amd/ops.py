@@ -56,6 +56,7 @@ class SortPlan:
         p = ctypes.c_void_p()
         check(_lib.load().rs_plan_create(ctypes.byref(desc), ctypes.byref(p)), "SortPlan")
         self._plan = p
+        _lib.apply_debug(p)
         self.capacity = capacity
         self.has_values = has_values
 

@@ -57,7 +57,77 @@ WORKLOADS = {
     "config3_texture": dict(n=1 << 28, values=True, local_shuffle=False, check_order=False,
                             kind="u32", seed=3, layout="aos",
                             desc="256M (Uint32 key, Uint32 value) texels, RadixSortTextureKernel"),
+    # the exported PrefixSumKernel (src/index.ts:3, PrefixSumKernel.ts:11-159) on its own
+    "prefix_sum": dict(n=1 << 28, values=False, local_shuffle=False, check_order=False, kind="scan",
+                       seed=6, desc="PrefixSumKernel: in-place exclusive scan of 256M u32 (single pass)"),
 }
+
+
+def bench_prefix_sum(args, wl, torch, json_out) -> None:
+    """--workload prefix_sum: K in-place exclusive scans of pre-generated 2^28 u32 batches (small
+    values: the reference test's data, example/tests.ts:135), timed wall-clock around all K and with
+    HIP events around each launch; roofline at 8 B/element (one read + one write); CPU baseline: the
+    reference's prefixSumCpu loop restated in numpy (example/tests.ts:288-296), 1 core, 2^26 sample."""
+    import numpy as np
+    from radix_sort_amd import PrefixSumKernel, ops
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    n = args.keys_per_gpu or wl["n"]
+    K, W = args.steps, args.warmup
+    dev = torch.device("cuda", 0)
+
+    def make(seed):
+        t = torch.empty(n, dtype=torch.int32, device=dev)
+        ops.fill_random_u32(t, seed)
+        t &= 7                                   # floor(random * 8), as the reference's test data
+        return t
+    batches = [make(wl["seed"] + i) for i in range(K)]
+    warm = make(wl["seed"] + 1000)
+    kw = PrefixSumKernel(data=warm, count=n)
+    for _ in range(W):
+        kw.dispatch()
+    kernels = [PrefixSumKernel(data=b, count=n) for b in batches]
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+    t0 = time.perf_counter()
+    for i in range(K):
+        ev[i][0].record()
+        kernels[i].dispatch()
+        ev[i][1].record()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    for k in kernels:
+        k.check()
+    kms = sum(a.elapsed_time(b) for a, b in ev) / K
+    # the last batch against the numpy restatement of prefixSumCpu
+    src = make(wl["seed"] + K - 1).cpu().numpy().view(np.uint32)
+    got = batches[-1].cpu().numpy().view(np.uint32)
+    if not (got == O.prefix_sum(src, n)).all():
+        raise SystemExit("bench: prefix sum differs from the reference's CPU scan")
+    value = n * K / elapsed / 1e9
+    achieved = n * 8 / (kms / 1e3) / 1e9
+    cpu = None
+    if not args.no_cpu_baseline:
+        m = 1 << 26
+        d = src[:m].copy()
+        t = time.perf_counter()
+        O.prefix_sum(d, m)
+        dt = time.perf_counter() - t
+        cpu = {"value": m / dt / 1e9, "unit": "Gelements/s", "cores": 1, "kind": "port",
+               "sample": f"2^26 u32, numpy cumsum restatement of prefixSumCpu (example/tests.ts:288-296), 1 thread; {dt:.3f} s"}
+    out = {"metric": "Gelements/s exclusive prefix sum (u32), PrefixSumKernel; % HBM roofline",
+           "value": round(value, 4), "unit": "Gelements/s", "n_gpus": 1, "steps": K, "warmup": W,
+           "ms_per_step": round(elapsed / K * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+           "vs_baseline": None, "dtype": "u32",
+           "data": "synthetic (splitmix64 counter generator, values in [0, 8))",
+           "config": {"workload": "prefix_sum", "description": wl["desc"], "elements": n},
+           "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                        "kernel": "k_scan_lookback (single pass, decoupled look-back)",
+                        "avg_launch_ms": round(kms, 4), "algorithmic_bytes_per_launch": n * 8,
+                        "lib_sha16": _lib_sha16()},
+           "cpu_baseline": cpu}
+    print(json.dumps(out), file=json_out, flush=True)
 
 
 def log(*a):
@@ -310,6 +380,12 @@ def main() -> None:
 
     import torch
     import torch.distributed as dist
+    if WORKLOADS[args.workload]["kind"] == "scan":
+        if args.gpus != 1:
+            raise SystemExit("bench: the prefix_sum workload runs on one GPU")
+        torch.cuda.set_device(0)
+        bench_prefix_sum(args, WORKLOADS[args.workload], torch, json_out)
+        return
     from radix_sort_amd import RadixSortKernel, RadixSortTextureKernel, ops
     from radix_sort_amd.distributed import (HipLocalOps, StepTimeline, distributed_sort,
                                             summarize_timelines, timeline_record)

@@ -234,6 +234,13 @@ rs_status rs_scan_plan_create(int32_t device, uint64_t count, uint32_t workgroup
                               uint32_t workgroup_y, uint32_t flags, rs_scan_plan** out);
 /* In-place exclusive scan (mod 2^32) of data[0..count); data[count..] untouched. */
 rs_status rs_scan_plan_run(rs_scan_plan* plan, void* data, void* stream);
+/* The scan is one pass (one read and one write of the data: tiles in order, each adding its
+ * predecessors' sums found by a bounded look-back).  rs_scan_plan_check waits for the plan's last
+ * scan and returns RS_ERR_DEVICE (once) if a look-back wait of a scan since the last check timed
+ * out (that scan's output is invalid); rs_scan_plan_set_wait_limit bounds the waits (s_sleep
+ * periods, default 2^20; 0: any wait on an unpublished predecessor times out - tests). */
+rs_status rs_scan_plan_check(rs_scan_plan* plan);
+rs_status rs_scan_plan_set_wait_limit(rs_scan_plan* plan, uint32_t sleeps);
 /* PrefixSumKernel.dispatch(pass, dispatchSizeBuffer, offset) (PrefixSumKernel.ts:147-158): the
  * scan as above, gated on the device: dispatch_size_buffer (device memory) holds u32 (x, y, z)
  * workgroup triples from byte `offset`, one per pipeline of rs_scan_plan_dispatch_chain; the scan

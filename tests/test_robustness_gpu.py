@@ -157,3 +157,51 @@ def test_prefix_sum_indirect_dispatch():
     k2 = PrefixSumKernel(data=d2, count=n)
     k2.dispatch(None, zero, 0)
     assert (_np(d2) == data).all()
+
+
+def test_scan_lookback_timeout_is_reported_then_plan_recovers():
+    """The single-pass PrefixSumKernel: with the wait bound at 0 a look-back wait on an unpublished
+    predecessor times out, check() reports it once (RS_ERR_DEVICE); with the default bound the same
+    plan scans correctly again."""
+    from radix_sort_amd import PrefixSumKernel, RadixSortError, _lib
+    n = (1 << 26) + 5
+    d = O.gen_u32(91, n) & np.uint32(0xFF)
+    t = _t(d)
+    k = PrefixSumKernel(data=t, count=n)
+    L = _lib.load()
+    _lib.check(L.rs_scan_plan_set_wait_limit(k._plan, 0), "wait limit")
+    seen = 0
+    for _ in range(4):
+        t.copy_(_t(d))
+        k.dispatch()
+        try:
+            k.check()
+        except RadixSortError as e:
+            assert e.status == _lib.RS_ERR_DEVICE and "timed out" in str(e)
+            seen += 1
+    assert seen >= 1, "no look-back wait ever found an unpublished predecessor"
+    k.check()
+    _lib.check(L.rs_scan_plan_set_wait_limit(k._plan, 1 << 20), "wait limit")
+    t.copy_(_t(d))
+    k.dispatch()
+    k.check()
+    assert (_np(t) == O.prefix_sum(d, n)).all()
+    k.destroy()
+
+
+@pytest.mark.parametrize("n,offset", [(1, 0), (4095, 0), (4096, 1), (4097, 3), (1_000_003, 1), ((1 << 24) + 7, 0)])
+def test_scan_sizes_and_unaligned_data(n, offset):
+    """Tile edges of the single-pass scan (4096-element tiles), one element, and data that is not
+    16-byte aligned (scalar loads / stores); the words after count are untouched."""
+    from radix_sort_amd import PrefixSumKernel
+    d = O.gen_u32(n + 17, n + offset + 8)
+    t = _t(d)
+    view = t[offset:offset + n + 8]
+    k = PrefixSumKernel(data=view, count=n)
+    k.dispatch()
+    k.check()
+    out = _np(t)
+    assert (out[:offset] == d[:offset]).all()
+    assert (out[offset:offset + n] == O.prefix_sum(d[offset:offset + n], n)).all()
+    assert (out[offset + n:] == d[offset + n:]).all()
+    k.destroy()

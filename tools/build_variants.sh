@@ -5,8 +5,8 @@
 set -e
 cd "$(dirname "$0")/../webgpu-radix-sort_amd/csrc"
 make -s ../build/rs_group.o
-mkdir -p ../lib/variants
+OUTD=${OUTD:-../lib/variants}; mkdir -p $OUTD
 for v in "$@"; do
   name=${v%%:*}; defs=${v#*:}; defs=${defs//,/ }
-  echo "/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -Wall -fvisibility=hidden --offload-arch=gfx950 $defs -shared -o ../lib/variants/librsort_$name.so rsort.hip -Wl,$PWD/../build/rs_group.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib"
+  echo "/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -Wall -fvisibility=hidden --offload-arch=gfx950 $defs -shared -o $OUTD/librsort_$name.so rsort.hip -Wl,$PWD/../build/rs_group.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib"
 done | xargs -P 6 -I{} bash -c "{}"

@@ -1716,6 +1716,12 @@ __global__ __launch_bounds__(256) void k_msd_plan(const uint32_t* __restrict__ t
 // is then a key array, R2 the caller's keys).
 // PF = 1: the next bucket's keys are loaded before the current bucket is sorted (a persistent grid;
 // keys only, where a bucket is a few KB and a workgroup's load latency is not hidden otherwise).
+#ifndef RS_BUCKET_PACK
+#define RS_BUCKET_PACK 0     // 1: k_bucket_sort keeps its ranks as 16-bit pairs (VGPRs)
+#endif
+#ifndef RS_BUCKET_MW
+#define RS_BUCKET_MW 3       // k_bucket_sort tiles of <= 18 records per thread: workgroups per CU
+#endif
 template <int BLOCK, int KPT, int RANK, int LO = LAYOUT_SOA, int MW = 1, int PF = 0>
 __global__ __launch_bounds__(BLOCK, MW) void k_bucket_sort(const uint32_t* rec,
                                                        const uint32_t* __restrict__ hist16,
@@ -1782,7 +1788,7 @@ __global__ __launch_bounds__(BLOCK, MW) void k_bucket_sort(const uint32_t* rec,
         if (cnt > 1u) {
             for (uint32_t p = 0, shift = 0; p < 2u; ++p, shift += 8u) {
                 const uint32_t mask = 255u;
-                Slots<KPT, false> rank;
+                Slots<KPT, RS_BUCKET_PACK != 0> rank;
                 uint32_t c;   // pads included (kPadKey: digit 255, after every real key)
                 const uint32_t tstart = rank_tile<R, NW, KPT, RANK>(k, rank, s_whist, s_scratch, shift, mask, 0u, c);
                 if (tid < (uint32_t)RADIX) set_wave_offsets<R, NW>(s_whist, tstart);
@@ -2187,6 +2193,121 @@ __global__ __launch_bounds__(kBlock) void k_scan_small(uint32_t* __restrict__ a,
             a[b0 + k] = run;
             run += c;
         }
+}
+
+// Single-pass exclusive scan (the PrefixSumKernel export, PrefixSumKernel.ts:11-159): one read and
+// one write of the data (8 B/element; the reduce-then-scan above reads it twice, 12 B/element).
+// Tiles of BLOCK x EPT elements come from a ticket counter in order; every thread scans EPT
+// CONTIGUOUS elements in registers, the workgroup scans the thread totals (wave scan + one LDS
+// exchange), publishes the tile's aggregate, and one wave looks back over up to 64 predecessors
+// per step (status words as k_onesweep's: ((epoch << 2 | flag) << 32) | value, agent-scope relaxed
+// 64-bit atomics, so flag and value travel together; the epoch tags this launch's words, so the
+// region is never cleared).  Waits are bounded like k_onesweep's (err[0] on a timeout).
+// tickets: a ring of kScanTickets counters; launch e uses tickets[e % ring] and clears the next
+// launch's.  VEC: the data is 16-byte aligned (4 x 16-byte loads / stores per thread).
+constexpr uint32_t kScanTickets = 64;
+template <int BLOCK, int EPT, bool VEC>
+__global__ __launch_bounds__(BLOCK) void k_scan_lookback(uint32_t* __restrict__ data, uint32_t n,
+                                                         unsigned long long* status, uint32_t* tickets,
+                                                         uint32_t epoch, uint32_t* err, uint32_t spin_max,
+                                                         const uint32_t* ind) {
+    static_assert(EPT % 4 == 0, "whole 16-byte vectors per thread");
+    constexpr int NW = BLOCK / 64;
+    constexpr uint32_t TILE = (uint32_t)BLOCK * EPT;
+    __shared__ uint32_t s_wave[NW];
+    __shared__ uint32_t s_t, s_prefix;
+    if (indirect_off(ind)) return;
+    const uint32_t tid = threadIdx.x, w = tid >> 6, lane = lane_id();
+    uint32_t* ticket = tickets + epoch % kScanTickets;
+    if (blockIdx.x == 0 && tid == 0) tickets[(epoch + 1) % kScanTickets] = 0u;   // the next launch's
+    const uint32_t ntiles = (uint32_t)(((uint64_t)n + TILE - 1) / TILE);
+    for (;;) {
+        if (tid == 0) s_t = atomicAdd(ticket, 1u);
+        __syncthreads();
+        const uint32_t T = s_t;
+        if (T >= ntiles) break;
+        const uint64_t base = (uint64_t)T * TILE + (uint64_t)tid * EPT;
+        const bool full = (uint64_t)T * TILE + TILE <= n;
+        uint32_t x[EPT];
+        if (VEC && full) {
+            const uint4* p = reinterpret_cast<const uint4*>(data + base);
+#pragma unroll
+            for (int j = 0; j < EPT / 4; ++j) {
+                const uint4 q = p[j];
+                x[4 * j] = q.x; x[4 * j + 1] = q.y; x[4 * j + 2] = q.z; x[4 * j + 3] = q.w;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < EPT; ++j) x[j] = base + j < n ? data[base + j] : 0u;
+        }
+        // thread-local exclusive scan (x becomes the exclusive prefix inside the thread)
+        uint32_t run = 0;
+#pragma unroll
+        for (int j = 0; j < EPT; ++j) { const uint32_t v = x[j]; x[j] = run; run += v; }
+        // workgroup exclusive scan of the thread totals
+        const uint32_t inc = wave_incl_scan(run);
+        if (lane == 63) s_wave[w] = inc;
+        __syncthreads();
+        uint32_t wpre = 0, agg = 0;
+#pragma unroll
+        for (int i = 0; i < NW; ++i) {
+            const uint32_t s = s_wave[i];
+            wpre += (i < (int)w) ? s : 0u;
+            agg += s;
+        }
+        const uint32_t texcl = wpre + inc - run;
+        // publish, then look back (wave 0): lane i reads predecessor T - 1 - i
+        if (w == 0) {
+            uint32_t prefix = 0;
+            if (T == 0) {
+                if (lane == 0) st_store(status, (epoch << 2) | kStInclusive, agg);
+            } else {
+                if (lane == 0) st_store(status + T, (epoch << 2) | kStAggregate, agg);
+                int64_t j = (int64_t)T - 1;   // predecessor read by lane 0 this step
+                uint32_t spins = 0;
+                for (;;) {
+                    const int64_t me = j - (int64_t)lane;
+                    const unsigned long long sv = me >= 0 ? st_load(status + me)
+                                                          : (((unsigned long long)((epoch << 2) | kStInclusive)) << 32);
+                    const uint32_t f = (uint32_t)(sv >> 32);
+                    const bool pub = (f >> 2) == epoch;
+                    const bool incl = pub && (f & 3u) == kStInclusive;
+                    const uint64_t unpub = __ballot(!pub), inclm = __ballot(incl);
+                    // the first inclusive word, and no unpublished word before it
+                    const uint32_t stop = inclm ? (uint32_t)__builtin_ctzll(inclm) : 64u;
+                    const uint64_t before = stop >= 64u ? ~0ull : ((2ull << stop) - 1ull);
+                    if ((unpub & before) == 0ull) {
+                        uint32_t v = lane <= stop ? (uint32_t)sv : 0u;
+                        prefix += wave_sum(v);
+                        if (stop < 64u) break;
+                        j -= 64;
+                        continue;
+                    }
+                    if (++spins > spin_max ||
+                        ((spins & 255u) == 0u && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+                        if (lane == 0) atomicOr(err, 1u);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+                if (lane == 0) st_store(status + T, (epoch << 2) | kStInclusive, prefix + agg);
+            }
+            if (lane == 0) s_prefix = prefix;
+        }
+        __syncthreads();
+        const uint32_t add = s_prefix + texcl;
+        if (VEC && full) {
+            uint4* p = reinterpret_cast<uint4*>(data + base);
+#pragma unroll
+            for (int j = 0; j < EPT / 4; ++j)
+                p[j] = make_uint4(x[4 * j] + add, x[4 * j + 1] + add, x[4 * j + 2] + add, x[4 * j + 3] + add);
+        } else {
+#pragma unroll
+            for (int j = 0; j < EPT; ++j)
+                if (base + j < n) data[base + j] = x[j] + add;
+        }
+        // s_t / s_wave / s_prefix are rewritten next tile only after the next barrier
+    }
 }
 
 // ---- self-test of the lane-ordered LDS atomics that RANK_LDS_ATOMIC relies on ----------------

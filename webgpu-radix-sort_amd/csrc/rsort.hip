@@ -289,7 +289,15 @@ struct rs_scan_plan {
     int device = 0;
     uint64_t count = 0;
     uint32_t threads = 256;       // workgroup_x * workgroup_y (reference dispatch-chain shape)
-    uint32_t* sums = nullptr;     // [kScanMaxGrid]
+    uint32_t* sums = nullptr;     // [kScanMaxGrid] (reduce-then-scan form, sweep builds)
+    // single-pass form (k_scan_lookback): status word per tile, ticket ring, device error word
+    unsigned long long* status = nullptr;
+    uint64_t status_words = 0;
+    uint32_t* tickets = nullptr;  // [kScanTickets] tickets, then [1] error word
+    uint32_t epoch = 0;
+    uint32_t grid = 0;
+    uint32_t spin_max = 1u << 20;
+    hipEvent_t done = nullptr;    // recorded after every run (rs_scan_plan_check waits for it)
 };
 
 namespace {
@@ -1117,7 +1125,7 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
         };
         auto both = [&](auto lo) {
             constexpr int LO = decltype(lo)::value;
-#define RS_BK(KP) case KP: ballot ? small(rs::k_bucket_sort<bb, KP, B0, LO, (KP <= 18 ? 3 : (KP == 34 ? 2 : 1))>) : small(rs::k_bucket_sort<bb, KP, A0, LO, (KP <= 18 ? 3 : (KP == 34 ? 2 : 1))>); break;
+#define RS_BK(KP) case KP: ballot ? small(rs::k_bucket_sort<bb, KP, B0, LO, (KP <= 18 ? RS_BUCKET_MW : (KP == 34 ? 2 : 1))>) : small(rs::k_bucket_sort<bb, KP, A0, LO, (KP <= 18 ? RS_BUCKET_MW : (KP == 34 ? 2 : 1))>); break;
             if constexpr (LO == K) {
                 bool wave_done = false;
 #if RS_SWEEP
@@ -1829,6 +1837,9 @@ RS_EXPORT rs_status rs_plan_reset_kernel_times(rs_plan* p) {
 namespace {
 constexpr int kScanTile = 4096;
 constexpr uint32_t kScanMaxGrid = 1024;
+// single-pass scan: 256 threads x 16 contiguous elements = 4096-element tiles, 8 workgroups per CU
+constexpr int kScanBlock = 256, kScanEpt = 16;
+constexpr uint32_t kScanLbTile = kScanBlock * kScanEpt;
 struct Geometry { uint32_t grid, base, extra; };
 Geometry geometry(uint64_t n, uint32_t tile, uint32_t max_grid) {
     const uint64_t tiles = (n + tile - 1) / tile;
@@ -1860,9 +1871,22 @@ RS_EXPORT rs_status rs_scan_plan_create(int32_t device, uint64_t count, uint32_t
     p->count = count;
     p->threads = (uint32_t)T;
     DeviceGuard guard(device);
+    p->status_words = std::max<uint64_t>(1, (count + kScanLbTile - 1) / kScanLbTile);
+    int cus = 256;
+    {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+            cus = prop.multiProcessorCount;
+    }
+    p->grid = (uint32_t)std::min<uint64_t>(p->status_words, 8ull * cus);
     hipError_t e = hipMalloc((void**)&p->sums, 4ull * kScanMaxGrid);
+    if (e == hipSuccess) e = hipMalloc((void**)&p->status, 8ull * p->status_words);
+    if (e == hipSuccess) e = hipMalloc((void**)&p->tickets, 4ull * (rs::kScanTickets + 1));
+    if (e == hipSuccess) e = hipMemset(p->status, 0, 8ull * p->status_words);
+    if (e == hipSuccess) e = hipMemset(p->tickets, 0, 4ull * (rs::kScanTickets + 1));
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&p->done, hipEventDisableTiming);
     if (e != hipSuccess) {
-        delete p;
+        rs_scan_plan_destroy(p);
         return fail(RS_ERR_OUT_OF_MEMORY, "rs_scan_plan_create: %s", hipGetErrorString(e));
     }
     *out = p;
@@ -1871,6 +1895,24 @@ RS_EXPORT rs_status rs_scan_plan_create(int32_t device, uint64_t count, uint32_t
 
 static rs_status scan_run(rs_scan_plan* p, void* data, const uint32_t* ind, hipStream_t s) {
     const uint64_t n = p->count;
+    if (RS_KNOB("RSORT_SCAN_3K", 0) == 0) {
+        // single pass: a new tag for this launch's status words (cleared when the tags wrap)
+        if (++p->epoch >= (1u << 30)) {
+            HIP_TRY(hipMemsetAsync(p->status, 0, 8ull * p->status_words, s));
+            HIP_TRY(hipMemsetAsync(p->tickets, 0, 4ull * rs::kScanTickets, s));
+            p->epoch = 1;
+        }
+        const bool vec = ((uintptr_t)data & 15u) == 0;
+        auto go = [&](auto kern) {
+            hipLaunchKernelGGL(kern, dim3(p->grid), dim3(kScanBlock), 0, s, (uint32_t*)data, (uint32_t)n,
+                               p->status, p->tickets, p->epoch, p->tickets + rs::kScanTickets, p->spin_max, ind);
+        };
+        if (vec) go(rs::k_scan_lookback<kScanBlock, kScanEpt, true>);
+        else go(rs::k_scan_lookback<kScanBlock, kScanEpt, false>);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(p->done, s));
+        return RS_OK;
+    }
     const Geometry geo = geometry(n, kScanTile, kScanMaxGrid);
     hipLaunchKernelGGL(rs::k_chunk_sums<kScanTile>, dim3(geo.grid), dim3(rs::kBlock), 0, s,
                        (const uint32_t*)data, (uint32_t)n, geo.base, geo.extra, p->sums, ind);
@@ -1935,10 +1977,32 @@ RS_EXPORT uint32_t rs_scan_plan_dispatch_chain(const rs_scan_plan* p, uint32_t* 
     return (uint32_t)chain.size();
 }
 
+RS_EXPORT rs_status rs_scan_plan_check(rs_scan_plan* p) {
+    if (!p) return fail(RS_ERR_INVALID_ARG, "rs_scan_plan_check: null plan");
+    DeviceGuard guard(p->device);
+    if (!p->tickets || !p->done) return RS_OK;
+    HIP_TRY(hipEventSynchronize(p->done));
+    uint32_t e = 0;
+    HIP_TRY(hipMemcpy(&e, p->tickets + rs::kScanTickets, 4, hipMemcpyDeviceToHost));
+    if (!e) return RS_OK;
+    HIP_TRY(hipMemset(p->tickets + rs::kScanTickets, 0, 4));
+    return fail(RS_ERR_DEVICE, "rs_scan_plan_check: a look-back wait of an earlier scan on this plan timed out; "
+                "that scan's output is invalid");
+}
+
+RS_EXPORT rs_status rs_scan_plan_set_wait_limit(rs_scan_plan* p, uint32_t sleeps) {
+    if (!p) return fail(RS_ERR_INVALID_ARG, "rs_scan_plan_set_wait_limit: null plan");
+    p->spin_max = sleeps;
+    return RS_OK;
+}
+
 RS_EXPORT void rs_scan_plan_destroy(rs_scan_plan* p) {
     if (!p) return;
     DeviceGuard guard(p->device);
+    if (p->done) (void)hipEventDestroy(p->done);
     (void)hipFree(p->sums);
+    (void)hipFree(p->status);
+    (void)hipFree(p->tickets);
     delete p;
 }
 

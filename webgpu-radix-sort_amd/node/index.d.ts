@@ -146,6 +146,8 @@ export declare class PrefixSumKernel {
   /** Indirect when dispatchSizeBuffer is given (PrefixSumKernel.ts:147-158). */
   dispatch(pass?: ComputePass, dispatchSizeBuffer?: DeviceBuffer, offset?: number): void;
   getDispatchChain(): number[];
+  /** Throws if a scan since the last check failed on the device (timed-out look-back wait). */
+  check(): void;
   destroy(): void;
 }
 
@@ -177,6 +179,11 @@ export declare class RadixSortGroup {
   readonly hasValues: boolean;
   sort(slices: Array<{ keys: DeviceBuffer | GroupBuffer; values?: DeviceBuffer | GroupBuffer; count?: number }>): void;
   synchronize(): void;
+  /** Timing events on every rank from the next sort on (rs_group_set_profiling). */
+  setProfiling(enable: boolean): void;
+  /** rank's last sort: ms since its start per step, and its off-rank exchange bytes. */
+  times(rank: number): { rounds: number; hist16Ms: number; partitionMs: number; roundDoneMs: number[];
+                         regionSortedMs: number[]; doneMs: number; bytesSent: number; bytesRecv: number };
   result(rank: number): { keys: GroupBuffer; values: GroupBuffer | null; count: number };
   results(): Array<{ keys: GroupBuffer; values: GroupBuffer | null; count: number }>;
   destroy(): void;

@@ -450,6 +450,10 @@ class PrefixSumKernel {
   /** PrefixSumKernel.getDispatchChain (PrefixSumKernel.ts:135-137): [x, y, 1] per pipeline. */
   getDispatchChain() { return addon.scanPlanDispatchChain(this._plan); }
 
+  /** Wait for the last dispatch; throws if a scan since the last check failed on the device (a
+   * timed-out look-back wait of the single-pass scan: its output is invalid). */
+  check() { addon.scanPlanCheck(this._plan); }
+
   destroy() {
     if (this._plan) addon.scanPlanDestroy(this._plan);
     this._plan = null;
@@ -516,6 +520,14 @@ class RadixSortGroup {
 
   /** Wait for the last sort on every device; throws if any of its kernels failed on the device. */
   synchronize() { addon.groupSynchronize(this._group); }
+
+  /** Timing events on every rank from the next sort on (rs_group_set_profiling). */
+  setProfiling(enable) { addon.groupSetProfiling(this._group, !!enable); }
+
+  /** Where rank's last sort spent its time (rs_group_times_get; waits for it): ms since the
+   * sort's start - hist16Ms, partitionMs, roundDoneMs[], regionSortedMs[], doneMs - and the
+   * rank's off-rank exchange bytes (bytesSent, bytesRecv). */
+  times(rank) { return addon.groupTimes(this._group, rank); }
 
   /** Rank r's slice of the global sorted order: {keys, values, count} (group-owned, valid until
    * the next sort or destroy). */

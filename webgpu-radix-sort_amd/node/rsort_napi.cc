@@ -460,6 +460,17 @@ napi_value PlanCheck(napi_env env, napi_callback_info info) {
     return nullptr;
 }
 
+napi_value ScanPlanCheck(napi_env env, napi_callback_info info) {
+    napi_value a[1];
+    if (!args(env, info, a)) return nullptr;
+    void* p = nullptr;
+    if (napi_get_value_external(env, a[0], &p) != napi_ok || !p)
+        return napi_throw_type_error(env, nullptr, "expected a scan plan handle"), nullptr;
+    auto* b = static_cast<ScanBox*>(p);
+    if (b->plan) RS_CALL(env, rs_scan_plan_check(b->plan), "PrefixSumKernel.check");
+    return nullptr;
+}
+
 napi_value ScanPlanDestroy(napi_env env, napi_callback_info info) {
     napi_value a[1];
     if (!args(env, info, a)) return nullptr;
@@ -627,6 +638,49 @@ napi_value GroupSynchronize(napi_env env, napi_callback_info info) {
     return nullptr;
 }
 
+napi_value GroupSetProfiling(napi_env env, napi_callback_info info) {
+    napi_value a[2];
+    if (!args(env, info, a)) return nullptr;
+    GroupBox* b = group_of(env, a[0]);
+    if (!b) return nullptr;
+    bool on = false;
+    napi_get_value_bool(env, a[1], &on);
+    RS_CALL(env, rs_group_set_profiling(b->group, on ? 1 : 0), "RadixSortGroup.setProfiling");
+    return nullptr;
+}
+
+// rs_group_times_get -> {rounds, hist16Ms, partitionMs, roundDoneMs[], regionSortedMs[], doneMs,
+// bytesSent, bytesRecv}
+napi_value GroupTimes(napi_env env, napi_callback_info info) {
+    napi_value a[2];
+    if (!args(env, info, a)) return nullptr;
+    GroupBox* b = group_of(env, a[0]);
+    if (!b) return nullptr;
+    uint64_t rank = 0;
+    if (!get_u64(env, a[1], &rank) || rank > 0x7FFFFFFF)
+        return napi_throw_type_error(env, nullptr, "groupTimes: bad rank"), nullptr;
+    rs_group_times t;
+    RS_CALL(env, rs_group_times_get(b->group, (int32_t)rank, &t), "RadixSortGroup.times");
+    napi_value o, x, arr;
+    napi_create_object(env, &o);
+    auto num = [&](const char* k, double v) { napi_create_double(env, v, &x); napi_set_named_property(env, o, k, x); };
+    num("rounds", t.rounds);
+    num("hist16Ms", t.hist16_ms);
+    num("partitionMs", t.partition_ms);
+    num("doneMs", t.done_ms);
+    num("bytesSent", (double)t.bytes_sent);
+    num("bytesRecv", (double)t.bytes_recv);
+    for (int which = 0; which < 2; ++which) {
+        napi_create_array_with_length(env, t.rounds, &arr);
+        for (uint32_t j = 0; j < t.rounds; ++j) {
+            napi_create_double(env, which ? t.region_sorted_ms[j] : t.round_done_ms[j], &x);
+            napi_set_element(env, arr, j, x);
+        }
+        napi_set_named_property(env, o, which ? "regionSortedMs" : "roundDoneMs", arr);
+    }
+    return o;
+}
+
 napi_value GroupDestroy(napi_env env, napi_callback_info info) {
     napi_value a[1];
     if (!args(env, info, a)) return nullptr;
@@ -676,6 +730,9 @@ napi_value Init(napi_env env, napi_value exports) {
     Define(env, exports, "groupResult", GroupResult);
     Define(env, exports, "groupSynchronize", GroupSynchronize);
     Define(env, exports, "groupDestroy", GroupDestroy);
+    Define(env, exports, "groupSetProfiling", GroupSetProfiling);
+    Define(env, exports, "groupTimes", GroupTimes);
+    Define(env, exports, "scanPlanCheck", ScanPlanCheck);
     napi_value v;
     napi_create_uint32(env, RS_FLAG_HAS_VALUES, &v); napi_set_named_property(env, exports, "FLAG_HAS_VALUES", v);
     napi_create_uint32(env, RS_FLAG_CHECK_ORDER, &v); napi_set_named_property(env, exports, "FLAG_CHECK_ORDER", v);

@@ -171,6 +171,8 @@ _SIGS = {
     "rs_scan_plan_run_indirect": (ctypes.c_int, [_VP, _VP, _VP, ctypes.c_uint64, _VP]),
     "rs_scan_plan_dispatch_chain": (ctypes.c_uint32, [_VP, ctypes.POINTER(ctypes.c_uint32),
                                                       ctypes.c_uint32]),
+    "rs_scan_plan_check": (ctypes.c_int, [_VP]),
+    "rs_scan_plan_set_wait_limit": (ctypes.c_int, [_VP, ctypes.c_uint32]),
     "rs_scan_plan_destroy": (None, [_VP]),
     "rs_group_create": (ctypes.c_int, [ctypes.c_int32, ctypes.POINTER(ctypes.c_int32),
                                        ctypes.POINTER(GroupDesc), ctypes.POINTER(_VP)]),

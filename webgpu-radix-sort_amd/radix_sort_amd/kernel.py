@@ -392,6 +392,11 @@ class PrefixSumKernel:
 
     getDispatchChain = get_dispatch_chain
 
+    def check(self) -> None:
+        """Wait for the last dispatch; raise RadixSortError (RS_ERR_DEVICE) if a scan since the
+        last check failed on the device (a timed-out look-back wait: its output is invalid)."""
+        check(_lib.load().rs_scan_plan_check(self._plan), "check")
+
     def destroy(self) -> None:
         if getattr(self, "_plan", None):
             _lib.load().rs_scan_plan_destroy(self._plan)

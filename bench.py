@@ -492,6 +492,7 @@ def main() -> None:
         verify_batch(torch, ops, wl, n, wl["seed"] + 7919 * last, batches[last], dev)
         info = kernels[0].info
         device_path = kernels[last].last_path()
+        split_levels = kernels[last].last_split()
         keys_per_step = n
         scatter_keys = n
         bucket_keys = n
@@ -519,6 +520,7 @@ def main() -> None:
         elapsed = time.perf_counter() - t0
         lo.check()      # no local sort or partition failed on the device
         device_path = lo.plan.last_path()
+        split_levels = lo.plan.last_split()
         ms = (ctypes.c_double * _lib.RS_KERNEL_KINDS)()
         cnt = (ctypes.c_uint64 * _lib.RS_KERNEL_KINDS)()
         _lib.load().rs_plan_kernel_times(lo.plan._plan, ms, cnt)
@@ -602,6 +604,11 @@ def main() -> None:
     # the path the device chose (rs_plan_last_path: the hybrid path's gate words, read back)
     msd = device_path == "hybrid"
     extra["device_path"] = device_path
+    sp = kernel_ms.get("split", {"ms": 0.0, "launches": 0})
+    if split_levels:
+        # skewed keys: the 16-bit buckets over the bucket tile were split (count + pass by byte 1 +
+        # in-LDS sort of the 24-bit sub-buckets; level 3: count + pass by byte 0)
+        extra["bucket_split"] = {"levels": split_levels, "ms_per_sort": round(sp["ms"] / max(K, 1), 4)}
     if device_path == "hybrid_fallback":
         sc = fb        # the device took the LSD fallback: its passes are the pass launches
     # one-sweep path: one digit-count launch per sort instead of one per pass

@@ -101,8 +101,10 @@ enum {
     RS_KERNEL_CHECK = 3,        /* order check                        (CheckSort.ts:70-145) */
     RS_KERNEL_BUCKET = 4,       /* hybrid MSD path: in-LDS sort of every 16-bit bucket */
     RS_KERNEL_FALLBACK = 5,     /* hybrid MSD path: the LSD passes it enqueues as its fallback
-                                   (gated off on the device unless the keys are too skewed) */
-    RS_KERNEL_KINDS = 6
+                                   (gated off on the device unless it is taken) */
+    RS_KERNEL_SPLIT = 6,        /* hybrid MSD path: the bucket split of over-full 16-bit buckets
+                                   (skewed keys; one span per sort, gated off for spread keys) */
+    RS_KERNEL_KINDS = 7
 };
 
 /* ---- errors / versions ------------------------------------------------------------------ */
@@ -184,10 +186,15 @@ enum {
     RS_PATH_NONE = 0,             /* no sort yet */
     RS_PATH_LSD = 1,              /* the LSD passes directly (small n, keys-only < 16M, radix_bits != 8 ...) */
     RS_PATH_HYBRID = 2,           /* hybrid MSD: top-byte pass, next-byte pass, in-LDS bucket sort */
-    RS_PATH_HYBRID_FALLBACK = 3,  /* the hybrid path's LSD fallback (a bucket too large, skewed keys) */
+    RS_PATH_HYBRID_FALLBACK = 3,  /* the hybrid path's LSD fallback (a key outside a range hint, or
+                                     a bucket over the tile with the bucket split off) */
     RS_PATH_IN_ORDER = 4          /* check_order found the input sorted: nothing moved */
 };
 rs_status rs_plan_last_path(rs_plan* plan, uint32_t* path);
+/* How deep the hybrid path's last sort split over-full 16-bit buckets (skewed keys, e.g. f32 in
+ * [0, 1) or few distinct keys): 0 not at all, 2 by byte 1 (24-bit sub-buckets sorted in LDS), 3 some
+ * sub-buckets by byte 0 as well.  Waits for the sort.  Diagnostics: the result never depends on it. */
+rs_status rs_plan_last_split(rs_plan* plan, uint32_t* levels);
 /* Kernel timing: when enabled, every launch of the plan is bracketed by HIP events on the
  * launch stream and per-kind durations are accumulated (read after synchronising). */
 rs_status rs_plan_set_profiling(rs_plan* plan, int enable);
@@ -223,6 +230,8 @@ typedef struct rs_plan_debug {
     int32_t kbucket_wave;   /* keys-only bucket pass: 0 a workgroup per bucket, 1 a wave per bucket */
     int32_t selftest_fail;  /* 1: treat the lane-order self-test as failed (ballot ranking,
                                rs_plan_info.lane_order_selftest = 0) */
+    int32_t split;          /* hybrid path, 16-bit buckets over the bucket tile (skewed keys): 1 split
+                               them (default), 0 take the LSD fallback for the whole sort */
 } rs_plan_debug;
 rs_status rs_plan_set_debug(rs_plan* plan, const rs_plan_debug* debug);
 void      rs_plan_destroy(rs_plan* plan);     /* frees the workspace (reference quirk Q9) */

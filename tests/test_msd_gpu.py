@@ -1,8 +1,8 @@
 """GPU: the hybrid MSD path (rsort.hip enqueue_sort_msd; rs_kernels.hpp "hybrid MSD path") —
 separate key / value arrays and interleaved records (RadixSortTextureKernel, sorted in place) of
 >= 12M keys: top-byte pass, 16-bit bucket histogram, segmented
-next-byte pass, in-LDS bucket sort — and both of its device-side fallbacks to the LSD passes
-(top byte too skewed: LSD on the input; a 16-bit bucket over the large tile: LSD on R1).
+next-byte pass, in-LDS bucket sort — skewed keys whose 16-bit buckets are over the tile (split, see
+test_split_gpu.py; with the split off, the device-side fallback to the LSD passes).
 Parity is the same contract as every other path: the stable sort of the input, bit-exact
 against the oracle (values = input index, so stability is checked too)."""
 import numpy as np
@@ -77,9 +77,12 @@ def test_msd_uniform_matches_oracle(n):
 
 
 @pytest.mark.parametrize("kind", ["top0", "low0"])
-def test_msd_device_fallbacks(kind):
+def test_msd_device_fallbacks(kind, plan_debug):
     t = _sort_and_check(1 << 24, kind)
-    # the LSD fallback ran (its passes carry the time), the bucket pass was gated off
+    assert t["path"] == "hybrid"            # the over-full buckets were split, no LSD pass ran
+    plan_debug(split=0)
+    t = _sort_and_check(1 << 24, kind)
+    # the split off: the LSD fallback ran (its passes carry the time), the bucket pass gated off
     assert t["path"] == "hybrid_fallback"   # the device chose the LSD passes
 
 
@@ -163,8 +166,7 @@ def test_msd_records_uniform_matches_oracle(n):
 @pytest.mark.parametrize("kind", ["top0", "low0", "few_big", "dups"])
 def test_msd_records_fallbacks_and_overflow(kind):
     t = _sort_tex_and_check((1 << 24) + 1, kind)
-    if kind in ("top0", "low0"):
-        assert t["path"] == "hybrid_fallback"   # the device chose the LSD passes
+    assert t["path"] == "hybrid"            # over-full buckets split: no LSD fallback
 
 
 def _records_sort(keys_u32, key_range=None, profile=False):
@@ -289,9 +291,12 @@ def test_msd_keys_uniform_matches_oracle(n):
 
 
 @pytest.mark.parametrize("kind", ["top0", "low0"])
-def test_msd_keys_device_fallbacks(kind):
+def test_msd_keys_device_fallbacks(kind, plan_debug):
     t = _sort_keys_and_check((1 << 24) + 4096, kind)
-    assert t["path"] == "hybrid_fallback"   # the device chose the LSD passes
+    assert t["path"] == "hybrid"            # over-full buckets split
+    plan_debug(split=0)
+    t = _sort_keys_and_check((1 << 24) + 4096, kind)
+    assert t["path"] == "hybrid_fallback"   # the split off: the device chose the LSD passes
 
 
 @pytest.mark.parametrize("kind", ["dups", "few_big"])
@@ -345,7 +350,7 @@ def _chk_keys(kind, n):
         return k
     if kind == "reverse":
         return np.sort(u)[::-1].copy()
-    if kind == "f32_nearly":           # config 4's input shape: the LSD fallback, totals from the read
+    if kind == "f32_nearly":           # config 4's input shape: over-full buckets, split
         import bench
         return bench.nearly_sorted_f32_bits(n, 4)
     raise ValueError(kind)
@@ -353,10 +358,10 @@ def _chk_keys(kind, n):
 
 @pytest.mark.parametrize("kind", ["uniform", "sorted", "last_pair", "reverse", "f32_nearly"])
 def test_msd_check_order(kind):
-    """check_order on the hybrid path: the input's order check (and the LSD fallback's byte-0
-    totals) ride on the 16-bit histogram read; an input in order gates every later launch off (the
-    reference's early exit, CheckSort.ts:138-145) and comes back untouched; otherwise the hybrid
-    path (or, for skewed keys, the LSD fallback) sorts it - separate arrays, keys only, records."""
+    """check_order on the hybrid path: the input's order check rides on the 16-bit histogram read;
+    an input in order gates every later launch off (the reference's early exit, CheckSort.ts:138-145)
+    and comes back untouched; otherwise the hybrid path (skewed keys: with the bucket split) sorts
+    it - separate arrays, keys only, records."""
     from radix_sort_amd import RadixSortTextureKernel
     n = (1 << 25) + 3
     keys = _chk_keys(kind, n)
@@ -374,10 +379,8 @@ def test_msd_check_order(kind):
     assert np.array_equal(kt.cpu().numpy().view(np.uint32), ek)
     assert np.array_equal(vt.cpu().numpy().view(np.uint32), ev)
     assert t["bucket"]["launches"] >= 1 and t["check"]["launches"] == 0   # the hybrid path's launches
-    if kind == "uniform":
-        assert path == "hybrid"
-    if kind == "f32_nearly":
-        assert path == "hybrid_fallback"
+    if kind in ("uniform", "f32_nearly"):
+        assert path == "hybrid"           # f32: over-full buckets split, no LSD fallback
     if kind == "sorted":                  # everything after the read gated off
         assert path == "in_order"
     kern.destroy()

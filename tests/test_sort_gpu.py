@@ -266,12 +266,19 @@ def test_config4_256M_nearly_sorted_f32_check_order():
     k_in = kt.clone()
     vt = torch.empty(n, dtype=torch.int32, device=DEV)
     ops.fill_iota_u32(vt)
-    RadixSortKernel(keys=kt, values=vt, count=n, check_order=True).dispatch()
+    kern = RadixSortKernel(keys=kt, values=vt, count=n, check_order=True)
+    kern.dispatch()
     torch.cuda.synchronize()
+    kern.check()
+    # the hybrid path with its over-full buckets split (half the keys share 128 buckets of ~1M)
+    assert kern.last_path() == "hybrid" and kern.last_split() >= 2
     _verify_kv_iota(k_in, kt, vt)
     # fully sorted variant: early exit leaves the data untouched
-    RadixSortKernel(keys=kt, values=vt, count=n, check_order=True).dispatch()
+    kern.dispatch()
     torch.cuda.synchronize()
+    kern.check()
+    assert kern.last_path() == "in_order"
+    kern.destroy()
     _verify_kv_iota(k_in, kt, vt)
 
 

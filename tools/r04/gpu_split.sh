@@ -1,0 +1,9 @@
+# Round 4: the bucket split (skewed keys on the hybrid path) - its GPU parity suite, the hybrid-path
+# suite, config4 / config3 bench lines and a kernel trace of config4.
+cd /tmp && export TMPDIR=/tmp; cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out
+timeout -k 10 400 python -u -m pytest tests/test_split_gpu.py -x -v --timeout 200 --timeout-method thread > gpurun_out/t_split.log 2>&1 || exit 11
+timeout -k 10 400 python -u -m pytest tests/test_msd_gpu.py -x -q --timeout 200 --timeout-method thread > gpurun_out/t_msd.log 2>&1 || exit 12
+timeout -k 10 300 python bench.py --workload config4 --no-cpu-baseline --steps 10 > gpurun_out/c4.json 2> gpurun_out/c4.err || exit 13
+timeout -k 10 200 python bench.py --workload config3 --no-cpu-baseline --steps 20 > gpurun_out/c3.json 2> gpurun_out/c3.err || exit 14
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c4 -o c4 -- python3 bench.py --workload config4 --no-cpu-baseline --steps 5 --warmup 2 > gpurun_out/prof_c4.log 2>&1 || exit 15
+exit 0

@@ -36,7 +36,7 @@ kern = RadixSortKernel(keys=k, values=v, count=n, local_shuffle=True)
 info = kern.info
 passes = info["passes"]
 max_tiles = (n + tile - 1) // tile
-st = torch.zeros(passes * max_tiles * 8, dtype=torch.int64, device="cuda")
+st = torch.zeros(passes * max_tiles * 16, dtype=torch.int64, device="cuda")
 for i in range(3):
     ops.fill_random_u32(k, 11 + i)
     ops.fill_iota_u32(v)
@@ -46,7 +46,7 @@ for i in range(3):
     kern.dispatch()
 torch.cuda.synchronize()
 _lib.check(fn(None), "stamps off")
-a = st.cpu().numpy().reshape(passes, max_tiles, 8)
+a = st.cpu().numpy().reshape(passes, max_tiles, 16)
 names = ["rank", "publish", "stage", "lookback", "scatter"]
 for p in range(passes):
     s = a[p]

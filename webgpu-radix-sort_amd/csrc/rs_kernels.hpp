@@ -51,13 +51,14 @@
 namespace rs {
 
 #if RS_STAMPS
-// [pass][tile][8] s_memtime stamps (thread 0 of the workgroup); slot 7 = workgroup id.  Set by
-// rs_debug_set_stamps (diagnostic builds only, tools/stamp_probe.py).
+// [pass][tile][16] s_memtime stamps (thread 0 of the workgroup); slot 7 = workgroup id, slots
+// 8-11 digit 0's look-back (first status round returned, rounds, predecessors consumed, sleeps).
+// Set by rs_debug_set_stamps (diagnostic builds only, tools/stamp_probe.py).
 __device__ unsigned long long* g_rs_stamps;
 #define RS_STAMP(pass, ntiles, T, i, v)                                                        \
     do {                                                                                       \
         if (threadIdx.x == 0 && g_rs_stamps)                                                   \
-            g_rs_stamps[((size_t)(pass) * (ntiles) + (T)) * 8 + (i)] = (v);                    \
+            g_rs_stamps[((size_t)(pass) * (ntiles) + (T)) * 16 + (i)] = (v);                   \
     } while (0)
 #else
 #define RS_STAMP(pass, ntiles, T, i, v) do { } while (0)
@@ -871,6 +872,14 @@ constexpr uint32_t kStAggregate = 1u, kStInclusive = 2u;
 #ifndef RS_EARLY_TICKET
 #define RS_EARLY_TICKET 0
 #endif
+// RS_AHEAD (speed only): every workgroup holds its next tile's ticket one tile ahead (taken at the
+// top of the previous tile, so the atomic's round trip is never waited for), and issues the next
+// tile's loads slot by slot while staging the current tile (k_onesweep without next-pass totals
+// or order check; else as RS_PREFETCH).  The tile prefetch then starts ~8K cycles earlier, and the
+// look-back's status loads, which queue behind it in the CU's memory pipeline, return earlier.
+#ifndef RS_AHEAD
+#define RS_AHEAD 0
+#endif
 constexpr int kLookback = RS_LOOKBACK;   // predecessors read per look-back step
 
 __device__ __forceinline__ unsigned long long st_load(const unsigned long long* p) {
@@ -910,6 +919,9 @@ __device__ __forceinline__ bool wave_inversion(const uint32_t (&k)[KPT], uint32_
 // look-back chain (its first tile publishes an inclusive prefix at once).  segtab = [257] first
 // tile of every segment (+ the total), [256] segment starts, [256] segment ends; the tile count is
 // segtab[256] (ntiles is only its bound).
+// SEG = 2 (the split of over-full buckets, k_split_count): the segments are listed buckets, their
+// table in global memory (split_tab: [0] segment count, then first tiles [smax + 1], starts [smax],
+// ends [smax]; ntiles = smax) and their digit bases absolute (base16[(seg << 8) | d]).
 // KB (the hybrid MSD path's first pass over a known key range): every real key is replaced by
 // key - kbase as it is loaded, so the digits and the output are of the range-relative keys.
 template <int R, int BLOCK, int KPT, int L, int RANK, int LO = L, int SR = 1, int SEG = 0, bool KB = false>
@@ -948,13 +960,18 @@ __global__ __launch_bounds__(BLOCK, pass_min_waves(BLOCK, KPT)) void k_onesweep(
     __shared__ uint32_t s_inv;
     constexpr bool SG = SEG != 0;
     static_assert(!SG || (SR == 1 && RADIX == 256), "segmented pass: one staging round, 8-bit digits");
-    __shared__ uint32_t s_seg[SG ? 769 : 1];
+    __shared__ uint32_t s_seg[SEG == 1 ? 769 : 1];
 
     if (gated_off(gate, chk ? pass - 1 : pass)) return;
     const uint32_t tid = threadIdx.x, w = tid >> 6;
     for (uint32_t d = tid; d < 256u; d += BLOCK) s_ntot[d] = 0u;
-    if (SG)
+    if (SEG == 1)
         for (uint32_t i = tid; i < 769u; i += BLOCK) s_seg[i] = segtab[i];
+    // SEG = 2: the split table (global): count, first tiles, starts, ends
+    const uint32_t nseg2 = SEG == 2 ? segtab[0] : 0u;
+    const uint32_t* first2 = segtab + 1;
+    const uint32_t* start2 = segtab + 2 + ntiles;
+    const uint32_t* end2 = segtab + 2 + 2 * ntiles;
     if (tid == 0) s_inv = 0u;
     {   // first output position of every digit
         const uint32_t c = (!SG && tid < (uint32_t)RADIX && tid <= mask) ? dtot[tid] : 0u;
@@ -965,10 +982,25 @@ __global__ __launch_bounds__(BLOCK, pass_min_waves(BLOCK, KPT)) void k_onesweep(
         __syncthreads();
     }
     uint32_t T = s_next;
-    const uint32_t nt = SG ? s_seg[256] : ntiles;   // SEG: the tile count the plan kernel wrote
+    // SEG: the tile count the plan kernel wrote
+    const uint32_t nt = SEG == 1 ? s_seg[SEG == 1 ? 256 : 0] : (SEG == 2 ? first2[nseg2] : ntiles);
     // first record and end of tile t (and, SEG, its segment and the segment's first tile)
     auto geom = [&](uint32_t t, uint32_t& t0, uint32_t& tend, uint32_t& seg, uint32_t& first) {
-        if (SG) {
+        if (SEG == 2) {
+            uint32_t lo = 0, hi = nseg2;                 // first2[lo] <= t < first2[hi]
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (first2[mid] <= t) lo = mid;
+                else hi = mid;
+            }
+            seg = lo;
+            first = first2[lo];
+            // (clamped to n: see k_split_count)
+            const uint32_t e = end2[lo] < n ? end2[lo] : n;
+            const uint32_t t0r = start2[lo] + (t - first) * (uint32_t)TILE;
+            t0 = t0r < e ? t0r : e;
+            tend = e - t0 < (uint32_t)TILE ? e : t0 + (uint32_t)TILE;
+        } else if (SG) {
             uint32_t lo = 0, hi = 256;                   // s_seg[lo] <= t < s_seg[hi]
             while (hi - lo > 1) {
                 const uint32_t mid = (lo + hi) >> 1;
@@ -1004,6 +1036,9 @@ __global__ __launch_bounds__(BLOCK, pass_min_waves(BLOCK, KPT)) void k_onesweep(
         load_at(t0, SG ? tend : n);
     };
     if (T < nt) load(T);
+    // RS_AHEAD: thread 0's request for the next tile's ticket, broadcast at the next publish barrier
+    uint32_t ahead_ticket = 0;
+    if (RS_AHEAD && tid == 0) ahead_ticket = atomicAdd(ticket, 1u);
     while (T < nt) {
         RS_STAMP(pass, ntiles, T, 0, __builtin_amdgcn_s_memtime());
         RS_STAMP(pass, ntiles, T, 7, blockIdx.x);
@@ -1014,7 +1049,8 @@ __global__ __launch_bounds__(BLOCK, pass_min_waves(BLOCK, KPT)) void k_onesweep(
         const bool full = tend - tile0 == (uint32_t)TILE;
         const uint32_t nvalid = tend - tile0;
         const bool first_tile = T == seg_first;   // publishes an inclusive prefix at once
-        if (SG && tid < (uint32_t)RADIX) s_dbase[tid] = s_seg[257 + seg] + base16[(seg << 8) | tid];
+        if (SEG == 1 && tid < (uint32_t)RADIX) s_dbase[tid] = s_seg[257 + seg] + base16[(seg << 8) | tid];
+        if (SEG == 2 && tid < (uint32_t)RADIX) s_dbase[tid] = base16[(seg << 8) | tid];
         if (SR > 1 && L == LAYOUT_AOS && !full) {
             const uint64_t wb = (uint64_t)tile0 + w * WAVE_KEYS + lane_id();
 #pragma unroll
@@ -1049,9 +1085,41 @@ __global__ __launch_bounds__(BLOCK, pass_min_waves(BLOCK, KPT)) void k_onesweep(
             else st_store(st, (epoch << 2) | kStAggregate, c);
             set_wave_offsets<R, NW>(s_whist, tstart);
         }
+        if (RS_AHEAD && tid == 0) {
+            s_next = ahead_ticket;                    // requested a tile ago
+            ahead_ticket = atomicAdd(ticket, 1u);     // the one after it: read next tile
+        }
         __syncthreads();
         RS_STAMP(pass, ntiles, T, 2, __builtin_amdgcn_s_memtime());
-        if (SR == 1) {
+        bool pf_done = false;                         // RS_AHEAD: next tile loaded while staging
+        if (RS_AHEAD && SR == 1 && !ntot && !chk) {
+            const uint32_t Ta = s_next;
+            uint32_t n0 = 0, nend = 0, nsg, nfi;
+            if (Ta < nt) geom(Ta, n0, nend, nsg, nfi);
+            const bool nfull = Ta < nt && nend - n0 == (uint32_t)TILE;
+            const size_t b = (size_t)n0 + w * WAVE_KEYS + lane_id();
+            const uint32_t* whist_w = s_whist[w];
+            const uint32_t sh = opaque_u(shift);
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) {
+                const uint32_t sp = whist_w[(k[j] >> sh) & mask] + rank.get(j);
+                if (sp < (uint32_t)TILE) {
+                    if (HAS_VALUES) s_kv[sp] = make_uint2(k[j], v[j]);
+                    else s_keys[sp] = k[j];
+                }
+                if (nfull) {   // slot j of the next tile into the registers just staged
+                    if (L == LAYOUT_AOS) {
+                        const unsigned long long r = ld_in(reinterpret_cast<const unsigned long long*>(in_k) + b + j * 64);
+                        k[j] = (uint32_t)r;
+                        if (HAS_VALUES) v[j] = (uint32_t)(r >> 32);
+                    } else {
+                        k[j] = ld_in(in_k + b + j * 64);
+                        if (HAS_VALUES) v[j] = ld_in(in_v + b + j * 64);
+                    }
+                }
+            }
+            pf_done = nfull;
+        } else if (SR == 1) {
             stage_tile<KPT, HAS_VALUES, TILE>(k, v, rank, s_whist[w], s_keys, s_kv, shift, mask,
                                               ntot ? s_ntot : nullptr, nshift, nmask);
         } else {
@@ -1060,14 +1128,14 @@ __global__ __launch_bounds__(BLOCK, pass_min_waves(BLOCK, KPT)) void k_onesweep(
             stage_round<KPT, HAS_VALUES, STAGE>(k, v, rank, s_keys, s_kv, 0u);
         }
         if (tid == 0) {
-            s_next = RS_EARLY_TICKET ? early_ticket : atomicAdd(ticket, 1u);
+            if (!RS_AHEAD) s_next = RS_EARLY_TICKET ? early_ticket : atomicAdd(ticket, 1u);
             if (ntot && npad) atomicSub(&s_ntot[nmask], npad);   // the pads' next digit
         }
         __syncthreads();
         const uint32_t Tn = s_next;
         RS_STAMP(pass, ntiles, T, 3, __builtin_amdgcn_s_memtime());
         // prefetch (RS_PREFETCH): hides under the look-back and this scatter
-        if (RS_PREFETCH == 0 && SR == 1 && Tn < nt) load(Tn);
+        if (RS_PREFETCH == 0 && SR == 1 && Tn < nt && !pf_done) load(Tn);
         if (tid < (uint32_t)RADIX) {
             uint32_t excl = s_dbase[tid];
             if (!first_tile) {
@@ -1077,6 +1145,9 @@ __global__ __launch_bounds__(BLOCK, pass_min_waves(BLOCK, KPT)) void k_onesweep(
                 excl = 0;
                 uint32_t j = T - 1;                  // next predecessor to consume
                 uint32_t spins = 0;
+#if RS_STAMPS
+                uint32_t st_rounds = 0;
+#endif
                 for (;;) {
                     unsigned long long sv[kLookback];
 #pragma unroll
@@ -1084,6 +1155,14 @@ __global__ __launch_bounds__(BLOCK, pass_min_waves(BLOCK, KPT)) void k_onesweep(
                         sv[i] = (j >= (uint32_t)i) ? st_load(status + (size_t)(j - i) * RADIX + tid) : 0ull;
                     uint32_t used = 0;
                     bool done = false;
+#if RS_STAMPS
+                    if (st_rounds++ == 0) {
+                        // the first round's status words have returned (behind the wave's
+                        // prefetch loads: one in-order vmcnt)
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                        RS_STAMP(pass, ntiles, T, 8, __builtin_amdgcn_s_memtime());
+                    }
+#endif
 #pragma unroll
                     for (int i = 0; i < kLookback; ++i) {
                         if (done || used != (uint32_t)i) break;
@@ -1120,6 +1199,11 @@ __global__ __launch_bounds__(BLOCK, pass_min_waves(BLOCK, KPT)) void k_onesweep(
                     }
                 }
                 st_store(st, (epoch << 2) | kStInclusive, excl + c);
+#if RS_STAMPS
+                RS_STAMP(pass, ntiles, T, 9, st_rounds);
+                RS_STAMP(pass, ntiles, T, 10, T - 1 - j);
+                RS_STAMP(pass, ntiles, T, 11, spins);
+#endif
             }
             s_gdelta[tid] = excl - tstart;
 #if RS_SCATTER_DEBUG >= 2
@@ -1128,16 +1212,16 @@ __global__ __launch_bounds__(BLOCK, pass_min_waves(BLOCK, KPT)) void k_onesweep(
             s_gdelta[tid] = ((((uint32_t)tid * ntiles + T) * 64u) & (n - 1u)) - tstart;
 #endif
         }
-        if (RS_PREFETCH == 1 && SR == 1 && Tn < nt) load(Tn);
+        if (RS_PREFETCH == 1 && SR == 1 && Tn < nt && !pf_done) load(Tn);
         __syncthreads();
-        if (RS_PREFETCH == 2 && SR == 1 && Tn < nt) load(Tn);
+        if (RS_PREFETCH == 2 && SR == 1 && Tn < nt && !pf_done) load(Tn);
         RS_STAMP(pass, ntiles, T, 4, __builtin_amdgcn_s_memtime());
 #pragma unroll
         for (int h = 0; h < SR; ++h) {
             if (h > 0) {   // the previous round's scatter has read the staging area
                 stage_round<KPT, HAS_VALUES, STAGE>(k, v, rank, s_keys, s_kv, h * (uint32_t)STAGE);
                 __syncthreads();
-                if (h == SR - 1 && Tn < nt) load(Tn);   // registers free: prefetch
+                if (h == SR - 1 && Tn < nt && !pf_done) load(Tn);   // registers free: prefetch
             }
             const uint32_t lo = h * (uint32_t)STAGE;
             if (lo < nvalid)
@@ -1360,18 +1444,25 @@ __device__ __forceinline__ void set_gate(uint32_t* g, uint32_t v) {
 // half bit 16, so a key costs ~3 VALU + 1 LDS atomic (the kernel is issue-bound, not HBM-bound).
 // CHECK (check_order on the hybrid path, FULL only): the same read also (a) checks the input's
 // order - *inv |= 1 if any adjacent pair is out of order (every pair, the reference's quirks Q1/Q2
-// fixed; CheckSort.ts:102-113) - and (b) counts the low byte of every key into b0rows[block][256]
-// (the LSD fallback's pass-0 totals: k_hist16_reduce adds them, so the fallback needs no read of
-// its own).
-template <int L, bool AOS_WIDE = false, bool FULL = false, bool CHECK = false>
+// fixed; CheckSort.ts:102-113) - and (b, CHECK = 2) counts the low byte of every key into
+// b0rows[block][256] (the LSD fallback's pass-0 totals: k_hist16_reduce adds them, so the fallback
+// needs no read of its own; CHECK = 1 when the sort has no fallback, see SplitWs).
+template <int L, bool AOS_WIDE = false, bool FULL = false, int CHECK = 0>
 __global__ __launch_bounds__(1024) void k_hist16_in(const uint32_t* __restrict__ keys, uint32_t n,
                                                      uint32_t* __restrict__ rows, uint32_t kbase,
                                                      uint32_t range, uint32_t shift,
                                                      uint32_t* __restrict__ z0, uint32_t* __restrict__ z1,
-                                                     uint32_t* inv = nullptr, uint32_t* __restrict__ b0rows = nullptr) {
+                                                     uint32_t* inv = nullptr, uint32_t* __restrict__ b0rows = nullptr,
+                                                     uint32_t* __restrict__ z2 = nullptr) {
+    // z2 (may be null): the bucket split's huge-bucket count (SplitWs::huge[0])
     static_assert(!CHECK || FULL, "the order check rides on whole-range histograms only");
+    constexpr bool B0 = CHECK == 2;   // the byte-0 counts too (the LSD fallback's pass-0 totals)
     // z0, z1: the reduction's overflow-bucket count and oversize flag (k_hist16_reduce adds to them)
-    if (blockIdx.x == 0 && threadIdx.x == 0) { *z0 = 0u; *z1 = 0u; }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        *z0 = 0u;
+        *z1 = 0u;
+        if (z2) *z2 = 0u;
+    }
     constexpr uint32_t B = 1024, W = 32768, PER = W / B;
     constexpr bool NARROW = L == LAYOUT_AOS && !AOS_WIDE;
     constexpr uint32_t KPL = NARROW ? 1u : (L == LAYOUT_AOS ? 2u : 4u);   // keys per load
@@ -1384,12 +1475,12 @@ __global__ __launch_bounds__(1024) void k_hist16_in(const uint32_t* __restrict__
     static_assert(STEPS % FLY == 0, "whole load groups per round");
     using Vec = typename std::conditional<NARROW, uint2, uint4>::type;
     __shared__ uint32_t h[W];
-    __shared__ uint32_t s_b0[CHECK ? 256 : 1];
+    __shared__ uint32_t s_b0[B0 ? 256 : 1];
     const uint32_t tid = threadIdx.x;
     uint32_t acc[2 * PER];
 #pragma unroll
     for (uint32_t i = 0; i < PER; ++i) { h[tid + B * i] = 0u; acc[2 * i] = 0u; acc[2 * i + 1] = 0u; }
-    if (CHECK && tid < 256u) s_b0[tid] = 0u;
+    if (B0 && tid < 256u) s_b0[tid] = 0u;
     constexpr uint32_t KS = L == LAYOUT_AOS ? 2u : 1u;   // words per key
     bool inverted = false;
     auto inv2 = [&](uint32_t a, uint32_t b) { inverted |= a > b; };
@@ -1430,7 +1521,7 @@ __global__ __launch_bounds__(1024) void k_hist16_in(const uint32_t* __restrict__
         for (int j = 1; j < m; ++j) uni &= (ks[j] >> 16) == b;
         if (!grouped(b, uni, (uint32_t)m, add16))
             for (int j = 0; j < m; ++j) add16(ks[j] >> 16, 1u);
-        if constexpr (CHECK) {
+        if constexpr (B0) {
             const uint32_t d = ks[0] & 255u;
             bool uni0 = true;
             for (int j = 1; j < m; ++j) uni0 &= (ks[j] & 255u) == d;
@@ -1442,7 +1533,7 @@ __global__ __launch_bounds__(1024) void k_hist16_in(const uint32_t* __restrict__
     auto count = [&](uint32_t key) {
         if constexpr (FULL) {
             atomicAdd(&h[key >> 17], 1u << ((key >> 12) & 16u));
-            if constexpr (CHECK) atomicAdd(&s_b0[key & 255u], 1u);
+            if constexpr (B0) atomicAdd(&s_b0[key & 255u], 1u);
         } else {
             const uint32_t rk = key - kbase;
             bad |= rk > range;
@@ -1514,7 +1605,7 @@ __global__ __launch_bounds__(1024) void k_hist16_in(const uint32_t* __restrict__
     flush();
     if constexpr (CHECK) {
         if (__ballot(inverted) != 0ull && lane_id() == 0) atomicOr(inv, 1u);
-        if (tid < 256u) b0rows[(size_t)blockIdx.x * 256u + tid] = s_b0[tid];   // flush()'s barriers passed
+        if (B0 && tid < 256u) b0rows[(size_t)blockIdx.x * 256u + tid] = s_b0[tid];   // flush()'s barriers passed
     }
     uint2* row = reinterpret_cast<uint2*>(rows + (size_t)blockIdx.x * 65536u);
 #pragma unroll
@@ -1534,7 +1625,7 @@ __global__ __launch_bounds__(1024) void k_hist16_in(const uint32_t* __restrict__
 // before row r (an exclusive scan over the rows of each top byte's row sums): where chunk r's
 // top-byte-t keys start inside segment t.  The static first MSD pass (k_static_pass) takes its
 // per-digit output bases from it, so it needs no look-back.
-constexpr uint32_t kOverMax = 4096;
+constexpr uint32_t kOverMax = 65536;   // every bucket can be listed (no overflow to the fallback)
 constexpr uint32_t kMaxRows = 1024;
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 #pragma unroll
@@ -1550,7 +1641,10 @@ __global__ __launch_bounds__(1024) void k_hist16_reduce(const uint32_t* __restri
                                                          uint32_t* __restrict__ big,
                                                          uint32_t* __restrict__ zero = nullptr, uint32_t nzero = 0,
                                                          const uint32_t* __restrict__ b0rows = nullptr,
-                                                         uint32_t* __restrict__ cbase = nullptr) {
+                                                         uint32_t* __restrict__ cbase = nullptr,
+                                                         uint32_t* __restrict__ huge = nullptr, uint32_t hmax = 0) {
+    // huge (may be null): buckets over `cap` are listed in huge[1..] (huge[0] counts them, up to hmax
+    // stored; zeroed with over[0]) for the bucket split instead of flagging *big
     // zero[0..nzero): the sort's pass totals, tile tickets and device error word (no memset launch);
     // with b0rows (check_order): zero[0..256) = pass 0's byte-0 totals, the rows' sums
     if (blockIdx.x == gridDim.x - 1) {
@@ -1611,13 +1705,18 @@ __global__ __launch_bounds__(1024) void k_hist16_reduce(const uint32_t* __restri
             make_uint4(ex, ex + t.x, ex + t.x + t.y, ex + t.x + t.y + t.z);
         if (tid == 63) top_tot[blockIdx.x] = inc;
         const uint32_t mx = max(max(t.x, t.y), max(t.z, t.w));
-        if (mx > cap) atomicOr(big, 1u);
+        if (mx > cap && !huge) atomicOr(big, 1u);
         if (mx > small) {
             const uint32_t c4[4] = {t.x, t.y, t.z, t.w};
             for (uint32_t j = 0; j < 4u; ++j) {
-                if (c4[j] > small) {
+                const uint32_t b = blockIdx.x * 256u + tid * 4u + j;
+                if (huge && c4[j] > cap) {   // split by the bucket split (k_msd_plan's level 2)
+                    const uint32_t slot = atomicAdd(&huge[0], 1u);
+                    if (slot < hmax) huge[1 + slot] = b;
+                    else atomicOr(big, 1u);
+                } else if (c4[j] > small) {
                     const uint32_t slot = atomicAdd(&over[0], 1u);
-                    if (slot < kOverMax) over[1 + slot] = blockIdx.x * 256u + tid * 4u + j;
+                    if (slot < kOverMax) over[1 + slot] = b;
                 }
             }
         }
@@ -1642,10 +1741,15 @@ __global__ __launch_bounds__(256) void k_hist16_sum(const uint32_t* __restrict__
 // senders' tables, so instead of k_hist16_in's rows there is one row, copied here, with a clear
 // range flag word; also clears the overflow count and the oversize flag (k_hist16_in's job).
 __global__ __launch_bounds__(256) void k_region_rows(const uint32_t* __restrict__ hist, uint32_t* __restrict__ row,
-                                                     uint32_t* z0, uint32_t* z1) {
+                                                     uint32_t* z0, uint32_t* z1, uint32_t* z2 = nullptr) {
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
     row[i] = hist[i];
-    if (i == 0) { row[65536] = 0u; *z0 = 0u; *z1 = 0u; }
+    if (i == 0) {
+        row[65536] = 0u;
+        *z0 = 0u;
+        *z1 = 0u;
+        if (z2) *z2 = 0u;
+    }
 }
 
 // One workgroup, after k_hist16_reduce: the segmented tile table of MSD pass 1 (segment = top
@@ -1662,15 +1766,99 @@ __global__ __launch_bounds__(256) void k_region_rows(const uint32_t* __restrict_
 // choice.  The populated buckets must lie in the top bytes [top_lo, top_hi) (a region's
 // table; counts outside them would never be sorted): otherwise the LSD passes run.
 constexpr uint32_t kGateSegStatic = 32, kGateSegLookback = 48;
+
+// The bucket split's workspace (see "splitting over-full buckets" below); huge == null: no split
+// (a bucket over the cap then sends the sort to the LSD fallback).
+struct SplitWs {
+    uint32_t* gate2 = nullptr;       // [16] level 2 runs (k_msd_plan)
+    uint32_t* gate3 = nullptr;       // [16] level 3 runs (set by level 2's counting)
+    uint32_t* huge = nullptr;        // [1 + smax2] count, then the buckets over the cap (k_hist16_reduce)
+    uint32_t* tab2 = nullptr;        // level 2's split table (its segments: the huge buckets)
+    uint32_t* rows2 = nullptr;       // [smax2][256] byte-1 counts -> absolute sub-bucket starts
+    uint32_t* arrive2 = nullptr;     // [smax2 + 1]
+    uint32_t smax2 = 0;
+    uint32_t* tab3 = nullptr;        // level 3's (its segments: the sub-buckets over kSub8Cap)
+    uint32_t* rows3 = nullptr;
+    uint32_t* arrive3 = nullptr;
+    uint32_t smax3 = 0;
+    uint32_t tmax = 0;               // tiles one level may have (the plan's look-back status words)
+    const uint32_t* hist16 = nullptr;
+    const uint32_t* base16 = nullptr;
+    uint32_t* err = nullptr;         // the sort's device error word ...
+    uint32_t* host_err = nullptr;    // ... and the host-mapped one (bit 2: counts did not add up)
+    uint32_t strict = 0;             // no LSD fallback is enqueued: a failed plan check is an error
+    uint32_t n = 0;                  // the sort's record count: every table position is clamped to it
+};
+
+__device__ __forceinline__ void split_fail(const SplitWs& sw) {
+    atomicOr(sw.err, 4u);
+    if (sw.host_err) __hip_atomic_fetch_or(sw.host_err, 4u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+constexpr uint32_t kSplitTile = 16384;          // k_onesweep's tile (tiles never straddle a segment)
+
+// Lays out one split level's table from its segments (segment i: `cnt` records from `start`, both
+// from seg_range): tiles per segment scanned into first tiles, rows and arrivals zeroed.  One
+// workgroup of BLOCK threads; nseg <= smax.  More than tmax tiles (never, by the plan's sizing):
+// an error and an empty level.  Returns the level's segment count.
+template <int BLOCK, class F>
+__device__ uint32_t split_layout(uint32_t nseg, uint32_t smax, uint32_t* tab, uint32_t* rows, uint32_t* arrive,
+                                 const SplitWs& sw, F&& seg_range) {
+    constexpr int NW = BLOCK / 64;
+    __shared__ uint32_t s_scr[NW];
+    const uint32_t tid = threadIdx.x;
+    // contiguous chunks of segments per thread: local tile sums, one block scan, then the firsts
+    const uint32_t per = (nseg + BLOCK - 1) / BLOCK;
+    const uint32_t a = tid * per < nseg ? tid * per : nseg;
+    const uint32_t b = a + per < nseg ? a + per : nseg;
+    uint32_t sum = 0;
+    for (uint32_t i = a; i < b; ++i) {
+        uint32_t st, c;
+        seg_range(i, st, c);
+        sum += (c + kSplitTile - 1) / kSplitTile;
+    }
+    uint32_t tot;
+    uint32_t run = block_excl_scan_n<NW>(sum, s_scr, tot);
+    if (tot > sw.tmax) {
+        if (tid == 0) {
+            tab[0] = 0u;
+            tab[1] = 0u;
+            split_fail(sw);
+        }
+        return 0u;
+    }
+    for (uint32_t i = a; i < b; ++i) {
+        uint32_t st, c;
+        seg_range(i, st, c);
+        tab[1 + i] = run;
+        tab[2 + smax + i] = st;
+        tab[2 + 2 * smax + i] = st + c;
+        run += (c + kSplitTile - 1) / kSplitTile;
+    }
+    if (tid == 0) {
+        tab[0] = nseg;
+        tab[1 + nseg] = tot;
+        arrive[smax] = 0u;
+    }
+    for (uint32_t i = tid; i < nseg; i += BLOCK) arrive[i] = 0u;
+    for (uint32_t i = tid; i < nseg * 256u; i += BLOCK) rows[i] = 0u;
+    return nseg;
+}
+
+// sw.huge != null: also the bucket split's level 2 - the huge buckets' table from the list
+// k_hist16_reduce made, its rows zeroed, gate2 set when there is any, gate3 cleared (level 2's
+// counting sets it).  sw.strict (whole-range sorts with the split: no LSD fallback enqueued): a
+// failed check - a histogram that does not add up to n - is a device error instead.
 template <int TILE>
 __global__ __launch_bounds__(256) void k_msd_plan(const uint32_t* __restrict__ top_tot,
                                                   uint32_t* __restrict__ segtab, uint32_t max_top,
                                                   uint32_t* over, const uint32_t* big, uint32_t* gates,
                                                   const uint32_t* __restrict__ range_bad, uint32_t n,
                                                   const uint32_t* inv = nullptr, uint32_t top_lo = 0,
-                                                  uint32_t top_hi = 256) {
+                                                  uint32_t top_hi = 256, SplitWs sw = SplitWs{}) {
     constexpr int NW = 4;
     __shared__ uint32_t s_scratch[NW];
+    __shared__ uint32_t s_sstart[256];
     const uint32_t tid = threadIdx.x;
     const uint32_t cnt = top_tot[tid];
     const int any_big = __syncthreads_or((cnt > max_top || (cnt != 0u && (tid < top_lo || tid >= top_hi))) ? 1 : 0);
@@ -1684,11 +1872,14 @@ __global__ __launch_bounds__(256) void k_msd_plan(const uint32_t* __restrict__ t
     segtab[tid] = tbase;
     segtab[257 + tid] = sbase;
     segtab[513 + tid] = sbase + cnt;
+    s_sstart[tid] = sbase;
     if (tid == 0) segtab[256] = ttot;
     const uint32_t nover = over[0];
+    const uint32_t nhuge = sw.huge ? sw.huge[0] : 0u;
     __syncthreads();   // every thread has read over[0]
     if (tid == 0) over[0] = nover < kOverMax ? nover : kOverMax;
-    const uint32_t ok = (any_big || *big || nover > kOverMax || *range_bad || stot != n) ? 0u : 1u;
+    const uint32_t ok = (any_big || *big || nover > kOverMax || *range_bad || stot != n || nhuge > sw.smax2)
+                            ? 0u : 1u;
     // check_order: an input already in order needs neither path (the reference's early exit,
     // CheckSort.ts:138-145: every later dispatch zeroed)
     const uint32_t run = (inv && *inv == 0u) ? 0u : 1u;
@@ -1696,6 +1887,223 @@ __global__ __launch_bounds__(256) void k_msd_plan(const uint32_t* __restrict__ t
     set_gate(gates + kGateLsd, (1u - ok) & run);
     set_gate(gates + kGateSegStatic, ok & run & (unbalanced ? 0u : 1u));
     set_gate(gates + kGateSegLookback, ok & run & (unbalanced ? 1u : 0u));
+    if (sw.strict && run && !ok && tid == 0) split_fail(sw);
+    if (sw.huge) {
+        set_gate(sw.gate3, 0u);
+        if (tid == 0) sw.tab3[0] = 0u;
+        uint32_t n2 = 0;
+        if (ok & run & (nhuge ? 1u : 0u))   // uniform
+            n2 = split_layout<256>(nhuge, sw.smax2, sw.tab2, sw.rows2, sw.arrive2, sw,
+                                   [&](uint32_t i, uint32_t& st, uint32_t& c) {
+                                       const uint32_t b = sw.huge[1 + i];
+                                       st = s_sstart[b >> 8] + sw.base16[b];
+                                       c = sw.hist16[b];
+                                   });
+        set_gate(sw.gate2, n2 ? 1u : 0u);
+    }
+}
+
+// ---- splitting over-full buckets (skewed keys on the hybrid path) ---------------------------
+// A 16-bit bucket over kBucketCap records (f32 keys in [0, 1): half of them share 128 buckets of
+// ~1M records; few distinct keys; one populated bucket) is split instead of sending the whole sort
+// to the LSD passes.  Level 2 partitions every such "huge" bucket by byte 1 (a segmented one-sweep
+// pass, k_onesweep SEG = 2, over the huge buckets' records only, R2 -> a free records buffer) into
+// 24-bit sub-buckets, which k_bucket_sort8 sorts by byte 0 in LDS into the output; a sub-bucket over
+// kSub8Cap records goes to level 3, a segmented pass by byte 0 straight into the output (its keys then
+// differ in no other bit).  The digit bases of a level come from k_split_count: every tile of the
+// level's segments counts its digits (run-aggregated LDS atomics) into the segment's global row, and
+// the workgroup that adds a segment's last tile turns the row into absolute bases; for level 2 it
+// also lists the sub-buckets over kSub8Cap, and the workgroup that finishes the last segment lays
+// out level 3's table and opens its gate.  Every step is stable, so the result is the stable sort.
+// Bytes per record of a huge bucket, after MSD passes 0 and 1: count 8 + level-2 pass 16 + bucket
+// sort 16 (level 3: + 8 + 16), where the LSD fallback read and wrote every record four times.
+//
+// Split table (per level): [0] segment count, [1 .. smax + 1] first tile of every segment (+ the
+// total), [smax + 2 ..] segment starts, [2 smax + 2 ..] segment ends (positions in the records
+// buffers).  rows: [smax][256] digit counts, turned into absolute bases in place.  arrive: [smax]
+// per-segment tile arrivals + [1] segments done (zeroed by the level's layout).
+constexpr uint32_t kSub8Small = 256u * 17u;     // k_bucket_sort8's small tile (4352 records)
+constexpr uint32_t kSub8Cap = 1024u * 17u;      // its large tile (17408): larger sub-buckets -> level 3
+__device__ __forceinline__ uint32_t split_seg_of(const uint32_t* first, uint32_t nseg, uint32_t t) {
+    uint32_t lo = 0, hi = nseg;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (first[mid] <= t) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// One split level's digit counts and bases (see above).  KS = words per record in `rec` (2:
+// (key, value) records, 1: keys); digit = (key >> shift) & 255.  LEVEL 2 (tab = sw.tab2 ...) also
+// lists and lays out level 3; LEVEL 3 (tab = sw.tab3 ...) only counts.  A list overflow or a count
+// that does not add up is an error (bit 2): never a silent wrong order.
+template <int KS, int LEVEL>
+__global__ __launch_bounds__(1024) void k_split_count(const uint32_t* __restrict__ rec, SplitWs sw,
+                                                      uint32_t shift) {
+    constexpr uint32_t B = 1024, NW = B / 64;
+    constexpr int KPT = kSplitTile / B;
+    __shared__ uint32_t s_h[NW][256];
+    __shared__ uint32_t s_scr[NW];
+    __shared__ uint32_t s_flag;
+    const uint32_t* gate = LEVEL == 2 ? sw.gate2 : sw.gate3;
+    if (gated_off(gate, 0)) return;
+    uint32_t* tab = LEVEL == 2 ? sw.tab2 : sw.tab3;
+    uint32_t* rows = LEVEL == 2 ? sw.rows2 : sw.rows3;
+    uint32_t* arrive = LEVEL == 2 ? sw.arrive2 : sw.arrive3;
+    const uint32_t smax = LEVEL == 2 ? sw.smax2 : sw.smax3;
+    const uint32_t tid = threadIdx.x, w = tid >> 6, lane = lane_id();
+    const uint32_t nseg = tab[0];
+    const uint32_t* first = tab + 1;
+    const uint32_t* start = tab + 2 + smax;
+    const uint32_t* end = tab + 2 + 2 * smax;
+    const uint32_t ntiles = first[nseg];
+    for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const uint32_t sg = split_seg_of(first, nseg, t);
+        // (positions clamped to n: a table is only ever wrong after a counting fault, which is
+        // reported; the reads and writes stay inside the buffers regardless)
+        const uint32_t e = end[sg] < sw.n ? end[sg] : sw.n;
+        const uint32_t t0r = start[sg] + (t - first[sg]) * kSplitTile;
+        const uint32_t t0 = t0r < e ? t0r : e;
+        const uint32_t te = e - t0 < kSplitTile ? e : t0 + kSplitTile;
+        for (uint32_t d = lane; d < 256u; d += 64) s_h[w][d] = 0u;
+        // wave w counts records [t0 + w * 1024, +1024): slot j of lane l = + j * 64 + l; the pads
+        // past the tile's end load as kPadKey (digit 255) and are taken off below
+        uint32_t k[KPT];
+        const uint64_t wb = (uint64_t)t0 + w * (64u * KPT) + lane;
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) k[j] = wb + j * 64 < te ? rec[(wb + j * 64) * KS] : kPadKey;
+        count_slots<KPT>(k, s_h[w], shift, 255u);
+        __syncthreads();
+        if (tid < 256u) {
+            uint32_t c = 0;
+#pragma unroll
+            for (uint32_t q = 0; q < NW; ++q) c += s_h[q][tid];
+            if (tid == 255u) c -= kSplitTile - (te - t0);
+            if (c) atomicAdd(&rows[(size_t)sg * 256u + tid], c);
+        }
+        // the workgroup's adds have completed (vmcnt covers atomics) before its arrival (release)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const uint32_t tiles = first[sg + 1] - first[sg];
+            s_flag = atomicAdd(&arrive[sg], 1u) + 1u == tiles ? 1u : 0u;
+        }
+        __syncthreads();
+        if (s_flag) {
+            // this workgroup added the segment's last tile: the row -> absolute digit bases
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            uint32_t c = 0, tot = 0;
+            if (tid < 256u)
+                c = __hip_atomic_load(&rows[(size_t)sg * 256u + tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t ex = block_excl_scan_n<NW>(c, s_scr, tot);
+            if (tid == 0 && tot != end[sg] - start[sg]) split_fail(sw);
+            if (tid < 256u) rows[(size_t)sg * 256u + tid] = start[sg] + ex;
+            if constexpr (LEVEL == 2) {
+                if (tid < 256u && c > kSub8Cap) {   // a sub-bucket over the bucket tile: level 3's
+                    const uint32_t slot = atomicAdd(&sw.tab3[0], 1u);
+                    if (slot < sw.smax3) {
+                        sw.tab3[2 + sw.smax3 + slot] = start[sg] + ex;   // its start and count
+                        sw.tab3[2 + 2 * sw.smax3 + slot] = c;             // (the layout makes it an end)
+                    } else {
+                        split_fail(sw);
+                    }
+                }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+                if (tid == 0) {
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    s_flag = atomicAdd(&arrive[smax], 1u) + 1u == nseg ? 2u : 0u;
+                }
+                __syncthreads();
+                if (s_flag == 2u) {
+                    // the last segment done: lay out level 3 from its list
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                    const uint32_t n3r = __hip_atomic_load(&sw.tab3[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const uint32_t n3 = n3r < sw.smax3 ? n3r : sw.smax3;
+                    const uint32_t got = split_layout<B>(n3, sw.smax3, sw.tab3, sw.rows3, sw.arrive3, sw,
+                                                         [&](uint32_t i, uint32_t& st, uint32_t& cn) {
+                                                             st = __hip_atomic_load(&sw.tab3[2 + sw.smax3 + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                                                             cn = __hip_atomic_load(&sw.tab3[2 + 2 * sw.smax3 + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                                                         });
+                    if (tid < 16u) sw.gate3[tid] = got ? 1u : 0u;
+                }
+            }
+        }
+        __syncthreads();   // s_h / s_flag are reused by the next tile
+    }
+}
+
+// The level-2 sub-buckets: sub-bucket (s, d) = records [rows2[s][d], next) of `rec` (next = the
+// following sub-bucket's start, or the segment's end), min_cnt < count <= BLOCK x KPT, sorted stably
+// by byte 0 in one LDS pass and written to the output at the same positions (sub-buckets over
+// kSub8Cap: level 3's).  A persistent grid over the segments x 256 sub-buckets.  LO: the output
+// layout (the caller's arrays, records, or keys); the input is records (or keys, LO = KEYS).  PACK:
+// ranks as 16-bit pairs (the 1024-thread tile's registers: at most 128 VGPRs).
+template <int BLOCK, int KPT, int RANK, int LO, int MW = 1, bool PACK = false>
+__global__ __launch_bounds__(BLOCK, MW) void k_bucket_sort8(const uint32_t* rec, SplitWs sw, uint32_t min_cnt,
+                                                            uint32_t* out_k, uint32_t* __restrict__ out_v) {
+    constexpr int NW = BLOCK / 64, TILE = BLOCK * KPT, WAVE_KEYS = 64 * KPT;
+    constexpr bool KV = LO != LAYOUT_KEYS;
+    constexpr int LI = KV ? LAYOUT_AOS : LAYOUT_KEYS;
+    static_assert(BLOCK >= 256, "one digit per thread in the scan");
+    __shared__ uint32_t s_whist[NW][256];
+    __shared__ uint32_t s_scratch[NW];
+    __shared__ uint2 s_kv[KV ? TILE : 1];
+    __shared__ uint32_t s_k[KV ? 1 : TILE];
+    if (gated_off(sw.gate2, 0)) return;
+    const uint32_t tid = threadIdx.x, w = tid >> 6, lane = lane_id();
+    const uint32_t wbase = w * WAVE_KEYS;
+    const uint32_t nseg = sw.tab2[0];
+    const uint32_t* end = sw.tab2 + 2 + 2 * sw.smax2;
+    for (uint32_t it = blockIdx.x; it < nseg * 256u; it += gridDim.x) {
+        const uint32_t sg = it >> 8, d = it & 255u;
+        const uint32_t base = sw.rows2[it];
+        const uint32_t nxt = d == 255u ? end[sg] : sw.rows2[it + 1];
+        const uint32_t cnt = nxt - base;
+        if (cnt <= min_cnt || cnt > (uint32_t)TILE) continue;   // the other launch's, or level 3's
+        if (nxt > sw.n || base > nxt) continue;                 // (never: a counting fault, reported)
+        uint32_t k[KPT], v[KV ? KPT : 1];
+        load_tile<KPT, LI>(rec + (KV ? 2ull : 1ull) * base, nullptr, wbase, cnt, false, k, v);
+        if (cnt > 1u) {
+            Slots<KPT, PACK> rank;
+            uint32_t c;   // pads: kPadKey, digit 255, after every real key
+            const uint32_t tstart = rank_tile<8, NW, KPT, RANK>(k, rank, s_whist, s_scratch, 0u, 255u, 0u, c);
+            if (tid < 256u) set_wave_offsets<8, NW>(s_whist, tstart);
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) {
+                const uint32_t q = s_whist[w][k[j] & 255u] + rank.get(j);
+                if constexpr (KV) s_kv[q] = make_uint2(k[j], v[j]);
+                else s_k[q] = k[j];
+            }
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) {
+                if constexpr (KV) {
+                    const uint2 kv = s_kv[wbase + j * 64 + lane];
+                    k[j] = kv.x;
+                    v[j] = kv.y;
+                } else {
+                    k[j] = s_k[wbase + j * 64 + lane];
+                }
+            }
+        }
+        const size_t o0 = (size_t)base + wbase + lane;
+        const int lim = (int)cnt - (int)(wbase + lane);
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) {
+            if (j * 64 < lim) {
+                if constexpr (LO == LAYOUT_AOS) (reinterpret_cast<uint2*>(out_k) + o0)[j * 64] = make_uint2(k[j], v[j]);
+                else if constexpr (LO == LAYOUT_KEYS) (out_k + o0)[j * 64] = k[j];
+                else { (out_k + o0)[j * 64] = k[j]; (out_v + o0)[j * 64] = v[j]; }
+            }
+        }
+        __syncthreads();   // s_whist / s_kv are reused
+    }
 }
 
 // In-LDS sort of the 16-bit buckets: a workgroup takes a bucket's records (R2, contiguous, at most
@@ -1898,8 +2306,8 @@ __global__ __launch_bounds__(BLOCK, MW) void k_bucket_sort_wide(const uint32_t* 
         for (; it < nb; it += gridDim.x) {
             cnt = hist16[bucket_of(it)];
             if (cnt == 0u || cnt <= min_cnt) continue;   // empty, or the smaller tile's launch took it
-            if (cnt > (uint32_t)TILE) {                   // never: k_hist16_reduce gates the path off
-                if (tid == 0) atomicOr(err, 8u);
+            if (cnt > (uint32_t)TILE) {   // unlisted: a huge bucket (the split's); listed: never
+                if (over && tid == 0) atomicOr(err, 8u);
                 continue;
             }
             break;

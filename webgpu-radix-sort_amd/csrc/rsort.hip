@@ -130,6 +130,15 @@ constexpr uint32_t kBucketCap = 1024u * kWideKpt;       // the largest 16-bit bu
 constexpr uint64_t kMsdMax = 65536ull * 33800;
 constexpr uint64_t kMsdWords = 65536ull * 2 + 1024 + 64 + 1024 + 1 + rs::kOverMax +   // hist16, base16,
                                  256ull * rs::kMaxRows;             // segtab, gates, mtot, over, cbase
+// The bucket split (rs_kernels.hpp, "splitting over-full buckets"): level 2 takes the 16-bit buckets
+// over kBucketCap records, level 3 the 24-bit sub-buckets over kSub8Cap - at most n / (cap + 1) of
+// each.  Words: gates [32], huge list [1 + smax2], per level a table [3 smax + 2], arrivals
+// [smax + 1] and rows [256 smax].
+inline uint32_t split_smax2(uint64_t cap) { return (uint32_t)(cap / (kBucketCap + 1ull) + 1); }
+inline uint32_t split_smax3(uint64_t cap) { return (uint32_t)(cap / (rs::kSub8Cap + 1ull) + 1); }
+inline uint64_t split_words(uint32_t s2, uint32_t s3) {
+    return 32ull + 1 + s2 + (3ull * s2 + 2) + (s2 + 1ull) + 256ull * s2 + (3ull * s3 + 2) + (s3 + 1ull) + 256ull * s3;
+}
 constexpr uint32_t kHistGrid = 2048;
 constexpr int kCheckGrid = 2048;
 
@@ -198,7 +207,8 @@ struct KernelTimer {
     template <class F>
     void run(int kind, hipStream_t s, F&& launch, const char* label = nullptr) {
         static const char* const names[RS_KERNEL_KINDS] = {"rsort.histogram", "rsort.scan", "rsort.scatter",
-                                                           "rsort.check", "rsort.bucket", "rsort.fallback"};
+                                                           "rsort.check", "rsort.bucket", "rsort.fallback",
+                                                           "rsort.split"};
         RoctxRange range(label ? label : names[kind]);
         if (!enabled || !((mask >> kind) & 1u)) { launch(); return; }
         Rec r{kind, get(), get()};
@@ -272,7 +282,11 @@ struct rs_plan {
     bool static_passes = false;      // hybrid MSD passes over static splits (sweep only, RSORT_STATIC=1: measured
                                      // slower than the look-back passes)
     uint32_t* msd = nullptr;         // its workspace: hist16 | base16 | segtab | gates | mtot
+    uint32_t* split = nullptr;       // the bucket split's workspace (rs::SplitWs; split_words())
+    uint32_t smax2 = 0, smax3 = 0;   // its level-2 / level-3 segment capacities
+    bool split_on = true;            // split over-full buckets (rs_plan_debug.split = 0: the LSD fallback)
     bool last_hybrid = false;        // the last sort enqueued the hybrid path (rs_plan_last_path)
+    bool last_split = false;         // ... with the bucket split's launches (rs_plan_last_split)
     bool path_none = false;          // the last sort moved nothing (n <= 1): rs_plan_last_path NONE
     int scatter_kind = RS_KERNEL_SCATTER;   // timer kind of the pass launches being enqueued
     uint32_t* host_err = nullptr;  // host-mapped error word: set by a timed-out look-back wait,
@@ -422,7 +436,7 @@ void launch_msd_pass(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint32_
         const uint32_t grid = std::min<uint32_t>(ntiles, p->cus * per_cu);
         hipLaunchKernelGGL(kern, dim3(grid), dim3(BLOCK), 0, s, ik, iv, ok, ov, n, shift, 255u,
                            ntiles, dtot, p->status, ticket, p->tickets + 16, nullptr, 0u, 0u, p->epoch,
-                           gate, 0, nullptr, 0xFFFFFFFFu, p->spin_max, p->host_err_dev, segtab, base16, kbase,
+                           gate, SEG, nullptr, 0xFFFFFFFFu, p->spin_max, p->host_err_dev, segtab, base16, kbase,
                            pmask);
     };
     if (p->rank_mode == rs::RANK_BALLOT)
@@ -664,10 +678,14 @@ rs_status take_device_error(rs_plan* p, const char* what) {
     if (!p->host_err) return RS_OK;
     const uint32_t e = __atomic_exchange_n(p->host_err, 0u, __ATOMIC_ACQ_REL);
     if (e == 0u) return RS_OK;
+    // bit 0: a look-back wait of a one-sweep pass timed out; bit 2: the hybrid path's counts did
+    // not add up (the bucket split's digit counts, or the histogram against n)
     return fail(RS_ERR_DEVICE,
-                "%s: an earlier sort on this plan failed on the device (error word 0x%x: a "
-                "look-back wait of the one-sweep pass timed out); that sort's output is invalid",
-                what, e);
+                "%s: an earlier sort on this plan failed on the device (error word 0x%x: %s); that "
+                "sort's output is invalid", what, e,
+                (e & 4u) ? (e & 1u) ? "a look-back wait timed out and the hybrid path's counts did not add up"
+                                    : "the hybrid path's counts did not add up"
+                         : "a look-back wait of the one-sweep pass timed out");
 }
 
 // Sort entry points need the full workspace (a RS_USAGE_PARTITION plan has no ping-pong copy).
@@ -776,8 +794,9 @@ RS_EXPORT rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out) {
     // look-back status words: one per (tile, digit) of the finest tile configuration in use
     // (the hybrid path's segmented pass: up to one partial tile per top-byte segment on top of
     // the 16K-key tiles, which dominates below ~4M keys)
+    // (and the bucket split's passes: one partial tile per segment on top, see split_smax3)
     const uint64_t max_tiles = std::max<uint64_t>(
-        (d.count + kLarge.tile - 1) / kLarge.tile + 257,
+        (d.count + kLarge.tile - 1) / kLarge.tile + 1 + std::max<uint64_t>(256, split_smax3(d.count)),
         std::max<uint64_t>((d.count + kMinOnesweepTile - 1) / kMinOnesweepTile,
                            (std::min<uint64_t>(d.count, RS_SMALL_MAX) + kSmall.tile - 1) / kSmall.tile));
     // sized whatever RSORT_ONESWEEP says: the records / partition entry points and the hybrid
@@ -811,6 +830,13 @@ RS_EXPORT rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out) {
         (e = alloc(&p->msd, 4ull * kMsdWords)) != hipSuccess)
         return cleanup(fail(e == hipErrorOutOfMemory ? RS_ERR_OUT_OF_MEMORY : RS_ERR_HIP,
                             "rs_plan_create: hipMalloc failed: %s", hipGetErrorString(e)));
+    if (p->msd) {
+        p->smax2 = split_smax2(d.count);
+        p->smax3 = split_smax3(d.count);
+        if ((e = alloc(&p->split, 4ull * split_words(p->smax2, p->smax3))) != hipSuccess)
+            return cleanup(fail(e == hipErrorOutOfMemory ? RS_ERR_OUT_OF_MEMORY : RS_ERR_HIP,
+                                "rs_plan_create: hipMalloc failed: %s", hipGetErrorString(e)));
+    }
     p->tickets = p->ptot + rs::kTotalsMax;   // [16] tickets, [16] error word
 
     if ((e = hipHostMalloc((void**)&p->host_err, 4, hipHostMallocMapped)) != hipSuccess ||
@@ -838,6 +864,7 @@ RS_EXPORT void rs_plan_destroy(rs_plan* p) {
     (void)hipFree(p->ptot);
     (void)hipFree(p->status);
     (void)hipFree(p->msd);
+    (void)hipFree(p->split);
     if (p->host_err) (void)hipHostFree(p->host_err);
     if (p->done) (void)hipEventDestroy(p->done);
     delete p;
@@ -866,6 +893,79 @@ static rs_status enqueue_lsd_gated(rs_plan* p, const uint32_t* sk, const uint32_
                       gate, (int)i, s, /*onesweep=*/true);
     p->scatter_kind = RS_KERNEL_SCATTER;
     return st;
+}
+
+// The bucket split's launches (rs_kernels.hpp, "splitting over-full buckets"; each exits at once
+// unless its gate is set): level 2's counts, its pass R2 -> R3 by byte 1, the sub-buckets' sort
+// R3 -> output (two tiles), level 3's counts and its pass R3 -> output by byte 0.  R2 / R3: records
+// (keys only: keys); output: the caller's arrays, records (out_aos) or keys.
+static rs_status enqueue_split(rs_plan* p, const rs::SplitWs& sw, bool keys, bool out_aos, uint32_t* r2,
+                               uint32_t* r3, uint32_t* uk, uint32_t* uv, uint32_t n32, hipStream_t s) {
+    constexpr int A = rs::LAYOUT_AOS, S = rs::LAYOUT_SOA, K = rs::LAYOUT_KEYS;
+    // the passes' tiles must be the split tables' (kSplitTile): keys only, the 512 x 32 tiles
+    static_assert(kLarge.tile == (int)rs::kSplitTile, "split passes: 16K-record tiles");
+    constexpr bool keys512 = kLargeKeys.tile == (int)rs::kSplitTile;
+    constexpr int KB_ = keys512 ? kLargeKeys.block : kLarge.block, KK = keys512 ? kLargeKeys.kpt : kLarge.kpt;
+    const bool ballot = p->rank_mode == rs::RANK_BALLOT;
+    constexpr int A0 = rs::RANK_LDS_ATOMIC, B0 = rs::RANK_BALLOT;
+    const uint32_t cgrid = 2u * p->cus;
+    auto count = [&](const uint32_t* rec, uint32_t shift, bool level3) {
+        RoctxRange r(level3 ? "rsort.msd.split3_count" : "rsort.msd.split2_count");
+        auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(cgrid), dim3(1024), 0, s, rec, sw, shift); };
+        if (keys) level3 ? go(rs::k_split_count<1, 3>) : go(rs::k_split_count<1, 2>);
+        else level3 ? go(rs::k_split_count<2, 3>) : go(rs::k_split_count<2, 2>);
+    };
+    rs_status st = RS_OK;
+    // one timed span (RS_KERNEL_SPLIT) for the split's launches, each also a roctx range
+    p->timer.run(RS_KERNEL_SPLIT, s, [&] {
+        count(r2, 8u, false);
+        st = next_epoch(p, s);
+        if (st != RS_OK) return;
+        {
+            RoctxRange r("rsort.msd.split2_pass");
+            if (keys)
+                launch_msd_pass<K, K, 2, false, KB_, KK>(p, r2, nullptr, r3, nullptr, n32, 8u, sw.smax2, nullptr,
+                                                         p->tickets + 6, sw.gate2, sw.tab2, sw.rows2, s);
+            else
+                launch_msd_pass<A, A, 2>(p, r2, nullptr, r3, nullptr, n32, 8u, sw.smax2, nullptr, p->tickets + 6,
+                                         sw.gate2, sw.tab2, sw.rows2, s);
+        }
+        {
+            RoctxRange r("rsort.msd.split2_bucket");
+            auto go = [&](auto lo) {
+                constexpr int LO = decltype(lo)::value;
+                auto small = [&](auto kern) {
+                    static const uint32_t per_cu = resident_per_cu(kern, 256);
+                    hipLaunchKernelGGL(kern, dim3(p->cus * per_cu), dim3(256), 0, s, (const uint32_t*)r3, sw, 0u, uk, uv);
+                };
+                auto large = [&](auto kern) {
+                    hipLaunchKernelGGL(kern, dim3(p->cus), dim3(1024), 0, s, (const uint32_t*)r3, sw, rs::kSub8Small, uk, uv);
+                };
+                // (4352-record tiles at 3 workgroups per CU, <= 168 VGPRs; 17408 at one, ranks packed)
+                ballot ? small(rs::k_bucket_sort8<256, 17, B0, LO, 3>) : small(rs::k_bucket_sort8<256, 17, A0, LO, 3>);
+                ballot ? large(rs::k_bucket_sort8<1024, 17, B0, LO, 4, true>) : large(rs::k_bucket_sort8<1024, 17, A0, LO, 4, true>);
+            };
+            if (keys) go(std::integral_constant<int, K>{});
+            else if (out_aos) go(std::integral_constant<int, A>{});
+            else go(std::integral_constant<int, S>{});
+        }
+        count(r3, 0u, true);
+        st = next_epoch(p, s);
+        if (st != RS_OK) return;
+        RoctxRange r("rsort.msd.split3_pass");
+        if (keys)
+            launch_msd_pass<K, K, 2, false, KB_, KK>(p, r3, nullptr, uk, nullptr, n32, 0u, sw.smax3, nullptr,
+                                                     p->tickets + 7, sw.gate3, sw.tab3, sw.rows3, s);
+        else if (out_aos)
+            launch_msd_pass<A, A, 2>(p, r3, nullptr, uk, nullptr, n32, 0u, sw.smax3, nullptr, p->tickets + 7,
+                                     sw.gate3, sw.tab3, sw.rows3, s);
+        else
+            launch_msd_pass<A, S, 2>(p, r3, nullptr, uk, uv, n32, 0u, sw.smax3, nullptr, p->tickets + 7,
+                                     sw.gate3, sw.tab3, sw.rows3, s);
+    }, "rsort.msd.split");
+    if (st != RS_OK) return st;
+    HIP_TRY(hipGetLastError());
+    return RS_OK;
 }
 
 // The hybrid MSD path (rs_kernels.hpp, "hybrid MSD path"): the 16-bit bucket histogram of the
@@ -905,6 +1005,46 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
     uint32_t* top_tot = mtot + 768;
     uint32_t* big = mtot + 1;          // a 16-bit bucket over the large bucket tile
     uint32_t* sstart = segtab + 257;   // top-byte segment starts (bucket bases are relative to them)
+    // the bucket split of over-full 16-bit buckets (whole-range sorts and regions; the key-range form
+    // keeps the LSD fallback): level 2 writes into a records buffer that is free by then (R1, or a
+    // region's tmp2).  Whole-range sorts then enqueue no LSD fallback at all (strict: the device's
+    // checks can only fail on a counting fault, reported as a device error).
+    bool split = p->split && p->split_on && (region ? p->tmp2 != nullptr : (kbase == 0u && vbits == 32u));
+#if RS_SWEEP
+    if (RS_KNOB("RSORT_EXP_RING", 0) > 0) split = false;
+#endif
+    const bool strict = split && !region;
+    p->last_split = split;
+    uint32_t* r3 = region ? p->tmp2 : r1;
+    rs::SplitWs sw{};
+    if (split) {
+        uint32_t* q = p->split;
+        sw.gate2 = q;
+        sw.gate3 = q + 16;
+        q += 32;
+        sw.huge = q;
+        q += 1 + p->smax2;
+        sw.tab2 = q;
+        q += 3ull * p->smax2 + 2;
+        sw.arrive2 = q;
+        q += p->smax2 + 1ull;
+        sw.rows2 = q;
+        q += 256ull * p->smax2;
+        sw.tab3 = q;
+        q += 3ull * p->smax3 + 2;
+        sw.arrive3 = q;
+        q += p->smax3 + 1ull;
+        sw.rows3 = q;
+        sw.smax2 = p->smax2;
+        sw.smax3 = p->smax3;
+        sw.tmax = (uint32_t)std::min<uint64_t>(p->status_words / 256u, 0xFFFFFFFFu);
+        sw.hist16 = hist16;
+        sw.base16 = base16;
+        sw.err = p->tickets + 16;
+        sw.host_err = p->host_err_dev;
+        sw.strict = strict ? 1u : 0u;
+        sw.n = n32;
+    }
     // keys only, pass tile configuration (RSORT_MSD_KEYS_CFG): 0 = 1024 x 16, 1 = 512 x 32 (two
     // workgroups per CU), 2 = 1024 x 32 (32K-key tiles: 512-B digit runs, as long as a 16K-record tile's)
     const int keys_cfg = p->msd_keys_cfg;
@@ -965,14 +1105,17 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
     // workgroups per CU).
     const bool static_p0 = !region && !keys && p->static_passes && hrows <= rs::kMaxRows;
     const bool static_p1 = !keys && p->static_passes;
-    uint32_t* b0rows = chk ? p->tmp_k + (size_t)hrows * 65537u : nullptr;
+    // (the fallback's byte-0 totals: only where a fallback is enqueued)
+    uint32_t* b0rows = (chk && !strict) ? p->tmp_k + (size_t)hrows * 65537u : nullptr;
     if (chk) HIP_TRY(hipMemsetAsync(p->flags, 0, 16 * 4, s));
     p->timer.run(RS_KERNEL_HISTOGRAM, s, [&] {
         if (region) {   // the senders counted: one row, their table
-            hipLaunchKernelGGL(rs::k_region_rows, dim3(256), dim3(256), 0, s, region_hist, p->tmp_k, over, big);
+            hipLaunchKernelGGL(rs::k_region_rows, dim3(256), dim3(256), 0, s, region_hist, p->tmp_k, over, big,
+                               sw.huge);
             hipLaunchKernelGGL(rs::k_hist16_reduce, dim3(256), dim3(1024), 0, s, (const uint32_t*)p->tmp_k,
                                1u, hist16, top_tot, range_bad, base16, small_cap, kBucketCap, over, big,
-                               p->ptot, (uint32_t)(rs::kTotalsMax + 32));
+                               p->ptot, (uint32_t)(rs::kTotalsMax + 32), (const uint32_t*)nullptr,
+                               (uint32_t*)nullptr, sw.huge, p->smax2);
             return;
         }
         // 16-byte aligned records: two per load (sweep: RSORT_HIST16_NARROW=1 keeps one per 8-byte load)
@@ -982,12 +1125,16 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
         const bool full = !generic && kbase == 0u && vbits == 32u;
         auto go = [&](auto kern) {
             hipLaunchKernelGGL(kern, dim3(hrows), dim3(1024), 0, s, sk, n32, p->tmp_k, kbase, range, vbits - 16,
-                               over, big, chk ? p->flags : (uint32_t*)nullptr, b0rows);
+                               over, big, chk ? p->flags : (uint32_t*)nullptr, b0rows, sw.huge);
         };
-        if (chk) {   // check_order: the order check and the fallback's byte-0 totals ride along
-            if (in_aos && !narrow && ((uintptr_t)sk & 15u) == 0) go(rs::k_hist16_in<A, true, true, true>);
-            else if (in_aos) go(rs::k_hist16_in<A, false, true, true>);
-            else go(rs::k_hist16_in<S, false, true, true>);
+        if (chk && b0rows) {   // check_order: the order check and the fallback's byte-0 totals ride along
+            if (in_aos && !narrow && ((uintptr_t)sk & 15u) == 0) go(rs::k_hist16_in<A, true, true, 2>);
+            else if (in_aos) go(rs::k_hist16_in<A, false, true, 2>);
+            else go(rs::k_hist16_in<S, false, true, 2>);
+        } else if (chk) {      // the order check only (no fallback enqueued)
+            if (in_aos && !narrow && ((uintptr_t)sk & 15u) == 0) go(rs::k_hist16_in<A, true, true, 1>);
+            else if (in_aos) go(rs::k_hist16_in<A, false, true, 1>);
+            else go(rs::k_hist16_in<S, false, true, 1>);
         } else if (in_aos && !narrow && ((uintptr_t)sk & 15u) == 0) {
             full ? go(rs::k_hist16_in<A, true, true>) : go(rs::k_hist16_in<A, true>);
         } else if (in_aos) {
@@ -1000,14 +1147,14 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
         hipLaunchKernelGGL(rs::k_hist16_reduce, dim3(256), dim3(1024), 0, s, (const uint32_t*)p->tmp_k,
                            hrows, hist16, top_tot, range_bad, base16, small_cap, kBucketCap, over, big,
                            p->ptot, (uint32_t)(rs::kTotalsMax + 32), (const uint32_t*)b0rows,
-                           static_p0 ? cbase : (uint32_t*)nullptr);
+                           static_p0 ? cbase : (uint32_t*)nullptr, sw.huge, p->smax2);
     }, region ? "rsort.msd.region_table" : "rsort.msd.hist16");
     HIP_TRY(hipGetLastError());
     p->timer.run(RS_KERNEL_SCAN, s, [&] {
         auto plan = [&](auto kern) {
             hipLaunchKernelGGL(kern, dim3(1), dim3(256), 0, s, (const uint32_t*)top_tot, segtab, 0xFFFFFFFFu, over,
                                (const uint32_t*)big, gates, (const uint32_t*)range_bad, n32,
-                               chk ? (const uint32_t*)p->flags : (const uint32_t*)nullptr, top_lo, top_hi);
+                               chk ? (const uint32_t*)p->flags : (const uint32_t*)nullptr, top_lo, top_hi, sw);
         };
         if (tile == 2u * kLarge.tile) plan(rs::k_msd_plan<2 * kLarge.tile>);
         else plan(rs::k_msd_plan<kLarge.tile>);
@@ -1201,6 +1348,9 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
         else both(std::integral_constant<int, S>{});
     }, "rsort.msd.bucket");
     HIP_TRY(hipGetLastError());
+    if (split)
+        if (rs_status st = enqueue_split(p, sw, keys, out_aos, r2, r3, uk, uv, n32, s)) return st;
+    if (strict) return RS_OK;
     // the fallback (gated off on the device unless taken): pass 0's byte-0 totals, then the four
     // LSD passes on the input
     const uint32_t* g_lsd = gates + rs::kGateLsd;
@@ -1434,6 +1584,19 @@ RS_EXPORT rs_status rs_plan_last_path(rs_plan* p, uint32_t* path) {
     HIP_TRY(hipMemcpy(&g[0], gates + rs::kGateMsd, 4, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(&g[1], gates + rs::kGateLsd, 4, hipMemcpyDeviceToHost));
     *path = g[0] ? RS_PATH_HYBRID : g[1] ? RS_PATH_HYBRID_FALLBACK : RS_PATH_IN_ORDER;
+    return RS_OK;
+}
+
+RS_EXPORT rs_status rs_plan_last_split(rs_plan* p, uint32_t* levels) {
+    if (!p || !levels) return fail(RS_ERR_INVALID_ARG, "rs_plan_last_split: null argument");
+    DeviceGuard guard(p->desc.device);
+    *levels = 0;
+    if (!p->done_recorded || p->path_none || !p->last_hybrid || !p->last_split) return RS_OK;
+    HIP_TRY(hipEventSynchronize(p->done));
+    uint32_t g[2] = {0u, 0u};   // gate2, gate3 (first words): SplitWs layout in enqueue_sort_msd
+    HIP_TRY(hipMemcpy(&g[0], p->split, 4, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(&g[1], p->split + 16, 4, hipMemcpyDeviceToHost));
+    *levels = g[1] ? 3u : g[0] ? 2u : 0u;
     return RS_OK;
 }
 
@@ -1677,7 +1840,7 @@ RS_EXPORT rs_status rs_plan_hist16(rs_plan* p, const void* keys, uint64_t n, voi
         uint32_t* z = p->tmp_k + (size_t)hrows * 65536u;
         auto go = [&](auto kern) {
             hipLaunchKernelGGL(kern, dim3(hrows), dim3(1024), 0, s, (const uint32_t*)keys, (uint32_t)n, p->tmp_k, 0u,
-                               0xFFFFFFFFu, 16u, z, z, (uint32_t*)nullptr, (uint32_t*)nullptr);
+                               0xFFFFFFFFu, 16u, z, z, (uint32_t*)nullptr, (uint32_t*)nullptr, (uint32_t*)nullptr);
         };
         if (aos && ((uintptr_t)keys & 15u) == 0) go(rs::k_hist16_in<rs::LAYOUT_AOS, true, true>);
         else if (aos) go(rs::k_hist16_in<rs::LAYOUT_AOS, false, true>);
@@ -1780,7 +1943,7 @@ RS_EXPORT rs_status rs_plan_set_debug(rs_plan* p, const rs_plan_debug* d) {
     auto tri = [](int32_t v, int hi) { return v >= -1 && v <= hi; };
     if (!tri(d->rank, 1) || !tri(d->tile, 1) || !tri(d->onesweep, 1) || !tri(d->msd, 1) ||
         !tri(d->keys_cfg, 1) || !tri(d->msd_keys_cfg, 2) || !tri(d->kbucket_wave, 1) ||
-        !tri(d->selftest_fail, 1))
+        !tri(d->selftest_fail, 1) || !tri(d->split, 1))
         return fail(RS_ERR_INVALID_ARG, "rs_plan_set_debug: every field must be -1 or a listed choice");
     if (d->selftest_fail == 1) {
         p->selftest = 0;
@@ -1793,6 +1956,7 @@ RS_EXPORT rs_status rs_plan_set_debug(rs_plan* p, const rs_plan_debug* d) {
     if (d->keys_cfg >= 0) p->keys_cfg = d->keys_cfg == 1;
     if (d->msd_keys_cfg >= 0) p->msd_keys_cfg = d->msd_keys_cfg;
     if (d->kbucket_wave >= 0) p->kbucket_wave = d->kbucket_wave == 1;
+    if (d->split >= 0) p->split_on = d->split == 1;
     return RS_OK;
 }
 

@@ -30,9 +30,9 @@ RS_FLAG_AVOID_BANK_CONFLICTS = 0x8
 RS_FLAG_INTERLEAVED = 0x10
 
 (RS_KERNEL_HISTOGRAM, RS_KERNEL_SCAN, RS_KERNEL_SCATTER, RS_KERNEL_CHECK, RS_KERNEL_BUCKET,
- RS_KERNEL_FALLBACK) = range(6)
-RS_KERNEL_KINDS = 6
-KERNEL_NAMES = ("histogram", "scan", "scatter", "check", "bucket", "fallback")
+ RS_KERNEL_FALLBACK, RS_KERNEL_SPLIT) = range(7)
+RS_KERNEL_KINDS = 7
+KERNEL_NAMES = ("histogram", "scan", "scatter", "check", "bucket", "fallback", "split")
 # rs_plan_last_path
 PATH_NAMES = ("none", "lsd", "hybrid", "hybrid_fallback", "in_order")
 
@@ -56,7 +56,8 @@ class PlanDebug(ctypes.Structure):
     """rs_plan_debug (test / diagnostics only): force a plan onto one of its paths; -1 = keep."""
     _fields_ = [("rank", ctypes.c_int32), ("tile", ctypes.c_int32), ("onesweep", ctypes.c_int32),
                 ("msd", ctypes.c_int32), ("keys_cfg", ctypes.c_int32), ("msd_keys_cfg", ctypes.c_int32),
-                ("kbucket_wave", ctypes.c_int32), ("selftest_fail", ctypes.c_int32)]
+                ("kbucket_wave", ctypes.c_int32), ("selftest_fail", ctypes.c_int32),
+                ("split", ctypes.c_int32)]
 
 
 # Path overrides applied to every plan the Python wrappers create (tests select kernels with
@@ -156,6 +157,7 @@ _SIGS = {
     "rs_plan_set_profiling": (ctypes.c_int, [_VP, ctypes.c_int]),
     "rs_plan_set_profiling_kinds": (ctypes.c_int, [_VP, ctypes.c_uint32]),
     "rs_plan_last_path": (ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_uint32)]),
+    "rs_plan_last_split": (ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_uint32)]),
     "rs_plan_kernel_times": (ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_double),
                                             ctypes.POINTER(ctypes.c_uint64)]),
     "rs_plan_reset_kernel_times": (ctypes.c_int, [_VP]),

@@ -260,11 +260,18 @@ class RadixSortKernel:
 
     def last_path(self) -> str:
         """Which path the last dispatch took (waits for it): "lsd", "hybrid", "hybrid_fallback"
-        (the device chose the LSD passes: skewed keys), "in_order" (check_order: nothing moved) or
-        "none" (rs_plan_last_path)."""
+        (the device chose the LSD passes), "in_order" (check_order: nothing moved) or "none"
+        (rs_plan_last_path)."""
         v = ctypes.c_uint32()
         check(_lib.load().rs_plan_last_path(self._plan, ctypes.byref(v)), "last_path")
         return _lib.PATH_NAMES[v.value]
+
+    def last_split(self) -> int:
+        """How deep the hybrid path's last dispatch split over-full 16-bit buckets (skewed keys):
+        0, 2 (by byte 1) or 3 (some sub-buckets by byte 0 too) (rs_plan_last_split)."""
+        v = ctypes.c_uint32()
+        check(_lib.load().rs_plan_last_split(self._plan, ctypes.byref(v)), "last_split")
+        return int(v.value)
 
     def kernel_times(self, reset: bool = False) -> dict:
         ms = (ctypes.c_double * _lib.RS_KERNEL_KINDS)()

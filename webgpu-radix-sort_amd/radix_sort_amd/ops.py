@@ -89,6 +89,12 @@ class SortPlan:
         check(_lib.load().rs_plan_last_path(self._plan, ctypes.byref(v)), "last_path")
         return _lib.PATH_NAMES[v.value]
 
+    def last_split(self) -> int:
+        """The bucket split depth of the plan's last sort: 0, 2 or 3 (rs_plan_last_split)."""
+        v = ctypes.c_uint32()
+        check(_lib.load().rs_plan_last_split(self._plan, ctypes.byref(v)), "last_split")
+        return int(v.value)
+
     def kernel_times(self) -> dict:
         """Accumulated per-kind kernel times of the plan's launches (after set_profiling)."""
         ms = (ctypes.c_double * _lib.RS_KERNEL_KINDS)()

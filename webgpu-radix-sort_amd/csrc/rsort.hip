@@ -136,8 +136,12 @@ constexpr uint64_t kMsdWords = 65536ull * 2 + 1024 + 64 + 1024 + 1 + rs::kOverMa
 // [smax + 1] and rows [256 smax].
 inline uint32_t split_smax2(uint64_t cap) { return (uint32_t)(cap / (kBucketCap + 1ull) + 1); }
 inline uint32_t split_smax3(uint64_t cap) { return (uint32_t)(cap / (rs::kSub8Cap + 1ull) + 1); }
-inline uint64_t split_words(uint32_t s2, uint32_t s3) {
-    return 32ull + 1 + s2 + (3ull * s2 + 2) + (s2 + 1ull) + 256ull * s2 + (3ull * s3 + 2) + (s3 + 1ull) + 256ull * s3;
+// level 2's tiles (each huge bucket's records in 16K-record tiles: at most one partial per bucket)
+inline uint32_t split_tiles2(uint64_t cap) { return (uint32_t)(cap / rs::kSplitTile + split_smax2(cap) + 1); }
+inline uint64_t split_words(uint64_t cap) {
+    const uint64_t s2 = split_smax2(cap), s3 = split_smax3(cap);
+    return 32ull + 1 + s2 + (3ull * s2 + 2) + (s2 + 1ull) + 256ull * s2 + (3ull * s3 + 2) + (s3 + 1ull) + 256ull * s3 +
+           s3 + 128ull * split_tiles2(cap);   // + level-3 parents, level 2's per-tile digit starts (u16)
 }
 constexpr uint32_t kHistGrid = 2048;
 constexpr int kCheckGrid = 2048;
@@ -284,6 +288,7 @@ struct rs_plan {
     uint32_t* msd = nullptr;         // its workspace: hist16 | base16 | segtab | gates | mtot
     uint32_t* split = nullptr;       // the bucket split's workspace (rs::SplitWs; split_words())
     uint32_t smax2 = 0, smax3 = 0;   // its level-2 / level-3 segment capacities
+    uint32_t tiles2 = 0;             // level 2's tile capacity (per-tile digit starts)
     bool split_on = true;            // split over-full buckets (rs_plan_debug.split = 0: the LSD fallback)
     bool last_hybrid = false;        // the last sort enqueued the hybrid path (rs_plan_last_path)
     bool last_split = false;         // ... with the bucket split's launches (rs_plan_last_split)
@@ -833,7 +838,8 @@ RS_EXPORT rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out) {
     if (p->msd) {
         p->smax2 = split_smax2(d.count);
         p->smax3 = split_smax3(d.count);
-        if ((e = alloc(&p->split, 4ull * split_words(p->smax2, p->smax3))) != hipSuccess)
+        p->tiles2 = split_tiles2(d.count);
+        if ((e = alloc(&p->split, 4ull * split_words(d.count))) != hipSuccess)
             return cleanup(fail(e == hipErrorOutOfMemory ? RS_ERR_OUT_OF_MEMORY : RS_ERR_HIP,
                                 "rs_plan_create: hipMalloc failed: %s", hipGetErrorString(e)));
     }
@@ -902,66 +908,70 @@ static rs_status enqueue_lsd_gated(rs_plan* p, const uint32_t* sk, const uint32_
 static rs_status enqueue_split(rs_plan* p, const rs::SplitWs& sw, bool keys, bool out_aos, uint32_t* r2,
                                uint32_t* r3, uint32_t* uk, uint32_t* uv, uint32_t n32, hipStream_t s) {
     constexpr int A = rs::LAYOUT_AOS, S = rs::LAYOUT_SOA, K = rs::LAYOUT_KEYS;
-    // the passes' tiles must be the split tables' (kSplitTile): keys only, the 512 x 32 tiles
+    // level 3's pass tiles must be the split tables' (kSplitTile): keys only, the 512 x 32 tiles
     static_assert(kLarge.tile == (int)rs::kSplitTile, "split passes: 16K-record tiles");
     constexpr bool keys512 = kLargeKeys.tile == (int)rs::kSplitTile;
     constexpr int KB_ = keys512 ? kLargeKeys.block : kLarge.block, KK = keys512 ? kLargeKeys.kpt : kLarge.kpt;
     const bool ballot = p->rank_mode == rs::RANK_BALLOT;
     constexpr int A0 = rs::RANK_LDS_ATOMIC, B0 = rs::RANK_BALLOT;
-    const uint32_t cgrid = 2u * p->cus;
-    auto count = [&](const uint32_t* rec, uint32_t shift, bool level3) {
-        RoctxRange r(level3 ? "rsort.msd.split3_count" : "rsort.msd.split2_count");
-        auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(cgrid), dim3(1024), 0, s, rec, sw, shift); };
-        if (keys) level3 ? go(rs::k_split_count<1, 3>) : go(rs::k_split_count<1, 2>);
-        else level3 ? go(rs::k_split_count<2, 3>) : go(rs::k_split_count<2, 2>);
-    };
     rs_status st = RS_OK;
     // one timed span (RS_KERNEL_SPLIT) for the split's launches, each also a roctx range
     p->timer.run(RS_KERNEL_SPLIT, s, [&] {
-        count(r2, 8u, false);
-        st = next_epoch(p, s);
-        if (st != RS_OK) return;
         {
-            RoctxRange r("rsort.msd.split2_pass");
-            if (keys)
-                launch_msd_pass<K, K, 2, false, KB_, KK>(p, r2, nullptr, r3, nullptr, n32, 8u, sw.smax2, nullptr,
-                                                         p->tickets + 6, sw.gate2, sw.tab2, sw.rows2, s);
-            else
-                launch_msd_pass<A, A, 2>(p, r2, nullptr, r3, nullptr, n32, 8u, sw.smax2, nullptr, p->tickets + 6,
-                                         sw.gate2, sw.tab2, sw.rows2, s);
+            RoctxRange r("rsort.msd.split2_local");
+            auto go = [&](auto kern) {
+                static const uint32_t per_cu = resident_per_cu(kern, 1024);
+                hipLaunchKernelGGL(kern, dim3(p->cus * per_cu), dim3(1024), 0, s, (const uint32_t*)r2, r3, sw);
+            };
+            if (keys) ballot ? go(rs::k_split_local<1024, 16, K, B0>) : go(rs::k_split_local<1024, 16, K, A0>);
+            else ballot ? go(rs::k_split_local<1024, 16, A, B0>) : go(rs::k_split_local<1024, 16, A, A0>);
         }
-        {
-            RoctxRange r("rsort.msd.split2_bucket");
-            auto go = [&](auto lo) {
-                constexpr int LO = decltype(lo)::value;
+        auto out3 = [&](auto lo) {
+            constexpr int LO = decltype(lo)::value;
+            {
+                RoctxRange r("rsort.msd.split2_bucket");
+                // one sub-bucket per workgroup (65536 of them: 256 huge buckets; more are taken
+                // grid-stride), so the hardware overlaps the workgroups' load latencies
                 auto small = [&](auto kern) {
-                    static const uint32_t per_cu = resident_per_cu(kern, 256);
-                    hipLaunchKernelGGL(kern, dim3(p->cus * per_cu), dim3(256), 0, s, (const uint32_t*)r3, sw, 0u, uk, uv);
+                    const uint32_t grid = (uint32_t)std::min<uint64_t>(65536u, 256ull * sw.smax2);
+                    hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, s, (const uint32_t*)r3, sw, 0u, uk, uv);
                 };
                 auto large = [&](auto kern) {
-                    hipLaunchKernelGGL(kern, dim3(p->cus), dim3(1024), 0, s, (const uint32_t*)r3, sw, rs::kSub8Small, uk, uv);
+                    static const uint32_t per_cu = resident_per_cu(kern, 512);
+                    hipLaunchKernelGGL(kern, dim3(p->cus * per_cu), dim3(512), 0, s, (const uint32_t*)r3, sw,
+                                       rs::kSub8Small, uk, uv);
                 };
-                // (4352-record tiles at 3 workgroups per CU, <= 168 VGPRs; 17408 at one, ranks packed)
+                // 4352-record tiles at 3 workgroups per CU (<= 168 VGPRs); 512 x 34 = 17408 at one
+                // (two waves per SIMD: <= 256 VGPRs)
                 ballot ? small(rs::k_bucket_sort8<256, 17, B0, LO, 3>) : small(rs::k_bucket_sort8<256, 17, A0, LO, 3>);
-                ballot ? large(rs::k_bucket_sort8<1024, 17, B0, LO, 4, true>) : large(rs::k_bucket_sort8<1024, 17, A0, LO, 4, true>);
-            };
-            if (keys) go(std::integral_constant<int, K>{});
-            else if (out_aos) go(std::integral_constant<int, A>{});
-            else go(std::integral_constant<int, S>{});
-        }
-        count(r3, 0u, true);
-        st = next_epoch(p, s);
-        if (st != RS_OK) return;
-        RoctxRange r("rsort.msd.split3_pass");
-        if (keys)
-            launch_msd_pass<K, K, 2, false, KB_, KK>(p, r3, nullptr, uk, nullptr, n32, 0u, sw.smax3, nullptr,
-                                                     p->tickets + 7, sw.gate3, sw.tab3, sw.rows3, s);
-        else if (out_aos)
-            launch_msd_pass<A, A, 2>(p, r3, nullptr, uk, nullptr, n32, 0u, sw.smax3, nullptr, p->tickets + 7,
-                                     sw.gate3, sw.tab3, sw.rows3, s);
-        else
-            launch_msd_pass<A, S, 2>(p, r3, nullptr, uk, uv, n32, 0u, sw.smax3, nullptr, p->tickets + 7,
-                                     sw.gate3, sw.tab3, sw.rows3, s);
+                ballot ? large(rs::k_bucket_sort8<512, 34, B0, LO, 2>) : large(rs::k_bucket_sort8<512, 34, A0, LO, 2>);
+            }
+            {
+                RoctxRange r("rsort.msd.split3");
+                hipLaunchKernelGGL(rs::k_split_gather3<LO>, dim3(2u * p->cus), dim3(256), 0, s, (const uint32_t*)r3,
+                                   sw, uk, uv);
+                constexpr int KS = LO == A ? 2 : 1;
+                hipLaunchKernelGGL((rs::k_split_count<KS, 3>), dim3(2u * p->cus), dim3(1024), 0, s, (const uint32_t*)uk,
+                                   sw, 0u);
+                st = next_epoch(p, s);
+                if (st != RS_OK) return;
+                // out -> R3 by byte 0, then back
+                if constexpr (LO == K)
+                    launch_msd_pass<K, K, 2, false, KB_, KK>(p, uk, nullptr, r3, nullptr, n32, 0u, sw.smax3, nullptr,
+                                                             p->tickets + 7, sw.gate3, sw.tab3, sw.rows3, s);
+                else if constexpr (LO == A)
+                    launch_msd_pass<A, A, 2>(p, uk, nullptr, r3, nullptr, n32, 0u, sw.smax3, nullptr, p->tickets + 7,
+                                             sw.gate3, sw.tab3, sw.rows3, s);
+                else
+                    launch_msd_pass<S, A, 2>(p, uk, uv, r3, nullptr, n32, 0u, sw.smax3, nullptr, p->tickets + 7,
+                                             sw.gate3, sw.tab3, sw.rows3, s);
+                hipLaunchKernelGGL(rs::k_split_copy3<LO>, dim3(2u * p->cus), dim3(256), 0, s, (const uint32_t*)r3, sw,
+                                   uk, uv);
+            }
+        };
+        if (keys) out3(std::integral_constant<int, K>{});
+        else if (out_aos) out3(std::integral_constant<int, A>{});
+        else out3(std::integral_constant<int, S>{});
     }, "rsort.msd.split");
     if (st != RS_OK) return st;
     HIP_TRY(hipGetLastError());
@@ -1035,6 +1045,11 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
         sw.arrive3 = q;
         q += p->smax3 + 1ull;
         sw.rows3 = q;
+        q += 256ull * p->smax3;
+        sw.l3par = q;
+        q += p->smax3;
+        sw.tdig = reinterpret_cast<uint16_t*>(q);
+        sw.tdig_tiles = p->tiles2;
         sw.smax2 = p->smax2;
         sw.smax3 = p->smax3;
         sw.tmax = (uint32_t)std::min<uint64_t>(p->status_words / 256u, 0xFFFFFFFFu);
@@ -2001,9 +2016,21 @@ RS_EXPORT rs_status rs_plan_reset_kernel_times(rs_plan* p) {
 namespace {
 constexpr int kScanTile = 4096;
 constexpr uint32_t kScanMaxGrid = 1024;
-// single-pass scan: 256 threads x 16 contiguous elements = 4096-element tiles, 8 workgroups per CU
-constexpr int kScanBlock = 256, kScanEpt = 16;
+// single-pass scan (k_scan_lookback): 1024 threads x 16 contiguous elements = 16K-element tiles, two
+// workgroups per CU, the next tile prefetched across the look-back (4096-element tiles were bound
+// by the look-back chain at 2 TB/s, see the kernel)
+#ifndef RS_SCAN_BLOCK
+#define RS_SCAN_BLOCK 1024
+#endif
+#ifndef RS_SCAN_EPT
+#define RS_SCAN_EPT 16
+#endif
+#ifndef RS_SCAN_PF
+#define RS_SCAN_PF 1
+#endif
+constexpr int kScanBlock = RS_SCAN_BLOCK, kScanEpt = RS_SCAN_EPT;
 constexpr uint32_t kScanLbTile = kScanBlock * kScanEpt;
+constexpr uint32_t kScanPerCu = 2048 / kScanBlock;   // resident workgroups per CU (32 waves)
 struct Geometry { uint32_t grid, base, extra; };
 Geometry geometry(uint64_t n, uint32_t tile, uint32_t max_grid) {
     const uint64_t tiles = (n + tile - 1) / tile;
@@ -2042,7 +2069,7 @@ RS_EXPORT rs_status rs_scan_plan_create(int32_t device, uint64_t count, uint32_t
         if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
             cus = prop.multiProcessorCount;
     }
-    p->grid = (uint32_t)std::min<uint64_t>(p->status_words, 8ull * cus);
+    p->grid = (uint32_t)std::min<uint64_t>(p->status_words, (uint64_t)kScanPerCu * cus);
     hipError_t e = hipMalloc((void**)&p->sums, 4ull * kScanMaxGrid);
     if (e == hipSuccess) e = hipMalloc((void**)&p->status, 8ull * p->status_words);
     if (e == hipSuccess) e = hipMalloc((void**)&p->tickets, 4ull * (rs::kScanTickets + 1));
@@ -2071,8 +2098,8 @@ static rs_status scan_run(rs_scan_plan* p, void* data, const uint32_t* ind, hipS
             hipLaunchKernelGGL(kern, dim3(p->grid), dim3(kScanBlock), 0, s, (uint32_t*)data, (uint32_t)n,
                                p->status, p->tickets, p->epoch, p->tickets + rs::kScanTickets, p->spin_max, ind);
         };
-        if (vec) go(rs::k_scan_lookback<kScanBlock, kScanEpt, true>);
-        else go(rs::k_scan_lookback<kScanBlock, kScanEpt, false>);
+        if (vec) go(rs::k_scan_lookback<kScanBlock, kScanEpt, true, RS_SCAN_PF != 0>);
+        else go(rs::k_scan_lookback<kScanBlock, kScanEpt, false, RS_SCAN_PF != 0>);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(p->done, s));
         return RS_OK;

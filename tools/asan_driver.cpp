@@ -73,6 +73,10 @@ static void sort_case(size_t n, bool kv, uint32_t flags_extra, uint32_t key_mask
         // (a count of 0 or 1 enqueues nothing: no sort to report)
         CHECK(n < 2 ? path == RS_PATH_NONE : (path >= RS_PATH_LSD && path <= RS_PATH_IN_ORDER),
               "last_path after a sort of %zu: %u", n, path);
+        uint32_t levels = 99;
+        OK(rs_plan_last_split(p, &levels));
+        CHECK(levels == 0 || levels == 2 || levels == 3, "last_split: %u", levels);
+        CHECK(rs_plan_last_split(p, nullptr) == RS_ERR_INVALID_ARG, "null levels accepted");
         double ms[RS_KERNEL_KINDS];
         uint64_t launches[RS_KERNEL_KINDS];
         OK(rs_plan_kernel_times(p, ms, launches));
@@ -98,6 +102,9 @@ static void sort_case(size_t n, bool kv, uint32_t flags_extra, uint32_t key_mask
         CHECK(rs_plan_set_debug(p, &dbg) == RS_ERR_INVALID_ARG, "bad debug field accepted");
         CHECK(rs_plan_set_debug(p, nullptr) == RS_ERR_INVALID_ARG, "null debug accepted");
         dbg.tile = -1;
+        dbg.split = 2;
+        CHECK(rs_plan_set_debug(p, &dbg) == RS_ERR_INVALID_ARG, "bad split field accepted");
+        dbg.split = 0;
         dbg.rank = 1;
         dbg.msd = 0;
         OK(rs_plan_set_debug(p, &dbg));

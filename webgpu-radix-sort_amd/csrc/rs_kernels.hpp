@@ -1791,6 +1791,8 @@ struct SplitWs {
     uint16_t* tdig = nullptr;        // [tdig_tiles][256] level 2's per-tile digit starts (k_split_local)
     uint32_t tdig_tiles = 0;
     uint32_t* l3par = nullptr;       // [smax3] level 3's parents: (huge bucket << 8) | byte 1
+    uint32_t* mid = nullptr;         // [1 + midmax] count, then the sub-buckets for the large tile
+    uint32_t midmax = 0;
 };
 
 __device__ __forceinline__ void split_fail(const SplitWs& sw) {
@@ -1893,7 +1895,10 @@ __global__ __launch_bounds__(256) void k_msd_plan(const uint32_t* __restrict__ t
     if (sw.strict && run && !ok && tid == 0) split_fail(sw);
     if (sw.huge) {
         set_gate(sw.gate3, 0u);
-        if (tid == 0) sw.tab3[0] = 0u;
+        if (tid == 0) {
+            sw.tab3[0] = 0u;
+            sw.mid[0] = 0u;
+        }
         uint32_t n2 = 0;
         if (ok & run & (nhuge ? 1u : 0u))   // uniform
             n2 = split_layout<256>(nhuge, sw.smax2, sw.tab2, sw.rows2, sw.arrive2, sw,
@@ -2241,13 +2246,14 @@ __device__ __forceinline__ void split_piece(const SplitWs& sw, uint32_t sg, uint
     len = b >= a && b <= nv ? b - a : 0u;   // (never otherwise: a counting fault, reported)
 }
 
-// The level-2 sub-buckets (sg, d) of min_cnt < count <= BLOCK x KPT records: their pieces gathered
-// from R3 into LDS (tile order: stable), sorted by byte 0 in one LDS pass, written to the output as
-// one run at [rows2[sg][d], +count) (sub-buckets over kSub8Cap: level 3's, k_split_gather3).  One
-// sub-bucket per workgroup (grid-stride beyond the grid).  LO: the output layout (the caller's
-// arrays, records, or keys); R3 holds records (keys, LO = KEYS).
-template <int BLOCK, int KPT, int RANK, int LO, int MW = 1, bool PACK = false>
-__global__ __launch_bounds__(BLOCK, MW) void k_bucket_sort8(const uint32_t* rec, SplitWs sw, uint32_t min_cnt,
+// The level-2 sub-buckets (sg, d) of up to BLOCK x KPT records: their pieces gathered from R3
+// (tile order: stable), sorted by byte 0 in one LDS pass, written to the output as one run at
+// [rows2[sg][d], +count) (sub-buckets over kSub8Cap: level 3's, k_split_gather3).  LISTED = false:
+// every sub-bucket, one per workgroup (grid-stride beyond the grid); those over this tile but within
+// kSub8Cap are listed in sw.mid for the LISTED = true launch (a larger tile on a small grid).  LO: the
+// output layout (the caller's arrays, records, or keys); R3 holds records (keys, LO = KEYS).
+template <int BLOCK, int KPT, int RANK, int LO, int MW = 1, bool PACK = false, bool LISTED = false>
+__global__ __launch_bounds__(BLOCK, MW) void k_bucket_sort8(const uint32_t* rec, SplitWs sw,
                                                             uint32_t* out_k, uint32_t* __restrict__ out_v) {
     constexpr int NW = BLOCK / 64, TILE = BLOCK * KPT, WAVE_KEYS = 64 * KPT;
     constexpr bool KV = LO != LAYOUT_KEYS;
@@ -2263,13 +2269,24 @@ __global__ __launch_bounds__(BLOCK, MW) void k_bucket_sort8(const uint32_t* rec,
     const uint32_t wbase = w * WAVE_KEYS;
     const uint32_t nseg = sw.tab2[0];
     const uint32_t* end = sw.tab2 + 2 + 2 * sw.smax2;
-    for (uint32_t it = blockIdx.x; it < nseg * 256u; it += gridDim.x) {
+    const uint32_t nmid = LISTED ? (sw.mid[0] < sw.midmax ? sw.mid[0] : sw.midmax) : 0u;
+    const uint32_t nit = LISTED ? nmid : nseg * 256u;
+    for (uint32_t ii = blockIdx.x; ii < nit; ii += gridDim.x) {
+        const uint32_t it = LISTED ? sw.mid[1 + ii] : ii;
         const uint32_t sg = it >> 8, d = it & 255u;
         const uint32_t base = sw.rows2[it];
         const uint32_t nxt = d == 255u ? end[sg] : sw.rows2[it + 1];
         const uint32_t cnt = nxt - base;
-        if (cnt <= min_cnt || cnt > (uint32_t)TILE) continue;   // the other launch's, or level 3's
+        if (cnt == 0u || cnt > kSub8Cap) continue;              // empty, or level 3's
         if (nxt > sw.n || base > nxt) continue;                 // (never: a counting fault, reported)
+        if (cnt > (uint32_t)TILE) {                             // the large tile's (LISTED: never)
+            if (!LISTED && tid == 0) {
+                const uint32_t slot = atomicAdd(&sw.mid[0], 1u);
+                if (slot < sw.midmax) sw.mid[1 + slot] = it;
+                else split_fail(sw);
+            }
+            continue;
+        }
         // gather straight into the registers: slot j of lane l of wave w = sub-bucket position
         // q = w * WAVE_KEYS + j * 64 + l (the layout the rank below expects), found in the piece
         // table (tile order: stable) by a walk from the previous slot's piece; per round the
@@ -2634,6 +2651,9 @@ __global__ __launch_bounds__(BLOCK, MW) void k_bucket_sort(const uint32_t* rec,
 // 1024 x 34 = one workgroup per CU, 512 x 34 two, 512 x 18 three).  VREG: the values ride in
 // registers through the sort (else the bucket's records are read again, from L2 / Infinity Cache,
 // for the value exchange).
+#ifndef RS_WIDE_GATHER
+#define RS_WIDE_GATHER 0   // sweep: 1 = values gathered from the records (see below)
+#endif
 template <int BLOCK, int KPT, int RANK, int LO, int MW = 4, bool VREG = false>
 __global__ __launch_bounds__(BLOCK, MW) void k_bucket_sort_wide(const uint32_t* rec,
                                                               const uint32_t* __restrict__ hist16,
@@ -2727,8 +2747,10 @@ __global__ __launch_bounds__(BLOCK, MW) void k_bucket_sort_wide(const uint32_t* 
         // the values to their sorted positions: the bucket's records are read again (this
         // workgroup read them moments ago: Infinity Cache / L2) into LDS by position, then each
         // sorted slot gathers its value by the position in w (holding the values in registers
-        // through the sort spilled)
-        if (KV) {
+        // through the sort spilled).  GATHER (separate output arrays: R2 is not the output): each
+        // sorted slot reads its value straight from the record instead (no LDS round).
+        constexpr bool GATHER = RS_WIDE_GATHER && KV && !VR && LO == LAYOUT_SOA;
+        if (KV && !GATHER) {
             const int lim = (int)cnt - (int)(wbase + lane);
             const uint2* sr = reinterpret_cast<const uint2*>(src) + wbase + lane;
             uint32_t* sw = s_w + wbase + lane;
@@ -2750,7 +2772,8 @@ __global__ __launch_bounds__(BLOCK, MW) void k_bucket_sort_wide(const uint32_t* 
             for (int j = 0; j < KPT; ++j) {
                 if (j * 64 < lim) {
                     const uint32_t key = (KV ? (hi | (x[j] >> 16)) : x[j]) + kbase;
-                    const uint32_t val = KV ? s_w[x[j] & 0xFFFFu] : 0u;
+                    const uint32_t val = GATHER ? reinterpret_cast<const uint2*>(src)[x[j] & 0xFFFFu].y
+                                         : KV ? s_w[x[j] & 0xFFFFu] : 0u;
                     if constexpr (LO == LAYOUT_AOS) {
                         oa[j * 64] = make_uint2(key, val);
                     } else {

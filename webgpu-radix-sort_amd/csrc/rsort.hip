@@ -137,11 +137,13 @@ constexpr uint64_t kMsdWords = 65536ull * 2 + 1024 + 64 + 1024 + 1 + rs::kOverMa
 inline uint32_t split_smax2(uint64_t cap) { return (uint32_t)(cap / (kBucketCap + 1ull) + 1); }
 inline uint32_t split_smax3(uint64_t cap) { return (uint32_t)(cap / (rs::kSub8Cap + 1ull) + 1); }
 // level 2's tiles (each huge bucket's records in 16K-record tiles: at most one partial per bucket)
+inline uint32_t split_midmax(uint64_t cap) { return (uint32_t)(cap / (rs::kSub8Small + 1ull) + 1); }
 inline uint32_t split_tiles2(uint64_t cap) { return (uint32_t)(cap / rs::kSplitTile + split_smax2(cap) + 1); }
 inline uint64_t split_words(uint64_t cap) {
     const uint64_t s2 = split_smax2(cap), s3 = split_smax3(cap);
     return 32ull + 1 + s2 + (3ull * s2 + 2) + (s2 + 1ull) + 256ull * s2 + (3ull * s3 + 2) + (s3 + 1ull) + 256ull * s3 +
-           s3 + 128ull * split_tiles2(cap);   // + level-3 parents, level 2's per-tile digit starts (u16)
+           s3 + 128ull * split_tiles2(cap) +   // + level-3 parents, level 2's per-tile digit starts (u16)
+           1ull + split_midmax(cap);           // + the sub-buckets for the large tile
 }
 constexpr uint32_t kHistGrid = 2048;
 constexpr int kCheckGrid = 2048;
@@ -934,17 +936,17 @@ static rs_status enqueue_split(rs_plan* p, const rs::SplitWs& sw, bool keys, boo
                 // grid-stride), so the hardware overlaps the workgroups' load latencies
                 auto small = [&](auto kern) {
                     const uint32_t grid = (uint32_t)std::min<uint64_t>(65536u, 256ull * sw.smax2);
-                    hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, s, (const uint32_t*)r3, sw, 0u, uk, uv);
+                    hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, s, (const uint32_t*)r3, sw, uk, uv);
                 };
-                auto large = [&](auto kern) {
+                auto large = [&](auto kern) {   // the sub-buckets the first launch listed
                     static const uint32_t per_cu = resident_per_cu(kern, 512);
-                    hipLaunchKernelGGL(kern, dim3(p->cus * per_cu), dim3(512), 0, s, (const uint32_t*)r3, sw,
-                                       rs::kSub8Small, uk, uv);
+                    hipLaunchKernelGGL(kern, dim3(p->cus * per_cu), dim3(512), 0, s, (const uint32_t*)r3, sw, uk, uv);
                 };
                 // 4352-record tiles at 3 workgroups per CU (<= 168 VGPRs); 512 x 34 = 17408 at one
                 // (two waves per SIMD: <= 256 VGPRs)
                 ballot ? small(rs::k_bucket_sort8<256, 17, B0, LO, 3>) : small(rs::k_bucket_sort8<256, 17, A0, LO, 3>);
-                ballot ? large(rs::k_bucket_sort8<512, 34, B0, LO, 2>) : large(rs::k_bucket_sort8<512, 34, A0, LO, 2>);
+                ballot ? large(rs::k_bucket_sort8<512, 34, B0, LO, 2, false, true>)
+                       : large(rs::k_bucket_sort8<512, 34, A0, LO, 2, false, true>);
             }
             {
                 RoctxRange r("rsort.msd.split3");
@@ -1050,6 +1052,9 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
         q += p->smax3;
         sw.tdig = reinterpret_cast<uint16_t*>(q);
         sw.tdig_tiles = p->tiles2;
+        q += 128ull * p->tiles2;
+        sw.mid = q;
+        sw.midmax = split_midmax(p->capacity);
         sw.smax2 = p->smax2;
         sw.smax3 = p->smax3;
         sw.tmax = (uint32_t)std::min<uint64_t>(p->status_words / 256u, 0xFFFFFFFFu);

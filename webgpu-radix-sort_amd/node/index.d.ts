@@ -114,6 +114,10 @@ export declare class RadixSortKernel {
   dispatch(pass?: ComputePass): void;
   /** Waits for the last sort; throws if a sort failed on the device since the last check. */
   check(): void;
+  /** The path the last sort took (waits for it; rs_plan_last_path). */
+  lastPath(): "none" | "lsd" | "hybrid" | "hybrid_fallback" | "in_order";
+  /** How deep the last hybrid sort split over-full 16-bit buckets: 0, 2 or 3 (rs_plan_last_split). */
+  lastSplit(): 0 | 2 | 3;
   destroy(): void;
 }
 export declare class RadixSortBufferKernel extends RadixSortKernel {}
@@ -138,6 +142,8 @@ export declare class RadixSortTextureKernel {
   readonly info: PlanInfo;
   dispatch(pass?: ComputePass): void;
   check(): void;
+  lastPath(): "none" | "lsd" | "hybrid" | "hybrid_fallback" | "in_order";
+  lastSplit(): 0 | 2 | 3;
   destroy(): void;
 }
 

@@ -335,6 +335,12 @@ class RadixSortKernel {
    * last check (its output is invalid; rs_plan_check). */
   check() { if (this._plan) addon.planCheck(this._plan); }
 
+  /** The path the last sort took (waits for it): "lsd", "hybrid", "hybrid_fallback", "in_order". */
+  lastPath() { return addon.planLastPath(this._plan); }
+
+  /** How deep the last hybrid sort split over-full 16-bit buckets (skewed keys): 0, 2 or 3. */
+  lastSplit() { return addon.planLastSplit(this._plan); }
+
   get workgroupCount() { return Math.ceil(this.count / this.threadsPerWorkgroup); }
 
   get info() { return addon.planInfo(this._plan); }
@@ -401,6 +407,10 @@ class RadixSortTextureKernel {
   get hasValues() { return true; }
 
   check() { if (this._plan) addon.planCheck(this._plan); }
+
+  lastPath() { return addon.planLastPath(this._plan); }
+
+  lastSplit() { return addon.planLastSplit(this._plan); }
 
   get info() { return addon.planInfo(this._plan); }
 

@@ -460,6 +460,35 @@ napi_value PlanCheck(napi_env env, napi_callback_info info) {
     return nullptr;
 }
 
+// planLastPath(plan): the path the plan's last sort took ("none", "lsd", "hybrid",
+// "hybrid_fallback", "in_order"; rs_plan_last_path, waits for it)
+napi_value PlanLastPath(napi_env env, napi_callback_info info) {
+    napi_value a[1];
+    if (!args(env, info, a)) return nullptr;
+    PlanBox* b = box_of<PlanBox>(env, a[0]);
+    if (!b || !b->plan) return napi_throw_error(env, nullptr, "plan destroyed"), nullptr;
+    uint32_t path = 0;
+    RS_CALL(env, rs_plan_last_path(b->plan, &path), "lastPath");
+    static const char* const names[] = {"none", "lsd", "hybrid", "hybrid_fallback", "in_order"};
+    napi_value v;
+    napi_create_string_utf8(env, path < 5 ? names[path] : "unknown", NAPI_AUTO_LENGTH, &v);
+    return v;
+}
+
+// planLastSplit(plan): 0, 2 or 3 - how deep the last hybrid sort split over-full 16-bit buckets
+// (rs_plan_last_split)
+napi_value PlanLastSplit(napi_env env, napi_callback_info info) {
+    napi_value a[1];
+    if (!args(env, info, a)) return nullptr;
+    PlanBox* b = box_of<PlanBox>(env, a[0]);
+    if (!b || !b->plan) return napi_throw_error(env, nullptr, "plan destroyed"), nullptr;
+    uint32_t levels = 0;
+    RS_CALL(env, rs_plan_last_split(b->plan, &levels), "lastSplit");
+    napi_value v;
+    napi_create_uint32(env, levels, &v);
+    return v;
+}
+
 napi_value ScanPlanCheck(napi_env env, napi_callback_info info) {
     napi_value a[1];
     if (!args(env, info, a)) return nullptr;
@@ -724,6 +753,8 @@ napi_value Init(napi_env env, napi_value exports) {
     Define(env, exports, "scanPlanRunIndirect", ScanPlanRunIndirect);
     Define(env, exports, "scanPlanDispatchChain", ScanPlanDispatchChain);
     Define(env, exports, "planCheck", PlanCheck);
+    Define(env, exports, "planLastPath", PlanLastPath);
+    Define(env, exports, "planLastSplit", PlanLastSplit);
     Define(env, exports, "scanPlanDestroy", ScanPlanDestroy);
     Define(env, exports, "groupCreate", GroupCreate);
     Define(env, exports, "groupSort", GroupSort);

@@ -132,6 +132,42 @@ async function testTextureSort(device, rand) {
   return cases;
 }
 
+// Skewed f32 keys on the hybrid path (>= 12M: half of the keys in [0, 1) share 128 16-bit buckets
+// of ~n/256 records): the over-full buckets are split, not sent to the LSD fallback.
+async function testSkewedFloatKeys(device, rand) {
+  const n = 12 * 1024 * 1024 + 77;
+  const f = new Float32Array(n);
+  for (let i = 0; i < n; i += 1) f[i] = Math.floor(rand() * 2 ** 24) * 2 ** -24;
+  const keys = new Uint32Array(f.buffer);
+  const values = new Uint32Array(n).map((_, i) => i);
+  const [keysBuffer, keysBufferMapped] = createBuffers(device, keys);
+  const [valuesBuffer, valuesBufferMapped] = createBuffers(device, values);
+  const kernel = new RadixSortKernel({ device, data: { keys: keysBuffer, values: valuesBuffer }, count: n, bitCount: 32 });
+  const encoder = device.createCommandEncoder();
+  const pass = encoder.beginComputePass();
+  kernel.dispatch(pass);
+  pass.end();
+  encoder.copyBufferToBuffer(kernel.buffers.keys, 0, keysBufferMapped, 0, n * 4);
+  encoder.copyBufferToBuffer(kernel.buffers.values, 0, valuesBufferMapped, 0, n * 4);
+  device.queue.submit([encoder.finish()]);
+  await keysBufferMapped.mapAsync(GPUMapMode.READ);
+  await valuesBufferMapped.mapAsync(GPUMapMode.READ);
+  const kr = new Uint32Array(keysBufferMapped.getMappedRange().slice());
+  const vr = new Uint32Array(valuesBufferMapped.getMappedRange().slice());
+  keysBufferMapped.unmap();
+  valuesBufferMapped.unmap();
+  assert.strictEqual(kernel.lastPath(), 'hybrid');
+  assert.ok(kernel.lastSplit() >= 2, `split levels ${kernel.lastSplit()}`);
+  const expected = keys.slice().sort();
+  for (let i = 0; i < n; i += 1) {
+    assert.strictEqual(kr[i], expected[i], `f32 key @${i}`);
+    assert.strictEqual(kr[i], keys[vr[i]], `f32 value @${i}`);
+    if (i && kr[i] === kr[i - 1]) assert.ok(vr[i] > vr[i - 1], 'stability');
+  }
+  kernel.destroy();
+  for (const b of [keysBuffer, valuesBuffer]) b.destroy();
+}
+
 (async () => {
   const adapter = await gpu.requestAdapter();
   assert.ok(adapter, 'no HIP device');
@@ -141,5 +177,6 @@ async function testTextureSort(device, rand) {
   const b = await testRadixSort(device, true, rand);
   const c = await testTextureSort(device, rand);
   await testPrefixSum(device, rand);
-  console.log(`node sort checks ok (${a + b} sort cases, ${c} texture cases, prefix sum)`);
+  await testSkewedFloatKeys(device, rand);
+  console.log(`node sort checks ok (${a + b} sort cases, ${c} texture cases, prefix sum, skewed f32 hybrid split)`);
 })().catch((e) => { console.error(e); process.exit(1); });

@@ -1788,9 +1788,6 @@ struct SplitWs {
     uint32_t* host_err = nullptr;    // ... and the host-mapped one (bit 2: counts did not add up)
     uint32_t strict = 0;             // no LSD fallback is enqueued: a failed plan check is an error
     uint32_t n = 0;                  // the sort's record count: every table position is clamped to it
-    uint16_t* tdig = nullptr;        // [tdig_tiles][256] level 2's per-tile digit starts (k_split_local)
-    uint32_t tdig_tiles = 0;
-    uint32_t* l3par = nullptr;       // [smax3] level 3's parents: (huge bucket << 8) | byte 1
     uint32_t* mid = nullptr;         // [1 + midmax] count, then the sub-buckets for the large tile
     uint32_t midmax = 0;
 };
@@ -1914,17 +1911,17 @@ __global__ __launch_bounds__(256) void k_msd_plan(const uint32_t* __restrict__ t
 // ---- splitting over-full buckets (skewed keys on the hybrid path) ---------------------------
 // A 16-bit bucket over kBucketCap records (f32 keys in [0, 1): half of them share 128 buckets of
 // ~1M records; few distinct keys; one populated bucket) is split instead of sending the whole sort
-// to the LSD passes.  Level 2 (k_split_local): every 16K-record tile of a huge bucket is sorted by
-// byte 1 in LDS and written back in place into a free records buffer R3, with its digit starts;
-// the counts add up per bucket into the absolute starts of its 24-bit sub-buckets.  A sub-bucket
-// (b, d) is then the tile-ordered concatenation of the d-runs of b's tiles, which k_bucket_sort8
-// gathers (in that order: stable) and sorts by byte 0 in LDS into the output.  A sub-bucket over
-// kSub8Cap records goes to level 3: gathered into its output range (k_split_gather3), counted
-// (k_split_count), sorted by byte 0 with a segmented one-sweep pass (k_onesweep SEG = 2) into R3 and
-// copied back (k_split_copy3) - its keys then differ in no other bit.  Every step is stable, so the
-// result is the stable sort.  Bytes per record of a huge bucket after MSD passes 0 and 1: local
-// sort 16 + bucket sort 16 (level 3: + gather 16 + count 8 + pass 16 + copy 16), where the LSD
-// fallback read and wrote every record of the input four times.
+// to the LSD passes.  Level 2: k_split_count counts byte 1 of the huge buckets' records (per bucket:
+// the workgroups whose tile ranges meet it add their counts to its row, the last one turns the row
+// into absolute sub-bucket starts), a segmented one-sweep pass (k_onesweep SEG = 2) partitions them
+// by byte 1 from R2 into a free records buffer R3, and k_bucket_sort8 sorts every 24-bit sub-bucket
+// by byte 0 in LDS into the output.  A sub-bucket over kSub8Cap records goes to level 3: the same
+// count and segmented pass by byte 0, R3 -> output (its keys then differ in no other bit).  Every
+// step is stable, so the result is the stable sort.  Bytes per record of a huge bucket after MSD
+// passes 0 and 1: count 8 + pass 16 + bucket sort 16 (level 3: + 8 + 16).  (Round 4 also tried
+// level 2 as an in-LDS sort of every 16K-record tile plus a sub-bucket sort that gathered its
+// pieces from the tiles: no count and no look-back, but the gather's dependent table reads made the
+// sub-bucket sort 3.5 ms for config 4 - DESIGN.md section 12.)
 //
 // Split table (per level): [0] segment count, [1 .. smax + 1] first tile of every segment (+ the
 // total), [smax + 2 ..] segment starts, [2 smax + 2 ..] segment ends (positions in the records
@@ -2088,183 +2085,26 @@ __global__ __launch_bounds__(1024) void k_split_count(const uint32_t* __restrict
     }
 }
 
-// Level 2 without a global scatter (k_split_local): every 16K-record tile of a huge bucket is
-// sorted stably by byte 1 IN LDS and written back to the same positions of R3 (whole lines, no
-// look-back), with its 256 digit starts (tdig, u16); its digit counts also accumulate into the
-// bucket's row, as in k_split_count, so the last workgroup of a bucket turns the row into absolute
-// sub-bucket starts and lists level 3.  A sub-bucket (b, d) is then the concatenation, in tile
-// order, of the d-runs of b's tiles (its "pieces", ~512 B each for f32 keys): k_bucket_sort8
-// gathers them into LDS in that order (stable) and sorts them by byte 0.  This replaces a count
-// read + a segmented one-sweep pass (8 + 16 B per record, with look-back) by one local sort.
-template <int BLOCK, int KPT, int L, int RANK>
-__global__ __launch_bounds__(BLOCK) void k_split_local(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
-                                                       SplitWs sw) {
-    constexpr bool KV = L != LAYOUT_KEYS;
-    constexpr int NW = BLOCK / 64, TILE = BLOCK * KPT, WAVE_KEYS = 64 * KPT;
-    constexpr uint32_t shift = 8;   // byte 1 (whole-range keys)
-    static_assert(TILE == (int)kSplitTile, "the split tables' tile");
-    __shared__ uint32_t s_whist[NW][256];
-    __shared__ uint32_t s_scr[NW];
-    __shared__ uint32_t s_cnt[256];   // this workgroup's counts of the current segment
-    __shared__ uint32_t s_flag;
-    __shared__ uint32_t s_keys[KV ? 1 : TILE];
-    __shared__ uint2 s_kv[KV ? TILE : 1];
-    if (gated_off(sw.gate2, 0)) return;
-    const uint32_t tid = threadIdx.x, w = tid >> 6;
-    const uint32_t* tab = sw.tab2;
-    uint32_t* rows = sw.rows2;
-    uint32_t* arrive = sw.arrive2;
-    const uint32_t smax = sw.smax2;
-    const uint32_t nseg = tab[0];
-    const uint32_t* first = tab + 1;
-    const uint32_t* start = tab + 2 + smax;
-    const uint32_t* end = tab + 2 + 2 * smax;
-    const uint32_t ntiles = first[nseg] < sw.tdig_tiles ? first[nseg] : sw.tdig_tiles;
-    const uint32_t per = (ntiles + gridDim.x - 1) / gridDim.x;
-    const uint32_t t_lo = blockIdx.x * per;
-    const uint32_t t_hi = t_lo + per < ntiles ? t_lo + per : ntiles;
-    if (t_lo >= t_hi) return;
-    if (tid < 256u) s_cnt[tid] = 0u;
-    auto geom = [&](uint32_t t, uint32_t sg, uint32_t& t0, uint32_t& te) {   // (clamped, see k_split_count)
-        const uint32_t e = end[sg] < sw.n ? end[sg] : sw.n;
-        const uint32_t t0r = start[sg] + (t - first[sg]) * kSplitTile;
-        t0 = t0r < e ? t0r : e;
-        te = e - t0 < kSplitTile ? e : t0 + kSplitTile;
-    };
-    uint32_t sg = split_seg_of(first, nseg, t_lo);
-    uint32_t t0, te;
-    geom(t_lo, sg, t0, te);
-    uint32_t k[KPT], v[KV ? KPT : 1];
-    load_tile<KPT, L>(in, nullptr, (uint64_t)t0 + w * WAVE_KEYS, te, te - t0 == (uint32_t)TILE, k, v);
-    for (uint32_t t = t_lo; t < t_hi; ++t) {
-        const uint32_t nvalid = te - t0;
-        Slots<KPT, false> rank;
-        uint32_t c;   // pads (kPadKey: digit 255) after every real key; c without them
-        const uint32_t tstart = rank_tile<8, NW, KPT, RANK>(k, rank, s_whist, s_scr, shift, 255u,
-                                                            (uint32_t)TILE - nvalid, c);
-        if (tid < 256u) {
-            set_wave_offsets<8, NW>(s_whist, tstart);
-            s_cnt[tid] += c;
-            sw.tdig[(size_t)t * 256u + tid] = (uint16_t)tstart;
-        }
-        __syncthreads();
-        stage_tile<KPT, KV, TILE>(k, v, rank, s_whist[w], s_keys, s_kv, shift, 255u, nullptr, 0u, 0u);
-        // the next tile's loads (the registers are free once staged) fly under the write-back
-        const uint32_t tn = t + 1;
-        const bool more = tn < t_hi;
-        const uint32_t sgn = (more && first[sg + 1] <= tn) ? sg + 1 : sg;
-        uint32_t t0n = 0, ten = 0;
-        if (more) {
-            geom(tn, sgn, t0n, ten);
-            load_tile<KPT, L>(in, nullptr, (uint64_t)t0n + w * WAVE_KEYS, ten, ten - t0n == (uint32_t)TILE, k, v);
-        }
-        __syncthreads();
-        for (uint32_t i = tid; i < nvalid; i += BLOCK) {
-            if constexpr (KV) st_out(reinterpret_cast<unsigned long long*>(out) + t0 + i,
-                                     (unsigned long long)s_kv[i].x | ((unsigned long long)s_kv[i].y << 32));
-            else st_out(out + t0 + i, s_keys[i]);
-        }
-        if (!more || sgn != sg) {
-            // this workgroup's last tile of segment sg: its counts to the row, then its arrival
-            if (tid < 256u) {
-                if (s_cnt[tid]) atomicAdd(&rows[(size_t)sg * 256u + tid], s_cnt[tid]);
-                s_cnt[tid] = 0u;
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            if (tid == 0) {
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                const uint32_t g0 = first[sg] / per, g1 = (first[sg + 1] - 1u) / per;
-                s_flag = atomicAdd(&arrive[sg], 1u) + 1u == g1 - g0 + 1u ? 1u : 0u;
-            }
-            __syncthreads();
-            if (s_flag) {
-                // the segment's last workgroup: the row -> absolute sub-bucket starts, level 3's list
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                uint32_t cc = 0, tot = 0;
-                if (tid < 256u)
-                    cc = __hip_atomic_load(&rows[(size_t)sg * 256u + tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const uint32_t ex = block_excl_scan_n<NW>(cc, s_scr, tot);
-                if (tid == 0 && tot != end[sg] - start[sg]) split_fail(sw);
-                if (tid < 256u) rows[(size_t)sg * 256u + tid] = start[sg] + ex;
-                if (tid < 256u && cc > kSub8Cap) {
-                    const uint32_t slot = atomicAdd(&sw.tab3[0], 1u);
-                    if (slot < sw.smax3) {
-                        sw.tab3[2 + sw.smax3 + slot] = start[sg] + ex;   // its start and count
-                        sw.tab3[2 + 2 * sw.smax3 + slot] = cc;            // (the layout makes it an end)
-                        sw.l3par[slot] = (sg << 8) | tid;                 // its parent: (bucket, byte 1)
-                    } else {
-                        split_fail(sw);
-                    }
-                }
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __syncthreads();
-                if (tid == 0) {
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    s_flag = atomicAdd(&arrive[smax], 1u) + 1u == nseg ? 2u : 0u;
-                }
-                __syncthreads();
-                if (s_flag == 2u) {
-                    // the last segment done: lay out level 3 from its list (starts, counts, parents
-                    // permuted alike: the layout keeps list order)
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                    const uint32_t n3r = __hip_atomic_load(&sw.tab3[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    const uint32_t n3 = n3r < sw.smax3 ? n3r : sw.smax3;
-                    const uint32_t got = split_layout<BLOCK>(n3, sw.smax3, sw.tab3, sw.rows3, sw.arrive3, sw,
-                                                             [&](uint32_t i, uint32_t& st, uint32_t& cn) {
-                                                                 st = __hip_atomic_load(&sw.tab3[2 + sw.smax3 + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                                                                 cn = __hip_atomic_load(&sw.tab3[2 + 2 * sw.smax3 + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                                                             });
-                    if (tid < 16u) sw.gate3[tid] = got ? 1u : 0u;
-                }
-            }
-        }
-        __syncthreads();   // the staging area and s_flag are reused
-        if (more) {
-            sg = sgn;
-            t0 = t0n;
-            te = ten;
-        }
-    }
-}
-
-// The d-run of tile t of huge bucket sg in R3 (a "piece" of sub-bucket (sg, d)): src, len.
-__device__ __forceinline__ void split_piece(const SplitWs& sw, uint32_t sg, uint32_t d, uint32_t t,
-                                            uint32_t& src, uint32_t& len) {
-    const uint32_t* first = sw.tab2 + 1;
-    const uint32_t* start = sw.tab2 + 2 + sw.smax2;
-    const uint32_t* end = sw.tab2 + 2 + 2 * sw.smax2;
-    const uint32_t e = end[sg] < sw.n ? end[sg] : sw.n;
-    const uint32_t t0r = start[sg] + (t - first[sg]) * kSplitTile;
-    const uint32_t t0 = t0r < e ? t0r : e;
-    const uint32_t nv = e - t0 < kSplitTile ? e - t0 : kSplitTile;
-    const uint32_t a = sw.tdig[(size_t)t * 256u + d];
-    const uint32_t b = d < 255u ? sw.tdig[(size_t)t * 256u + d + 1] : nv;
-    src = t0 + a;
-    len = b >= a && b <= nv ? b - a : 0u;   // (never otherwise: a counting fault, reported)
-}
-
-// The level-2 sub-buckets (sg, d) of up to BLOCK x KPT records: their pieces gathered from R3
-// (tile order: stable), sorted by byte 0 in one LDS pass, written to the output as one run at
-// [rows2[sg][d], +count) (sub-buckets over kSub8Cap: level 3's, k_split_gather3).  LISTED = false:
-// every sub-bucket, one per workgroup (grid-stride beyond the grid); those over this tile but within
-// kSub8Cap are listed in sw.mid for the LISTED = true launch (a larger tile on a small grid).  LO: the
-// output layout (the caller's arrays, records, or keys); R3 holds records (keys, LO = KEYS).
+// The level-2 sub-buckets: sub-bucket (s, d) = records [rows2[s][d], next) of `rec` (next = the
+// following sub-bucket's start, or the segment's end), sorted stably by byte 0 in one LDS pass and
+// written to the output at the same positions (sub-buckets over kSub8Cap: level 3's).  LISTED =
+// false: every sub-bucket, one per workgroup (grid-stride beyond the grid: a persistent grid of 3
+// workgroups per CU left each workgroup's load latency exposed, 1.3 ms for 2^28 records); those
+// over this tile but within kSub8Cap are listed in sw.mid for the LISTED = true launch (a larger
+// tile on a small grid).  LO: the output layout (the caller's arrays, records, or keys); the input
+// is records (keys, LO = KEYS).  PACK: ranks as 16-bit pairs.
 template <int BLOCK, int KPT, int RANK, int LO, int MW = 1, bool PACK = false, bool LISTED = false>
 __global__ __launch_bounds__(BLOCK, MW) void k_bucket_sort8(const uint32_t* rec, SplitWs sw,
                                                             uint32_t* out_k, uint32_t* __restrict__ out_v) {
     constexpr int NW = BLOCK / 64, TILE = BLOCK * KPT, WAVE_KEYS = 64 * KPT;
     constexpr bool KV = LO != LAYOUT_KEYS;
+    constexpr int LI = KV ? LAYOUT_AOS : LAYOUT_KEYS;
     static_assert(BLOCK >= 256, "one digit per thread in the scan");
     __shared__ uint32_t s_whist[NW][256];
     __shared__ uint32_t s_scratch[NW];
-    __shared__ uint32_t s_ps[BLOCK], s_pl[BLOCK], s_po[BLOCK];
     __shared__ uint2 s_kv[KV ? TILE : 1];
     __shared__ uint32_t s_k[KV ? 1 : TILE];
     if (gated_off(sw.gate2, 0)) return;
-    if (blockIdx.x == 0 && threadIdx.x == 0 && sw.tab2[1 + sw.tab2[0]] > sw.tdig_tiles) split_fail(sw);
     const uint32_t tid = threadIdx.x, w = tid >> 6, lane = lane_id();
     const uint32_t wbase = w * WAVE_KEYS;
     const uint32_t nseg = sw.tab2[0];
@@ -2287,53 +2127,8 @@ __global__ __launch_bounds__(BLOCK, MW) void k_bucket_sort8(const uint32_t* rec,
             }
             continue;
         }
-        // gather straight into the registers: slot j of lane l of wave w = sub-bucket position
-        // q = w * WAVE_KEYS + j * 64 + l (the layout the rank below expects), found in the piece
-        // table (tile order: stable) by a walk from the previous slot's piece; per round the
-        // table of BLOCK tiles' pieces (block scan of their lengths)
         uint32_t k[KPT], v[KV ? KPT : 1];
-#pragma unroll
-        for (int j = 0; j < KPT; ++j) {
-            k[j] = kPadKey;
-            if constexpr (KV) v[j] = 0u;
-        }
-        const uint32_t* first2 = sw.tab2 + 1;
-        const uint32_t tf = first2[sg], tl = first2[sg + 1] < sw.tdig_tiles ? first2[sg + 1] : sw.tdig_tiles;
-        uint32_t off = 0;
-        for (uint32_t c0 = tf; c0 < tl; c0 += BLOCK) {
-            uint32_t src = 0, len = 0;
-            if (c0 + tid < tl) split_piece(sw, sg, d, c0 + tid, src, len);
-            uint32_t tot;
-            const uint32_t ex = block_excl_scan_n<NW>(len, s_scratch, tot);
-            s_ps[tid] = src;
-            s_po[tid] = off + ex;
-            s_pl[tid] = len;
-            __syncthreads();
-            const uint32_t np = tl - c0 < (uint32_t)BLOCK ? tl - c0 : (uint32_t)BLOCK;
-            const uint32_t hi = off + tot < cnt ? off + tot : cnt;
-            uint32_t pc = 0;   // the piece of the previous slot (positions only grow with j)
-#pragma unroll
-            for (int j = 0; j < KPT; ++j) {
-                const uint32_t q = wbase + j * 64 + lane;
-                if (q >= off && q < hi) {
-                    while (pc + 1 < np && s_po[pc] + s_pl[pc] <= q) ++pc;
-                    const uint32_t r = s_ps[pc] + (q - s_po[pc]);
-                    if constexpr (KV) {
-                        const unsigned long long x = ld_in(reinterpret_cast<const unsigned long long*>(rec) + r);
-                        k[j] = (uint32_t)x;
-                        v[j] = (uint32_t)(x >> 32);
-                    } else {
-                        k[j] = ld_in(rec + r);
-                    }
-                }
-            }
-            off += tot;
-            __syncthreads();   // the piece table is reused
-        }
-        if (off != cnt) {      // (never: a counting fault)
-            if (tid == 0) split_fail(sw);
-            continue;
-        }
+        load_tile<KPT, LI>(rec + (KV ? 2ull : 1ull) * base, nullptr, wbase, cnt, false, k, v);
         if (cnt > 1u) {
             Slots<KPT, PACK> rank;
             uint32_t c;   // pads: kPadKey, digit 255, after every real key
@@ -2369,121 +2164,6 @@ __global__ __launch_bounds__(BLOCK, MW) void k_bucket_sort8(const uint32_t* rec,
             }
         }
         __syncthreads();   // s_whist / s_kv are reused
-    }
-}
-
-// Level 3's input: every sub-bucket over kSub8Cap gathered from its pieces in R3 into one run of
-// the OUTPUT at its final range (free: the other sub-buckets are written elsewhere), from which
-// level 3 counts and sorts it (out -> R3) and k_split_copy3 brings it back.  Work items: (level-3
-// segment, 256-tile chunk of its parent bucket), grid-stride; each item sums the pieces of the
-// parent's tiles before its chunk for its offset, then every wave copies pieces, 8 loads in
-// flight per lane.  LO: the output layout.
-template <int LO>
-__global__ __launch_bounds__(256) void k_split_gather3(const uint32_t* rec, SplitWs sw, uint32_t* out_k,
-                                                       uint32_t* __restrict__ out_v) {
-    constexpr int BLOCK = 256, NW = 4, U = 8;
-    constexpr bool KV = LO != LAYOUT_KEYS;
-    __shared__ uint32_t s_ps[BLOCK], s_pl[BLOCK], s_po[BLOCK], s_scr[NW];
-    if (gated_off(sw.gate3, 0)) return;
-    const uint32_t tid = threadIdx.x, w = tid >> 6, lane = lane_id();
-    const uint32_t n3 = sw.tab3[0];
-    const uint32_t* first2 = sw.tab2 + 1;
-    const uint32_t* start3 = sw.tab3 + 2 + sw.smax3;
-    const uint32_t* end3 = sw.tab3 + 2 + 2 * sw.smax3;
-    uint32_t item = 0;
-    for (uint32_t s3 = 0; s3 < n3; ++s3) {
-        const uint32_t par = sw.l3par[s3], sg = par >> 8, d = par & 255u;
-        const uint32_t tf = first2[sg], tl = first2[sg + 1] < sw.tdig_tiles ? first2[sg + 1] : sw.tdig_tiles;
-        const uint32_t nch = (tl - tf + BLOCK - 1) / BLOCK;
-        for (uint32_t ch = 0; ch < nch; ++ch, ++item) {
-            if (item % gridDim.x != blockIdx.x) continue;   // (uniform)
-            const uint32_t c0 = tf + ch * BLOCK;
-            // offset of this chunk's pieces: the parent's pieces in the tiles before it
-            uint32_t pre = 0;
-            for (uint32_t t = tf + tid; t < c0; t += BLOCK) {
-                uint32_t src, len;
-                split_piece(sw, sg, d, t, src, len);
-                pre += len;
-            }
-            uint32_t pre_tot;
-            (void)block_excl_scan_n<NW>(pre, s_scr, pre_tot);
-            uint32_t src = 0, len = 0;
-            if (c0 + tid < tl) split_piece(sw, sg, d, c0 + tid, src, len);
-            uint32_t tot;
-            const uint32_t ex = block_excl_scan_n<NW>(len, s_scr, tot);
-            s_ps[tid] = src;
-            s_pl[tid] = len;
-            s_po[tid] = start3[s3] + pre_tot + ex;
-            __syncthreads();
-            const uint32_t e3 = end3[s3] < sw.n ? end3[s3] : sw.n;
-            const uint32_t np = tl - c0 < (uint32_t)BLOCK ? tl - c0 : (uint32_t)BLOCK;
-            for (uint32_t pi = w; pi < np; pi += NW) {
-                const uint32_t ps = s_ps[pi], pl = s_pl[pi], po = s_po[pi];
-                for (uint32_t r0 = 0; r0 < pl; r0 += 64 * U) {
-                    unsigned long long x[U];
-#pragma unroll
-                    for (int u = 0; u < U; ++u) {
-                        const uint32_t r = r0 + u * 64 + lane;
-                        if (r < pl) {
-                            if constexpr (KV) x[u] = ld_in(reinterpret_cast<const unsigned long long*>(rec) + ps + r);
-                            else x[u] = ld_in(rec + ps + r);
-                        }
-                    }
-#pragma unroll
-                    for (int u = 0; u < U; ++u) {
-                        const uint32_t r = r0 + u * 64 + lane;
-                        const uint32_t q = po + r;
-                        if (r < pl && q < e3) {   // (q < e3: never otherwise, see k_split_count)
-                            if constexpr (LO == LAYOUT_AOS) st_out(reinterpret_cast<unsigned long long*>(out_k) + q, x[u]);
-                            else if constexpr (LO == LAYOUT_KEYS) st_out(out_k + q, (uint32_t)x[u]);
-                            else { st_out(out_k + q, (uint32_t)x[u]); st_out(out_v + q, (uint32_t)(x[u] >> 32)); }
-                        }
-                    }
-                }
-            }
-            __syncthreads();   // the piece table is reused
-        }
-    }
-}
-
-// Level 3's result back from R3 to the output (its segments' ranges).  LO: the output layout; R3
-// holds records (keys, LO = KEYS).
-template <int LO>
-__global__ __launch_bounds__(256) void k_split_copy3(const uint32_t* rec, SplitWs sw, uint32_t* out_k,
-                                                     uint32_t* __restrict__ out_v) {
-    if (gated_off(sw.gate3, 0)) return;
-    const uint32_t n3 = sw.tab3[0];
-    const uint32_t* first = sw.tab3 + 1;
-    const uint32_t* start = sw.tab3 + 2 + sw.smax3;
-    const uint32_t* end = sw.tab3 + 2 + 2 * sw.smax3;
-    const uint32_t ntiles = first[n3];
-    for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-        const uint32_t s3 = split_seg_of(first, n3, t);
-        const uint32_t e = end[s3] < sw.n ? end[s3] : sw.n;
-        const uint32_t t0r = start[s3] + (t - first[s3]) * kSplitTile;
-        const uint32_t t0 = t0r < e ? t0r : e;
-        const uint32_t te = e - t0 < kSplitTile ? e : t0 + kSplitTile;
-        constexpr int U = 8;   // loads in flight per lane
-        for (uint32_t q0 = t0; q0 < te; q0 += 256 * U) {
-            unsigned long long x[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const uint32_t q = q0 + u * 256 + threadIdx.x;
-                if (q < te) {
-                    if constexpr (LO == LAYOUT_KEYS) x[u] = ld_in(rec + q);
-                    else x[u] = ld_in(reinterpret_cast<const unsigned long long*>(rec) + q);
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const uint32_t q = q0 + u * 256 + threadIdx.x;
-                if (q < te) {
-                    if constexpr (LO == LAYOUT_AOS) st_out(reinterpret_cast<unsigned long long*>(out_k) + q, x[u]);
-                    else if constexpr (LO == LAYOUT_KEYS) st_out(out_k + q, (uint32_t)x[u]);
-                    else { st_out(out_k + q, (uint32_t)x[u]); st_out(out_v + q, (uint32_t)(x[u] >> 32)); }
-                }
-            }
-        }
     }
 }
 
@@ -2797,6 +2477,12 @@ __global__ __launch_bounds__(BLOCK, MW) void k_bucket_sort_wide(const uint32_t* 
 // ~28 buckets in flight.  Two stable 8-bit passes (low byte, then the next), pads (kPadKey) after
 // every real key.  Buckets of more than 64 * KPT keys are listed by k_msd_plan for the large-tile
 // launch; empty and one-key buckets are skipped.
+#ifndef RS_KWAVE_PF
+#define RS_KWAVE_PF 0     // sweep: 1 = persistent waves that load their next bucket while sorting one
+#endif
+#ifndef RS_KWAVE_PACK
+#define RS_KWAVE_PACK 0   // sweep: 1 = ranks as 16-bit pairs (fewer VGPRs: more waves per SIMD)
+#endif
 template <int KPT, int RANK, int WPB, int MW = 1>
 __global__ __launch_bounds__(64 * WPB, MW) void k_bucket_sort_keys_wave(uint32_t* keys,
                                                                  const uint32_t* __restrict__ hist16,
@@ -2811,22 +2497,42 @@ __global__ __launch_bounds__(64 * WPB, MW) void k_bucket_sort_keys_wave(uint32_t
     uint32_t* h = s_h[w];
     uint32_t* sk = s_k[w];
     auto wave_sync = [] { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); __builtin_amdgcn_wave_barrier(); };
-    for (uint32_t b = blockIdx.x * WPB + w; b < 65536u; b += gridDim.x * WPB) {
-        const uint32_t cnt = hist16[b];
-        if (cnt <= 1u || cnt > CAP) continue;
-        uint32_t* src = keys + sstart[b >> 8] + base16[b];
-        uint32_t k[KPT];
+    const uint32_t stride = gridDim.x * WPB;
+    // the next bucket at or after b this wave sorts (2 or more keys, within the wave tile)
+    auto next_bucket = [&](uint32_t b, uint32_t& cnt) {
+        for (; b < 65536u; b += stride) {
+            cnt = hist16[b];
+            if (cnt > 1u && cnt <= CAP) break;
+        }
+        return b;
+    };
+    auto load = [&](uint32_t b, uint32_t cnt, uint32_t (&k)[KPT]) {
+        const uint32_t* src = keys + sstart[b >> 8] + base16[b];
 #pragma unroll
         for (int j = 0; j < KPT; ++j) {
             const uint32_t q = (uint32_t)j * 64u + lane;
             k[j] = q < cnt ? src[q] : kPadKey;
+        }
+    };
+    uint32_t cnt = 0;
+    uint32_t b = next_bucket(blockIdx.x * WPB + w, cnt);
+    uint32_t k[KPT];
+    if (b < 65536u) load(b, cnt, k);
+    while (b < 65536u) {
+        uint32_t* src = keys + sstart[b >> 8] + base16[b];
+        // RS_KWAVE_PF: the next bucket's keys in flight while this one is sorted
+        uint32_t ncnt = 0, nb = 65536u;
+        uint32_t kn[RS_KWAVE_PF ? KPT : 1];
+        if (RS_KWAVE_PF) {
+            nb = next_bucket(b + stride, ncnt);
+            if (nb < 65536u) load(nb, ncnt, reinterpret_cast<uint32_t(&)[KPT]>(kn));
         }
 #pragma unroll 1
         for (uint32_t shift = 0; shift < 16u; shift += 8u) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) h[lane * 4 + i] = 0u;
             wave_sync();
-            Slots<KPT, false> rank;
+            Slots<KPT, RS_KWAVE_PACK != 0> rank;
             rank_slots<8, KPT, RANK>(k, rank, h, shift, 255u);
             wave_sync();
             // exclusive scan of the 256 counters: lane l owns digits 4l .. 4l + 3
@@ -2846,6 +2552,15 @@ __global__ __launch_bounds__(64 * WPB, MW) void k_bucket_sort_keys_wave(uint32_t
         for (int j = 0; j < KPT; ++j) {
             const uint32_t q = (uint32_t)j * 64u + lane;
             if (q < cnt) src[q] = k[j];
+        }
+        if (RS_KWAVE_PF) {
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) k[j] = kn[RS_KWAVE_PF ? j : 0];
+            b = nb;
+            cnt = ncnt;
+        } else {
+            b = next_bucket(b + stride, cnt);
+            if (b < 65536u) load(b, cnt, k);
         }
     }
 }

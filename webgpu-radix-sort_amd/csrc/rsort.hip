@@ -138,11 +138,9 @@ inline uint32_t split_smax2(uint64_t cap) { return (uint32_t)(cap / (kBucketCap 
 inline uint32_t split_smax3(uint64_t cap) { return (uint32_t)(cap / (rs::kSub8Cap + 1ull) + 1); }
 // level 2's tiles (each huge bucket's records in 16K-record tiles: at most one partial per bucket)
 inline uint32_t split_midmax(uint64_t cap) { return (uint32_t)(cap / (rs::kSub8Small + 1ull) + 1); }
-inline uint32_t split_tiles2(uint64_t cap) { return (uint32_t)(cap / rs::kSplitTile + split_smax2(cap) + 1); }
 inline uint64_t split_words(uint64_t cap) {
     const uint64_t s2 = split_smax2(cap), s3 = split_smax3(cap);
     return 32ull + 1 + s2 + (3ull * s2 + 2) + (s2 + 1ull) + 256ull * s2 + (3ull * s3 + 2) + (s3 + 1ull) + 256ull * s3 +
-           s3 + 128ull * split_tiles2(cap) +   // + level-3 parents, level 2's per-tile digit starts (u16)
            1ull + split_midmax(cap);           // + the sub-buckets for the large tile
 }
 constexpr uint32_t kHistGrid = 2048;
@@ -290,7 +288,6 @@ struct rs_plan {
     uint32_t* msd = nullptr;         // its workspace: hist16 | base16 | segtab | gates | mtot
     uint32_t* split = nullptr;       // the bucket split's workspace (rs::SplitWs; split_words())
     uint32_t smax2 = 0, smax3 = 0;   // its level-2 / level-3 segment capacities
-    uint32_t tiles2 = 0;             // level 2's tile capacity (per-tile digit starts)
     bool split_on = true;            // split over-full buckets (rs_plan_debug.split = 0: the LSD fallback)
     bool last_hybrid = false;        // the last sort enqueued the hybrid path (rs_plan_last_path)
     bool last_split = false;         // ... with the bucket split's launches (rs_plan_last_split)
@@ -840,7 +837,6 @@ RS_EXPORT rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out) {
     if (p->msd) {
         p->smax2 = split_smax2(d.count);
         p->smax3 = split_smax3(d.count);
-        p->tiles2 = split_tiles2(d.count);
         if ((e = alloc(&p->split, 4ull * split_words(d.count))) != hipSuccess)
             return cleanup(fail(e == hipErrorOutOfMemory ? RS_ERR_OUT_OF_MEMORY : RS_ERR_HIP,
                                 "rs_plan_create: hipMalloc failed: %s", hipGetErrorString(e)));
@@ -910,28 +906,38 @@ static rs_status enqueue_lsd_gated(rs_plan* p, const uint32_t* sk, const uint32_
 static rs_status enqueue_split(rs_plan* p, const rs::SplitWs& sw, bool keys, bool out_aos, uint32_t* r2,
                                uint32_t* r3, uint32_t* uk, uint32_t* uv, uint32_t n32, hipStream_t s) {
     constexpr int A = rs::LAYOUT_AOS, S = rs::LAYOUT_SOA, K = rs::LAYOUT_KEYS;
-    // level 3's pass tiles must be the split tables' (kSplitTile): keys only, the 512 x 32 tiles
+    // the passes' tiles must be the split tables' (kSplitTile): keys only, the 512 x 32 tiles
     static_assert(kLarge.tile == (int)rs::kSplitTile, "split passes: 16K-record tiles");
     constexpr bool keys512 = kLargeKeys.tile == (int)rs::kSplitTile;
     constexpr int KB_ = keys512 ? kLargeKeys.block : kLarge.block, KK = keys512 ? kLargeKeys.kpt : kLarge.kpt;
     const bool ballot = p->rank_mode == rs::RANK_BALLOT;
     constexpr int A0 = rs::RANK_LDS_ATOMIC, B0 = rs::RANK_BALLOT;
+    const uint32_t cgrid = 2u * p->cus;
+    auto count = [&](const uint32_t* rec, uint32_t shift, bool level3) {
+        RoctxRange r(level3 ? "rsort.msd.split3_count" : "rsort.msd.split2_count");
+        auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(cgrid), dim3(1024), 0, s, rec, sw, shift); };
+        if (keys) level3 ? go(rs::k_split_count<1, 3>) : go(rs::k_split_count<1, 2>);
+        else level3 ? go(rs::k_split_count<2, 3>) : go(rs::k_split_count<2, 2>);
+    };
     rs_status st = RS_OK;
     // one timed span (RS_KERNEL_SPLIT) for the split's launches, each also a roctx range
     p->timer.run(RS_KERNEL_SPLIT, s, [&] {
+        count(r2, 8u, false);
+        st = next_epoch(p, s);
+        if (st != RS_OK) return;
         {
-            RoctxRange r("rsort.msd.split2_local");
-            auto go = [&](auto kern) {
-                static const uint32_t per_cu = resident_per_cu(kern, 1024);
-                hipLaunchKernelGGL(kern, dim3(p->cus * per_cu), dim3(1024), 0, s, (const uint32_t*)r2, r3, sw);
-            };
-            if (keys) ballot ? go(rs::k_split_local<1024, 16, K, B0>) : go(rs::k_split_local<1024, 16, K, A0>);
-            else ballot ? go(rs::k_split_local<1024, 16, A, B0>) : go(rs::k_split_local<1024, 16, A, A0>);
+            RoctxRange r("rsort.msd.split2_pass");
+            if (keys)
+                launch_msd_pass<K, K, 2, false, KB_, KK>(p, r2, nullptr, r3, nullptr, n32, 8u, sw.smax2, nullptr,
+                                                         p->tickets + 6, sw.gate2, sw.tab2, sw.rows2, s);
+            else
+                launch_msd_pass<A, A, 2>(p, r2, nullptr, r3, nullptr, n32, 8u, sw.smax2, nullptr, p->tickets + 6,
+                                         sw.gate2, sw.tab2, sw.rows2, s);
         }
-        auto out3 = [&](auto lo) {
-            constexpr int LO = decltype(lo)::value;
-            {
-                RoctxRange r("rsort.msd.split2_bucket");
+        {
+            RoctxRange r("rsort.msd.split2_bucket");
+            auto go = [&](auto lo) {
+                constexpr int LO = decltype(lo)::value;
                 // one sub-bucket per workgroup (65536 of them: 256 huge buckets; more are taken
                 // grid-stride), so the hardware overlaps the workgroups' load latencies
                 auto small = [&](auto kern) {
@@ -947,33 +953,24 @@ static rs_status enqueue_split(rs_plan* p, const rs::SplitWs& sw, bool keys, boo
                 ballot ? small(rs::k_bucket_sort8<256, 17, B0, LO, 3>) : small(rs::k_bucket_sort8<256, 17, A0, LO, 3>);
                 ballot ? large(rs::k_bucket_sort8<512, 34, B0, LO, 2, false, true>)
                        : large(rs::k_bucket_sort8<512, 34, A0, LO, 2, false, true>);
-            }
-            {
-                RoctxRange r("rsort.msd.split3");
-                hipLaunchKernelGGL(rs::k_split_gather3<LO>, dim3(2u * p->cus), dim3(256), 0, s, (const uint32_t*)r3,
-                                   sw, uk, uv);
-                constexpr int KS = LO == A ? 2 : 1;
-                hipLaunchKernelGGL((rs::k_split_count<KS, 3>), dim3(2u * p->cus), dim3(1024), 0, s, (const uint32_t*)uk,
-                                   sw, 0u);
-                st = next_epoch(p, s);
-                if (st != RS_OK) return;
-                // out -> R3 by byte 0, then back
-                if constexpr (LO == K)
-                    launch_msd_pass<K, K, 2, false, KB_, KK>(p, uk, nullptr, r3, nullptr, n32, 0u, sw.smax3, nullptr,
-                                                             p->tickets + 7, sw.gate3, sw.tab3, sw.rows3, s);
-                else if constexpr (LO == A)
-                    launch_msd_pass<A, A, 2>(p, uk, nullptr, r3, nullptr, n32, 0u, sw.smax3, nullptr, p->tickets + 7,
-                                             sw.gate3, sw.tab3, sw.rows3, s);
-                else
-                    launch_msd_pass<S, A, 2>(p, uk, uv, r3, nullptr, n32, 0u, sw.smax3, nullptr, p->tickets + 7,
-                                             sw.gate3, sw.tab3, sw.rows3, s);
-                hipLaunchKernelGGL(rs::k_split_copy3<LO>, dim3(2u * p->cus), dim3(256), 0, s, (const uint32_t*)r3, sw,
-                                   uk, uv);
-            }
-        };
-        if (keys) out3(std::integral_constant<int, K>{});
-        else if (out_aos) out3(std::integral_constant<int, A>{});
-        else out3(std::integral_constant<int, S>{});
+            };
+            if (keys) go(std::integral_constant<int, K>{});
+            else if (out_aos) go(std::integral_constant<int, A>{});
+            else go(std::integral_constant<int, S>{});
+        }
+        count(r3, 0u, true);
+        st = next_epoch(p, s);
+        if (st != RS_OK) return;
+        RoctxRange r("rsort.msd.split3_pass");
+        if (keys)
+            launch_msd_pass<K, K, 2, false, KB_, KK>(p, r3, nullptr, uk, nullptr, n32, 0u, sw.smax3, nullptr,
+                                                     p->tickets + 7, sw.gate3, sw.tab3, sw.rows3, s);
+        else if (out_aos)
+            launch_msd_pass<A, A, 2>(p, r3, nullptr, uk, nullptr, n32, 0u, sw.smax3, nullptr, p->tickets + 7,
+                                     sw.gate3, sw.tab3, sw.rows3, s);
+        else
+            launch_msd_pass<A, S, 2>(p, r3, nullptr, uk, uv, n32, 0u, sw.smax3, nullptr, p->tickets + 7,
+                                     sw.gate3, sw.tab3, sw.rows3, s);
     }, "rsort.msd.split");
     if (st != RS_OK) return st;
     HIP_TRY(hipGetLastError());
@@ -1048,11 +1045,6 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
         q += p->smax3 + 1ull;
         sw.rows3 = q;
         q += 256ull * p->smax3;
-        sw.l3par = q;
-        q += p->smax3;
-        sw.tdig = reinterpret_cast<uint16_t*>(q);
-        sw.tdig_tiles = p->tiles2;
-        q += 128ull * p->tiles2;
         sw.mid = q;
         sw.midmax = split_midmax(p->capacity);
         sw.smax2 = p->smax2;
@@ -1316,7 +1308,14 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
                 if (wave_kpt && !wave_done) {
                     constexpr int WPB = 4;
                     auto wave = [&](auto kern) {
-                        hipLaunchKernelGGL(kern, dim3(65536 / WPB), dim3(64 * WPB), 0, s, uk, (const uint32_t*)hist16,
+                        // one bucket per wave; RS_KWAVE_PF (sweep): persistent waves, two resident
+                        // grids' worth of workgroups
+                        uint32_t grid = 65536 / WPB;
+                        if (RS_KWAVE_PF) {
+                            static const uint32_t per_cu = resident_per_cu(kern, 64 * WPB);
+                            grid = std::min<uint32_t>(grid, 2u * per_cu * p->cus);
+                        }
+                        hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * WPB), 0, s, uk, (const uint32_t*)hist16,
                                            (const uint32_t*)base16, g_msd, (const uint32_t*)sstart);
                     };
                     if (wave_kpt == 10)

@@ -1790,6 +1790,8 @@ struct SplitWs {
     uint32_t n = 0;                  // the sort's record count: every table position is clamped to it
     uint32_t* mid = nullptr;         // [1 + midmax] count, then the sub-buckets for the large tile
     uint32_t midmax = 0;
+    uint32_t* chunks = nullptr;      // [1 + 2 chunkmax] count, then (start, count) of the runs of
+    uint32_t chunkmax = 0;           // consecutive small sub-buckets sorted together
 };
 
 __device__ __forceinline__ void split_fail(const SplitWs& sw) {
@@ -1895,6 +1897,7 @@ __global__ __launch_bounds__(256) void k_msd_plan(const uint32_t* __restrict__ t
         if (tid == 0) {
             sw.tab3[0] = 0u;
             sw.mid[0] = 0u;
+            sw.chunks[0] = 0u;
         }
         uint32_t n2 = 0;
         if (ok & run & (nhuge ? 1u : 0u))   // uniform
@@ -1957,6 +1960,7 @@ __global__ __launch_bounds__(1024) void k_split_count(const uint32_t* __restrict
     __shared__ uint32_t s_h[NW][256];
     __shared__ uint32_t s_scr[NW];
     __shared__ uint32_t s_flag;
+    __shared__ uint32_t s_c[LEVEL == 2 ? 256 : 1];
     const uint32_t* gate = LEVEL == 2 ? sw.gate2 : sw.gate3;
     if (gated_off(gate, 0)) return;
     uint32_t* tab = LEVEL == 2 ? sw.tab2 : sw.tab3;
@@ -2051,6 +2055,44 @@ __global__ __launch_bounds__(1024) void k_split_count(const uint32_t* __restrict
                             split_fail(sw);
                         }
                     }
+                    // the bucket sort's work list: runs of consecutive sub-buckets of at most
+                    // kSub8Small records together (one 16-bit LDS sort each: as many items as the
+                    // bucket pass has for uniform keys, where one item per sub-bucket made 163840
+                    // mostly small ones for config 4), the larger ones alone (mid list)
+                    if (tid < 256u) s_c[tid] = c;
+                    __syncthreads();
+                    if (tid == 0) {
+                        auto emit = [&](uint32_t st, uint32_t cn) {
+                            const uint32_t slot = atomicAdd(&sw.chunks[0], 1u);
+                            if (slot < sw.chunkmax) {
+                                sw.chunks[1 + 2 * slot] = st;
+                                sw.chunks[2 + 2 * slot] = cn;
+                            } else {
+                                split_fail(sw);
+                            }
+                        };
+                        uint32_t cst = start[sg], acc = 0;
+                        for (uint32_t dd = 0; dd < 256u; ++dd) {
+                            const uint32_t cd = s_c[dd];
+                            if (cd > kSub8Small) {
+                                if (acc) emit(cst, acc);
+                                if (cd <= kSub8Cap) {
+                                    const uint32_t slot = atomicAdd(&sw.mid[0], 1u);
+                                    if (slot < sw.midmax) sw.mid[1 + slot] = (sg << 8) | dd;
+                                    else split_fail(sw);
+                                }
+                                cst += acc + cd;
+                                acc = 0;
+                            } else if (acc + cd > kSub8Small) {
+                                emit(cst, acc);
+                                cst += acc;
+                                acc = cd;
+                            } else {
+                                acc += cd;
+                            }
+                        }
+                        if (acc) emit(cst, acc);
+                    }
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     __syncthreads();
                     if (tid == 0) {
@@ -2085,13 +2127,12 @@ __global__ __launch_bounds__(1024) void k_split_count(const uint32_t* __restrict
     }
 }
 
-// The level-2 sub-buckets: sub-bucket (s, d) = records [rows2[s][d], next) of `rec` (next = the
-// following sub-bucket's start, or the segment's end), sorted stably by byte 0 in one LDS pass and
-// written to the output at the same positions (sub-buckets over kSub8Cap: level 3's).  LISTED =
-// false: every sub-bucket, one per workgroup (grid-stride beyond the grid: a persistent grid of 3
-// workgroups per CU left each workgroup's load latency exposed, 1.3 ms for 2^28 records); those
-// over this tile but within kSub8Cap are listed in sw.mid for the LISTED = true launch (a larger
-// tile on a small grid).  LO: the output layout (the caller's arrays, records, or keys); the input
+// The level-2 sub-buckets, sorted in LDS and written to the output at their positions.  LISTED =
+// false: the work list's runs of consecutive sub-buckets of one huge bucket (at most BLOCK x KPT
+// records; their keys share the top 16 bits), sorted stably by the low 16 bits in two 8-bit LDS
+// passes, one run per workgroup (grid-stride beyond the grid); LISTED = true: the sub-buckets of
+// more than kSub8Small records (up to kSub8Cap; their keys share the top 24 bits), by byte 0 in one
+// pass, on a small grid.  LO: the output layout (the caller's arrays, records, or keys); the input
 // is records (keys, LO = KEYS).  PACK: ranks as 16-bit pairs.
 template <int BLOCK, int KPT, int RANK, int LO, int MW = 1, bool PACK = false, bool LISTED = false>
 __global__ __launch_bounds__(BLOCK, MW) void k_bucket_sort8(const uint32_t* rec, SplitWs sw,
@@ -2107,50 +2148,50 @@ __global__ __launch_bounds__(BLOCK, MW) void k_bucket_sort8(const uint32_t* rec,
     if (gated_off(sw.gate2, 0)) return;
     const uint32_t tid = threadIdx.x, w = tid >> 6, lane = lane_id();
     const uint32_t wbase = w * WAVE_KEYS;
-    const uint32_t nseg = sw.tab2[0];
     const uint32_t* end = sw.tab2 + 2 + 2 * sw.smax2;
-    const uint32_t nmid = LISTED ? (sw.mid[0] < sw.midmax ? sw.mid[0] : sw.midmax) : 0u;
-    const uint32_t nit = LISTED ? nmid : nseg * 256u;
-    for (uint32_t ii = blockIdx.x; ii < nit; ii += gridDim.x) {
-        const uint32_t it = LISTED ? sw.mid[1 + ii] : ii;
-        const uint32_t sg = it >> 8, d = it & 255u;
-        const uint32_t base = sw.rows2[it];
-        const uint32_t nxt = d == 255u ? end[sg] : sw.rows2[it + 1];
-        const uint32_t cnt = nxt - base;
-        if (cnt == 0u || cnt > kSub8Cap) continue;              // empty, or level 3's
-        if (nxt > sw.n || base > nxt) continue;                 // (never: a counting fault, reported)
-        if (cnt > (uint32_t)TILE) {                             // the large tile's (LISTED: never)
-            if (!LISTED && tid == 0) {
-                const uint32_t slot = atomicAdd(&sw.mid[0], 1u);
-                if (slot < sw.midmax) sw.mid[1 + slot] = it;
-                else split_fail(sw);
-            }
-            continue;
+    const uint32_t nitems = LISTED ? (sw.mid[0] < sw.midmax ? sw.mid[0] : sw.midmax)
+                                   : (sw.chunks[0] < sw.chunkmax ? sw.chunks[0] : sw.chunkmax);
+    for (uint32_t ii = blockIdx.x; ii < nitems; ii += gridDim.x) {
+        uint32_t base, cnt;
+        if (LISTED) {
+            const uint32_t it = sw.mid[1 + ii];
+            const uint32_t sg = it >> 8, d = it & 255u;
+            base = sw.rows2[it];
+            const uint32_t nxt = d == 255u ? end[sg] : sw.rows2[it + 1];
+            cnt = nxt - base;
+        } else {
+            base = sw.chunks[1 + 2 * ii];
+            cnt = sw.chunks[2 + 2 * ii];
         }
+        if (cnt == 0u || cnt > (uint32_t)TILE) continue;        // (never: the lists' bounds)
+        if ((uint64_t)base + cnt > sw.n) continue;              // (never: a counting fault, reported)
         uint32_t k[KPT], v[KV ? KPT : 1];
         load_tile<KPT, LI>(rec + (KV ? 2ull : 1ull) * base, nullptr, wbase, cnt, false, k, v);
         if (cnt > 1u) {
-            Slots<KPT, PACK> rank;
-            uint32_t c;   // pads: kPadKey, digit 255, after every real key
-            const uint32_t tstart = rank_tile<8, NW, KPT, RANK>(k, rank, s_whist, s_scratch, 0u, 255u, 0u, c);
-            if (tid < 256u) set_wave_offsets<8, NW>(s_whist, tstart);
-            __syncthreads();
+            for (uint32_t p = 0, shift = 0; p < (LISTED ? 1u : 2u); ++p, shift += 8u) {
+                Slots<KPT, PACK> rank;
+                uint32_t c;   // pads: kPadKey, digit 255, after every real key
+                const uint32_t tstart = rank_tile<8, NW, KPT, RANK>(k, rank, s_whist, s_scratch, shift, 255u, 0u, c);
+                if (tid < 256u) set_wave_offsets<8, NW>(s_whist, tstart);
+                __syncthreads();
 #pragma unroll
-            for (int j = 0; j < KPT; ++j) {
-                const uint32_t q = s_whist[w][k[j] & 255u] + rank.get(j);
-                if constexpr (KV) s_kv[q] = make_uint2(k[j], v[j]);
-                else s_k[q] = k[j];
-            }
-            __syncthreads();
-#pragma unroll
-            for (int j = 0; j < KPT; ++j) {
-                if constexpr (KV) {
-                    const uint2 kv = s_kv[wbase + j * 64 + lane];
-                    k[j] = kv.x;
-                    v[j] = kv.y;
-                } else {
-                    k[j] = s_k[wbase + j * 64 + lane];
+                for (int j = 0; j < KPT; ++j) {
+                    const uint32_t q = s_whist[w][(k[j] >> shift) & 255u] + rank.get(j);
+                    if constexpr (KV) s_kv[q] = make_uint2(k[j], v[j]);
+                    else s_k[q] = k[j];
                 }
+                __syncthreads();
+#pragma unroll
+                for (int j = 0; j < KPT; ++j) {
+                    if constexpr (KV) {
+                        const uint2 kv = s_kv[wbase + j * 64 + lane];
+                        k[j] = kv.x;
+                        v[j] = kv.y;
+                    } else {
+                        k[j] = s_k[wbase + j * 64 + lane];
+                    }
+                }
+                __syncthreads();
             }
         }
         const size_t o0 = (size_t)base + wbase + lane;
@@ -2163,7 +2204,6 @@ __global__ __launch_bounds__(BLOCK, MW) void k_bucket_sort8(const uint32_t* rec,
                 else { (out_k + o0)[j * 64] = k[j]; (out_v + o0)[j * 64] = v[j]; }
             }
         }
-        __syncthreads();   // s_whist / s_kv are reused
     }
 }
 
@@ -2707,19 +2747,19 @@ __global__ __launch_bounds__(kBlock) void k_scan_small(uint32_t* __restrict__ a,
 
 // Single-pass exclusive scan (the PrefixSumKernel export, PrefixSumKernel.ts:11-159): one read and
 // one write of the data (8 B/element; the reduce-then-scan above reads it twice, 12 B/element).
-// Tiles of BLOCK x EPT elements come from a ticket counter in order; every thread scans EPT
-// CONTIGUOUS elements in registers, the workgroup scans the thread totals (wave scan + one LDS
-// exchange), publishes the tile's aggregate, and one wave looks back over up to 64 predecessors
-// per step (status words as k_onesweep's: ((epoch << 2 | flag) << 32) | value, agent-scope relaxed
-// 64-bit atomics, so flag and value travel together; the epoch tags this launch's words, so the
-// region is never cleared).  Waits are bounded like k_onesweep's (err[0] on a timeout).
-// Throughput bound of the chained look-back: a tile walks back to the nearest inclusive prefix 64
-// words per L2 round trip, so the tiles in flight finish at about 64 tiles per round trip (~1 us):
-// 4096-element tiles capped the scan at ~2 TB/s (0.26 of HBM); 16K-element tiles (1024 x 16) lift
-// that bound to ~4x the data rate.  PF: the next tile's ticket is taken and its loads issued before
-// the look-back, so they are in flight while this tile waits and stores.
+// Tiles of BLOCK x EPT elements come from a ticket counter in order; each wave scans its 64 x EPT
+// elements (striped: coalesced 16-byte loads, see below) with wave scans, the workgroup scans the
+// wave totals, publishes the tile's aggregate, and looks back for its prefix: status words as
+// k_onesweep's (((epoch << 2 | flag) << 32) | value, agent-scope relaxed 64-bit atomics, so flag
+// and value travel together; the epoch tags this launch's words, so the region is never cleared),
+// every wave reading 64 predecessors per round.  Waits are bounded like k_onesweep's (err[0] on a
+// timeout).  PF: the next tile's ticket is taken and its loads issued before the look-back.
+// History (round 4, 2^28 u32): 256 x 16 tiles, one look-back wave, per-thread contiguous elements
+// 1.04 ms; 1024 x 16 tiles + PF 0.78 ms; + every wave looking back 0.78 ms (so the look-back walk
+// was not the limit); the per-thread contiguous layout touched every line with four load
+// instructions at 64-B lane strides - the striped layout reads each line once.
 // tickets: a ring of kScanTickets counters; launch e uses tickets[e % ring] and clears the next
-// launch's.  VEC: the data is 16-byte aligned (4 x 16-byte loads / stores per thread).
+// launch's.  VEC: the data is 16-byte aligned (16-byte loads / stores; else 4-byte ones).
 constexpr uint32_t kScanTickets = 64;
 template <int BLOCK, int EPT, bool VEC, bool PF = true>
 __global__ __launch_bounds__(BLOCK) void k_scan_lookback(uint32_t* __restrict__ data, uint32_t n,
@@ -2731,23 +2771,35 @@ __global__ __launch_bounds__(BLOCK) void k_scan_lookback(uint32_t* __restrict__ 
     constexpr uint32_t TILE = (uint32_t)BLOCK * EPT;
     __shared__ uint32_t s_wave[NW];
     __shared__ uint32_t s_t, s_prefix;
+    __shared__ uint2 s_lb[NW];   // per wave of a look-back round: (sum, found | unpublished << 1)
+    __shared__ uint32_t s_abort;
     if (indirect_off(ind)) return;
     const uint32_t tid = threadIdx.x, w = tid >> 6, lane = lane_id();
     uint32_t* ticket = tickets + epoch % kScanTickets;
     if (blockIdx.x == 0 && tid == 0) tickets[(epoch + 1) % kScanTickets] = 0u;   // the next launch's
     const uint32_t ntiles = (uint32_t)(((uint64_t)n + TILE - 1) / TILE);
+    // striped layout (coalesced: each load instruction of a wave reads 1 KB contiguous): wave w's
+    // EPT x 64 elements are EPT / 4 chunks of 256, lane l holding elements 4l .. 4l + 3 of each
+    // (the first version gave each thread EPT contiguous elements - 64-B lane strides, every line
+    // touched by 4 instructions - and ran at 2.7 TB/s)
+    constexpr int NV = EPT / 4;
+    auto elem0 = [&](uint32_t T, int j) {   // first element of this thread's vector j
+        return (uint64_t)T * TILE + (uint64_t)w * (64u * EPT) + (uint64_t)j * 256u + lane * 4u;
+    };
     auto load = [&](uint32_t T, uint32_t (&x)[EPT]) {
-        const uint64_t base = (uint64_t)T * TILE + (uint64_t)tid * EPT;
         if (VEC && (uint64_t)T * TILE + TILE <= n) {
-            const uint4* p = reinterpret_cast<const uint4*>(data + base);
 #pragma unroll
-            for (int j = 0; j < EPT / 4; ++j) {
-                const uint4 q = p[j];
+            for (int j = 0; j < NV; ++j) {
+                const uint4 q = *reinterpret_cast<const uint4*>(data + elem0(T, j));
                 x[4 * j] = q.x; x[4 * j + 1] = q.y; x[4 * j + 2] = q.z; x[4 * j + 3] = q.w;
             }
         } else {
 #pragma unroll
-            for (int j = 0; j < EPT; ++j) x[j] = base + j < n ? data[base + j] : 0u;
+            for (int j = 0; j < NV; ++j) {
+                const uint64_t e = elem0(T, j);
+#pragma unroll
+                for (int c = 0; c < 4; ++c) x[4 * j + c] = e + c < n ? data[e + c] : 0u;
+            }
         }
     };
     if (tid == 0) s_t = atomicAdd(ticket, 1u);
@@ -2757,76 +2809,119 @@ __global__ __launch_bounds__(BLOCK) void k_scan_lookback(uint32_t* __restrict__ 
     uint32_t x[EPT];
     if (T < ntiles) load(T, x);
     while (T < ntiles) {
-        const uint64_t base = (uint64_t)T * TILE + (uint64_t)tid * EPT;
         const bool full = (uint64_t)T * TILE + TILE <= n;
-        // thread-local exclusive scan (x becomes the exclusive prefix inside the thread)
-        uint32_t run = 0;
+        // the wave's exclusive scan, chunk by chunk (x becomes the exclusive prefix inside the wave)
+        uint32_t carry = 0;
 #pragma unroll
-        for (int j = 0; j < EPT; ++j) { const uint32_t v = x[j]; x[j] = run; run += v; }
-        // workgroup exclusive scan of the thread totals
-        const uint32_t inc = wave_incl_scan(run);
-        if (lane == 63) s_wave[w] = inc;
+        for (int j = 0; j < NV; ++j) {
+            const uint32_t a0 = x[4 * j], a1 = x[4 * j + 1], a2 = x[4 * j + 2], a3 = x[4 * j + 3];
+            const uint32_t sum = a0 + a1 + a2 + a3;
+            const uint32_t inc = wave_incl_scan(sum);
+            const uint32_t pre = carry + inc - sum;
+            x[4 * j] = pre;
+            x[4 * j + 1] = pre + a0;
+            x[4 * j + 2] = pre + a0 + a1;
+            x[4 * j + 3] = pre + a0 + a1 + a2;
+            carry += (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+        }
+        // workgroup exclusive scan of the wave totals
+        if (lane == 0) s_wave[w] = carry;
         if (tid == 0) s_t = atomicAdd(ticket, 1u);   // the next tile (read after the barrier)
         __syncthreads();
         uint32_t wpre = 0, agg = 0;
 #pragma unroll
         for (int i = 0; i < NW; ++i) {
-            const uint32_t s = s_wave[i];
-            wpre += (i < (int)w) ? s : 0u;
-            agg += s;
+            const uint32_t sv = s_wave[i];
+            wpre += (i < (int)w) ? sv : 0u;
+            agg += sv;
         }
-        const uint32_t texcl = wpre + inc - run;
+        const uint32_t texcl = wpre;
         const uint32_t Tn = s_t;
         // publish the aggregate at once (wave 0), then the next tile's loads, then the look-back
         if (w == 0 && lane == 0)
             st_store(status + T, (epoch << 2) | (T == 0 ? kStInclusive : kStAggregate), agg);
         uint32_t y[PF ? EPT : 1];
         if (PF && Tn < ntiles) load(Tn, reinterpret_cast<uint32_t(&)[EPT]>(y));
-        if (w == 0) {
+        // look-back by every wave at once: wave w reads predecessors T-1-64w-63 .. T-1-64w (NW x 64
+        // words per round: the nearest inclusive prefix is about as far back as there are tiles in
+        // flight, and a single wave's 64-word steps made that walk several round trips per tile)
+        if (T != 0) {
             uint32_t prefix = 0;
-            if (T != 0) {
-                int64_t j = (int64_t)T - 1;   // predecessor read by lane 0 this step
-                uint32_t spins = 0;
-                for (;;) {
-                    const int64_t me = j - (int64_t)lane;
-                    const unsigned long long sv = me >= 0 ? st_load(status + me)
-                                                          : (((unsigned long long)((epoch << 2) | kStInclusive)) << 32);
-                    const uint32_t f = (uint32_t)(sv >> 32);
-                    const bool pub = (f >> 2) == epoch;
-                    const bool incl = pub && (f & 3u) == kStInclusive;
-                    const uint64_t unpub = __ballot(!pub), inclm = __ballot(incl);
-                    // the first inclusive word, and no unpublished word before it
-                    const uint32_t stop = inclm ? (uint32_t)__builtin_ctzll(inclm) : 64u;
-                    const uint64_t before = stop >= 64u ? ~0ull : ((2ull << stop) - 1ull);
-                    if ((unpub & before) == 0ull) {
-                        uint32_t v = lane <= stop ? (uint32_t)sv : 0u;
-                        prefix += wave_sum(v);
-                        if (stop < 64u) break;
-                        j -= 64;
-                        continue;
+            int64_t j0 = (int64_t)T - 1;   // predecessor read by wave 0 lane 0 this round
+            uint32_t spins = 0;
+            for (;;) {
+                const int64_t me = j0 - (int64_t)(w * 64u + lane);
+                const unsigned long long sv = me >= 0 ? st_load(status + me)
+                                                      : (((unsigned long long)((epoch << 2) | kStInclusive)) << 32);
+                const uint32_t f = (uint32_t)(sv >> 32);
+                const bool pub = (f >> 2) == epoch;
+                const bool incl = pub && (f & 3u) == kStInclusive;
+                const uint64_t unpub = __ballot(!pub), inclm = __ballot(incl);
+                const uint32_t stop = inclm ? (uint32_t)__builtin_ctzll(inclm) : 64u;
+                const uint64_t before = stop >= 64u ? ~0ull : ((2ull << stop) - 1ull);
+                const bool bad = (unpub & before) != 0ull;
+                const uint32_t wsum = wave_sum(lane <= stop && pub ? (uint32_t)sv : 0u);
+                if (lane == 0) s_lb[w] = make_uint2(wsum, (stop < 64u ? 1u : 0u) | (bad ? 2u : 0u));
+                __syncthreads();
+                // waves in order: aggregates add up until the first inclusive prefix; an unpublished
+                // word stops the round (the waves before it are consumed)
+                uint32_t acc = 0, used = 0, state = 0;   // state 1 done, 2 wait
+#pragma unroll
+                for (int i = 0; i < NW; ++i) {
+                    const uint2 e = s_lb[i];
+                    if (state == 0) {
+                        if (e.y & 2u) {
+                            state = 2;
+                        } else {
+                            acc += e.x;
+                            if (e.y & 1u) state = 1;
+                            else ++used;
+                        }
                     }
-                    if (++spins > spin_max ||
-                        ((spins & 255u) == 0u && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
-                        if (lane == 0) atomicOr(err, 1u);
+                }
+                // a wait: bounded like k_onesweep's; thread 0 decides for the workgroup (the abort
+                // must be uniform: every thread passes the same barriers)
+                if (state == 2 && tid == 0) {
+                    const uint32_t sp = spins + 1u;
+                    s_abort = (sp > spin_max ||
+                               ((sp & 255u) == 0u && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)))
+                                  ? 1u : 0u;
+                }
+                __syncthreads();   // s_lb is rewritten next round; s_abort is read
+                prefix += acc;
+                if (state == 1) break;
+                j0 -= (int64_t)used * 64;
+                if (state == 2) {
+                    ++spins;
+                    if (s_abort) {
+                        if (tid == 0) atomicOr(err, 1u);
                         break;
                     }
                     __builtin_amdgcn_s_sleep(1);
                 }
-                if (lane == 0) st_store(status + T, (epoch << 2) | kStInclusive, prefix + agg);
             }
-            if (lane == 0) s_prefix = prefix;
+            if (tid == 0) {
+                st_store(status + T, (epoch << 2) | kStInclusive, prefix + agg);
+                s_prefix = prefix;
+            }
+        } else if (tid == 0) {
+            s_prefix = 0u;
         }
         __syncthreads();
         const uint32_t add = s_prefix + texcl;
         if (VEC && full) {
-            uint4* p = reinterpret_cast<uint4*>(data + base);
 #pragma unroll
-            for (int j = 0; j < EPT / 4; ++j)
-                p[j] = make_uint4(x[4 * j] + add, x[4 * j + 1] + add, x[4 * j + 2] + add, x[4 * j + 3] + add);
+            for (int j = 0; j < NV; ++j)
+                *reinterpret_cast<uint4*>(data + elem0(T, j)) =
+                    make_uint4(x[4 * j] + add, x[4 * j + 1] + add, x[4 * j + 2] + add, x[4 * j + 3] + add);
         } else {
 #pragma unroll
-            for (int j = 0; j < EPT; ++j)
-                if (base + j < n) data[base + j] = x[j] + add;
+            for (int j = 0; j < NV; ++j) {
+                const uint64_t e = elem0(T, j);
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+                    if (e + c < n) data[e + c] = x[4 * j + c] + add;
+            }
         }
         if (PF) {
 #pragma unroll

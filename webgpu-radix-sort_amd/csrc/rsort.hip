@@ -138,10 +138,16 @@ inline uint32_t split_smax2(uint64_t cap) { return (uint32_t)(cap / (kBucketCap 
 inline uint32_t split_smax3(uint64_t cap) { return (uint32_t)(cap / (rs::kSub8Cap + 1ull) + 1); }
 // level 2's tiles (each huge bucket's records in 16K-record tiles: at most one partial per bucket)
 inline uint32_t split_midmax(uint64_t cap) { return (uint32_t)(cap / (rs::kSub8Small + 1ull) + 1); }
+// runs of small sub-buckets: two consecutive runs of one bucket hold more than kSub8Small records,
+// unless a larger sub-bucket (at most cap / (kSub8Small + 1) of them) or the bucket's end is between
+inline uint32_t split_chunkmax(uint64_t cap) {
+    return (uint32_t)(3 * cap / (rs::kSub8Small + 1ull) + split_smax2(cap) + 1);
+}
 inline uint64_t split_words(uint64_t cap) {
     const uint64_t s2 = split_smax2(cap), s3 = split_smax3(cap);
     return 32ull + 1 + s2 + (3ull * s2 + 2) + (s2 + 1ull) + 256ull * s2 + (3ull * s3 + 2) + (s3 + 1ull) + 256ull * s3 +
-           1ull + split_midmax(cap);           // + the sub-buckets for the large tile
+           1ull + split_midmax(cap) +          // + the sub-buckets for the large tile
+           1ull + 2ull * split_chunkmax(cap);  // + the runs of small sub-buckets
 }
 constexpr uint32_t kHistGrid = 2048;
 constexpr int kCheckGrid = 2048;
@@ -1047,6 +1053,9 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
         q += 256ull * p->smax3;
         sw.mid = q;
         sw.midmax = split_midmax(p->capacity);
+        q += 1ull + sw.midmax;
+        sw.chunks = q;
+        sw.chunkmax = split_chunkmax(p->capacity);
         sw.smax2 = p->smax2;
         sw.smax3 = p->smax3;
         sw.tmax = (uint32_t)std::min<uint64_t>(p->status_words / 256u, 0xFFFFFFFFu);
@@ -2034,7 +2043,6 @@ constexpr uint32_t kScanMaxGrid = 1024;
 #endif
 constexpr int kScanBlock = RS_SCAN_BLOCK, kScanEpt = RS_SCAN_EPT;
 constexpr uint32_t kScanLbTile = kScanBlock * kScanEpt;
-constexpr uint32_t kScanPerCu = 2048 / kScanBlock;   // resident workgroups per CU (32 waves)
 struct Geometry { uint32_t grid, base, extra; };
 Geometry geometry(uint64_t n, uint32_t tile, uint32_t max_grid) {
     const uint64_t tiles = (n + tile - 1) / tile;
@@ -2073,7 +2081,7 @@ RS_EXPORT rs_status rs_scan_plan_create(int32_t device, uint64_t count, uint32_t
         if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
             cus = prop.multiProcessorCount;
     }
-    p->grid = (uint32_t)std::min<uint64_t>(p->status_words, (uint64_t)kScanPerCu * cus);
+    p->grid = (uint32_t)cus;   // resident workgroups per CU: scan_run (occupancy of the instantiation)
     hipError_t e = hipMalloc((void**)&p->sums, 4ull * kScanMaxGrid);
     if (e == hipSuccess) e = hipMalloc((void**)&p->status, 8ull * p->status_words);
     if (e == hipSuccess) e = hipMalloc((void**)&p->tickets, 4ull * (rs::kScanTickets + 1));
@@ -2099,7 +2107,10 @@ static rs_status scan_run(rs_scan_plan* p, void* data, const uint32_t* ind, hipS
         }
         const bool vec = ((uintptr_t)data & 15u) == 0;
         auto go = [&](auto kern) {
-            hipLaunchKernelGGL(kern, dim3(p->grid), dim3(kScanBlock), 0, s, (uint32_t*)data, (uint32_t)n,
+            // the resident workgroups of the device (tiles come from tickets in order)
+            static const uint32_t per_cu = resident_per_cu(kern, kScanBlock);
+            const uint32_t grid = (uint32_t)std::min<uint64_t>(p->status_words, (uint64_t)per_cu * p->grid);
+            hipLaunchKernelGGL(kern, dim3(grid), dim3(kScanBlock), 0, s, (uint32_t*)data, (uint32_t)n,
                                p->status, p->tickets, p->epoch, p->tickets + rs::kScanTickets, p->spin_max, ind);
         };
         if (vec) go(rs::k_scan_lookback<kScanBlock, kScanEpt, true, RS_SCAN_PF != 0>);

@@ -190,9 +190,9 @@ def test_scan_lookback_timeout_is_reported_then_plan_recovers():
 
 
 @pytest.mark.parametrize("n,offset", [(1, 0), (4095, 0), (4096, 1), (4097, 3), (16383, 0), (16384, 1),
-                                      (16385, 3), (1_000_003, 1), ((1 << 24) + 7, 0)])
+                                      (32767, 0), (32768, 1), (32769, 3), (1_000_003, 1), ((1 << 24) + 7, 0)])
 def test_scan_sizes_and_unaligned_data(n, offset):
-    """Tile edges of the single-pass scan (16K-element tiles), one element, and data that is not
+    """Tile edges of the single-pass scan (32K-element tiles), one element, and data that is not
     16-byte aligned (scalar loads / stores); the words after count are untouched."""
     from radix_sort_amd import PrefixSumKernel
     d = O.gen_u32(n + 17, n + offset + 8)

@@ -1961,6 +1961,8 @@ __global__ __launch_bounds__(1024) void k_split_count(const uint32_t* __restrict
     __shared__ uint32_t s_scr[NW];
     __shared__ uint32_t s_flag;
     __shared__ uint32_t s_c[LEVEL == 2 ? 256 : 1];
+    __shared__ uint32_t s_cs[LEVEL == 2 ? 256 : 1], s_cn[LEVEL == 2 ? 256 : 1], s_md[LEVEL == 2 ? 256 : 1];
+    __shared__ uint32_t s_nl[4];
     const uint32_t* gate = LEVEL == 2 ? sw.gate2 : sw.gate3;
     if (gated_off(gate, 0)) return;
     uint32_t* tab = LEVEL == 2 ? sw.tab2 : sw.tab3;
@@ -2059,39 +2061,48 @@ __global__ __launch_bounds__(1024) void k_split_count(const uint32_t* __restrict
                     // kSub8Small records together (one 16-bit LDS sort each: as many items as the
                     // bucket pass has for uniform keys, where one item per sub-bucket made 163840
                     // mostly small ones for config 4), the larger ones alone (mid list)
+                    // (one thread lays the runs out in LDS, two atomics claim their list slots,
+                    // every thread writes its entry: a list atomic per run made this 2x slower)
                     if (tid < 256u) s_c[tid] = c;
                     __syncthreads();
                     if (tid == 0) {
-                        auto emit = [&](uint32_t st, uint32_t cn) {
-                            const uint32_t slot = atomicAdd(&sw.chunks[0], 1u);
-                            if (slot < sw.chunkmax) {
-                                sw.chunks[1 + 2 * slot] = st;
-                                sw.chunks[2 + 2 * slot] = cn;
-                            } else {
-                                split_fail(sw);
-                            }
-                        };
-                        uint32_t cst = start[sg], acc = 0;
+                        uint32_t cst = start[sg], acc = 0, nch = 0, nmid = 0;
                         for (uint32_t dd = 0; dd < 256u; ++dd) {
                             const uint32_t cd = s_c[dd];
                             if (cd > kSub8Small) {
-                                if (acc) emit(cst, acc);
-                                if (cd <= kSub8Cap) {
-                                    const uint32_t slot = atomicAdd(&sw.mid[0], 1u);
-                                    if (slot < sw.midmax) sw.mid[1 + slot] = (sg << 8) | dd;
-                                    else split_fail(sw);
-                                }
+                                if (acc) { s_cs[nch] = cst; s_cn[nch++] = acc; }
+                                if (cd <= kSub8Cap) s_md[nmid++] = dd;
                                 cst += acc + cd;
                                 acc = 0;
                             } else if (acc + cd > kSub8Small) {
-                                emit(cst, acc);
+                                s_cs[nch] = cst;
+                                s_cn[nch++] = acc;
                                 cst += acc;
                                 acc = cd;
                             } else {
                                 acc += cd;
                             }
                         }
-                        if (acc) emit(cst, acc);
+                        if (acc) { s_cs[nch] = cst; s_cn[nch++] = acc; }
+                        s_nl[0] = nch;
+                        s_nl[1] = nmid;
+                        s_nl[2] = nch ? atomicAdd(&sw.chunks[0], nch) : 0u;
+                        s_nl[3] = nmid ? atomicAdd(&sw.mid[0], nmid) : 0u;
+                    }
+                    __syncthreads();
+                    if (tid < s_nl[0]) {
+                        const uint32_t slot = s_nl[2] + tid;
+                        if (slot < sw.chunkmax) {
+                            sw.chunks[1 + 2 * slot] = s_cs[tid];
+                            sw.chunks[2 + 2 * slot] = s_cn[tid];
+                        } else {
+                            split_fail(sw);
+                        }
+                    }
+                    if (tid < s_nl[1]) {
+                        const uint32_t slot = s_nl[3] + tid;
+                        if (slot < sw.midmax) sw.mid[1 + slot] = (sg << 8) | s_md[tid];
+                        else split_fail(sw);
                     }
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     __syncthreads();
@@ -2757,7 +2768,9 @@ __global__ __launch_bounds__(kBlock) void k_scan_small(uint32_t* __restrict__ a,
 // History (round 4, 2^28 u32): 256 x 16 tiles, one look-back wave, per-thread contiguous elements
 // 1.04 ms; 1024 x 16 tiles + PF 0.78 ms; + every wave looking back 0.78 ms (so the look-back walk
 // was not the limit); the per-thread contiguous layout touched every line with four load
-// instructions at 64-B lane strides - the striped layout reads each line once.
+// instructions at 64-B lane strides - the striped layout reads each line once: 0.59 ms; 1024 x 32
+// (one workgroup per CU, 128 KB of next tile in flight) 0.453 ms = 0.59 of peak (x 8: 1.33 ms,
+// 512 x 16: 1.49 ms).
 // tickets: a ring of kScanTickets counters; launch e uses tickets[e % ring] and clears the next
 // launch's.  VEC: the data is 16-byte aligned (16-byte loads / stores; else 4-byte ones).
 constexpr uint32_t kScanTickets = 64;

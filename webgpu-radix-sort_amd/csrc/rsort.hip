@@ -2029,14 +2029,13 @@ RS_EXPORT rs_status rs_plan_reset_kernel_times(rs_plan* p) {
 namespace {
 constexpr int kScanTile = 4096;
 constexpr uint32_t kScanMaxGrid = 1024;
-// single-pass scan (k_scan_lookback): 1024 threads x 16 contiguous elements = 16K-element tiles, two
-// workgroups per CU, the next tile prefetched across the look-back (4096-element tiles were bound
-// by the look-back chain at 2 TB/s, see the kernel)
+// single-pass scan (k_scan_lookback): 1024 threads x 32 elements = 32K-element tiles, one workgroup
+// per CU, the next tile's 128 KB in flight across the look-back and the stores (profiles/r04/scan*)
 #ifndef RS_SCAN_BLOCK
 #define RS_SCAN_BLOCK 1024
 #endif
 #ifndef RS_SCAN_EPT
-#define RS_SCAN_EPT 16
+#define RS_SCAN_EPT 32   // 32K-element tiles, one workgroup per CU (0.453 vs 0.591 ms at 16, 1.33 at 8)
 #endif
 #ifndef RS_SCAN_PF
 #define RS_SCAN_PF 1

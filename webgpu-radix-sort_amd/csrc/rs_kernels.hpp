@@ -1953,10 +1953,11 @@ __device__ __forceinline__ uint32_t split_seg_of(const uint32_t* first, uint32_t
 // row once, when its range leaves the segment; the segment's arrivals are then the workgroups whose
 // ranges meet it, and the last of them scans the row.
 template <int KS, int LEVEL>
-__global__ __launch_bounds__(1024) void k_split_count(const uint32_t* __restrict__ rec, SplitWs sw,
+__global__ __launch_bounds__(1024, 8) void k_split_count(const uint32_t* __restrict__ rec, SplitWs sw,
                                                       uint32_t shift) {
     constexpr uint32_t B = 1024, NW = B / 64;
-    constexpr int KPT = kSplitTile / B;
+    constexpr uint32_t HALF = kSplitTile / 2;   // a table tile is counted in two halves: 8 keys per
+    constexpr int KPT = HALF / B;               // thread + 8 in flight fit 64 VGPRs (two workgroups per CU)
     __shared__ uint32_t s_h[NW][256];
     __shared__ uint32_t s_scr[NW];
     __shared__ uint32_t s_flag;
@@ -1988,29 +1989,38 @@ __global__ __launch_bounds__(1024) void k_split_count(const uint32_t* __restrict
         t0 = t0r < e ? t0r : e;
         te = e - t0 < kSplitTile ? e : t0 + kSplitTile;
     };
-    // wave w counts records [t0 + w * 1024, +1024): slot j of lane l = + j * 64 + l; the pads past
-    // the tile's end load as kPadKey (digit 255) and are taken off at the flush
+    // wave w counts records [t0 + w * 512, +512): slot j of lane l = + j * 64 + l; the pads past
+    // the half's end load as kPadKey (digit 255) and are taken off at the flush
     auto load = [&](uint32_t t0, uint32_t te, uint32_t (&k)[KPT]) {
         const uint64_t wb = (uint64_t)t0 + w * (64u * KPT) + lane;
 #pragma unroll
         for (int j = 0; j < KPT; ++j) k[j] = wb + j * 64 < te ? rec[(wb + j * 64) * KS] : kPadKey;
     };
+    // half u of the range: tile u / 2, records [t0 + (u & 1) HALF, ...) of it
+    auto half = [&](uint32_t u, uint32_t sgu, uint32_t& h0, uint32_t& he) {
+        uint32_t t0, te;
+        geom(u >> 1, sgu, t0, te);
+        const uint32_t a = (u & 1u) ? (te - t0 > HALF ? t0 + HALF : te) : t0;
+        h0 = a;
+        he = te - a < HALF ? te : a + HALF;
+    };
     uint32_t sg = split_seg_of(first, nseg, t_lo);
-    uint32_t t0, te;
-    geom(t_lo, sg, t0, te);
+    uint32_t h0, he;
+    half(2 * t_lo, sg, h0, he);
     uint32_t k[KPT];
-    load(t0, te, k);
+    load(h0, he, k);
     uint32_t pads = 0;   // pads counted as digit 255 of segment sg so far
-    for (uint32_t t = t_lo; t < t_hi; ++t) {
-        pads += kSplitTile - (te - t0);
-        // the next tile's segment and keys (in flight while this tile is counted)
-        const uint32_t tn = t + 1;
-        const bool more = tn < t_hi;
-        const uint32_t sgn = (more && first[sg + 1] <= tn) ? sg + 1 : sg;   // segments have >= 1 tile
-        uint32_t kn[KPT], t0n = 0, ten = 0;
+    for (uint32_t u = 2 * t_lo; u < 2 * t_hi; ++u) {
+        pads += HALF - (he - h0);
+        // the next half's segment and keys (in flight while this half is counted)
+        const uint32_t un = u + 1;
+        const bool more = un < 2 * t_hi;
+        const uint32_t tn = un >> 1;
+        const uint32_t sgn = (more && (un & 1u) == 0u && first[sg + 1] <= tn) ? sg + 1 : sg;   // >= 1 tile each
+        uint32_t kn[KPT], h0n = 0, hen = 0;
         if (more) {
-            geom(tn, sgn, t0n, ten);
-            load(t0n, ten, kn);
+            half(un, sgn, h0n, hen);
+            load(h0n, hen, kn);
         }
         count_slots<KPT>(k, s_h[w], shift, 255u);
         if (!more || sgn != sg) {
@@ -2132,8 +2142,8 @@ __global__ __launch_bounds__(1024) void k_split_count(const uint32_t* __restrict
 #pragma unroll
             for (int j = 0; j < KPT; ++j) k[j] = kn[j];
             sg = sgn;
-            t0 = t0n;
-            te = ten;
+            h0 = h0n;
+            he = hen;
         }
     }
 }

@@ -1365,11 +1365,13 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
                 }
             } else {
 #if RS_BUCKET_POS
-                if (small_kpt == 17) {
-                    ballot ? smallw(rs::k_bucket_sort_wide<bb, 17, B0, LO, RS_BUCKET_POS_MW>)
-                           : smallw(rs::k_bucket_sort_wide<bb, 17, A0, LO, RS_BUCKET_POS_MW>);
-                    small_kpt = 0;
+#define RS_BKW(KP, MWP) case KP: ballot ? smallw(rs::k_bucket_sort_wide<bb, KP, B0, LO, MWP>) : smallw(rs::k_bucket_sort_wide<bb, KP, A0, LO, MWP>); small_kpt = 0; break;
+                switch (small_kpt) {
+                    RS_BKW(4, 8) RS_BKW(8, 7) RS_BKW(12, 6) RS_BKW(17, RS_BUCKET_POS_MW) RS_BKW(18, RS_BUCKET_POS_MW)
+                    RS_BKW(24, 4) RS_BKW(34, 3)
+                    default: break;
                 }
+#undef RS_BKW
 #endif
                 switch (small_kpt) {
                     RS_BK(4) RS_BK(8) RS_BK(12) RS_BK(17) RS_BK(18) RS_BK(24) RS_BK(34)

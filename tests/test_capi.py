@@ -69,7 +69,24 @@ def test_null_arguments():
     assert L.rs_plan_check(None) == _lib.RS_ERR_INVALID_ARG
     assert L.rs_scan_plan_run_indirect(None, None, None, 0, None) == _lib.RS_ERR_INVALID_ARG
     assert L.rs_scan_plan_dispatch_chain(None, None, 0) == 0
+    assert L.rs_plan_last_path(None, None) == _lib.RS_ERR_INVALID_ARG
+    assert L.rs_plan_last_split(None, None) == _lib.RS_ERR_INVALID_ARG
+    assert L.rs_plan_set_debug(None, None) == _lib.RS_ERR_INVALID_ARG
     L.rs_plan_destroy(None)  # no-op
+
+
+def test_debug_struct_and_kernel_kinds_match_the_header():
+    """The Python mirrors of rs_plan_debug (every field, the split switch last) and of the kernel
+    kinds (RS_KERNEL_SPLIT = 6, RS_KERNEL_KINDS = 7) agree with include/rsort.h."""
+    import os
+    import re
+    hdr = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "rsort.h")).read()
+    body = hdr[hdr.index("typedef struct rs_plan_debug"):hdr.index("} rs_plan_debug;")]
+    fields = re.findall(r"int32_t\s+(\w+);", body)
+    assert [f for f, _ in _lib.PlanDebug._fields_] == fields
+    assert fields[-1] == "split"
+    assert re.search(r"RS_KERNEL_SPLIT = 6", hdr) and re.search(r"RS_KERNEL_KINDS = 7", hdr)
+    assert _lib.RS_KERNEL_KINDS == 7 and _lib.KERNEL_NAMES[_lib.RS_KERNEL_SPLIT] == "split"
 
 
 def test_python_facade_validates_both_spellings():

@@ -119,12 +119,6 @@ constexpr uint32_t kTinyMax = 1024 * 16;
 // Hybrid MSD path (enqueue_sort_msd): used for key/value arrays and records of kMsdMin ... kMsdMax
 // keys when no 16-bit bucket exceeds kBucketCap records (decided on the device); buckets are sorted
 // in LDS by k_bucket_sort (tiles sized to the population) or, the largest, k_bucket_sort_wide.
-#ifndef RS_BUCKET_POS
-#define RS_BUCKET_POS 0      // sweep: see smallw in enqueue_sort_msd
-#endif
-#ifndef RS_BUCKET_POS_MW
-#define RS_BUCKET_POS_MW 5
-#endif
 #ifndef RS_MSD_DEFAULT
 #define RS_MSD_DEFAULT 1
 #endif
@@ -1270,15 +1264,6 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
                                p->tickets + 16, 0u, (const uint32_t*)nullptr, kbase, (const uint32_t*)sstart, rmask,
                                b_lo, b_cnt);
         };
-        // RS_BUCKET_POS (sweep): the population-sized KV tile through k_bucket_sort_wide's 4-byte
-        // (key bits, position) staging instead of 8-byte records (fewer VGPRs and LDS per
-        // workgroup: more workgroups per CU), one bucket per workgroup
-        auto smallw = [&](auto kern) {
-            hipLaunchKernelGGL(kern, dim3(b_cnt), dim3(bb), 0, s, ring ? ring : r2, hist16, base16, uk, uv, g_msd,
-                               p->tickets + 16, 0u, (const uint32_t*)nullptr, kbase, (const uint32_t*)sstart, rmask,
-                               vbits - 16, b_lo, b_cnt);
-        };
-        (void)smallw;
         auto big = [&](auto kern) {   // the 1024 x 17 tile (big_tile), one bucket per workgroup
             hipLaunchKernelGGL(kern, dim3(b_cnt), dim3(1024), 0, s, ring ? ring : r2, hist16, base16, uk, uv, g_msd,
                                p->tickets + 16, 0u, (const uint32_t*)nullptr, kbase, (const uint32_t*)sstart, rmask,
@@ -1364,15 +1349,6 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
                     default: break;
                 }
             } else {
-#if RS_BUCKET_POS
-#define RS_BKW(KP, MWP) case KP: ballot ? smallw(rs::k_bucket_sort_wide<bb, KP, B0, LO, MWP>) : smallw(rs::k_bucket_sort_wide<bb, KP, A0, LO, MWP>); small_kpt = 0; break;
-                switch (small_kpt) {
-                    RS_BKW(4, 8) RS_BKW(8, 7) RS_BKW(12, 6) RS_BKW(17, RS_BUCKET_POS_MW) RS_BKW(18, RS_BUCKET_POS_MW)
-                    RS_BKW(24, 4) RS_BKW(34, 3)
-                    default: break;
-                }
-#undef RS_BKW
-#endif
                 switch (small_kpt) {
                     RS_BK(4) RS_BK(8) RS_BK(12) RS_BK(17) RS_BK(18) RS_BK(24) RS_BK(34)
                     default: break;   // every bucket goes to the listed large-tile launch

@@ -2780,9 +2780,17 @@ __global__ __launch_bounds__(kBlock) void k_scan_small(uint32_t* __restrict__ a,
 // was not the limit); the per-thread contiguous layout touched every line with four load
 // instructions at 64-B lane strides - the striped layout reads each line once: 0.59 ms; 1024 x 32
 // (one workgroup per CU, 128 KB of next tile in flight) 0.453 ms = 0.59 of peak (x 8: 1.33 ms,
-// 512 x 16: 1.49 ms).
+// 512 x 16: 1.49 ms).  A wave's loads return in order, so the look-back's status words, read after
+// the 128 KB of next-tile loads, waited for all of them and the stores never overlapped the loads:
+// LB_FIRST reads the first round's words before those loads (0.440 ms = 0.63; profiles/r04/
+// scan_lbfirst_ab).  Taking the ticket after the prefetched tile during the look-back instead of
+// before it (off the critical path) ran 7.5x slower: tiles held two ahead stall their successors'
+// look-backs.
 // tickets: a ring of kScanTickets counters; launch e uses tickets[e % ring] and clears the next
 // launch's.  VEC: the data is 16-byte aligned (16-byte loads / stores; else 4-byte ones).
+#ifndef RS_SCAN_LB_FIRST
+#define RS_SCAN_LB_FIRST 1   // the look-back's first status words read before the next tile's loads
+#endif
 constexpr uint32_t kScanTickets = 64;
 template <int BLOCK, int EPT, bool VEC, bool PF = true>
 __global__ __launch_bounds__(BLOCK) void k_scan_lookback(uint32_t* __restrict__ data, uint32_t n,
@@ -2827,10 +2835,88 @@ __global__ __launch_bounds__(BLOCK) void k_scan_lookback(uint32_t* __restrict__ 
     };
     if (tid == 0) s_t = atomicAdd(ticket, 1u);
     __syncthreads();
-    uint32_t T = s_t;
+    // uniform values (tiles, sums read back from LDS) are moved to scalar registers: the 32 + 32
+    // elements in flight leave no vector registers to spare
+    auto uni = [](uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); };
+    uint32_t T = uni(s_t), Tn = 0;
     __syncthreads();   // every thread has read s_t before thread 0 takes the next ticket into it
     uint32_t x[EPT];
     if (T < ntiles) load(T, x);
+    // one look-back round over the status words sv (wave w lane l: predecessor j0 - 64w - l):
+    // 1 = the prefix is complete, 2 = aborted (timeout), 0 = go on from the updated j0
+    auto lb_word = [&](int64_t j0) -> unsigned long long {
+        const int64_t me = j0 - (int64_t)(w * 64u + lane);
+        return me >= 0 ? st_load(status + me) : (((unsigned long long)((epoch << 2) | kStInclusive)) << 32);
+    };
+    auto lb_round = [&](unsigned long long sv, uint32_t& prefix, int64_t& j0, uint32_t& spins) -> int {
+        const uint32_t f = (uint32_t)(sv >> 32);
+        const bool pub = (f >> 2) == epoch;
+        const bool incl = pub && (f & 3u) == kStInclusive;
+        const uint64_t unpub = __ballot(!pub), inclm = __ballot(incl);
+        const uint32_t stop = inclm ? (uint32_t)__builtin_ctzll(inclm) : 64u;
+        const uint64_t before = stop >= 64u ? ~0ull : ((2ull << stop) - 1ull);
+        const bool bad = (unpub & before) != 0ull;
+        const uint32_t wsum = wave_sum(lane <= stop && pub ? (uint32_t)sv : 0u);
+        if (lane == 0) s_lb[w] = make_uint2(wsum, (stop < 64u ? 1u : 0u) | (bad ? 2u : 0u));
+        __syncthreads();
+        // waves in order: aggregates add up until the first inclusive prefix; an unpublished word
+        // stops the round (the waves before it are consumed)
+        uint32_t acc = 0, used = 0, state = 0;   // state 1 done, 2 wait
+#pragma unroll
+        for (int i = 0; i < NW; ++i) {
+            const uint2 e = s_lb[i];
+            if (state == 0) {
+                if (e.y & 2u) {
+                    state = 2;
+                } else {
+                    acc += e.x;
+                    if (e.y & 1u) state = 1;
+                    else ++used;
+                }
+            }
+        }
+        // a wait: bounded like k_onesweep's; thread 0 decides for the workgroup (the abort must be
+        // uniform: every thread passes the same barriers)
+        if (state == 2 && tid == 0) {
+            const uint32_t sp = spins + 1u;
+            s_abort = (sp > spin_max ||
+                       ((sp & 255u) == 0u && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)))
+                          ? 1u : 0u;
+        }
+        __syncthreads();   // s_lb is rewritten next round; s_abort is read
+        acc = uni(acc);
+        used = uni(used);
+        state = uni(state);
+        prefix += acc;
+        if (state == 1) return 1;
+        j0 -= (int64_t)used * 64;
+        if (state == 2) {
+            ++spins;
+            if (s_abort) {
+                if (tid == 0) atomicOr(err, 1u);
+                return 2;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        return 0;
+    };
+    // the look-back of tile T (every wave at once: NW x 64 predecessors per round - the nearest
+    // inclusive prefix is about as far back as there are tiles in flight); sv0: its first round's
+    // words when LB_FIRST read them before the next tile's loads
+    auto lookback = [&](unsigned long long sv0, uint32_t agg) {
+        if (T != 0) {
+            uint32_t prefix = 0, spins = 0;
+            int64_t j0 = (int64_t)T - 1;
+            int r = RS_SCAN_LB_FIRST ? lb_round(sv0, prefix, j0, spins) : 0;
+            while (r == 0) r = lb_round(lb_word(j0), prefix, j0, spins);
+            if (tid == 0) {
+                st_store(status + T, (epoch << 2) | kStInclusive, prefix + agg);
+                s_prefix = prefix;
+            }
+        } else if (tid == 0) {
+            s_prefix = 0u;
+        }
+    };
     while (T < ntiles) {
         const bool full = (uint64_t)T * TILE + TILE <= n;
         // the wave's exclusive scan, chunk by chunk (x becomes the exclusive prefix inside the wave)
@@ -2858,80 +2944,36 @@ __global__ __launch_bounds__(BLOCK) void k_scan_lookback(uint32_t* __restrict__ 
             wpre += (i < (int)w) ? sv : 0u;
             agg += sv;
         }
-        const uint32_t texcl = wpre;
-        const uint32_t Tn = s_t;
-        // publish the aggregate at once (wave 0), then the next tile's loads, then the look-back
+        agg = uni(agg);
+        const uint32_t texcl = uni(wpre);   // uniform in the wave
+        Tn = uni(s_t);
+        // publish the aggregate at once (wave 0); then (LB_FIRST) the look-back's first status words
+        // and the next tile's loads: a wave's loads return in order, so status words read after the
+        // 128 KB of next-tile loads wait for all of them
         if (w == 0 && lane == 0)
             st_store(status + T, (epoch << 2) | (T == 0 ? kStInclusive : kStAggregate), agg);
+        const unsigned long long sv0 = (RS_SCAN_LB_FIRST && T != 0) ? lb_word((int64_t)T - 1) : 0ull;
         uint32_t y[PF ? EPT : 1];
-        if (PF && Tn < ntiles) load(Tn, reinterpret_cast<uint32_t(&)[EPT]>(y));
-        // look-back by every wave at once: wave w reads predecessors T-1-64w-63 .. T-1-64w (NW x 64
-        // words per round: the nearest inclusive prefix is about as far back as there are tiles in
-        // flight, and a single wave's 64-word steps made that walk several round trips per tile)
-        if (T != 0) {
-            uint32_t prefix = 0;
-            int64_t j0 = (int64_t)T - 1;   // predecessor read by wave 0 lane 0 this round
-            uint32_t spins = 0;
-            for (;;) {
-                const int64_t me = j0 - (int64_t)(w * 64u + lane);
-                const unsigned long long sv = me >= 0 ? st_load(status + me)
-                                                      : (((unsigned long long)((epoch << 2) | kStInclusive)) << 32);
-                const uint32_t f = (uint32_t)(sv >> 32);
-                const bool pub = (f >> 2) == epoch;
-                const bool incl = pub && (f & 3u) == kStInclusive;
-                const uint64_t unpub = __ballot(!pub), inclm = __ballot(incl);
-                const uint32_t stop = inclm ? (uint32_t)__builtin_ctzll(inclm) : 64u;
-                const uint64_t before = stop >= 64u ? ~0ull : ((2ull << stop) - 1ull);
-                const bool bad = (unpub & before) != 0ull;
-                const uint32_t wsum = wave_sum(lane <= stop && pub ? (uint32_t)sv : 0u);
-                if (lane == 0) s_lb[w] = make_uint2(wsum, (stop < 64u ? 1u : 0u) | (bad ? 2u : 0u));
-                __syncthreads();
-                // waves in order: aggregates add up until the first inclusive prefix; an unpublished
-                // word stops the round (the waves before it are consumed)
-                uint32_t acc = 0, used = 0, state = 0;   // state 1 done, 2 wait
+        if (PF && VEC) {
+            // without a branch, so that the wait for sv0 counts only these loads (after a join it
+            // would wait for all of them): a vector whose first element is past the end reads the
+            // first vector instead and drops it; one that straddles the end reads within the
+            // 16-byte block of its first element (data is 16-byte aligned) and drops the rest
 #pragma unroll
-                for (int i = 0; i < NW; ++i) {
-                    const uint2 e = s_lb[i];
-                    if (state == 0) {
-                        if (e.y & 2u) {
-                            state = 2;
-                        } else {
-                            acc += e.x;
-                            if (e.y & 1u) state = 1;
-                            else ++used;
-                        }
-                    }
-                }
-                // a wait: bounded like k_onesweep's; thread 0 decides for the workgroup (the abort
-                // must be uniform: every thread passes the same barriers)
-                if (state == 2 && tid == 0) {
-                    const uint32_t sp = spins + 1u;
-                    s_abort = (sp > spin_max ||
-                               ((sp & 255u) == 0u && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)))
-                                  ? 1u : 0u;
-                }
-                __syncthreads();   // s_lb is rewritten next round; s_abort is read
-                prefix += acc;
-                if (state == 1) break;
-                j0 -= (int64_t)used * 64;
-                if (state == 2) {
-                    ++spins;
-                    if (s_abort) {
-                        if (tid == 0) atomicOr(err, 1u);
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(1);
-                }
+            for (int j = 0; j < NV; ++j) {
+                const uint64_t e = elem0(Tn, j);
+                const uint4 q = *reinterpret_cast<const uint4*>(data + (e < n ? e : 0));
+                y[4 * j] = e < n ? q.x : 0u;
+                y[4 * j + 1] = e + 1 < n ? q.y : 0u;
+                y[4 * j + 2] = e + 2 < n ? q.z : 0u;
+                y[4 * j + 3] = e + 3 < n ? q.w : 0u;
             }
-            if (tid == 0) {
-                st_store(status + T, (epoch << 2) | kStInclusive, prefix + agg);
-                s_prefix = prefix;
-            }
-        } else if (tid == 0) {
-            s_prefix = 0u;
+        } else if (PF && Tn < ntiles) {
+            load(Tn, reinterpret_cast<uint32_t(&)[EPT]>(y));
         }
+        lookback(sv0, agg);
         __syncthreads();
-        const uint32_t add = s_prefix + texcl;
+        const uint32_t add = uni(s_prefix + texcl);
         if (VEC && full) {
 #pragma unroll
             for (int j = 0; j < NV; ++j)

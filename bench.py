@@ -106,6 +106,15 @@ def bench_prefix_sum(args, wl, torch, json_out) -> None:
         raise SystemExit("bench: prefix sum differs from the reference's CPU scan")
     value = n * K / elapsed / 1e9
     achieved = n * 8 / (kms / 1e3) / 1e9
+    # PMC traffic of the scan kernel (tools/pmc_traffic.py prefix_sum), for this library only
+    traffic = None
+    try:
+        with open(args.traffic_json) as f:
+            tj = json.load(f).get("prefix_sum")
+        if tj and n == tj.get("n") and tj.get("lib_sha16") == _lib_sha16():
+            traffic = tj.get("scan_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
     cpu = None
     if not args.no_cpu_baseline:
         m = 1 << 26
@@ -122,7 +131,7 @@ def bench_prefix_sum(args, wl, torch, json_out) -> None:
            "data": "synthetic (splitmix64 counter generator, values in [0, 8))",
            "config": {"workload": "prefix_sum", "description": wl["desc"], "elements": n},
            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                        "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                         "kernel": "k_scan_lookback (single pass, decoupled look-back)",
                         "avg_launch_ms": round(kms, 4), "algorithmic_bytes_per_launch": n * 8,
                         "lib_sha16": _lib_sha16()},

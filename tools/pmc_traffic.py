@@ -7,7 +7,7 @@ doubled.  Both corrections are re-checked in the same run on kernels with a know
 k_fill_random writes exactly n*4 bytes, k_histogram / k_pass_totals / k_hist16_in (the hybrid MSD
 path's 16-bit bucket count) read exactly n*4 bytes.
 
-    python3 tools/pmc_traffic.py [config3|config2|config4] [out.json]
+    python3 tools/pmc_traffic.py [config3|config2|config4|prefix_sum] [out.json]
 
 This script never touches the GPU itself: rocprofv3 runs tools/prof_driver.py as a child.
 """
@@ -39,6 +39,7 @@ def run_pass(counter: str, wl: str, outdir: str) -> dict:
                                         or "k_hist16_in" in name)
                    else "bucket" if "k_bucket_sort" in name
                    else "fill_random" if "k_fill_random" in name else "scan" if "k_scan_rows" in name
+                   else "scan_lb" if "k_scan_lookback" in name
                    else None)
             if key:
                 agg.setdefault(key, []).append(float(r["Counter_Value"]) * 1024.0)
@@ -58,6 +59,8 @@ def main():
     outdir = os.path.join(ROOT, "gpurun_out", "pmc_" + wl)
     fetch = run_pass("FETCH_SIZE", wl, outdir)
     write = run_pass("WRITE_SIZE", wl, outdir)
+    if wl == "prefix_sum":
+        return prefix_sum(fetch, write, out)
     n = N[wl]
     read_scale = (n * 4) / fetch["histogram"]          # expect ~2.0 (gfx950 FETCH_SIZE = 1/2)
     # expect ~1.0; config4's input is generated on the host (no k_fill_random launch): the scale of
@@ -92,6 +95,43 @@ def main():
     with open(out, "w") as f:
         json.dump(allres, f, indent=1)
     print(json.dumps(res))
+
+
+def lib_sha16() -> str:
+    import hashlib
+    lib = os.environ.get("RSORT_LIB", os.path.join(ROOT, "webgpu-radix-sort_amd", "lib", "librsort.so"))
+    return hashlib.sha256(open(lib, "rb").read()).hexdigest()[:16]
+
+
+def save(out: str, wl: str, res: dict) -> None:
+    try:
+        allres = json.load(open(out))
+    except (OSError, ValueError):
+        allres = {}
+    allres[wl] = res
+    with open(out, "w") as f:
+        json.dump(allres, f, indent=1)
+    print(json.dumps(res))
+
+
+def prefix_sum(fetch: dict, write: dict, out: str) -> None:
+    """k_scan_lookback per launch (2^28 u32 in place: 2 GiB algorithmic).  No kernel of this run
+    reads a known byte count, so FETCH_SIZE takes the gfx950 factor 2 that the sort workloads
+    calibrate (k_hist16_in: 1.9995 on config3); WRITE_SIZE is checked on k_fill_random (n * 4)."""
+    n = 1 << 28
+    write_scale = (n * 4) / write["fill_random"] if write.get("fill_random") else None
+    alg = n * 8
+    res = {"workload": "prefix_sum", "n": n,
+           "calibration": {"read_scale_from_histogram": "n/a (2.0 assumed, as calibrated on config3)",
+                           "write_scale_from_fill": round(write_scale, 4) if write_scale else None},
+           "raw_bytes": {"fetch": fetch, "write": write},
+           "scan_read_bytes_per_launch": fetch["scan_lb"] * 2.0,
+           "scan_write_bytes_per_launch": write["scan_lb"],
+           "scan_bytes_per_launch": fetch["scan_lb"] * 2.0 + write["scan_lb"],
+           "scan_algorithmic_bytes_per_launch": alg}
+    res["scan_traffic_over_algorithmic"] = round(res["scan_bytes_per_launch"] / alg, 4)
+    res["lib_sha16"] = lib_sha16()
+    save(out, "prefix_sum", res)
 
 
 if __name__ == "__main__":

@@ -26,6 +26,8 @@ def main():
     radix_bits = int(sys.argv[3]) if len(sys.argv) > 3 else 0
     if name == "region":
         return region(reps)
+    if name == "prefix_sum":
+        return prefix_sum(reps)
     n, kv, ls = WL[name]
     k = torch.empty(n, dtype=torch.int32, device="cuda")
     v = torch.empty(n, dtype=torch.int32, device="cuda") if kv else None
@@ -47,6 +49,20 @@ def main():
     torch.cuda.synchronize()
     assert ops.is_sorted(k)
     print(f"prof_driver: {reps} sorts of {name} done")
+
+
+def prefix_sum(reps, n=1 << 28):
+    """PrefixSumKernel over bench.py's prefix_sum shape (2^28 u32, values in [0, 8))."""
+    from radix_sort_amd import PrefixSumKernel
+    t = torch.empty(n, dtype=torch.int32, device="cuda")
+    kern = PrefixSumKernel(data=t, count=n)
+    for r in range(reps):
+        ops.fill_random_u32(t, 2000 + r)
+        t &= 7
+        kern.dispatch()
+    torch.cuda.synchronize()
+    kern.check()
+    print(f"prof_driver: {reps} prefix sums of 2^28 u32 done")
 
 
 def region(reps, n=1 << 28, span=32, rounds=4):

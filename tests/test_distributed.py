@@ -321,9 +321,14 @@ def test_multi_gpu_breakdown_fields():
     """The N-rank bench line's multi_gpu breakdown (bench.py, distributed.summarize_timelines):
     the layout every rank gathers (timeline_record) and the fields rank 0 derives from it - the
     exchange time E and xGMI GB/s per rank, the slowest rank's local terms, rank edges."""
+    from radix_sort_amd import _lib
     from radix_sort_amd.distributed import StepTimeline, summarize_timelines, timeline_record
     G = 4
-    names = ["histogram", "scan", "scatter", "check", "bucket", "fallback", "sender_hist16", "sender_partition"]
+    # the layout bench.py ships: the library's kernel kinds, then the sender's two terms
+    names = list(_lib.KERNEL_NAMES) + ["sender_hist16", "sender_partition"]
+    kinds = {"histogram": 0.3, "scan": 0.0, "scatter": 2.0, "check": 0.0, "bucket": 2.06, "fallback": 0.0,
+             "split": 0.0, "sender_hist16": 0.3, "sender_partition": 1.05}
+    assert set(names) == set(kinds), "a kernel kind was added: give it a value here"
     tl = StepTimeline()
     tl.bytes_sent, tl.bytes_recv = 7 * 10**8, 7 * 10**8
     empty = timeline_record(tl, G, 10, 20, 1000, [0.0] * len(names), 1.5)   # no GPU marks: zeros
@@ -332,7 +337,7 @@ def test_multi_gpu_breakdown_fields():
     def row(t_off, k0, k1, n):
         return ([0.3, 0.35, 1.4] + [1.4 + 0.6 * (g + 1) + t_off for g in range(G)]
                 + [2.5 + 0.6 * (g + 1) + t_off for g in range(G)]
-                + [7e8, 7e8, k0, k1, n, 2.2] + [0.3, 0.0, 2.0, 0.0, 2.06, 0.0, 0.3, 1.05])
+                + [7e8, 7e8, k0, k1, n, 2.2] + [kinds[nm] for nm in names])
 
     s = summarize_timelines([row(0.0, 5, 100, 10), row(0.5, 100, 300, 12), row(0.0, 0, 0, 0)], G, names)
     assert s["ranks"] == 3

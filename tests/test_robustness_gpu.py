@@ -159,6 +159,28 @@ def test_prefix_sum_indirect_dispatch():
     assert (_np(d2) == data).all()
 
 
+def test_prefix_sum_gated_dispatch_after_ticket_ring_wraps():
+    """every launch clears the NEXT launch's ticket slot (a ring of 64).  A launch gated
+    off by a zeroed indirect triple must clear it too, else after >= 64 launches the next live
+    dispatch finds a stale count in its slot and scans nothing without an error."""
+    from radix_sort_amd import PrefixSumKernel
+    n = 200_003
+    data = O.gen_u32(17, n) % np.uint32(1000)
+    d = _t(data)
+    k = PrefixSumKernel(data=d, count=n)
+    chain = k.get_dispatch_chain()
+    live = _t(np.array(chain, dtype=np.uint32))
+    zero = _t(np.array([0] + chain[1:], dtype=np.uint32))
+    for _ in range(70):          # wraps the 64-slot ticket ring
+        k.dispatch(None, live, 0)
+    k.dispatch(None, zero, 0)    # gated off on the device
+    d.copy_(_t(data))
+    k.dispatch(None, live, 0)    # the launch whose slot the gated one had to clear
+    k.check()
+    assert (_np(d) == O.prefix_sum(data, n)).all()
+    k.destroy()
+
+
 def test_scan_lookback_timeout_is_reported_then_plan_recovers():
     """The single-pass PrefixSumKernel: with the wait bound at 0 a look-back wait on an unpublished
     predecessor times out, check() reports it once (RS_ERR_DEVICE); with the default bound the same

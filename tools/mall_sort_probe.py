@@ -4,7 +4,10 @@ re-generated right before every sort (so small sorts run with their whole workin
 Infinity Cache).  One plan, one pair of arrays, `iters` sorts.  Run under rocprofv3 --stats for
 per-kernel averages, or alone for the plan's own HIP-event kernel times.
 
-    RSORT_TILE=large RSORT_ONESWEEP=1 python tools/mall_sort_probe.py LOG2N [iters]
+    python tools/mall_sort_probe.py LOG2N [iters]
+
+(the plan picks its path by size; the library reads no environment variables - force a path with
+``radix_sort_amd._lib.plan_debug(tile="large", onesweep=1)`` around the plan's creation)
 """
 import json
 import os

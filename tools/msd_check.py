@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
-"""Hybrid MSD path (RSORT_MSD=1) check + timing on the GPU (diagnostic, not a test file):
+"""Hybrid MSD path check + timing on the GPU (diagnostic, not a test file):
 parity against the oracle at 13M-64M keys, property checks at 256M, both device fallbacks
 (skewed top byte -> LSD on the input; 16-bit buckets over capacity -> LSD on R1), and the
-config3 timing with the MSD path on and off.  Prints JSON lines."""
+config3 timing.  The path is the plan's own choice; each line records the one the device took
+(rs_plan_last_path).  To force a path, wrap a run in ``_lib.plan_debug(msd=0)``.  Prints JSON lines."""
 import json
 import os
 import sys
@@ -58,7 +59,7 @@ def run(n, kind, seed, exact):
         ek, ev = O.stable_sort_masked_c(kin.cpu().numpy().view(np.uint32), np.arange(n, dtype=np.uint32), 32)
         ok = ok and np.array_equal(k.cpu().numpy().view(np.uint32), ek) and \
             np.array_equal(v.cpu().numpy().view(np.uint32), ev)
-    print(json.dumps({"n": n, "kind": kind, "msd_env": os.environ.get("RSORT_MSD"), "ok": bool(ok),
+    print(json.dumps({"n": n, "kind": kind, "device_path": kern.last_path(), "ok": bool(ok),
                       "kernel_ms": kt}), flush=True)
     kern.destroy()
     return ok
@@ -89,7 +90,7 @@ def timing(n, steps=10):
                 e = kt.setdefault(a, [0.0, 0])
                 e[0] += b["ms"] / steps
                 e[1] += b["launches"] / steps
-    print(json.dumps({"timing_n": n, "msd_env": os.environ.get("RSORT_MSD"),
+    print(json.dumps({"timing_n": n, "device_path": ks[0].last_path(),
                       "ms_per_sort": round(dt * 1e3, 4), "gkeys": round(n / dt / 1e9, 2),
                       "kernel_ms_per_sort": {a: [round(b[0], 4), b[1]] for a, b in kt.items()}}),
           flush=True)

@@ -371,7 +371,7 @@ RS_EXPORT rs_status rs_group_sort(rs_group* g, void* const* keys, void* const* v
     for (int i = 0; i < W; ++i) {
         Rank& k = g->r[i];
         Dev dev(k.device);
-        k.t_valid = prof;
+        k.t_valid = false;   // set once t_done is recorded: a sort that fails partway has no timing
         k.t_rounds = W == 1 ? 0u : G;
         k.bytes_sent = k.bytes_recv = 0;
         G_TRY(mark(k, k.t_start, k.sort_s));
@@ -551,6 +551,7 @@ RS_EXPORT rs_status rs_group_sort(rs_group* g, void* const* keys, void* const* v
         Rank& k = g->r[i];
         Dev dev(k.device);
         G_TRY(mark(k, k.t_done, k.sort_s));
+        k.t_valid = prof;
         G_HIP(hipEventRecord(k.ev_done, k.sort_s));
         if (streams && streams[i]) G_HIP(hipStreamWaitEvent((hipStream_t)streams[i], k.ev_done, 0));
     }

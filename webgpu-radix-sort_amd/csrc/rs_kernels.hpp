@@ -22,29 +22,47 @@
 #include <type_traits>
 #include <stdint.h>
 
-#ifndef RS_XCD_GROUP
+// Tuning and diagnostic knobs (RS_* below): product builds fix every one at its default, whatever
+// -D says, so no flag can change what librsort computes; sweep and diagnostic builds (make variants,
+// tools/build_variants.sh) compile with -DRS_SWEEP=1 to vary them.
+#if defined(RS_SWEEP) && RS_SWEEP
+#define RS_KNOB_OPEN 1
+#else
+#define RS_KNOB_OPEN 0
+#endif
+
+#if !RS_KNOB_OPEN || !defined(RS_XCD_GROUP)
+#undef RS_XCD_GROUP
 #define RS_XCD_GROUP 1       // consecutive tiles run on one XCD in the same round (speed only)
 #endif
-#ifndef RS_HIST_XCD
+#if !RS_KNOB_OPEN || !defined(RS_HIST_XCD)
+#undef RS_HIST_XCD
 #define RS_HIST_XCD 1        // k_histogram: adjacent tiles' counts written from one XCD (speed only)
 #endif
-#ifndef RS_ONESWEEP_TRACE
+#if !RS_KNOB_OPEN || !defined(RS_ONESWEEP_TRACE)
+#undef RS_ONESWEEP_TRACE
 #define RS_ONESWEEP_TRACE 0  // 1: printf the stuck tile when a look-back wait times out
 #endif
-#ifndef RS_PACK_POS
+#if !RS_KNOB_OPEN || !defined(RS_PACK_POS)
+#undef RS_PACK_POS
 #define RS_PACK_POS 1        // 1: staging-round kernels keep tile positions as 16-bit pairs
 #endif
-#ifndef RS_SCATTER_DEBUG
-#define RS_SCATTER_DEBUG 0   // ablation (tools/sweep.py): 1 = linear writes (output pos = input pos)
-#endif
-#ifndef RS_NT_STORE
+#if !RS_KNOB_OPEN || !defined(RS_NT_STORE)
+#undef RS_NT_STORE
 #define RS_NT_STORE 0        // pass output stores: 1 non-temporal, 2 write-through (sc1), 3 system scope
 #endif
-#ifndef RS_NT_LOAD
+#if !RS_KNOB_OPEN || !defined(RS_NT_LOAD)
+#undef RS_NT_LOAD
 #define RS_NT_LOAD 0         // 1: pass inputs (full tiles) loaded non-temporal (read once per pass)
 #endif
 
-#ifndef RS_STAMPS
+#if !RS_KNOB_OPEN || !defined(RS_STAGE_BATCH)
+#undef RS_STAGE_BATCH
+#define RS_STAGE_BATCH 1     // stage_tile: all slots' offsets read before the staging writes
+#endif
+
+#if !RS_KNOB_OPEN || !defined(RS_STAMPS)
+#undef RS_STAMPS
 #define RS_STAMPS 0          // diagnostic build: per-tile phase timestamps of k_onesweep
 #endif
 
@@ -306,7 +324,7 @@ __global__ __launch_bounds__(kBlock) void k_scan_rows(uint32_t* __restrict__ cou
 //    earlier slots and lower lanes: the stable rank, for ~3 VALU + 1 LDS op per 64 keys.
 //  * RANK_BALLOT: match mask from R ballots (lanes sharing my digit), mbcnt for the rank in
 //    the slot, the lowest lane bumps the wave counter (ds_add_rtn) and broadcasts it
-//    (ds_bpermute).  Architecture-guaranteed; ~60 VALU per 64 keys.  RSORT_RANK=ballot.
+//    (ds_bpermute).  Architecture-guaranteed; ~60 VALU per 64 keys.  rs_plan_debug.rank = 1.
 enum RankMode { RANK_LDS_ATOMIC = 0, RANK_BALLOT = 1 };
 
 // Per-slot 32-bit values (ranks, then tile positions) of a thread's KPT keys.  PACK keeps two
@@ -416,7 +434,8 @@ __device__ __forceinline__ uint64_t match_mask(uint32_t d, uint64_t valid) {
 // (the uniform-key path, unchanged).  Both rank a digit's lanes in lane order (stable): the LDS
 // resolves one instruction's same-address atomics in lane order, so runs of one digit get their
 // bases in lane order too.
-#ifndef RS_RUN_HEADS_MAX
+#if !RS_KNOB_OPEN || !defined(RS_RUN_HEADS_MAX)
+#undef RS_RUN_HEADS_MAX
 #define RS_RUN_HEADS_MAX 32   // average run heads per slot at or below which a wave counts runs
 #endif
 
@@ -429,7 +448,8 @@ __device__ __forceinline__ uint64_t run_heads(uint32_t d) {
 
 // Does this wave's tile have at most RS_RUN_HEADS_MAX run heads per slot on average?  Sampled
 // on every RS_RUN_SAMPLE-th slot (the test runs on every tile of uniform keys too).
-#ifndef RS_RUN_SAMPLE
+#if !RS_KNOB_OPEN || !defined(RS_RUN_SAMPLE)
+#undef RS_RUN_SAMPLE
 #define RS_RUN_SAMPLE 4
 #endif
 template <int KPT>
@@ -571,6 +591,20 @@ __device__ __forceinline__ void stage_tile(const uint32_t (&k)[KPT], const uint3
                                            uint32_t mask, uint32_t* s_ntot, uint32_t nshift,
                                            uint32_t nmask) {
     shift = opaque_u(shift);
+#if RS_STAGE_BATCH
+    // every slot's wave offset read first (KPT LDS reads in flight), then the KPT writes: the
+    // read -> write dependency of one slot no longer serialises the LDS latency slot by slot
+    uint32_t s[KPT];
+#pragma unroll
+    for (int j = 0; j < KPT; ++j) s[j] = whist_w[(k[j] >> shift) & mask] + rank.get(j);
+#pragma unroll
+    for (int j = 0; j < KPT; ++j) {
+        if (s[j] < (uint32_t)TILE) {   // always; keeps a bug from writing past the staging area
+            if (HAS_VALUES) s_kv[s[j]] = make_uint2(k[j], v[j]);
+            else s_keys[s[j]] = k[j];
+        }
+    }
+#else
 #pragma unroll
     for (int j = 0; j < KPT; ++j) {
         const uint32_t s = whist_w[(k[j] >> shift) & mask] + rank.get(j);
@@ -579,6 +613,7 @@ __device__ __forceinline__ void stage_tile(const uint32_t (&k)[KPT], const uint3
             else s_keys[s] = k[j];
         }
     }
+#endif
     if (s_ntot) count_slots<KPT>(k, s_ntot, nshift, nmask);
 }
 
@@ -635,12 +670,8 @@ __device__ __forceinline__ void scatter_tile(const uint32_t* s_keys, const uint2
         } else {
             key = s_keys[i];
         }
-#if RS_SCATTER_DEBUG == 1
-        const uint32_t pos = tile0 + pbase + i + (s_gdelta[(key >> shift) & mask] & 0);  // ablation
-#else
         const uint32_t pos = s_gdelta[(key >> shift) & mask] + pbase + i;
         (void)tile0;
-#endif
         if (pos < n) {  // never false for consistent offsets; keeps a bug from faulting
             const uint32_t q = pos & pmask;
             if (LO == LAYOUT_AOS) {
@@ -741,13 +772,16 @@ struct PassList {
 // chk (may be null, check_order): the order check of pass 0's input fused into this read of it,
 // *chk |= 1 if any adjacent pair is out of order under fmask (k_check's job, one read fewer).
 constexpr int kTotalsMax = 1024;
-#ifndef RS_TOT_BLOCK
+#if !RS_KNOB_OPEN || !defined(RS_TOT_BLOCK)
+#undef RS_TOT_BLOCK
 #define RS_TOT_BLOCK 256     // k_pass_totals threads per workgroup
 #endif
-#ifndef RS_TOT_PER_CU
+#if !RS_KNOB_OPEN || !defined(RS_TOT_PER_CU)
+#undef RS_TOT_PER_CU
 #define RS_TOT_PER_CU 8      // k_pass_totals workgroups per CU
 #endif
-#ifndef RS_TOT_U
+#if !RS_KNOB_OPEN || !defined(RS_TOT_U)
+#undef RS_TOT_U
 #define RS_TOT_U 1           // k_pass_totals 16-byte loads per lane issued together
 #endif
 // only (bit p): count pass p's digit (its slot of out stays as it is otherwise).
@@ -857,29 +891,16 @@ __global__ __launch_bounds__(BLOCK) void k_pass_totals(const uint32_t* __restric
 // published" and the region never needs clearing (the host clears it when the epoch wraps).
 // Waits are bounded: a timeout sets err[0] (never a hang).
 constexpr uint32_t kStAggregate = 1u, kStInclusive = 2u;
-#ifndef RS_LOOKBACK
+#if !RS_KNOB_OPEN || !defined(RS_LOOKBACK)
+#undef RS_LOOKBACK
 #define RS_LOOKBACK 4
 #endif
-// Where k_onesweep issues the next tile's loads (speed only).  A wave's vector-memory operations
-// complete in issue order (one vmcnt), so look-back status loads issued behind the wave's prefetch
-// wait for the whole prefetch to land.  0: every wave before the look-back; 1: the look-back waves
-// after their look-back, the others before it; 2: every wave after the look-back barrier.
-#ifndef RS_PREFETCH
-#define RS_PREFETCH 0
-#endif
-// 1: thread 0 takes the next tile's ticket at the top of the current tile (the atomic's round
-// trip overlaps the rank phase instead of stalling the staging barrier).
-#ifndef RS_EARLY_TICKET
-#define RS_EARLY_TICKET 0
-#endif
-// RS_AHEAD (speed only): every workgroup holds its next tile's ticket one tile ahead (taken at the
-// top of the previous tile, so the atomic's round trip is never waited for), and issues the next
-// tile's loads slot by slot while staging the current tile (k_onesweep without next-pass totals
-// or order check; else as RS_PREFETCH).  The tile prefetch then starts ~8K cycles earlier, and the
-// look-back's status loads, which queue behind it in the CU's memory pipeline, return earlier.
-#ifndef RS_AHEAD
-#define RS_AHEAD 0
-#endif
+// k_onesweep issues the next tile's loads after staging, before the look-back, in every wave.
+// Measured and dropped (profiles/r03_prefetch_placement_ab.json, profiles/r04/quick1, profiles/r05/
+// ab_vmwait; the code is in the history): the loads after the look-back (slower), the next ticket
+// taken at the top of the tile, the loads issued slot by slot while staging with the ticket held a
+// tile ahead (RS_AHEAD, within noise), and explicit vmcnt waits so that the next tile's rank runs
+// while this tile's stores drain (0.5 % slower).
 constexpr int kLookback = RS_LOOKBACK;   // predecessors read per look-back step
 
 __device__ __forceinline__ unsigned long long st_load(const unsigned long long* p) {
@@ -933,7 +954,7 @@ __global__ __launch_bounds__(BLOCK, pass_min_waves(BLOCK, KPT)) void k_onesweep(
     uint32_t nshift, uint32_t nmask, uint32_t epoch, const uint32_t* gate, int pass,
     uint32_t* chk, uint32_t fmask, uint32_t spin_max, uint32_t* host_err,
     const uint32_t* __restrict__ segtab = nullptr, const uint32_t* __restrict__ base16 = nullptr,
-    uint32_t kbase = 0, uint32_t pmask = 0xFFFFFFFFu) {
+    uint32_t kbase = 0, uint32_t pmask = 0xFFFFFFFFu, uint32_t* xticket = nullptr, uint32_t xk = 0) {
     // ntot (may be null): whole-array totals of the NEXT pass's digit (key >> nshift) & nmask,
     // counted here from the keys this workgroup stages, so only pass 0 needs k_pass_totals.
     // chk (may be null, check_order, pass > 0): the order check of this pass's input, fused:
@@ -973,12 +994,29 @@ __global__ __launch_bounds__(BLOCK, pass_min_waves(BLOCK, KPT)) void k_onesweep(
     const uint32_t* start2 = segtab + 2 + ntiles;
     const uint32_t* end2 = segtab + 2 + 2 * ntiles;
     if (tid == 0) s_inv = 0u;
+    // Tile claims.  xk == 0: one ticket counter, tiles in ticket order.  xk > 0 (a grid of 8 * xk
+    // workgroups): XCD-grouped claims - workgroup g draws from counter xticket[g % 8] (workgroups
+    // are dealt round-robin over the 8 XCDs, so that is its XCD), and the c-th claim of counter x
+    // is tile (c / xk) * 8xk + x * xk + c % xk: every round of 8xk consecutive tiles gives each XCD
+    // xk ADJACENT tiles, which its xk workgroups process at the same time.  The 128-B line where a
+    // digit run of tile T meets the run of tile T + 1 is then completed in one L2 instead of reaching
+    // HBM as two partial writes (tools/run_probe.hip: 1.07 -> 0.88 ms for the pass's write pattern).
+    // Correctness does not depend on the placement: each counter's claims are in tile order and
+    // every counter has workgroups (grid >= 8, dispatched in order), so every tile is claimed by a
+    // running workgroup whose predecessors are claimed too (look-back progress as with one counter).
+    const uint32_t xq = blockIdx.x & 7u;
+    auto claim = [&]() -> uint32_t {
+        if (!xticket) return atomicAdd(ticket, 1u);
+        const uint32_t c = atomicAdd(xticket + xq, 1u);
+        const uint32_t r = c / xk;
+        return r * 8u * xk + xq * xk + (c - r * xk);   // monotone in c: past nt once, past for good
+    };
     {   // first output position of every digit
         const uint32_t c = (!SG && tid < (uint32_t)RADIX && tid <= mask) ? dtot[tid] : 0u;
         uint32_t all;
         const uint32_t ex = block_excl_scan_n<NW>(c, s_scratch, all);
         if (tid < (uint32_t)RADIX) s_dbase[tid] = ex;
-        if (tid == 0) s_next = atomicAdd(ticket, 1u);
+        if (tid == 0) s_next = claim();
         __syncthreads();
     }
     uint32_t T = s_next;
@@ -1030,20 +1068,23 @@ __global__ __launch_bounds__(BLOCK, pass_min_waves(BLOCK, KPT)) void k_onesweep(
         else
             load_tile<KPT, L, (SR > 1)>(in_k, in_v, (uint64_t)t0 + w * WAVE_KEYS, bound, (uint64_t)t0 + TILE <= bound, k, v);
     };
+    // chk: the key after this wave's slots (next wave or next tile) is loaded with the tile, so
+    // that no load is issued behind the scatter's stores (a wave's vector-memory operations
+    // complete in issue order: waiting for such a load would wait for every store before it)
+    uint32_t bkey_nx = kPadKey;
     auto load = [&](uint32_t t) {
         uint32_t t0, tend, sg, fi;
         geom(t, t0, tend, sg, fi);
         load_at(t0, SG ? tend : n);
+        if (chk) {
+            const uint64_t q = (uint64_t)t0 + (w + 1) * (uint32_t)WAVE_KEYS;
+            bkey_nx = q < n ? in_k[q * (L == LAYOUT_AOS ? 2u : 1u)] : kPadKey;
+        }
     };
     if (T < nt) load(T);
-    // RS_AHEAD: thread 0's request for the next tile's ticket, broadcast at the next publish barrier
-    uint32_t ahead_ticket = 0;
-    if (RS_AHEAD && tid == 0) ahead_ticket = atomicAdd(ticket, 1u);
     while (T < nt) {
         RS_STAMP(pass, ntiles, T, 0, __builtin_amdgcn_s_memtime());
         RS_STAMP(pass, ntiles, T, 7, blockIdx.x);
-        uint32_t early_ticket = 0;
-        if (RS_EARLY_TICKET && tid == 0) early_ticket = atomicAdd(ticket, 1u);
         uint32_t tile0, tend, seg, seg_first;
         geom(T, tile0, tend, seg, seg_first);
         const bool full = tend - tile0 == (uint32_t)TILE;
@@ -1064,11 +1105,7 @@ __global__ __launch_bounds__(BLOCK, pass_min_waves(BLOCK, KPT)) void k_onesweep(
                 if (wb + j * 64 < nvalid) k[j] -= kbase;
         }
         const uint32_t npad = (uint32_t)TILE - nvalid;
-        uint32_t bkey = kPadKey;   // the key after this wave's slots (next wave or next tile)
-        if (chk) {
-            const uint64_t q = (uint64_t)tile0 + (w + 1) * (uint32_t)WAVE_KEYS;
-            if (q < n) bkey = in_k[q * (L == LAYOUT_AOS ? 2u : 1u)];
-        }
+        const uint32_t bkey = bkey_nx;   // the key after this wave's slots (chk)
         Slots<KPT, RS_PACK_POS && (SR > 1)> rank;
         uint32_t c;
         const uint32_t tstart = rank_tile<R, NW, KPT, RANK>(k, rank, s_whist, s_scratch, shift,
@@ -1085,41 +1122,9 @@ __global__ __launch_bounds__(BLOCK, pass_min_waves(BLOCK, KPT)) void k_onesweep(
             else st_store(st, (epoch << 2) | kStAggregate, c);
             set_wave_offsets<R, NW>(s_whist, tstart);
         }
-        if (RS_AHEAD && tid == 0) {
-            s_next = ahead_ticket;                    // requested a tile ago
-            ahead_ticket = atomicAdd(ticket, 1u);     // the one after it: read next tile
-        }
         __syncthreads();
         RS_STAMP(pass, ntiles, T, 2, __builtin_amdgcn_s_memtime());
-        bool pf_done = false;                         // RS_AHEAD: next tile loaded while staging
-        if (RS_AHEAD && SR == 1 && !ntot && !chk) {
-            const uint32_t Ta = s_next;
-            uint32_t n0 = 0, nend = 0, nsg, nfi;
-            if (Ta < nt) geom(Ta, n0, nend, nsg, nfi);
-            const bool nfull = Ta < nt && nend - n0 == (uint32_t)TILE;
-            const size_t b = (size_t)n0 + w * WAVE_KEYS + lane_id();
-            const uint32_t* whist_w = s_whist[w];
-            const uint32_t sh = opaque_u(shift);
-#pragma unroll
-            for (int j = 0; j < KPT; ++j) {
-                const uint32_t sp = whist_w[(k[j] >> sh) & mask] + rank.get(j);
-                if (sp < (uint32_t)TILE) {
-                    if (HAS_VALUES) s_kv[sp] = make_uint2(k[j], v[j]);
-                    else s_keys[sp] = k[j];
-                }
-                if (nfull) {   // slot j of the next tile into the registers just staged
-                    if (L == LAYOUT_AOS) {
-                        const unsigned long long r = ld_in(reinterpret_cast<const unsigned long long*>(in_k) + b + j * 64);
-                        k[j] = (uint32_t)r;
-                        if (HAS_VALUES) v[j] = (uint32_t)(r >> 32);
-                    } else {
-                        k[j] = ld_in(in_k + b + j * 64);
-                        if (HAS_VALUES) v[j] = ld_in(in_v + b + j * 64);
-                    }
-                }
-            }
-            pf_done = nfull;
-        } else if (SR == 1) {
+        if (SR == 1) {
             stage_tile<KPT, HAS_VALUES, TILE>(k, v, rank, s_whist[w], s_keys, s_kv, shift, mask,
                                               ntot ? s_ntot : nullptr, nshift, nmask);
         } else {
@@ -1128,14 +1133,14 @@ __global__ __launch_bounds__(BLOCK, pass_min_waves(BLOCK, KPT)) void k_onesweep(
             stage_round<KPT, HAS_VALUES, STAGE>(k, v, rank, s_keys, s_kv, 0u);
         }
         if (tid == 0) {
-            if (!RS_AHEAD) s_next = RS_EARLY_TICKET ? early_ticket : atomicAdd(ticket, 1u);
+            s_next = claim();
             if (ntot && npad) atomicSub(&s_ntot[nmask], npad);   // the pads' next digit
         }
         __syncthreads();
         const uint32_t Tn = s_next;
         RS_STAMP(pass, ntiles, T, 3, __builtin_amdgcn_s_memtime());
-        // prefetch (RS_PREFETCH): hides under the look-back and this scatter
-        if (RS_PREFETCH == 0 && SR == 1 && Tn < nt && !pf_done) load(Tn);
+        // the next tile's loads: they hide under the look-back and this scatter
+        if (SR == 1 && Tn < nt) load(Tn);
         if (tid < (uint32_t)RADIX) {
             uint32_t excl = s_dbase[tid];
             if (!first_tile) {
@@ -1206,22 +1211,15 @@ __global__ __launch_bounds__(BLOCK, pass_min_waves(BLOCK, KPT)) void k_onesweep(
 #endif
             }
             s_gdelta[tid] = excl - tstart;
-#if RS_SCATTER_DEBUG >= 2
-            // ablation (write-pattern study, n a power of 2): every (tile, digit) run starts on
-            // its own 512-B-aligned slot; mode 2 also fills the run's last line with padding
-            s_gdelta[tid] = ((((uint32_t)tid * ntiles + T) * 64u) & (n - 1u)) - tstart;
-#endif
         }
-        if (RS_PREFETCH == 1 && SR == 1 && Tn < nt && !pf_done) load(Tn);
         __syncthreads();
-        if (RS_PREFETCH == 2 && SR == 1 && Tn < nt && !pf_done) load(Tn);
         RS_STAMP(pass, ntiles, T, 4, __builtin_amdgcn_s_memtime());
 #pragma unroll
         for (int h = 0; h < SR; ++h) {
             if (h > 0) {   // the previous round's scatter has read the staging area
                 stage_round<KPT, HAS_VALUES, STAGE>(k, v, rank, s_keys, s_kv, h * (uint32_t)STAGE);
                 __syncthreads();
-                if (h == SR - 1 && Tn < nt && !pf_done) load(Tn);   // registers free: prefetch
+                if (h == SR - 1 && Tn < nt) load(Tn);   // registers free: prefetch
             }
             const uint32_t lo = h * (uint32_t)STAGE;
             if (lo < nvalid)
@@ -1230,17 +1228,6 @@ __global__ __launch_bounds__(BLOCK, pass_min_waves(BLOCK, KPT)) void k_onesweep(
                                                     tile0, shift, mask, lo, pmask);
             __syncthreads();
         }
-#if RS_SCATTER_DEBUG == 2
-        if (tid < (uint32_t)RADIX) {
-            constexpr uint32_t LINE = LO == LAYOUT_AOS ? 16u : 32u;
-            const uint32_t e = s_gdelta[tid] + tstart + c;
-            for (uint32_t q = e; q < ((e + LINE - 1u) & ~(LINE - 1u)) && q < n; ++q) {
-                if (LO == LAYOUT_AOS) reinterpret_cast<uint2*>(out_k)[q] = make_uint2(q, 0u);
-                else { out_k[q] = q; if (HAS_VALUES) out_v[q] = 0u; }
-            }
-        }
-        __syncthreads();
-#endif
         RS_STAMP(pass, ntiles, T, 5, __builtin_amdgcn_s_memtime());
         T = Tn;
     }
@@ -1432,21 +1419,31 @@ __device__ __forceinline__ void set_gate(uint32_t* g, uint32_t v) {
 
 // hist16[key >> 16] of keys[0..n) (L = LAYOUT_AOS: the keys of n 8-byte records), one 1024-thread
 // workgroup per CU over a contiguous chunk.  All 65536 buckets live in LDS as the 16-bit halves of
-// 32768 words (128 KB, one ds_add per key); after every kRound keys (fewer than 2^16: no half can
-// wrap) each thread adds its 32 words' halves into 64 u32 registers and clears them.  The
-// workgroup's 65536 counts go to rows[blockIdx.x] (k_hist16_reduce adds the rows).
+// 32768 words (128 KB, one ds_add per key).  A half never wraps: every add returns the old word, and
+// the add that takes a half from below kHalfT to kHalfT or more (exactly one add per crossing) takes
+// kHalfT back off the half and logs the bucket in LDS (s_ev); at the end each logged bucket gets
+// kHalfT added to its count.  The adds in flight between a crossing and its take-back are far fewer
+// than the 2^15 headroom above kHalfT (16 waves x a few loads x at most 256 per add).  Uniform keys
+// never cross (2^28 keys over 256 chunks: ~16 per bucket and chunk), so the loop is one returning
+// ds_add per key and the next loads are issued before the current ones are counted.  (Up to round 4
+// each thread folded its 32 words into 64 registers and cleared them every 60K keys: the folds cost
+// as many LDS operations as the counting, and the 64 registers left one group of loads in flight.)
+// The workgroup's 65536 counts go to rows[blockIdx.x] (k_hist16_reduce adds the rows).
 // Range form (the multi-GPU group sorts): the buckets are of key - kbase >> shift, and a key
 // outside [kbase, kbase + range] sets the workgroup's flag word (rows[gridDim.x * 65536 + block];
 // k_msd_plan then picks the LSD passes over the whole 32-bit keys).  Records load 8 bytes per lane
 // (a receive region is only 8-byte aligned), arrays 16.
 // AOS_WIDE (records 16-byte aligned): two records per 16-byte load instead of one per 8-byte load.
 // FULL (kbase = 0, the whole 32-bit range, shift = 16): the bucket is key >> 16 and its counter
-// half bit 16, so a key costs ~3 VALU + 1 LDS atomic (the kernel is issue-bound, not HBM-bound).
+// half bit 16, so a key costs ~4 VALU + 1 LDS atomic.
 // CHECK (check_order on the hybrid path, FULL only): the same read also (a) checks the input's
 // order - *inv |= 1 if any adjacent pair is out of order (every pair, the reference's quirks Q1/Q2
 // fixed; CheckSort.ts:102-113) - and (b, CHECK = 2) counts the low byte of every key into
 // b0rows[block][256] (the LSD fallback's pass-0 totals: k_hist16_reduce adds them, so the fallback
 // needs no read of its own; CHECK = 1 when the sort has no fallback, see SplitWs).
+constexpr uint32_t kHalfT = 1u << 15;   // a 16-bit LDS half is brought back under this
+constexpr uint32_t kEvMax = 4096;       // crossings logged per workgroup: chunk / kHalfT at most, so any
+                                        // chunk of up to 2^27 keys (n < 2^32 over >= 32 workgroups)
 template <int L, bool AOS_WIDE = false, bool FULL = false, int CHECK = 0>
 __global__ __launch_bounds__(1024) void k_hist16_in(const uint32_t* __restrict__ keys, uint32_t n,
                                                      uint32_t* __restrict__ rows, uint32_t kbase,
@@ -1466,21 +1463,22 @@ __global__ __launch_bounds__(1024) void k_hist16_in(const uint32_t* __restrict__
     constexpr uint32_t B = 1024, W = 32768, PER = W / B;
     constexpr bool NARROW = L == LAYOUT_AOS && !AOS_WIDE;
     constexpr uint32_t KPL = NARROW ? 1u : (L == LAYOUT_AOS ? 2u : 4u);   // keys per load
-    constexpr uint32_t STEPS = 61440u / (B * KPL);                // loads per thread per round
-    // loads in flight (CHECK: 3, the order check's registers spilled at 5)
-#ifndef RS_H16_FLY
-#define RS_H16_FLY 5
+    // loads per thread per group; two groups in flight (the next one issued before this one is counted)
+#if !RS_KNOB_OPEN || !defined(RS_H16_FLY)
+#undef RS_H16_FLY
+#define RS_H16_FLY 6
 #endif
     constexpr uint32_t FLY = CHECK ? 3 : RS_H16_FLY;
-    static_assert(STEPS % FLY == 0, "whole load groups per round");
     using Vec = typename std::conditional<NARROW, uint2, uint4>::type;
     __shared__ uint32_t h[W];
     __shared__ uint32_t s_b0[B0 ? 256 : 1];
+    __shared__ uint32_t s_ev[kEvMax];
+    __shared__ uint32_t s_nev;
     const uint32_t tid = threadIdx.x;
-    uint32_t acc[2 * PER];
 #pragma unroll
-    for (uint32_t i = 0; i < PER; ++i) { h[tid + B * i] = 0u; acc[2 * i] = 0u; acc[2 * i + 1] = 0u; }
+    for (uint32_t i = 0; i < PER; ++i) h[tid + B * i] = 0u;
     if (B0 && tid < 256u) s_b0[tid] = 0u;
+    if (tid == 0) s_nev = 0u;
     constexpr uint32_t KS = L == LAYOUT_AOS ? 2u : 1u;   // words per key
     bool inverted = false;
     auto inv2 = [&](uint32_t a, uint32_t b) { inverted |= a > b; };
@@ -1492,6 +1490,29 @@ __global__ __launch_bounds__(1024) void k_hist16_in(const uint32_t* __restrict__
     const uint64_t nv = (hi - lo) / KPL;                          // whole vectors
     const Vec* v4 = reinterpret_cast<const Vec*>(keys + (L == LAYOUT_AOS ? 2 : 1) * lo);
     bool bad = false;
+    // c added to bucket b's half; a crossing of kHalfT is taken back and logged (see above)
+    auto take_back = [&](uint32_t b, uint32_t old, uint32_t c) {
+        const uint32_t sh = (b & 1u) << 4;
+        const uint32_t o = (old >> sh) & 0xFFFFu;
+        if (o < kHalfT && o + c >= kHalfT) {
+            atomicSub(&h[b >> 1], kHalfT << sh);
+            const uint32_t e = atomicAdd(&s_nev, 1u);
+            if (e < kEvMax) s_ev[e] = b;
+        }
+    };
+    auto add16 = [&](uint32_t b, uint32_t c) {
+        take_back(b, atomicAdd(&h[b >> 1], c << ((b & 1u) << 4)), c);
+    };
+    // m buckets + 1 each: every add issued before the first is checked (one LDS round trip, not m)
+    auto add16n = [&](const uint32_t (&bs)[4], int m) {
+        uint32_t old[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (j < m) old[j] = atomicAdd(&h[bs[j] >> 1], 1u << ((bs[j] & 1u) << 4));
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (j < m) take_back(bs[j], old[j], 1u);
+    };
     // FULL, one load's keys (1, 2 or 4): sorted or duplicate-heavy input puts a whole wave's keys in
     // one 16-bit bucket (and, check_order, one low byte: config 4's small floats have few mantissa
     // bits, so a whole chunk has low byte 0), and 64 lanes adding to one LDS address serialise
@@ -1514,102 +1535,138 @@ __global__ __launch_bounds__(1024) void k_hist16_in(const uint32_t* __restrict__
         if (!done && uni) add(c, m);
         return done || uni;
     };
-    auto add16 = [&](uint32_t b, uint32_t c) { atomicAdd(&h[b >> 1], c << ((b & 1u) << 4)); };
-    auto count_load = [&](const uint32_t (&ks)[4], int m) {
+    // (ok: the lane's vector lies in the chunk; only the adds are predicated on it, so that the
+    // loaded registers are used - waited for - on every path)
+    auto count_load = [&](const uint32_t (&ks)[4], int m, bool ok) {
         const uint32_t b = ks[0] >> 16;
-        bool uni = true;
+        bool uni = ok;
         for (int j = 1; j < m; ++j) uni &= (ks[j] >> 16) == b;
-        if (!grouped(b, uni, (uint32_t)m, add16))
-            for (int j = 0; j < m; ++j) add16(ks[j] >> 16, 1u);
+        if (!grouped(b, uni, (uint32_t)m, add16) && ok) {
+            const uint32_t bs[4] = {ks[0] >> 16, ks[1] >> 16, ks[2] >> 16, ks[3] >> 16};
+            add16n(bs, m);
+        }
         if constexpr (B0) {
             const uint32_t d = ks[0] & 255u;
-            bool uni0 = true;
+            bool uni0 = ok;
             for (int j = 1; j < m; ++j) uni0 &= (ks[j] & 255u) == d;
             auto add0 = [&](uint32_t x, uint32_t c) { atomicAdd(&s_b0[x], c); };
-            if (!grouped(d, uni0, (uint32_t)m, add0))
+            if (!grouped(d, uni0, (uint32_t)m, add0) && ok)
                 for (int j = 0; j < m; ++j) add0(ks[j] & 255u, 1u);
         }
     };
-    auto count = [&](uint32_t key) {
+    auto count = [&](uint32_t key, bool ok) {
         if constexpr (FULL) {
-            atomicAdd(&h[key >> 17], 1u << ((key >> 12) & 16u));
-            if constexpr (B0) atomicAdd(&s_b0[key & 255u], 1u);
+            const uint32_t b = key >> 16;
+            if (ok) add16(b, 1u);
+            if constexpr (B0) if (ok) atomicAdd(&s_b0[key & 255u], 1u);
         } else {
             const uint32_t rk = key - kbase;
-            bad |= rk > range;
+            bad |= ok && rk > range;
             const uint32_t b = (rk >> shift) & 0xFFFFu;
-            atomicAdd(&h[b >> 1], 1u << ((b & 1u) << 4));
+            if (ok) add16(b, 1u);
         }
     };
-    auto flush = [&]() {
-        __syncthreads();
+    // branch-free loads (a vector past nv loads vector nv - 1 and is not counted): with a branch per
+    // load the compiler waited for every load in flight before each one, and before counting
+    auto load_group = [&](uint64_t g0, Vec (&q)[FLY]) {
 #pragma unroll
-        for (uint32_t i = 0; i < PER; ++i) {
-            const uint32_t x = h[tid + B * i];
-            acc[2 * i] += x & 0xFFFFu;
-            acc[2 * i + 1] += x >> 16;
-            h[tid + B * i] = 0u;
+        for (uint32_t u = 0; u < FLY; ++u) {
+            const uint64_t i = g0 + (uint64_t)u * B + tid;
+            q[u] = v4[i < nv ? i : nv - 1];
         }
-        __syncthreads();
+    };
+    auto count_group = [&](uint64_t g0, const Vec (&q)[FLY]) {
+#pragma unroll
+        for (uint32_t u = 0; u < FLY; ++u) {
+            const uint64_t i = g0 + (uint64_t)u * B + tid;
+            uint32_t nxt = 0;
+            if constexpr (CHECK) {
+                // the first key of vector i + 1: the next lane's (DPP wave_shl:1, in uniform
+                // control flow), or loaded where that lane has none (lane 63, the chunk's last
+                // vector: then the key after the vectors, which may be the next chunk's)
+                nxt = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)q[u].x, 0x130, 0xf, 0xf, false);
+                if (i < nv && (lane_id() == 63 || i + 1 >= nv)) {
+                    const uint64_t j = lo + KPL * (i + 1);
+                    nxt = j < n ? keys[KS * j] : 0xFFFFFFFFu;
+                }
+            }
+            const bool ok = i < nv;
+            if constexpr (FULL) {
+                if constexpr (NARROW) { const uint32_t ks[4] = {q[u].x, 0u, 0u, 0u}; count_load(ks, 1, ok); }
+                else if constexpr (L == LAYOUT_AOS) { const uint32_t ks[4] = {q[u].x, q[u].z, 0u, 0u}; count_load(ks, 2, ok); }
+                else { const uint32_t ks[4] = {q[u].x, q[u].y, q[u].z, q[u].w}; count_load(ks, 4, ok); }
+            }
+            else if constexpr (NARROW) { count(q[u].x, ok); }
+            else {   // the range form: every key's bucket, then the adds issued together
+                constexpr int m = L == LAYOUT_AOS ? 2 : 4;
+                const uint32_t ks[4] = {q[u].x, L == LAYOUT_AOS ? q[u].z : q[u].y, q[u].z, q[u].w};
+                uint32_t bs[4];
+#pragma unroll
+                for (int j = 0; j < m; ++j) {
+                    const uint32_t rk = ks[j] - kbase;
+                    bad |= ok && rk > range;
+                    bs[j] = (rk >> shift) & 0xFFFFu;
+                }
+                if (ok) add16n(bs, m);
+            }
+            if constexpr (CHECK) {
+                if (ok) {
+                    if constexpr (NARROW) { inv2(q[u].x, nxt); }
+                    else if constexpr (L == LAYOUT_AOS) { inv2(q[u].x, q[u].z); inv2(q[u].z, nxt); }
+                    else { inv2(q[u].x, q[u].y); inv2(q[u].y, q[u].z); inv2(q[u].z, q[u].w); inv2(q[u].w, nxt); }
+                }
+            }
+        }
     };
     __syncthreads();
-    for (uint64_t base = 0; base < nv; base += (uint64_t)STEPS * B) {
-        for (uint32_t s0 = 0; s0 < STEPS; s0 += FLY) {
-            Vec q[FLY];
-#pragma unroll
-            for (uint32_t u = 0; u < FLY; ++u) {
-                const uint64_t i = base + (uint64_t)(s0 + u) * B + tid;
-                if (CHECK) q[u] = Vec{};   // defined for the neighbour read of lanes past nv
-                if (i < nv) q[u] = v4[i];
-            }
-#pragma unroll
-            for (uint32_t u = 0; u < FLY; ++u) {
-                const uint64_t i = base + (uint64_t)(s0 + u) * B + tid;
-                uint32_t nxt = 0;
-                if constexpr (CHECK) {
-                    // the first key of vector i + 1: the next lane's (DPP wave_shl:1, in uniform
-                    // control flow), or loaded where that lane has none (lane 63, the chunk's last
-                    // vector: then the key after the vectors, which may be the next chunk's)
-                    nxt = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)q[u].x, 0x130, 0xf, 0xf, false);
-                    if (i < nv && (lane_id() == 63 || i + 1 >= nv)) {
-                        const uint64_t j = lo + KPL * (i + 1);
-                        nxt = j < n ? keys[KS * j] : 0xFFFFFFFFu;
-                    }
-                }
-                if (i < nv) {
-                    if constexpr (FULL) {
-                        if constexpr (NARROW) { const uint32_t ks[4] = {q[u].x, 0u, 0u, 0u}; count_load(ks, 1); }
-                        else if constexpr (L == LAYOUT_AOS) { const uint32_t ks[4] = {q[u].x, q[u].z, 0u, 0u}; count_load(ks, 2); }
-                        else { const uint32_t ks[4] = {q[u].x, q[u].y, q[u].z, q[u].w}; count_load(ks, 4); }
-                    }
-                    else if constexpr (NARROW) { count(q[u].x); }
-                    else if constexpr (L == LAYOUT_AOS) { count(q[u].x); count(q[u].z); }
-                    else { count(q[u].x); count(q[u].y); count(q[u].z); count(q[u].w); }
-                    if constexpr (CHECK) {
-                        if constexpr (NARROW) { inv2(q[u].x, nxt); }
-                        else if constexpr (L == LAYOUT_AOS) { inv2(q[u].x, q[u].z); inv2(q[u].z, nxt); }
-                        else { inv2(q[u].x, q[u].y); inv2(q[u].y, q[u].z); inv2(q[u].z, q[u].w); inv2(q[u].w, nxt); }
-                    }
-                }
-            }
+    constexpr uint64_t GS = (uint64_t)FLY * B;   // vectors per group
+    if (nv) {
+        // two groups per iteration, so that the registers of the group in flight are named statically;
+        // the next group is loaded unconditionally (past the end: vector nv - 1 again, uncounted), so
+        // that every path into the counting has the same loads outstanding (the compiler's wait for
+        // the group being counted is otherwise the one of the path with fewer loads: all of them)
+        // (the loop's only exit is its uniform test at the end, for the same reason)
+        Vec qa[FLY], qb[FLY];
+        load_group(0, qa);
+        uint64_t g = 0;
+        for (; g + 2 * GS < nv; g += 2 * GS) {   // a group follows the pair
+            load_group(g + GS, qb);
+            count_group(g, qa);
+            load_group(g + 2 * GS, qa);
+            count_group(g + GS, qb);
         }
-        flush();
+        load_group(g + GS, qb);                  // the last one or two groups
+        count_group(g, qa);
+        count_group(g + GS, qb);
     }
     // the last (hi - lo) % KPL keys of the chunk
     const uint64_t rest = lo + nv * KPL;
     if (rest + tid < hi) {
         const uint32_t key = keys[KS * (rest + tid)];
-        count(key);
+        count(key, true);
         if (CHECK && rest + tid + 1 < n) inv2(key, keys[KS * (rest + tid + 1)]);
     }
-    flush();
+    __syncthreads();
     if constexpr (CHECK) {
         if (__ballot(inverted) != 0ull && lane_id() == 0) atomicOr(inv, 1u);
-        if (B0 && tid < 256u) b0rows[(size_t)blockIdx.x * 256u + tid] = s_b0[tid];   // flush()'s barriers passed
+        if (B0 && tid < 256u) b0rows[(size_t)blockIdx.x * 256u + tid] = s_b0[tid];
     }
     uint2* row = reinterpret_cast<uint2*>(rows + (size_t)blockIdx.x * 65536u);
 #pragma unroll
-    for (uint32_t i = 0; i < PER; ++i) row[tid + B * i] = make_uint2(acc[2 * i], acc[2 * i + 1]);
+    for (uint32_t i = 0; i < PER; ++i) {
+        const uint32_t x = h[tid + B * i];
+        row[tid + B * i] = make_uint2(x & 0xFFFFu, x >> 16);
+    }
+    // the logged crossings: kHalfT more for each, added to the row once every thread's stores have
+    // completed (device-scope atomics after a release fence and the barrier)
+    const uint32_t nev = s_nev;   // uniform (read after the barrier above)
+    if (nev) {
+        if (nev > kEvMax) bad = true;   // (never: the hosts launch chunks of <= 2^27 keys) -> flagged
+        __threadfence();
+        __syncthreads();
+        for (uint32_t e = tid; e < nev && e < kEvMax; e += B)
+            atomicAdd(rows + (size_t)blockIdx.x * 65536u + s_ev[e], kHalfT);
+    }
     const int any_bad = __syncthreads_or(bad ? 1 : 0);
     if (tid == 0) rows[(size_t)gridDim.x * 65536u + blockIdx.x] = any_bad ? 1u : 0u;
 }
@@ -2246,10 +2303,12 @@ __global__ __launch_bounds__(BLOCK, MW) void k_bucket_sort8(const uint32_t* rec,
 // is then a key array, R2 the caller's keys).
 // PF = 1: the next bucket's keys are loaded before the current bucket is sorted (a persistent grid;
 // keys only, where a bucket is a few KB and a workgroup's load latency is not hidden otherwise).
-#ifndef RS_BUCKET_PACK
+#if !RS_KNOB_OPEN || !defined(RS_BUCKET_PACK)
+#undef RS_BUCKET_PACK
 #define RS_BUCKET_PACK 0     // 1: k_bucket_sort keeps its ranks as 16-bit pairs (VGPRs)
 #endif
-#ifndef RS_BUCKET_MW
+#if !RS_KNOB_OPEN || !defined(RS_BUCKET_MW)
+#undef RS_BUCKET_MW
 #define RS_BUCKET_MW 3       // k_bucket_sort tiles of <= 18 records per thread: workgroups per CU
 #endif
 template <int BLOCK, int KPT, int RANK, int LO = LAYOUT_SOA, int MW = 1, int PF = 0>
@@ -2392,7 +2451,8 @@ __global__ __launch_bounds__(BLOCK, MW) void k_bucket_sort(const uint32_t* rec,
 // 1024 x 34 = one workgroup per CU, 512 x 34 two, 512 x 18 three).  VREG: the values ride in
 // registers through the sort (else the bucket's records are read again, from L2 / Infinity Cache,
 // for the value exchange).
-#ifndef RS_WIDE_GATHER
+#if !RS_KNOB_OPEN || !defined(RS_WIDE_GATHER)
+#undef RS_WIDE_GATHER
 #define RS_WIDE_GATHER 0   // sweep: 1 = values gathered from the records (see below)
 #endif
 template <int BLOCK, int KPT, int RANK, int LO, int MW = 4, bool VREG = false>
@@ -2538,10 +2598,12 @@ __global__ __launch_bounds__(BLOCK, MW) void k_bucket_sort_wide(const uint32_t* 
 // ~28 buckets in flight.  Two stable 8-bit passes (low byte, then the next), pads (kPadKey) after
 // every real key.  Buckets of more than 64 * KPT keys are listed by k_msd_plan for the large-tile
 // launch; empty and one-key buckets are skipped.
-#ifndef RS_KWAVE_PF
+#if !RS_KNOB_OPEN || !defined(RS_KWAVE_PF)
+#undef RS_KWAVE_PF
 #define RS_KWAVE_PF 0     // sweep: 1 = persistent waves that load their next bucket while sorting one
 #endif
-#ifndef RS_KWAVE_PACK
+#if !RS_KNOB_OPEN || !defined(RS_KWAVE_PACK)
+#undef RS_KWAVE_PACK
 #define RS_KWAVE_PACK 0   // sweep: 1 = ranks as 16-bit pairs (fewer VGPRs: more waves per SIMD)
 #endif
 template <int KPT, int RANK, int WPB, int MW = 1>
@@ -2788,7 +2850,8 @@ __global__ __launch_bounds__(kBlock) void k_scan_small(uint32_t* __restrict__ a,
 // look-backs.
 // tickets: a ring of kScanTickets counters; launch e uses tickets[e % ring] and clears the next
 // launch's.  VEC: the data is 16-byte aligned (16-byte loads / stores; else 4-byte ones).
-#ifndef RS_SCAN_LB_FIRST
+#if !RS_KNOB_OPEN || !defined(RS_SCAN_LB_FIRST)
+#undef RS_SCAN_LB_FIRST
 #define RS_SCAN_LB_FIRST 1   // the look-back's first status words read before the next tile's loads
 #endif
 constexpr uint32_t kScanTickets = 64;
@@ -2804,10 +2867,13 @@ __global__ __launch_bounds__(BLOCK) void k_scan_lookback(uint32_t* __restrict__ 
     __shared__ uint32_t s_t, s_prefix;
     __shared__ uint2 s_lb[NW];   // per wave of a look-back round: (sum, found | unpublished << 1)
     __shared__ uint32_t s_abort;
-    if (indirect_off(ind)) return;
     const uint32_t tid = threadIdx.x, w = tid >> 6, lane = lane_id();
+    // the next launch's ticket is cleared first, also by a launch that the indirect dispatch gates
+    // off: otherwise that slot would keep the count of the launch kScanTickets earlier and the next
+    // live launch's first tickets would all be past the last tile (nothing scanned, no error)
+    if (blockIdx.x == 0 && tid == 0) tickets[(epoch + 1) % kScanTickets] = 0u;
+    if (indirect_off(ind)) return;
     uint32_t* ticket = tickets + epoch % kScanTickets;
-    if (blockIdx.x == 0 && tid == 0) tickets[(epoch + 1) % kScanTickets] = 0u;   // the next launch's
     const uint32_t ntiles = (uint32_t)(((uint64_t)n + TILE - 1) / TILE);
     // striped layout (coalesced: each load instruction of a wave reads 1 KB contiguous): wave w's
     // EPT x 64 elements are EPT / 4 chunks of 256, lane l holding elements 4l .. 4l + 3 of each

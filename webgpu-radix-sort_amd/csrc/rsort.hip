@@ -36,6 +36,10 @@
 // (`make variants`, tools/sweep.py: -DRS_SWEEP=1) adds the process-wide experiment knobs (RSORT_*
 // environment variables) and the alternative kernel instantiations they select; a product build
 // compiles neither.
+#if !RS_KNOB_OPEN || !defined(RS_P0_SR2)
+#undef RS_P0_SR2
+#define RS_P0_SR2 0   // experiment: MSD pass 0 over 32K-record tiles in two staging rounds
+#endif
 #ifndef RS_SWEEP
 #define RS_SWEEP 0
 #endif
@@ -76,10 +80,12 @@ rs_status fail(rs_status s, const char* fmt, ...) {
 //   large: 1024 threads x 16 keys = 16384-key tiles, 145 KiB LDS, one workgroup per CU
 //   small:  256 threads x 16 keys =  4096-key tiles,  37 KiB LDS, four workgroups per CU
 // and a single-workgroup sort for n <= kTinyMax.
-#ifndef RS_SMALL_MAX
+#if !RS_KNOB_OPEN || !defined(RS_SMALL_MAX)
+#undef RS_SMALL_MAX
 #define RS_SMALL_MAX (12u << 20)  // n below this uses the small-tile configuration
 #endif
-#ifndef RS_HIST_U
+#if !RS_KNOB_OPEN || !defined(RS_HIST_U)
+#undef RS_HIST_U
 #define RS_HIST_U 4               // 16-byte loads per lane per histogram iteration (x2 in flight)
 #endif
 struct TileCfg {
@@ -87,13 +93,22 @@ struct TileCfg {
     uint32_t max_grid;
 };
 constexpr TileCfg kLarge{1024, 16, 16384, 512};
+// Words after the digit totals: [16] tile tickets (one per k_onesweep launch slot), [16] error words,
+// [16][8] the launch slots' XCD claim counters (k_onesweep's XCD-grouped claims)
+constexpr uint32_t kTicketWords = 32 + 16 * 8;
+#if !RS_KNOB_OPEN || !defined(RS_XCD_CLAIM)
+#undef RS_XCD_CLAIM
+#define RS_XCD_CLAIM 1   // k_onesweep: XCD-grouped tile claims (0: one ticket counter)
+#endif
 constexpr TileCfg kSmall{256, 16, 4096, 1024};
 // keys-only at >= 12M keys: the same 16K-key tile from 512 threads x 32 keys (75 KiB LDS), so
 // two workgroups share a CU and one's waits (look-back, barriers) overlap the other's work
-#ifndef RS_KEYS_BLOCK
+#if !RS_KNOB_OPEN || !defined(RS_KEYS_BLOCK)
+#undef RS_KEYS_BLOCK
 #define RS_KEYS_BLOCK 512
 #endif
-#ifndef RS_KEYS_KPT
+#if !RS_KNOB_OPEN || !defined(RS_KEYS_KPT)
+#undef RS_KEYS_KPT
 #define RS_KEYS_KPT 32
 #endif
 constexpr TileCfg kLargeKeys{RS_KEYS_BLOCK, RS_KEYS_KPT, RS_KEYS_BLOCK * RS_KEYS_KPT, 512};
@@ -119,7 +134,8 @@ constexpr uint32_t kTinyMax = 1024 * 16;
 // Hybrid MSD path (enqueue_sort_msd): used for key/value arrays and records of kMsdMin ... kMsdMax
 // keys when no 16-bit bucket exceeds kBucketCap records (decided on the device); buckets are sorted
 // in LDS by k_bucket_sort (tiles sized to the population) or, the largest, k_bucket_sort_wide.
-#ifndef RS_MSD_DEFAULT
+#if !RS_KNOB_OPEN || !defined(RS_MSD_DEFAULT)
+#undef RS_MSD_DEFAULT
 #define RS_MSD_DEFAULT 1
 #endif
 constexpr uint64_t kMsdMin = 12ull << 20;
@@ -254,8 +270,8 @@ struct rs_plan {
     uint32_t radix_bits = 8;
     bool has_values = false, check_order = false, local_shuffle = false;
     int layout = rs::LAYOUT_KEYS;          // rs::Layout of the caller's data
-    int rank_mode = rs::RANK_LDS_ATOMIC;   // RSORT_RANK=ballot selects the ballot-match ranking
-    int tile_mode = -1;                    // RSORT_TILE: -1 by size, 0 large tiles, 1 small tiles
+    int rank_mode = rs::RANK_LDS_ATOMIC;   // rs_plan_debug.rank = 1: the ballot-match ranking
+    int tile_mode = -1;                    // rs_plan_debug.tile: -1 by size, 0 large tiles, 1 small tiles
     uint32_t usage = RS_USAGE_SORT;        // RS_USAGE_PARTITION: hist16 + partition passes only
     uint64_t rows_words = 0;               // words of tmp_k available to k_hist16_in's rows
     uint32_t passes = 0;
@@ -267,10 +283,10 @@ struct rs_plan {
     uint32_t* totals = nullptr;    // [256]
     uint32_t* flags = nullptr;     // [16] check_order results
     // one-sweep path (k_pass_totals + k_onesweep)
-    int onesweep_mode = -1;                // -1 auto (use_onesweep), 0 off, 1 on (RSORT_ONESWEEP)
+    int onesweep_mode = -1;                // -1 auto (use_onesweep), 0 off, 1 on (rs_plan_debug.onesweep)
     bool aos_tmp = true;                   // one-sweep KV: records as the ping-pong copy (sweep: RSORT_AOS_TMP)
     uint32_t* tmp2 = nullptr;              // one-sweep KV: second records buffer (sweep: RSORT_RECS2=0: none)
-    bool keys_cfg = true;                  // keys-only 512x32 tiles (RSORT_KEYS_CFG=0: 1024x16)
+    bool keys_cfg = true;                  // keys-only 512x32 tiles (rs_plan_debug.keys_cfg = 0: 1024x16)
     int kv_cfg = 0;                        // one-sweep KV tile configuration (sweep: RSORT_KV_CFG)
     int huge_tiles = 0;                    // one-sweep KV: 24K-record tiles (sweep: RSORT_HUGE=1: every
                                            // pass; 2: the records -> arrays pass only)
@@ -280,14 +296,15 @@ struct rs_plan {
     uint64_t status_words = 0;
     uint32_t* ptot = nullptr;      // [kTotalsMax] whole-array digit totals of every pass
     uint32_t ptot_off[16] = {};    // offset of pass i's totals in ptot
-    uint32_t* tickets = nullptr;   // = ptot + kTotalsMax: [16] per-pass tile tickets, [16] error
+    uint32_t* tickets = nullptr;   // = ptot + kTotalsMax: [16] per-pass tile tickets, [16] error,
+                                   // [16][8] per-pass XCD claim counters (xticket_of)
     uint32_t epoch = 0;            // tag of the last k_onesweep launch's status words
-    uint32_t spin_max = 1u << 20;  // look-back wait bound in sleeps (RSORT_SPIN_MAX; tests force 0)
-    int msd_mode = RS_MSD_DEFAULT;   // hybrid MSD path for values (RSORT_MSD=0/1)
+    uint32_t spin_max = 1u << 20;  // look-back wait bound in sleeps (rs_plan_set_wait_limit; tests force 0)
+    int msd_mode = RS_MSD_DEFAULT;   // hybrid MSD path for values (rs_plan_debug.msd = 0/1)
     // keys-only form of the hybrid MSD path, read per plan (tests switch them):
-    int msd_keys_cfg = 1;            // pass tiles (RSORT_MSD_KEYS_CFG): 0 1024x16, 1 512x32, 2 1024x32
+    int msd_keys_cfg = 1;            // pass tiles (rs_plan_debug.msd_keys_cfg): 0 1024x16, 1 512x32, 2 1024x32
                                      // (32K-key tiles for pass 0 only: no faster, r03_keys_pass0_tiles_ab)
-    bool kbucket_wave = true;        // one wave per 16-bit bucket (RSORT_KBUCKET_WAVE=0: workgroups)
+    bool kbucket_wave = true;        // one wave per 16-bit bucket (rs_plan_debug.kbucket_wave = 0: workgroups)
     bool kbucket_pf = false;         // workgroup kernel on a persistent prefetching grid (sweep: RSORT_KBUCKET_PF=1)
     bool static_passes = false;      // hybrid MSD passes over static splits (sweep only, RSORT_STATIC=1: measured
                                      // slower than the look-back passes)
@@ -389,6 +406,18 @@ uint32_t resident_per_cu(F kernel, int block) {
     return (uint32_t)api;
 }
 
+// The XCD claim counters of the k_onesweep launch slot whose ticket is `ticket` (zeroed with it),
+// and xk = tiles per XCD per round, when the grid splits evenly over the 8 XCDs (else null: one
+// ticket counter).
+uint32_t* xticket_of(rs_plan* p, uint32_t* ticket, uint32_t grid, uint32_t& xk) {
+    xk = 0;
+    if (!RS_XCD_CLAIM || grid < 8u || grid % 8u != 0u) return nullptr;
+    const ptrdiff_t slot = ticket - p->tickets;
+    if (slot < 0 || slot >= 16) return nullptr;
+    xk = grid / 8u;
+    return p->tickets + 32 + 8 * slot;
+}
+
 template <int R, int BLOCK, int KPT, int L, int RANK, int LO, int SR>
 void launch_onesweep_t(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint32_t* ok,
                        uint32_t* ov, uint32_t n, uint32_t shift, uint32_t mask, uint32_t ntiles,
@@ -401,6 +430,8 @@ void launch_onesweep_t(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint3
     uint32_t grid = std::min<uint32_t>(ntiles, p->cus * per_cu);
     if (cap > 0 && cap < grid) grid = cap;
     const bool last = (uint32_t)pass + 1 >= p->passes;
+    uint32_t xk = 0;
+    uint32_t* xt = xticket_of(p, p->tickets + pass, grid, xk);
     uint32_t* ntot = last ? nullptr : p->ptot + p->ptot_off[pass + 1];
     const uint32_t nshift = last ? 0u : shift + p->widths[pass];
     const uint32_t nmask = last ? 0u : (1u << p->widths[pass + 1]) - 1u;
@@ -410,7 +441,7 @@ void launch_onesweep_t(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint3
                        p->ptot + p->ptot_off[pass], p->status, p->tickets + pass,
                        p->tickets + 16, ntot, nshift, nmask, p->epoch, gate, pass, chk,
                        full_mask(p->bit_count), p->spin_max, p->host_err_dev,
-                       (const uint32_t*)nullptr, (const uint32_t*)nullptr, 0u, 0xFFFFFFFFu);
+                       (const uint32_t*)nullptr, (const uint32_t*)nullptr, 0u, 0xFFFFFFFFu, xt, xk);
 }
 
 template <int R, int BLOCK, int KPT, int L, int LO, int SR>
@@ -435,24 +466,27 @@ rs_status next_epoch(rs_plan* p, hipStream_t s) {
 // One pass of the hybrid MSD path (16K-record tiles, 8-bit digit at `shift`): SEG = 0 the
 // top-byte pass over the whole input, SEG = 1 the next-byte pass inside every top-byte segment.
 // BLOCK x KPT = 16K keys (kLarge; keys only: kLargeKeys, two workgroups per CU).
-template <int L, int LO, int SEG, bool KB = false, int BLOCK = kLarge.block, int KPT = kLarge.kpt>
+template <int L, int LO, int SEG, bool KB = false, int BLOCK = kLarge.block, int KPT = kLarge.kpt, int SR = 1>
 void launch_msd_pass(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint32_t* ok, uint32_t* ov,
                      uint32_t n, uint32_t shift, uint32_t ntiles, const uint32_t* dtot, uint32_t* ticket,
                      const uint32_t* gate, const uint32_t* segtab, const uint32_t* base16,
                      hipStream_t s, uint32_t kbase = 0, uint32_t pmask = 0xFFFFFFFFu) {
     static_assert(BLOCK * KPT == kLarge.tile || BLOCK * KPT == 2 * kLarge.tile, "k_msd_plan tile sizes");
+    static_assert(SR == 1 || SEG == 0, "staging rounds: the top-byte pass only");
     auto go = [&](auto kern) {
         static const uint32_t per_cu = resident_per_cu(kern, BLOCK);
         const uint32_t grid = std::min<uint32_t>(ntiles, p->cus * per_cu);
+        uint32_t xk = 0;
+        uint32_t* xt = xticket_of(p, ticket, grid, xk);
         hipLaunchKernelGGL(kern, dim3(grid), dim3(BLOCK), 0, s, ik, iv, ok, ov, n, shift, 255u,
                            ntiles, dtot, p->status, ticket, p->tickets + 16, nullptr, 0u, 0u, p->epoch,
                            gate, SEG, nullptr, 0xFFFFFFFFu, p->spin_max, p->host_err_dev, segtab, base16, kbase,
-                           pmask);
+                           pmask, xt, xk);
     };
     if (p->rank_mode == rs::RANK_BALLOT)
-        go(rs::k_onesweep<8, BLOCK, KPT, L, rs::RANK_BALLOT, LO, 1, SEG, KB>);
+        go(rs::k_onesweep<8, BLOCK, KPT, L, rs::RANK_BALLOT, LO, SR, SEG, KB>);
     else
-        go(rs::k_onesweep<8, BLOCK, KPT, L, rs::RANK_LDS_ATOMIC, LO, 1, SEG, KB>);
+        go(rs::k_onesweep<8, BLOCK, KPT, L, rs::RANK_LDS_ATOMIC, LO, SR, SEG, KB>);
 }
 
 // The hybrid path's passes over a static split (k_static_pass; 16K-record tiles, one 1024-thread
@@ -809,7 +843,7 @@ RS_EXPORT rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out) {
         (d.count + kLarge.tile - 1) / kLarge.tile + 1 + std::max<uint64_t>(256, split_smax3(d.count)),
         std::max<uint64_t>((d.count + kMinOnesweepTile - 1) / kMinOnesweepTile,
                            (std::min<uint64_t>(d.count, RS_SMALL_MAX) + kSmall.tile - 1) / kSmall.tile));
-    // sized whatever RSORT_ONESWEEP says: the records / partition entry points and the hybrid
+    // sized whatever rs_plan_debug.onesweep says: the records / partition entry points and the hybrid
     // path's passes are one-sweep passes on every plan
     p->status_words = max_tiles * 256;
     hipError_t e;
@@ -830,7 +864,7 @@ RS_EXPORT rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out) {
         (e = alloc(&p->counts, 4ull * 256 * std::max<uint64_t>(1, (d.count + kSmall.tile - 1) / kSmall.tile))) != hipSuccess ||
         (e = alloc(&p->totals, 4ull * 256)) != hipSuccess ||
         (e = alloc(&p->flags, 4ull * 16)) != hipSuccess ||
-        (e = alloc(&p->ptot, 4ull * (rs::kTotalsMax + 32))) != hipSuccess ||
+        (e = alloc(&p->ptot, 4ull * (rs::kTotalsMax + kTicketWords))) != hipSuccess ||
         (e = alloc((uint32_t**)&p->status, 8ull * p->status_words)) != hipSuccess)
         return cleanup(fail(e == hipErrorOutOfMemory ? RS_ERR_OUT_OF_MEMORY : RS_ERR_HIP,
                             "rs_plan_create: hipMalloc failed: %s", hipGetErrorString(e)));
@@ -847,7 +881,7 @@ RS_EXPORT rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out) {
             return cleanup(fail(e == hipErrorOutOfMemory ? RS_ERR_OUT_OF_MEMORY : RS_ERR_HIP,
                                 "rs_plan_create: hipMalloc failed: %s", hipGetErrorString(e)));
     }
-    p->tickets = p->ptot + rs::kTotalsMax;   // [16] tickets, [16] error word
+    p->tickets = p->ptot + rs::kTotalsMax;   // [16] tickets, [16] error word, [16][8] XCD counters
 
     if ((e = hipHostMalloc((void**)&p->host_err, 4, hipHostMallocMapped)) != hipSuccess ||
         (e = hipHostGetDevicePointer((void**)&p->host_err_dev, p->host_err, 0)) != hipSuccess ||
@@ -855,7 +889,7 @@ RS_EXPORT rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out) {
         return cleanup(fail(RS_ERR_HIP, "rs_plan_create: host error word: %s", hipGetErrorString(e)));
     *p->host_err = 0u;
     if (p->layout == rs::LAYOUT_SOA && sorts) p->tmp_v = p->tmp_k + d.count;
-    if ((e = hipMemset(p->ptot, 0, 4ull * (rs::kTotalsMax + 32))) != hipSuccess ||
+    if ((e = hipMemset(p->ptot, 0, 4ull * (rs::kTotalsMax + kTicketWords))) != hipSuccess ||
         (e = hipMemset(p->status, 0, 8ull * p->status_words)) != hipSuccess)
         return cleanup(fail(RS_ERR_HIP, "rs_plan_create: hipMemset failed: %s", hipGetErrorString(e)));
     *out = p;
@@ -1066,7 +1100,7 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
         sw.strict = strict ? 1u : 0u;
         sw.n = n32;
     }
-    // keys only, pass tile configuration (RSORT_MSD_KEYS_CFG): 0 = 1024 x 16, 1 = 512 x 32 (two
+    // keys only, pass tile configuration (rs_plan_debug.msd_keys_cfg): 0 = 1024 x 16, 1 = 512 x 32 (two
     // workgroups per CU), 2 = 1024 x 32 (32K-key tiles: 512-B digit runs, as long as a 16K-record tile's)
     const int keys_cfg = p->msd_keys_cfg;
     const uint32_t tile = (keys && keys_cfg == 2) ? 2u * kLarge.tile : (uint32_t)kLarge.tile;
@@ -1091,7 +1125,7 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
     for (uint32_t kpt : keys ? kpts_keys : kpts)
         if (kpt && !small_cap && want <= bb * kpt) { small_cap = bb * kpt; small_kpt = kpt; }
     // keys only, buckets of up to ~1K keys (<= ~80M keys): one wave per bucket
-    // (k_bucket_sort_keys_wave, 64 x wave_kpt keys; RSORT_KBUCKET_WAVE=0 keeps the workgroup kernel)
+    // (k_bucket_sort_keys_wave, 64 x wave_kpt keys; rs_plan_debug.kbucket_wave = 0 keeps the workgroup kernel)
     const bool wave_ok = p->kbucket_wave;
     uint32_t wave_kpt = 0;
     if (keys && wave_ok) {
@@ -1128,6 +1162,9 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
     const bool static_p1 = !keys && p->static_passes;
     // (the fallback's byte-0 totals: only where a fallback is enqueued)
     uint32_t* b0rows = (chk && !strict) ? p->tmp_k + (size_t)hrows * 65537u : nullptr;
+    if (!region && (uint64_t)n / hrows >= (uint64_t)rs::kEvMax * rs::kHalfT)   // k_hist16_in's crossing log
+        return fail(RS_ERR_CAPACITY, "%llu keys over %u histogram rows (at most 2^27 keys per row)",
+                    (unsigned long long)n, hrows);
     if (chk) HIP_TRY(hipMemsetAsync(p->flags, 0, 16 * 4, s));
     p->timer.run(RS_KERNEL_HISTOGRAM, s, [&] {
         if (region) {   // the senders counted: one row, their table
@@ -1135,7 +1172,7 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
                                sw.huge);
             hipLaunchKernelGGL(rs::k_hist16_reduce, dim3(256), dim3(1024), 0, s, (const uint32_t*)p->tmp_k,
                                1u, hist16, top_tot, range_bad, base16, small_cap, kBucketCap, over, big,
-                               p->ptot, (uint32_t)(rs::kTotalsMax + 32), (const uint32_t*)nullptr,
+                               p->ptot, (uint32_t)(rs::kTotalsMax + kTicketWords), (const uint32_t*)nullptr,
                                (uint32_t*)nullptr, sw.huge, p->smax2);
             return;
         }
@@ -1167,7 +1204,7 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
         // overflow list, the oversize flag): the plan kernel is left with the 256 segments
         hipLaunchKernelGGL(rs::k_hist16_reduce, dim3(256), dim3(1024), 0, s, (const uint32_t*)p->tmp_k,
                            hrows, hist16, top_tot, range_bad, base16, small_cap, kBucketCap, over, big,
-                           p->ptot, (uint32_t)(rs::kTotalsMax + 32), (const uint32_t*)b0rows,
+                           p->ptot, (uint32_t)(rs::kTotalsMax + kTicketWords), (const uint32_t*)b0rows,
                            static_p0 ? cbase : (uint32_t*)nullptr, sw.huge, p->smax2);
     }, region ? "rsort.msd.region_table" : "rsort.msd.hist16");
     HIP_TRY(hipGetLastError());
@@ -1225,9 +1262,16 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
         else if (kbase)
             launch_msd_pass<S, A, 0, true>(p, sk, sv, r1, nullptr, n32, vbits - 8, ntiles, top_tot,
                                            p->tickets + 4, g_msd, nullptr, nullptr, s, kbase);
+#if RS_P0_SR2
+        else   // 32K-record tiles staged in two rounds: 128-record digit runs (tools/run_probe.hip)
+            launch_msd_pass<S, A, 0, false, kLarge.block, 2 * kLarge.kpt, 2>(
+                p, sk, sv, r1, nullptr, n32, vbits - 8, (uint32_t)((n + 2 * kLarge.tile - 1) / (2 * kLarge.tile)),
+                top_tot, p->tickets + 4, g_msd, nullptr, nullptr, s);
+#else
         else
             launch_msd_pass<S, A, 0>(p, sk, sv, r1, nullptr, n32, vbits - 8, ntiles, top_tot, p->tickets + 4,
                                      g_msd, nullptr, nullptr, s);
+#endif
     }, "rsort.msd.pass0");
     HIP_TRY(hipGetLastError());
     // MSD pass 1: R1 -> R2 records, by the next byte inside every top-byte segment
@@ -1435,7 +1479,7 @@ static rs_status enqueue_sort(rs_plan* p, uint32_t* uk, uint32_t* uv, uint64_t n
     const bool onesweep = use_onesweep(p, n);
     if (onesweep) {
         // totals, tickets and the device error word (a timeout never outlives its sort)
-        HIP_TRY(hipMemsetAsync(p->ptot, 0, 4ull * (rs::kTotalsMax + 32), s));
+        HIP_TRY(hipMemsetAsync(p->ptot, 0, 4ull * (rs::kTotalsMax + kTicketWords), s));
         // pass 0's digit totals from one read of the input; every later pass's totals are
         // counted by the pass before it (k_onesweep's ntot)
         rs::PassList pl{};
@@ -1701,6 +1745,7 @@ static rs_status onesweep_digit_pass(rs_plan* p, const uint32_t* ik, const uint3
     const int pass = (int)p->passes - 1;
     uint32_t* slot = p->ptot + p->ptot_off[pass];   // 2^bits words fit: kTotalsMax >= off + 256
     HIP_TRY(hipMemsetAsync(p->tickets + pass, 0, 4, s));
+    HIP_TRY(hipMemsetAsync(p->tickets + 32 + 8 * pass, 0, 32, s));   // its XCD claim counters
     HIP_TRY(hipMemsetAsync(p->tickets + 16, 0, 4, s));
     if (d_totals) {
         HIP_TRY(hipMemcpyAsync(slot, d_totals, 4u << bits, hipMemcpyDeviceToDevice, s));
@@ -1749,7 +1794,7 @@ RS_EXPORT rs_status rs_plan_partition_records(rs_plan* p, const void* in_keys, c
 static rs_status enqueue_sort_records(rs_plan* p, const uint32_t* rec, uint32_t* uk, uint32_t* uv,
                                       uint64_t n, hipStream_t s) {
     const uint32_t n32 = (uint32_t)n;
-    HIP_TRY(hipMemsetAsync(p->ptot, 0, 4ull * (rs::kTotalsMax + 32), s));
+    HIP_TRY(hipMemsetAsync(p->ptot, 0, 4ull * (rs::kTotalsMax + kTicketWords), s));
     {
         rs::PassList pl{};
         pl.count = 1;
@@ -1863,6 +1908,9 @@ RS_EXPORT rs_status rs_plan_hist16(rs_plan* p, const void* keys, uint64_t n, voi
     if (hrows == 0)
         return fail(RS_ERR_CAPACITY, "rs_plan_hist16: the plan's workspace holds no histogram row (a keys-only "
                     "sort plan needs capacity >= 65537; plans with values and RS_USAGE_PARTITION plans always hold one)");
+    if (n / hrows >= (uint64_t)rs::kEvMax * rs::kHalfT)
+        return fail(RS_ERR_CAPACITY, "rs_plan_hist16: %llu keys over %u histogram rows (at most 2^27 keys per row)",
+                    (unsigned long long)n, hrows);
     p->timer.run(RS_KERNEL_HISTOGRAM, s, [&] {
         // z0 / z1 (the MSD path's overflow words) point into the rows' flag area: unused here
         uint32_t* z = p->tmp_k + (size_t)hrows * 65536u;
@@ -2031,13 +2079,16 @@ constexpr int kScanTile = 4096;
 constexpr uint32_t kScanMaxGrid = 1024;
 // single-pass scan (k_scan_lookback): 1024 threads x 32 elements = 32K-element tiles, one workgroup
 // per CU, the next tile's 128 KB in flight across the look-back and the stores (profiles/r04/scan*)
-#ifndef RS_SCAN_BLOCK
+#if !RS_KNOB_OPEN || !defined(RS_SCAN_BLOCK)
+#undef RS_SCAN_BLOCK
 #define RS_SCAN_BLOCK 1024
 #endif
-#ifndef RS_SCAN_EPT
+#if !RS_KNOB_OPEN || !defined(RS_SCAN_EPT)
+#undef RS_SCAN_EPT
 #define RS_SCAN_EPT 32   // 32K-element tiles, one workgroup per CU (0.453 vs 0.591 ms at 16, 1.33 at 8)
 #endif
-#ifndef RS_SCAN_PF
+#if !RS_KNOB_OPEN || !defined(RS_SCAN_PF)
+#undef RS_SCAN_PF
 #define RS_SCAN_PF 1
 #endif
 constexpr int kScanBlock = RS_SCAN_BLOCK, kScanEpt = RS_SCAN_EPT;

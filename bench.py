@@ -369,6 +369,9 @@ def main() -> None:
     # ranks, rejects it as an ambiguous abbreviation of its own options)
     ap.add_argument("--keys-per-gpu", type=int, default=0, help="override keys per GPU (testing only)")
     ap.add_argument("--radix-bits", type=int, default=0)
+    ap.add_argument("--rank", default="lds", choices=["lds", "ballot"],
+                    help="in-wave ranking: lane-ordered LDS atomics (default, self-tested per device) or "
+                         "the architecture-guaranteed ballot ranking (rs_plan_debug.rank = 1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--distributed", action="store_true",
                     help="use the bucket-exchange path even at world size 1 (testing)")
@@ -395,7 +398,9 @@ def main() -> None:
         torch.cuda.set_device(0)
         bench_prefix_sum(args, WORKLOADS[args.workload], torch, json_out)
         return
-    from radix_sort_amd import RadixSortKernel, RadixSortTextureKernel, ops
+    from radix_sort_amd import RadixSortKernel, RadixSortTextureKernel, _lib, ops
+    if args.rank == "ballot":   # every plan of this process ranks by ballot
+        _lib.plan_debug(rank="ballot").__enter__()
     from radix_sort_amd.distributed import (HipLocalOps, StepTimeline, distributed_sort,
                                             summarize_timelines, timeline_record)
 
@@ -701,7 +706,7 @@ def main() -> None:
             "config": {"workload": args.workload, "description": wl["desc"], "keys_per_gpu": n,
                        "global_keys": n * world, "bit_count": 32, "has_values": wl["values"],
                        "local_shuffle": wl["local_shuffle"], "check_order": wl["check_order"],
-                       "radix_bits": args.radix_bits or 8,
+                       "radix_bits": args.radix_bits or 8, "ranking": args.rank,
                        "parallelism": "single GPU" if world == 1 else
                        f"{world} ranks, top-byte bucket exchange (RCCL point-to-point rounds)"},
             "rccl_ranks": dist.get_world_size() if use_dist and backend == "nccl" else 0,

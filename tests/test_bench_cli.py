@@ -60,7 +60,8 @@ def test_spawned_command_line_parses_under_torchrun():
     from torch.distributed.run import get_args_parser
     what, cmd = bench.launch_plan(2, {}, 2, ["--gpus", "2", "--steps", "3", "--warmup", "1",
                                              "--workload", "config3", "--keys-per-gpu", "1024",
-                                             "--no-cpu-baseline", "--share-gpu", "--radix-bits", "8"])
+                                             "--no-cpu-baseline", "--share-gpu", "--radix-bits", "8",
+                                             "--rank", "ballot"])
     args = get_args_parser().parse_args(cmd[3:])
     assert args.nproc_per_node == "2" and args.training_script.endswith("bench.py")
     assert "--keys-per-gpu" in args.training_script_args

@@ -591,29 +591,27 @@ __device__ __forceinline__ void stage_tile(const uint32_t (&k)[KPT], const uint3
                                            uint32_t mask, uint32_t* s_ntot, uint32_t nshift,
                                            uint32_t nmask) {
     shift = opaque_u(shift);
-#if RS_STAGE_BATCH
-    // every slot's wave offset read first (KPT LDS reads in flight), then the KPT writes: the
-    // read -> write dependency of one slot no longer serialises the LDS latency slot by slot
-    uint32_t s[KPT];
+    if constexpr (RS_STAGE_BATCH && HAS_VALUES) {
+        // every slot's wave offset read first (KPT LDS reads in flight), then the KPT writes: the
+        // read -> write dependency of one slot no longer serialises the LDS latency slot by slot
+        // (records only: keys only measured 1.5 % slower, profiles/r05/ab_hist16 config2)
+        uint32_t s[KPT];
 #pragma unroll
-    for (int j = 0; j < KPT; ++j) s[j] = whist_w[(k[j] >> shift) & mask] + rank.get(j);
+        for (int j = 0; j < KPT; ++j) s[j] = whist_w[(k[j] >> shift) & mask] + rank.get(j);
 #pragma unroll
-    for (int j = 0; j < KPT; ++j) {
-        if (s[j] < (uint32_t)TILE) {   // always; keeps a bug from writing past the staging area
-            if (HAS_VALUES) s_kv[s[j]] = make_uint2(k[j], v[j]);
-            else s_keys[s[j]] = k[j];
+        for (int j = 0; j < KPT; ++j)
+            if (s[j] < (uint32_t)TILE)   // always; keeps a bug from writing past the staging area
+                s_kv[s[j]] = make_uint2(k[j], v[j]);
+    } else {
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) {
+            const uint32_t s = whist_w[(k[j] >> shift) & mask] + rank.get(j);
+            if (s < (uint32_t)TILE) {   // always; keeps a bug from writing past the staging area
+                if (HAS_VALUES) s_kv[s] = make_uint2(k[j], v[j]);
+                else s_keys[s] = k[j];
+            }
         }
     }
-#else
-#pragma unroll
-    for (int j = 0; j < KPT; ++j) {
-        const uint32_t s = whist_w[(k[j] >> shift) & mask] + rank.get(j);
-        if (s < (uint32_t)TILE) {   // always; keeps a bug from writing past the staging area
-            if (HAS_VALUES) s_kv[s] = make_uint2(k[j], v[j]);
-            else s_keys[s] = k[j];
-        }
-    }
-#endif
     if (s_ntot) count_slots<KPT>(k, s_ntot, nshift, nmask);
 }
 
@@ -1236,6 +1234,241 @@ __global__ __launch_bounds__(BLOCK, pass_min_waves(BLOCK, KPT)) void k_onesweep(
             if (s_ntot[d]) atomicAdd(&ntot[d], s_ntot[d]);
     }
     if (chk && tid == 0 && s_inv) atomicOr(chk + pass, 1u);
+}
+
+// ---- the hybrid path's MSD passes with values: k_msd_pass -------------------------------------
+// k_onesweep's algorithm (rank, publish, local shuffle, decoupled look-back, scatter of 16K-record
+// tiles by an 8-bit digit; SEG = 1: inside every top-byte segment) specialised for the two MSD
+// passes of a sort with values (BASELINE config 3's hot path: 2 of its ~3.1 ms), so that a tile's
+// memory traffic is in flight throughout instead of in two separate phases:
+//  * the look-back's first status words are read BEFORE the next tile's loads are issued (a wave's
+//    vector-memory operations complete in issue order: read after them, the words waited for the
+//    whole 128 KB prefetch, so the scatter's stores could only start once the next tile had
+//    arrived); the scatter's stores of this tile now overlap the next tile's loads;
+//  * the next tile's loads are branch-free (buffer loads whose range is the tile's valid records:
+//    the lanes past it read 0 and become pads at the next rank) and the scatter is a fixed 16 stores
+//    per thread (lanes past the tile's end repeat the tile's last record), so every path through
+//    the loop has the same memory operations in flight and the compiler's waits count exactly:
+//    the next tile's rank waits for its own loads only, while this tile's stores drain;
+//  * the next tile's ticket is requested at the top of the tile and read after staging;
+//  * tiles are claimed XCD-grouped (xk > 0, see k_onesweep).
+// No order check, no next-pass totals, no staging rounds (k_onesweep keeps those for the LSD passes).
+// L: input layout (SOA arrays: pass 0 of separate arrays; AOS records: R1, or a texture), LO: output
+// layout (AOS: R1 / R2 records; SOA: arrays).  KB: range-relative keys (key - kbase) as in k_onesweep.
+template <int L, int LO, int SEG, bool KB = false, int RANK = RANK_LDS_ATOMIC>
+__global__ __launch_bounds__(1024, 4) void k_msd_pass(
+    const uint32_t* __restrict__ in_k, const uint32_t* __restrict__ in_v,
+    uint32_t* __restrict__ out_k, uint32_t* __restrict__ out_v, uint32_t n, uint32_t shift,
+    uint32_t ntiles, const uint32_t* __restrict__ dtot, unsigned long long* status,
+    uint32_t* ticket, uint32_t* err, uint32_t epoch, const uint32_t* gate, int gate_pass,
+    uint32_t spin_max, uint32_t* host_err, const uint32_t* __restrict__ segtab,
+    const uint32_t* __restrict__ base16, uint32_t kbase, uint32_t* xticket, uint32_t xk_log2) {
+    static_assert(L != LAYOUT_KEYS && LO != LAYOUT_KEYS, "with values");
+    static_assert(SEG == 0 || SEG == 1, "the two MSD passes");
+    constexpr int BLOCK = 1024, KPT = 16, R = 8, RADIX = 256, NW = BLOCK / 64;
+    constexpr int TILE = BLOCK * KPT, WAVE_KEYS = 64 * KPT;
+    constexpr uint32_t mask = RADIX - 1;
+    constexpr uint32_t ESZ = L == LAYOUT_AOS ? 8u : 4u;   // bytes per input element (record / key)
+    __shared__ uint32_t s_whist[NW][RADIX];
+    __shared__ uint32_t s_gdelta[RADIX];
+    __shared__ uint32_t s_dbase[RADIX];
+    __shared__ uint32_t s_scratch[NW];
+    __shared__ uint32_t s_next;
+    __shared__ uint2 s_kv[TILE];
+    __shared__ uint32_t s_seg[SEG == 1 ? 769 : 1];
+
+    if (gated_off(gate, gate_pass)) return;
+    const uint32_t tid = threadIdx.x, w = tid >> 6, lane = lane_id();
+    if (SEG == 1)
+        for (uint32_t i = tid; i < 769u; i += BLOCK) s_seg[i] = segtab[i];
+    const uint32_t xq = blockIdx.x & 7u;
+    // (k_onesweep's claims) the counter value is requested first and turned into a tile only where
+    // it is needed: using it at once would wait for every earlier store of the wave
+    uint32_t* const ctr = xticket ? xticket + xq : ticket;
+    // (xk = 2^xk_log2 tiles per XCD and round)
+    auto tile_of = [&](uint32_t c) -> uint32_t {
+        if (!xticket) return c;
+        return ((c >> xk_log2) << (xk_log2 + 3)) | (xq << xk_log2) | (c & ((1u << xk_log2) - 1u));
+    };
+    {   // first output position of every digit (SEG = 0; SEG = 1 per segment, below)
+        const uint32_t c = (SEG == 0 && tid < (uint32_t)RADIX) ? dtot[tid] : 0u;
+        uint32_t all;
+        const uint32_t ex = block_excl_scan_n<NW>(c, s_scratch, all);
+        if (tid < (uint32_t)RADIX) s_dbase[tid] = ex;
+        if (tid == 0) s_next = tile_of(atomicAdd(ctr, 1u));
+        __syncthreads();
+    }
+    uint32_t T = s_next;
+    const uint32_t nt = SEG == 1 ? s_seg[SEG == 1 ? 256 : 0] : ntiles;
+    auto geom = [&](uint32_t t, uint32_t& t0, uint32_t& tend, uint32_t& seg, uint32_t& first) {
+        if (SEG == 1) {
+            uint32_t lo = 0, hi = 256;                   // s_seg[lo] <= t < s_seg[hi]
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (s_seg[mid] <= t) lo = mid;
+                else hi = mid;
+            }
+            seg = lo;
+            first = s_seg[lo];
+            t0 = s_seg[257 + lo] + (t - first) * (uint32_t)TILE;
+            const uint32_t e = s_seg[513 + lo];
+            tend = e - t0 < (uint32_t)TILE ? e : t0 + (uint32_t)TILE;
+        } else {
+            seg = 0;
+            first = 0;
+            t0 = t * (uint32_t)TILE;
+            tend = (uint64_t)t0 + TILE <= n ? t0 + (uint32_t)TILE : n;
+        }
+    };
+    // Tile t's loads into k / v: buffer loads over [t0, tend) only (no branch; lanes past the end
+    // read 0), t >= nt: none (range 0).  The 64-bit base is rebased to the tile (32-bit offsets).
+    uint32_t k[KPT], v[KPT];
+    uint32_t nb16 = 0;   // SEG = 1, thread d < 256: base16 of digit d in the loaded tile's segment
+    const uint32_t lofs = (w * (uint32_t)WAVE_KEYS + lane) * ESZ;   // this lane's slot 0, bytes
+    auto load = [&](uint32_t t) {
+        uint32_t t0 = 0, tend = 0, sg = 0, fi;
+        if (t < nt) geom(t, t0, tend, sg, fi);
+        const uint32_t nbytes = (tend - t0) * ESZ;
+        // one offset register with immediate slot offsets (left to itself the compiler hoists the
+        // 16 per-slot offsets out of the tile loop: 16 registers)
+        uint32_t lo = lofs;
+        asm volatile("" : "+v"(lo));
+        if constexpr (L == LAYOUT_AOS) {
+            const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+                (void*)(in_k + 2ull * t0), (short)0, (int)nbytes, 0x00020000);
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) {
+                const auto q = __builtin_amdgcn_raw_buffer_load_b64(rr, (int)(lo + j * 64 * 8), 0, 0);
+                k[j] = q[0];
+                v[j] = q[1];
+            }
+        } else {
+            const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(
+                (void*)(in_k + t0), (short)0, (int)nbytes, 0x00020000);
+            const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(
+                (void*)(in_v + t0), (short)0, (int)nbytes, 0x00020000);
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) k[j] = __builtin_amdgcn_raw_buffer_load_b32(rk, (int)(lo + j * 256), 0, 0);
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) v[j] = __builtin_amdgcn_raw_buffer_load_b32(rv, (int)(lo + j * 256), 0, 0);
+        }
+        // (loaded with the tile: read at the top of a tile it would wait for every store before it)
+        if (SEG == 1) nb16 = base16[(sg << 8) | (tid & 255u)];
+    };
+    load(T);
+    // the first tile's registers used (waited for) here, so that the loop top's state - which the
+    // compiler merges over the loop's entry and its back edge - has only the back edge's operations
+    // pending: the next tile's loads, then this tile's stores.  Its waits for the loads then let the
+    // stores after them drain (an explicit s_waitcnt is dropped by the compiler's own wait pass)
+#pragma unroll
+    for (int j = 0; j < KPT; ++j) asm volatile("" ::"v"(k[j]), "v"(v[j]));
+    if (SEG == 1) asm volatile("" ::"v"(nb16));
+    uint32_t Tq = 0;   // thread 0: the next tile's ticket, requested at the top of this tile
+    while (T < nt) {
+        if (tid == 0) {
+            // a lane-varying address as far as the compiler knows: its atomic optimizer would turn a
+            // uniform-address add into a wave-aggregated one whose result is broadcast at once
+            uint32_t z = 0;
+            asm volatile("" : "+v"(z));
+            Tq = atomicAdd(ctr + z, 1u);
+        }
+        uint32_t tile0, tend, seg, seg_first;
+        geom(T, tile0, tend, seg, seg_first);
+        const uint32_t nvalid = tend - tile0;
+        const bool first_tile = T == seg_first;   // publishes an inclusive prefix at once
+        if (SEG == 1 && tid < (uint32_t)RADIX) s_dbase[tid] = s_seg[257 + seg] + nb16;
+        {   // slots past the tile's end become pads (kPadKey: after every real key); KB: relative keys
+            const uint32_t wb = w * (uint32_t)WAVE_KEYS + lane;
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) {
+                const bool ok = wb + j * 64u < nvalid;
+                k[j] = ok ? (KB ? k[j] - kbase : k[j]) : kPadKey;
+            }
+        }
+        Slots<KPT, false> rank;
+        uint32_t c;
+        const uint32_t tstart = rank_tile<R, NW, KPT, RANK>(k, rank, s_whist, s_scratch, shift, mask,
+                                                            (uint32_t)TILE - nvalid, c);
+        unsigned long long* st = status + (size_t)T * RADIX + tid;
+        if (tid < (uint32_t)RADIX) {
+            if (first_tile) st_store(st, (epoch << 2) | kStInclusive, s_dbase[tid] + c);
+            else st_store(st, (epoch << 2) | kStAggregate, c);
+            set_wave_offsets<R, NW>(s_whist, tstart);
+        }
+        __syncthreads();
+        stage_tile<KPT, true, TILE>(k, v, rank, s_whist[w], nullptr, s_kv, shift, mask, nullptr, 0u, 0u);
+        if (tid == 0) s_next = tile_of(Tq);
+        __syncthreads();
+        const uint32_t Tn = s_next;
+        // the look-back's first status words, then the next tile's loads behind them
+        const bool lb = tid < (uint32_t)RADIX && !first_tile;
+        unsigned long long sv[kLookback];
+        if (lb) {
+#pragma unroll
+            for (int i = 0; i < kLookback; ++i)
+                sv[i] = (T - 1 >= (uint32_t)i) ? st_load(status + (size_t)(T - 1 - i) * RADIX + tid) : 0ull;
+        }
+        load(Tn);
+        if (tid < (uint32_t)RADIX) {
+            uint32_t excl = s_dbase[tid];
+            if (lb) {
+                excl = 0;
+                uint32_t j = T - 1;                  // next predecessor to consume
+                uint32_t spins = 0;
+                for (;;) {
+                    uint32_t used = 0;
+                    bool done = false;
+#pragma unroll
+                    for (int i = 0; i < kLookback; ++i) {
+                        if (done || used != (uint32_t)i) break;
+                        const uint32_t f = (uint32_t)(sv[i] >> 32);
+                        if ((f >> 2) != epoch || j < (uint32_t)i) break;   // not yet published
+                        excl += (uint32_t)sv[i];
+                        ++used;
+                        done = (f & 3u) == kStInclusive;
+                    }
+                    if (done) break;
+                    j -= used;
+                    if (used == 0u) {   // bounded wait (k_onesweep's)
+                        ++spins;
+                        if (spins > spin_max ||
+                            ((spins & 255u) == 0u &&
+                             __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+                            atomicOr(err, 1u);
+                            if (host_err)
+                                __hip_atomic_fetch_or(host_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(1);
+                    }
+#pragma unroll
+                    for (int i = 0; i < kLookback; ++i)
+                        sv[i] = (j >= (uint32_t)i) ? st_load(status + (size_t)(j - i) * RADIX + tid) : 0ull;
+                }
+                st_store(st, (epoch << 2) | kStInclusive, excl + c);
+            }
+            s_gdelta[tid] = excl - tstart;
+        }
+        __syncthreads();
+        // the scatter: a fixed KPT stores per thread (staged positions past the tile's end repeat the
+        // last record: the same value to the same address), while the next tile's loads arrive
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) {
+            const uint32_t i0 = (uint32_t)j * BLOCK + tid;
+            const uint32_t i = i0 < nvalid ? i0 : nvalid - 1u;
+            const uint2 kv = s_kv[i];
+            uint32_t pos = s_gdelta[(kv.x >> shift) & mask] + i;
+            pos = pos < n ? pos : n - 1u;   // never clamps for consistent offsets (no fault on a bug)
+            if constexpr (LO == LAYOUT_AOS) {
+                reinterpret_cast<uint2*>(out_k)[pos] = kv;   // (KB: the range-relative key)
+            } else {
+                out_k[pos] = kv.x;
+                out_v[pos] = kv.y;
+            }
+        }
+        __syncthreads();
+        T = Tn;
+    }
 }
 
 // ---- one MSD pass over a static split: no look-back, no tickets -----------------------------

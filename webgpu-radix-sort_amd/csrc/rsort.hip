@@ -96,6 +96,10 @@ constexpr TileCfg kLarge{1024, 16, 16384, 512};
 // Words after the digit totals: [16] tile tickets (one per k_onesweep launch slot), [16] error words,
 // [16][8] the launch slots' XCD claim counters (k_onesweep's XCD-grouped claims)
 constexpr uint32_t kTicketWords = 32 + 16 * 8;
+#if !RS_KNOB_OPEN || !defined(RS_MSD_LEAN)
+#undef RS_MSD_LEAN
+#define RS_MSD_LEAN 1    // the MSD passes with values on k_msd_pass (0: k_onesweep)
+#endif
 #if !RS_KNOB_OPEN || !defined(RS_XCD_CLAIM)
 #undef RS_XCD_CLAIM
 #define RS_XCD_CLAIM 1   // k_onesweep: XCD-grouped tile claims (0: one ticket counter)
@@ -407,11 +411,11 @@ uint32_t resident_per_cu(F kernel, int block) {
 }
 
 // The XCD claim counters of the k_onesweep launch slot whose ticket is `ticket` (zeroed with it),
-// and xk = tiles per XCD per round, when the grid splits evenly over the 8 XCDs (else null: one
-// ticket counter).
+// and xk = tiles per XCD per round, when the grid splits evenly over the 8 XCDs and xk is a power of
+// two (else null: one ticket counter).
 uint32_t* xticket_of(rs_plan* p, uint32_t* ticket, uint32_t grid, uint32_t& xk) {
     xk = 0;
-    if (!RS_XCD_CLAIM || grid < 8u || grid % 8u != 0u) return nullptr;
+    if (!RS_XCD_CLAIM || grid < 8u || grid % 8u != 0u || ((grid / 8u) & (grid / 8u - 1u)) != 0u) return nullptr;
     const ptrdiff_t slot = ticket - p->tickets;
     if (slot < 0 || slot >= 16) return nullptr;
     xk = grid / 8u;
@@ -483,6 +487,24 @@ void launch_msd_pass(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint32_
                            gate, SEG, nullptr, 0xFFFFFFFFu, p->spin_max, p->host_err_dev, segtab, base16, kbase,
                            pmask, xt, xk);
     };
+    constexpr bool LEAN = RS_MSD_LEAN && SEG <= 1 && SR == 1 && L != rs::LAYOUT_KEYS && BLOCK == kLarge.block &&
+                          KPT == kLarge.kpt;
+    if constexpr (LEAN) {
+        if (pmask == 0xFFFFFFFFu) {   // (the ring experiment keeps k_onesweep)
+            auto lean = [&](auto kern) {
+                static const uint32_t per_cu = resident_per_cu(kern, BLOCK);
+                const uint32_t grid = std::min<uint32_t>(ntiles, p->cus * per_cu);
+                uint32_t xk = 0;
+                uint32_t* xt = xticket_of(p, ticket, grid, xk);
+                hipLaunchKernelGGL(kern, dim3(grid), dim3(BLOCK), 0, s, ik, iv, ok, ov, n, shift, ntiles, dtot,
+                                   p->status, ticket, p->tickets + 16, p->epoch, gate, SEG, p->spin_max,
+                                   p->host_err_dev, segtab, base16, kbase, xt, xk ? (uint32_t)__builtin_ctz(xk) : 0u);
+            };
+            if (p->rank_mode == rs::RANK_BALLOT) lean(rs::k_msd_pass<L, LO, SEG, KB, rs::RANK_BALLOT>);
+            else lean(rs::k_msd_pass<L, LO, SEG, KB, rs::RANK_LDS_ATOMIC>);
+            return;
+        }
+    }
     if (p->rank_mode == rs::RANK_BALLOT)
         go(rs::k_onesweep<8, BLOCK, KPT, L, rs::RANK_BALLOT, LO, SR, SEG, KB>);
     else

@@ -32,7 +32,7 @@ __global__ __launch_bounds__(1024) void run_tile(const uint2* __restrict__ in, u
                                                  uint32_t shifted, uint32_t off, uint32_t linear, uint32_t xcd) {
     __shared__ uint32_t s_t;
     const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-    const uint32_t x = xcd ? xcc_id() : 0u;
+    const uint32_t x = xcd == 1 ? xcc_id() : (xcd == 2 ? (blockIdx.x & 7u) : 0u);   // 2: the blockIdx % 8 guess
     auto claim = [&]() -> uint32_t {
         if (!xcd) return atomicAdd(ticket, 1u);
         const uint32_t c = atomicAdd(ticket + 1 + x, 1u);
@@ -76,6 +76,10 @@ __global__ __launch_bounds__(1024) void run_tile(const uint2* __restrict__ in, u
     }
 }
 
+__global__ void placement(uint32_t* out) {
+    if (threadIdx.x == 0) out[blockIdx.x] = xcc_id();
+}
+
 int main() {
     const size_t recs = 1ull << 28, bytes = recs * 8;
     int cus = 256;
@@ -94,6 +98,20 @@ int main() {
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     const uint32_t ntiles = (uint32_t)(recs / TILE);
+    {   // where a grid of `cus` 1024-thread workgroups lands: XCC_ID of every block vs blockIdx % 8
+        uint32_t* pl = nullptr;
+        CK(hipMalloc((void**)&pl, 4 * cus));
+        hipLaunchKernelGGL(placement, dim3(cus), dim3(1024), 0, 0, pl);
+        CK(hipDeviceSynchronize());
+        uint32_t h[1024];
+        CK(hipMemcpy(h, pl, 4 * cus, hipMemcpyDeviceToHost));
+        int match = 0, per[8] = {0};
+        for (int i = 0; i < cus; ++i) { match += (h[i] & 7u) == (uint32_t)(i & 7); per[h[i] & 7u]++; }
+        printf("{\"probe\": \"placement\", \"blocks\": %d, \"xcc_eq_blockidx_mod8\": %d, \"per_xcc\": [%d,%d,%d,%d,%d,%d,%d,%d], \"first16\": [", cus, match,
+               per[0], per[1], per[2], per[3], per[4], per[5], per[6], per[7]);
+        for (int i = 0; i < 16; ++i) printf("%u%s", h[i], i < 15 ? "," : "]}\n");
+        CK(hipFree(pl));
+    }
     struct V { const char* name; uint32_t R, shifted, off, linear, xcd; };
     const V vs[] = {
         {"linear", 64, 0, 0, 1, 0},
@@ -107,6 +125,8 @@ int main() {
         {"shifted_R64_split_xcd", 64, 1, 37, 0, 1},
         {"shifted_R128_xcd", 128, 1, 0, 0, 1},
         {"shifted_R32_split_xcd", 32, 1, 37, 0, 1},
+        {"shifted_R64_xcdguess", 64, 1, 0, 0, 2},
+        {"linear_xcdguess", 64, 0, 0, 1, 2},
     };
     for (int pass = 0; pass < 2; ++pass) {
         for (const V& v : vs) {

@@ -952,7 +952,7 @@ __global__ __launch_bounds__(BLOCK, pass_min_waves(BLOCK, KPT)) void k_onesweep(
     uint32_t nshift, uint32_t nmask, uint32_t epoch, const uint32_t* gate, int pass,
     uint32_t* chk, uint32_t fmask, uint32_t spin_max, uint32_t* host_err,
     const uint32_t* __restrict__ segtab = nullptr, const uint32_t* __restrict__ base16 = nullptr,
-    uint32_t kbase = 0, uint32_t pmask = 0xFFFFFFFFu, uint32_t* xticket = nullptr, uint32_t xk = 0) {
+    uint32_t kbase = 0, uint32_t pmask = 0xFFFFFFFFu) {
     // ntot (may be null): whole-array totals of the NEXT pass's digit (key >> nshift) & nmask,
     // counted here from the keys this workgroup stages, so only pass 0 needs k_pass_totals.
     // chk (may be null, check_order, pass > 0): the order check of this pass's input, fused:
@@ -992,29 +992,12 @@ __global__ __launch_bounds__(BLOCK, pass_min_waves(BLOCK, KPT)) void k_onesweep(
     const uint32_t* start2 = segtab + 2 + ntiles;
     const uint32_t* end2 = segtab + 2 + 2 * ntiles;
     if (tid == 0) s_inv = 0u;
-    // Tile claims.  xk == 0: one ticket counter, tiles in ticket order.  xk > 0 (a grid of 8 * xk
-    // workgroups): XCD-grouped claims - workgroup g draws from counter xticket[g % 8] (workgroups
-    // are dealt round-robin over the 8 XCDs, so that is its XCD), and the c-th claim of counter x
-    // is tile (c / xk) * 8xk + x * xk + c % xk: every round of 8xk consecutive tiles gives each XCD
-    // xk ADJACENT tiles, which its xk workgroups process at the same time.  The 128-B line where a
-    // digit run of tile T meets the run of tile T + 1 is then completed in one L2 instead of reaching
-    // HBM as two partial writes (tools/run_probe.hip: 1.07 -> 0.88 ms for the pass's write pattern).
-    // Correctness does not depend on the placement: each counter's claims are in tile order and
-    // every counter has workgroups (grid >= 8, dispatched in order), so every tile is claimed by a
-    // running workgroup whose predecessors are claimed too (look-back progress as with one counter).
-    const uint32_t xq = blockIdx.x & 7u;
-    auto claim = [&]() -> uint32_t {
-        if (!xticket) return atomicAdd(ticket, 1u);
-        const uint32_t c = atomicAdd(xticket + xq, 1u);
-        const uint32_t r = c / xk;
-        return r * 8u * xk + xq * xk + (c - r * xk);   // monotone in c: past nt once, past for good
-    };
     {   // first output position of every digit
         const uint32_t c = (!SG && tid < (uint32_t)RADIX && tid <= mask) ? dtot[tid] : 0u;
         uint32_t all;
         const uint32_t ex = block_excl_scan_n<NW>(c, s_scratch, all);
         if (tid < (uint32_t)RADIX) s_dbase[tid] = ex;
-        if (tid == 0) s_next = claim();
+        if (tid == 0) s_next = atomicAdd(ticket, 1u);
         __syncthreads();
     }
     uint32_t T = s_next;
@@ -1131,7 +1114,7 @@ __global__ __launch_bounds__(BLOCK, pass_min_waves(BLOCK, KPT)) void k_onesweep(
             stage_round<KPT, HAS_VALUES, STAGE>(k, v, rank, s_keys, s_kv, 0u);
         }
         if (tid == 0) {
-            s_next = claim();
+            s_next = atomicAdd(ticket, 1u);
             if (ntot && npad) atomicSub(&s_ntot[nmask], npad);   // the pads' next digit
         }
         __syncthreads();
@@ -1250,8 +1233,14 @@ __global__ __launch_bounds__(BLOCK, pass_min_waves(BLOCK, KPT)) void k_onesweep(
 //    per thread (lanes past the tile's end repeat the tile's last record), so every path through
 //    the loop has the same memory operations in flight and the compiler's waits count exactly:
 //    the next tile's rank waits for its own loads only, while this tile's stores drain;
-//  * the next tile's ticket is requested at the top of the tile and read after staging;
-//  * tiles are claimed XCD-grouped (xk > 0, see k_onesweep).
+//  * the next tile's ticket is requested at the top of the tile and read after staging (its value,
+//    used at once, would wait for every earlier store of the wave).
+// Measured against k_onesweep on config3: the same time (the pass is bound by its scattered write
+// pattern: tools/run_probe.hip copies 2^28 records in that pattern in 1.07 ms, the pass takes 0.99;
+// profiles/r05/ab_lean_xcd).  XCD-grouped tile claims (adjacent tiles on one XCD, so that the line
+// two tiles' runs share is completed in one L2) cut the probe from 1.07 to 0.89 ms but made the
+// pass 4 % slower (the look-back chain then runs across the XCDs' claim rounds;
+// profiles/r05/ab_xcd_hw); they are in the history (8b24fac), not here.
 // No order check, no next-pass totals, no staging rounds (k_onesweep keeps those for the LSD passes).
 // L: input layout (SOA arrays: pass 0 of separate arrays; AOS records: R1, or a texture), LO: output
 // layout (AOS: R1 / R2 records; SOA: arrays).  KB: range-relative keys (key - kbase) as in k_onesweep.
@@ -1262,7 +1251,7 @@ __global__ __launch_bounds__(1024, 4) void k_msd_pass(
     uint32_t ntiles, const uint32_t* __restrict__ dtot, unsigned long long* status,
     uint32_t* ticket, uint32_t* err, uint32_t epoch, const uint32_t* gate, int gate_pass,
     uint32_t spin_max, uint32_t* host_err, const uint32_t* __restrict__ segtab,
-    const uint32_t* __restrict__ base16, uint32_t kbase, uint32_t* xticket, uint32_t xk_log2) {
+    const uint32_t* __restrict__ base16, uint32_t kbase) {
     static_assert(L != LAYOUT_KEYS && LO != LAYOUT_KEYS, "with values");
     static_assert(SEG == 0 || SEG == 1, "the two MSD passes");
     constexpr int BLOCK = 1024, KPT = 16, R = 8, RADIX = 256, NW = BLOCK / 64;
@@ -1281,21 +1270,12 @@ __global__ __launch_bounds__(1024, 4) void k_msd_pass(
     const uint32_t tid = threadIdx.x, w = tid >> 6, lane = lane_id();
     if (SEG == 1)
         for (uint32_t i = tid; i < 769u; i += BLOCK) s_seg[i] = segtab[i];
-    const uint32_t xq = blockIdx.x & 7u;
-    // (k_onesweep's claims) the counter value is requested first and turned into a tile only where
-    // it is needed: using it at once would wait for every earlier store of the wave
-    uint32_t* const ctr = xticket ? xticket + xq : ticket;
-    // (xk = 2^xk_log2 tiles per XCD and round)
-    auto tile_of = [&](uint32_t c) -> uint32_t {
-        if (!xticket) return c;
-        return ((c >> xk_log2) << (xk_log2 + 3)) | (xq << xk_log2) | (c & ((1u << xk_log2) - 1u));
-    };
     {   // first output position of every digit (SEG = 0; SEG = 1 per segment, below)
         const uint32_t c = (SEG == 0 && tid < (uint32_t)RADIX) ? dtot[tid] : 0u;
         uint32_t all;
         const uint32_t ex = block_excl_scan_n<NW>(c, s_scratch, all);
         if (tid < (uint32_t)RADIX) s_dbase[tid] = ex;
-        if (tid == 0) s_next = tile_of(atomicAdd(ctr, 1u));
+        if (tid == 0) s_next = atomicAdd(ticket, 1u);
         __syncthreads();
     }
     uint32_t T = s_next;
@@ -1370,7 +1350,7 @@ __global__ __launch_bounds__(1024, 4) void k_msd_pass(
             // uniform-address add into a wave-aggregated one whose result is broadcast at once
             uint32_t z = 0;
             asm volatile("" : "+v"(z));
-            Tq = atomicAdd(ctr + z, 1u);
+            Tq = atomicAdd(ticket + z, 1u);
         }
         uint32_t tile0, tend, seg, seg_first;
         geom(T, tile0, tend, seg, seg_first);
@@ -1397,7 +1377,7 @@ __global__ __launch_bounds__(1024, 4) void k_msd_pass(
         }
         __syncthreads();
         stage_tile<KPT, true, TILE>(k, v, rank, s_whist[w], nullptr, s_kv, shift, mask, nullptr, 0u, 0u);
-        if (tid == 0) s_next = tile_of(Tq);
+        if (tid == 0) s_next = Tq;
         __syncthreads();
         const uint32_t Tn = s_next;
         // the look-back's first status words, then the next tile's loads behind them

@@ -93,16 +93,11 @@ struct TileCfg {
     uint32_t max_grid;
 };
 constexpr TileCfg kLarge{1024, 16, 16384, 512};
-// Words after the digit totals: [16] tile tickets (one per k_onesweep launch slot), [16] error words,
-// [16][8] the launch slots' XCD claim counters (k_onesweep's XCD-grouped claims)
-constexpr uint32_t kTicketWords = 32 + 16 * 8;
+// Words after the digit totals: [16] tile tickets (one per k_onesweep launch slot), [16] error words
+constexpr uint32_t kTicketWords = 32;
 #if !RS_KNOB_OPEN || !defined(RS_MSD_LEAN)
 #undef RS_MSD_LEAN
 #define RS_MSD_LEAN 1    // the MSD passes with values on k_msd_pass (0: k_onesweep)
-#endif
-#if !RS_KNOB_OPEN || !defined(RS_XCD_CLAIM)
-#undef RS_XCD_CLAIM
-#define RS_XCD_CLAIM 1   // k_onesweep: XCD-grouped tile claims (0: one ticket counter)
 #endif
 constexpr TileCfg kSmall{256, 16, 4096, 1024};
 // keys-only at >= 12M keys: the same 16K-key tile from 512 threads x 32 keys (75 KiB LDS), so
@@ -300,8 +295,7 @@ struct rs_plan {
     uint64_t status_words = 0;
     uint32_t* ptot = nullptr;      // [kTotalsMax] whole-array digit totals of every pass
     uint32_t ptot_off[16] = {};    // offset of pass i's totals in ptot
-    uint32_t* tickets = nullptr;   // = ptot + kTotalsMax: [16] per-pass tile tickets, [16] error,
-                                   // [16][8] per-pass XCD claim counters (xticket_of)
+    uint32_t* tickets = nullptr;   // = ptot + kTotalsMax: [16] per-pass tile tickets, [16] error
     uint32_t epoch = 0;            // tag of the last k_onesweep launch's status words
     uint32_t spin_max = 1u << 20;  // look-back wait bound in sleeps (rs_plan_set_wait_limit; tests force 0)
     int msd_mode = RS_MSD_DEFAULT;   // hybrid MSD path for values (rs_plan_debug.msd = 0/1)
@@ -410,18 +404,6 @@ uint32_t resident_per_cu(F kernel, int block) {
     return (uint32_t)api;
 }
 
-// The XCD claim counters of the k_onesweep launch slot whose ticket is `ticket` (zeroed with it),
-// and xk = tiles per XCD per round, when the grid splits evenly over the 8 XCDs and xk is a power of
-// two (else null: one ticket counter).
-uint32_t* xticket_of(rs_plan* p, uint32_t* ticket, uint32_t grid, uint32_t& xk) {
-    xk = 0;
-    if (!RS_XCD_CLAIM || grid < 8u || grid % 8u != 0u || ((grid / 8u) & (grid / 8u - 1u)) != 0u) return nullptr;
-    const ptrdiff_t slot = ticket - p->tickets;
-    if (slot < 0 || slot >= 16) return nullptr;
-    xk = grid / 8u;
-    return p->tickets + 32 + 8 * slot;
-}
-
 template <int R, int BLOCK, int KPT, int L, int RANK, int LO, int SR>
 void launch_onesweep_t(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint32_t* ok,
                        uint32_t* ov, uint32_t n, uint32_t shift, uint32_t mask, uint32_t ntiles,
@@ -434,8 +416,6 @@ void launch_onesweep_t(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint3
     uint32_t grid = std::min<uint32_t>(ntiles, p->cus * per_cu);
     if (cap > 0 && cap < grid) grid = cap;
     const bool last = (uint32_t)pass + 1 >= p->passes;
-    uint32_t xk = 0;
-    uint32_t* xt = xticket_of(p, p->tickets + pass, grid, xk);
     uint32_t* ntot = last ? nullptr : p->ptot + p->ptot_off[pass + 1];
     const uint32_t nshift = last ? 0u : shift + p->widths[pass];
     const uint32_t nmask = last ? 0u : (1u << p->widths[pass + 1]) - 1u;
@@ -445,7 +425,7 @@ void launch_onesweep_t(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint3
                        p->ptot + p->ptot_off[pass], p->status, p->tickets + pass,
                        p->tickets + 16, ntot, nshift, nmask, p->epoch, gate, pass, chk,
                        full_mask(p->bit_count), p->spin_max, p->host_err_dev,
-                       (const uint32_t*)nullptr, (const uint32_t*)nullptr, 0u, 0xFFFFFFFFu, xt, xk);
+                       (const uint32_t*)nullptr, (const uint32_t*)nullptr, 0u, 0xFFFFFFFFu);
 }
 
 template <int R, int BLOCK, int KPT, int L, int LO, int SR>
@@ -480,12 +460,10 @@ void launch_msd_pass(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint32_
     auto go = [&](auto kern) {
         static const uint32_t per_cu = resident_per_cu(kern, BLOCK);
         const uint32_t grid = std::min<uint32_t>(ntiles, p->cus * per_cu);
-        uint32_t xk = 0;
-        uint32_t* xt = xticket_of(p, ticket, grid, xk);
         hipLaunchKernelGGL(kern, dim3(grid), dim3(BLOCK), 0, s, ik, iv, ok, ov, n, shift, 255u,
                            ntiles, dtot, p->status, ticket, p->tickets + 16, nullptr, 0u, 0u, p->epoch,
                            gate, SEG, nullptr, 0xFFFFFFFFu, p->spin_max, p->host_err_dev, segtab, base16, kbase,
-                           pmask, xt, xk);
+                           pmask);
     };
     constexpr bool LEAN = RS_MSD_LEAN && SEG <= 1 && SR == 1 && L != rs::LAYOUT_KEYS && BLOCK == kLarge.block &&
                           KPT == kLarge.kpt;
@@ -494,11 +472,9 @@ void launch_msd_pass(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint32_
             auto lean = [&](auto kern) {
                 static const uint32_t per_cu = resident_per_cu(kern, BLOCK);
                 const uint32_t grid = std::min<uint32_t>(ntiles, p->cus * per_cu);
-                uint32_t xk = 0;
-                uint32_t* xt = xticket_of(p, ticket, grid, xk);
                 hipLaunchKernelGGL(kern, dim3(grid), dim3(BLOCK), 0, s, ik, iv, ok, ov, n, shift, ntiles, dtot,
                                    p->status, ticket, p->tickets + 16, p->epoch, gate, SEG, p->spin_max,
-                                   p->host_err_dev, segtab, base16, kbase, xt, xk ? (uint32_t)__builtin_ctz(xk) : 0u);
+                                   p->host_err_dev, segtab, base16, kbase);
             };
             if (p->rank_mode == rs::RANK_BALLOT) lean(rs::k_msd_pass<L, LO, SEG, KB, rs::RANK_BALLOT>);
             else lean(rs::k_msd_pass<L, LO, SEG, KB, rs::RANK_LDS_ATOMIC>);
@@ -903,7 +879,7 @@ RS_EXPORT rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out) {
             return cleanup(fail(e == hipErrorOutOfMemory ? RS_ERR_OUT_OF_MEMORY : RS_ERR_HIP,
                                 "rs_plan_create: hipMalloc failed: %s", hipGetErrorString(e)));
     }
-    p->tickets = p->ptot + rs::kTotalsMax;   // [16] tickets, [16] error word, [16][8] XCD counters
+    p->tickets = p->ptot + rs::kTotalsMax;   // [16] tickets, [16] error word
 
     if ((e = hipHostMalloc((void**)&p->host_err, 4, hipHostMallocMapped)) != hipSuccess ||
         (e = hipHostGetDevicePointer((void**)&p->host_err_dev, p->host_err, 0)) != hipSuccess ||
@@ -1767,7 +1743,6 @@ static rs_status onesweep_digit_pass(rs_plan* p, const uint32_t* ik, const uint3
     const int pass = (int)p->passes - 1;
     uint32_t* slot = p->ptot + p->ptot_off[pass];   // 2^bits words fit: kTotalsMax >= off + 256
     HIP_TRY(hipMemsetAsync(p->tickets + pass, 0, 4, s));
-    HIP_TRY(hipMemsetAsync(p->tickets + 32 + 8 * pass, 0, 32, s));   // its XCD claim counters
     HIP_TRY(hipMemsetAsync(p->tickets + 16, 0, 4, s));
     if (d_totals) {
         HIP_TRY(hipMemcpyAsync(slot, d_totals, 4u << bits, hipMemcpyDeviceToDevice, s));

@@ -9,7 +9,7 @@ A step = one full sort of one batch of synthetic input resident in HBM:
   local_shuffle=true, bit_count 32, one RadixSortKernel.dispatch() per step.  Every step sorts a
   different pre-generated batch (sorting already-sorted data would be a different workload).
   The library takes its hybrid MSD path here: `roofline` is the scatter kernel
-  (k_onesweep, 2 launches per sort), `bucket_pass` the in-LDS bucket kernel.  `--workload
+  (k_msd_pass, 2 launches per sort), `bucket_pass` the in-LDS bucket kernel.  `--workload
   config2` (64M keys only) takes the keys-only form of the same path (one wave per 16-bit bucket).
 * N > 1 (torch.distributed.run, one process per GPU, RCCL): BASELINE configs[4] shape with
   2^28 keys+values per rank (2^31 at 8 GPUs): histogram all_gather -> stable top-byte partition
@@ -659,7 +659,8 @@ def main() -> None:
             pass
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "kernel": ("k_onesweep (rank + look-back + local shuffle + scatter)"
+                "kernel": (("k_msd_pass" if (msd and wl["values"]) else "k_onesweep")
+                           + " (rank + look-back + local shuffle + scatter)"
                            if onesweep else "k_scatter (rank + local shuffle + scatter)"),
                 "avg_launch_ms": round(avg_ms, 4),
                 "algorithmic_bytes_per_launch": scatter_keys * bytes_per_key,

@@ -32,9 +32,10 @@ def run_pass(counter: str, wl: str, outdir: str) -> dict:
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             name = r["Kernel_Name"]
-            # the pass kernel (k_scatter, or k_onesweep on the one-sweep path) and a kernel that
+            # the pass kernel (k_scatter, k_onesweep on the one-sweep path, k_msd_pass on the hybrid
+            # path's passes with values) and a kernel that
             # reads exactly the n keys once (k_histogram per pass, or k_pass_totals per sort)
-            key = ("scatter" if ("k_scatter" in name or "k_onesweep" in name)
+            key = ("scatter" if ("k_scatter" in name or "k_onesweep" in name or "k_msd_pass" in name)
                    else "histogram" if ("k_histogram" in name or "k_pass_totals" in name
                                         or "k_hist16_in" in name)
                    else "bucket" if "k_bucket_sort" in name

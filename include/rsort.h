@@ -104,7 +104,10 @@ enum {
                                    (gated off on the device unless it is taken) */
     RS_KERNEL_SPLIT = 6,        /* hybrid MSD path: the bucket split of over-full 16-bit buckets
                                    (skewed keys; one span per sort, gated off for spread keys) */
-    RS_KERNEL_KINDS = 7
+    RS_KERNEL_PRESORTED = 7,    /* hybrid MSD path with check_order: the nearly-sorted path (mark
+                                   the displaced keys, sort them, merge; one span per sort, gated
+                                   off on the device when the input is not nearly sorted) */
+    RS_KERNEL_KINDS = 8
 };
 
 /* ---- errors / versions ------------------------------------------------------------------ */
@@ -188,7 +191,9 @@ enum {
     RS_PATH_HYBRID = 2,           /* hybrid MSD: top-byte pass, next-byte pass, in-LDS bucket sort */
     RS_PATH_HYBRID_FALLBACK = 3,  /* the hybrid path's LSD fallback (a key outside a range hint, or
                                      a bucket over the tile with the bucket split off) */
-    RS_PATH_IN_ORDER = 4          /* check_order found the input sorted: nothing moved */
+    RS_PATH_IN_ORDER = 4,         /* check_order found the input sorted: nothing moved */
+    RS_PATH_PRESORTED = 5         /* check_order found the input nearly sorted: its displaced keys
+                                     were extracted, sorted and merged back (no radix pass) */
 };
 rs_status rs_plan_last_path(rs_plan* plan, uint32_t* path);
 /* How deep the hybrid path's last sort split over-full 16-bit buckets (skewed keys, e.g. f32 in
@@ -232,6 +237,8 @@ typedef struct rs_plan_debug {
                                rs_plan_info.lane_order_selftest = 0) */
     int32_t split;          /* hybrid path, 16-bit buckets over the bucket tile (skewed keys): 1 split
                                them (default), 0 take the LSD fallback for the whole sort */
+    int32_t presorted;      /* hybrid path with check_order: 1 the nearly-sorted path where the
+                               device finds it applies (default), 0 never (the radix passes) */
 } rs_plan_debug;
 rs_status rs_plan_set_debug(rs_plan* plan, const rs_plan_debug* debug);
 void      rs_plan_destroy(rs_plan* plan);     /* frees the workspace (reference quirk Q9) */

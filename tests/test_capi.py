@@ -77,16 +77,19 @@ def test_null_arguments():
 
 def test_debug_struct_and_kernel_kinds_match_the_header():
     """The Python mirrors of rs_plan_debug (every field, the split switch last) and of the kernel
-    kinds (RS_KERNEL_SPLIT = 6, RS_KERNEL_KINDS = 7) agree with include/rsort.h."""
+    kinds (RS_KERNEL_PRESORTED = 7, RS_KERNEL_KINDS = 8) agree with include/rsort.h."""
     import os
     import re
     hdr = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "rsort.h")).read()
     body = hdr[hdr.index("typedef struct rs_plan_debug"):hdr.index("} rs_plan_debug;")]
     fields = re.findall(r"int32_t\s+(\w+);", body)
     assert [f for f, _ in _lib.PlanDebug._fields_] == fields
-    assert fields[-1] == "split"
-    assert re.search(r"RS_KERNEL_SPLIT = 6", hdr) and re.search(r"RS_KERNEL_KINDS = 7", hdr)
-    assert _lib.RS_KERNEL_KINDS == 7 and _lib.KERNEL_NAMES[_lib.RS_KERNEL_SPLIT] == "split"
+    assert fields[-1] == "presorted"
+    assert re.search(r"RS_KERNEL_SPLIT = 6", hdr) and re.search(r"RS_KERNEL_PRESORTED = 7", hdr)
+    assert re.search(r"RS_KERNEL_KINDS = 8", hdr)
+    assert _lib.RS_KERNEL_KINDS == 8 and _lib.KERNEL_NAMES[_lib.RS_KERNEL_SPLIT] == "split"
+    assert _lib.KERNEL_NAMES[_lib.RS_KERNEL_PRESORTED] == "presorted"
+    assert re.search(r"RS_PATH_PRESORTED = 5", hdr) and _lib.PATH_NAMES[5] == "presorted"
 
 
 def test_python_facade_validates_both_spellings():

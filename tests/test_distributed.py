@@ -327,7 +327,7 @@ def test_multi_gpu_breakdown_fields():
     # the layout bench.py ships: the library's kernel kinds, then the sender's two terms
     names = list(_lib.KERNEL_NAMES) + ["sender_hist16", "sender_partition"]
     kinds = {"histogram": 0.3, "scan": 0.0, "scatter": 2.0, "check": 0.0, "bucket": 2.06, "fallback": 0.0,
-             "split": 0.0, "sender_hist16": 0.3, "sender_partition": 1.05}
+             "split": 0.0, "presorted": 0.0, "sender_hist16": 0.3, "sender_partition": 1.05}
     assert set(names) == set(kinds), "a kernel kind was added: give it a value here"
     tl = StepTimeline()
     tl.bytes_sent, tl.bytes_recv = 7 * 10**8, 7 * 10**8

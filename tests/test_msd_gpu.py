@@ -360,8 +360,9 @@ def _chk_keys(kind, n):
 def test_msd_check_order(kind):
     """check_order on the hybrid path: the input's order check rides on the 16-bit histogram read;
     an input in order gates every later launch off (the reference's early exit, CheckSort.ts:138-145)
-    and comes back untouched; otherwise the hybrid path (skewed keys: with the bucket split) sorts
-    it - separate arrays, keys only, records."""
+    and comes back untouched; nearly-sorted input (a swapped last pair, config 4's f32 keys) takes
+    the presorted path (test_presorted_gpu.py); otherwise the hybrid path (skewed keys: with the
+    bucket split) sorts it - separate arrays, keys only, records."""
     from radix_sort_amd import RadixSortTextureKernel
     n = (1 << 25) + 3
     keys = _chk_keys(kind, n)
@@ -379,8 +380,10 @@ def test_msd_check_order(kind):
     assert np.array_equal(kt.cpu().numpy().view(np.uint32), ek)
     assert np.array_equal(vt.cpu().numpy().view(np.uint32), ev)
     assert t["bucket"]["launches"] >= 1 and t["check"]["launches"] == 0   # the hybrid path's launches
-    if kind in ("uniform", "f32_nearly"):
-        assert path == "hybrid"           # f32: over-full buckets split, no LSD fallback
+    if kind in ("uniform", "reverse"):
+        assert path == "hybrid"
+    if kind in ("last_pair", "f32_nearly"):
+        assert path == "presorted"
     if kind == "sorted":                  # everything after the read gated off
         assert path == "in_order"
     kern.destroy()

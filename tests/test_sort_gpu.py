@@ -270,8 +270,8 @@ def test_config4_256M_nearly_sorted_f32_check_order():
     kern.dispatch()
     torch.cuda.synchronize()
     kern.check()
-    # the hybrid path with its over-full buckets split (half the keys share 128 buckets of ~1M)
-    assert kern.last_path() == "hybrid" and kern.last_split() >= 2
+    # the presorted path: the displaced keys extracted, sorted and merged back
+    assert kern.last_path() == "presorted"
     _verify_kv_iota(k_in, kt, vt)
     # fully sorted variant: early exit leaves the data untouched
     kern.dispatch()

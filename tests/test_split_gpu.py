@@ -171,7 +171,10 @@ def test_split_ballot_ranking_and_repeat(plan_debug):
 
 
 @pytest.mark.parametrize("kind", ["f32_nearly", "few"])
-def test_split_check_order(kind):
+def test_split_check_order(plan_debug, kind):
+    # the radix path with check_order (nearly-sorted input would take the presorted path:
+    # test_presorted_gpu.py)
+    plan_debug(presorted=0)
     keys = _keys_u32(kind, N)
     ek, ev = _expect(keys)
     k = torch.from_numpy(keys.view(np.int32)).to(DEV)

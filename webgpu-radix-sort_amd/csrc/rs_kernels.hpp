@@ -1663,8 +1663,11 @@ __global__ __launch_bounds__(1024) void k_hist16_in(const uint32_t* __restrict__
                                                      uint32_t range, uint32_t shift,
                                                      uint32_t* __restrict__ z0, uint32_t* __restrict__ z1,
                                                      uint32_t* inv = nullptr, uint32_t* __restrict__ b0rows = nullptr,
-                                                     uint32_t* __restrict__ z2 = nullptr) {
+                                                     uint32_t* __restrict__ z2 = nullptr,
+                                                     const uint32_t* skip = nullptr) {
     // z2 (may be null): the bucket split's huge-bucket count (SplitWs::huge[0])
+    // skip (may be null): *skip != 0 - the presorted path has sorted the data (rs_presorted.hpp):
+    // nothing is read, the order check stays "in order"
     static_assert(!CHECK || FULL, "the order check rides on whole-range histograms only");
     constexpr bool B0 = CHECK == 2;   // the byte-0 counts too (the LSD fallback's pass-0 totals)
     // z0, z1: the reduction's overflow-bucket count and oversize flag (k_hist16_reduce adds to them)
@@ -1673,6 +1676,7 @@ __global__ __launch_bounds__(1024) void k_hist16_in(const uint32_t* __restrict__
         *z1 = 0u;
         if (z2) *z2 = 0u;
     }
+    if (skip && *skip) return;
     constexpr uint32_t B = 1024, W = 32768, PER = W / B;
     constexpr bool NARROW = L == LAYOUT_AOS && !AOS_WIDE;
     constexpr uint32_t KPL = NARROW ? 1u : (L == LAYOUT_AOS ? 2u : 4u);   // keys per load
@@ -1912,19 +1916,24 @@ __global__ __launch_bounds__(1024) void k_hist16_reduce(const uint32_t* __restri
                                                          uint32_t* __restrict__ zero = nullptr, uint32_t nzero = 0,
                                                          const uint32_t* __restrict__ b0rows = nullptr,
                                                          uint32_t* __restrict__ cbase = nullptr,
-                                                         uint32_t* __restrict__ huge = nullptr, uint32_t hmax = 0) {
+                                                         uint32_t* __restrict__ huge = nullptr, uint32_t hmax = 0,
+                                                         const uint32_t* skip = nullptr) {
     // huge (may be null): buckets over `cap` are listed in huge[1..] (huge[0] counts them, up to hmax
     // stored; zeroed with over[0]) for the bucket split instead of flagging *big
     // zero[0..nzero): the sort's pass totals, tile tickets and device error word (no memset launch);
     // with b0rows (check_order): zero[0..256) = pass 0's byte-0 totals, the rows' sums
+    // skip (may be null): *skip != 0 - the presorted path sorted the data and k_hist16_in wrote no
+    // rows: only the zeroing (k_msd_plan then gates every launch off on the order check)
+    const bool skipped = skip && *skip;
     if (blockIdx.x == gridDim.x - 1) {
         for (uint32_t i = threadIdx.x; i < nzero; i += blockDim.x) zero[i] = 0u;
-        if (b0rows && threadIdx.x < 256u) {   // the same thread zeroed zero[threadIdx.x] above
+        if (b0rows && !skipped && threadIdx.x < 256u) {   // the same thread zeroed zero[threadIdx.x] above
             uint32_t c = 0;
             for (uint32_t r = 0; r < nrows; ++r) c += b0rows[(size_t)r * 256u + threadIdx.x];
             zero[threadIdx.x] = c;
         }
     }
+    if (skipped) return;
     __shared__ uint4 s_part[16][64];
     __shared__ uint32_t s_rowsum[kMaxRows];
     __shared__ uint32_t s_scan[16];

@@ -1,0 +1,566 @@
+// rs_presorted.hpp — the presorted path of check_order sorts (CDNA4 / gfx950).
+//
+// check_order (README.md:85, AbstractRadixSortKernel.ts:249-276) exists for input that is already in
+// order: the reference checks the order between its passes and skips the rest once the data is
+// sorted.  Input that is NEARLY in order - sorted data with a few displaced elements, BASELINE
+// config 4's "nearly sorted" f32 keys - still pays every pass there (and here, on the radix path:
+// 80 B/key for config 4's skewed floats).  This path sorts such input in O(n) traffic instead:
+//
+//   1. k_ns_mark: the descents (i, i + 1: key[i] > key[i + 1] under the bit_count mask) mark both
+//      their elements; the unmarked remainder is then re-checked around every marked run (the last
+//      unmarked element before a run against the first after it) and both ends of any inversion
+//      marked, until the remainder is in order.  Tiles of 4096 keys iterate in LDS with a 64-key
+//      halo of context on each side (marks in the halo are the neighbour's business: any marking
+//      whose remainder is in order is a valid one, and a pair of remainder elements in two tiles is
+//      checked by k_ns_decide).  More than 16 rounds, too many descents, or a tile marked whole
+//      sends the sort to the radix path (decided on the device: k_ns_decide).  Workgroups stop
+//      reading once the running descent count exceeds half the extraction capacity (random input
+//      costs a few million keys of reading, not a pass).
+//   2. k_ns_extract: the marked elements, in position order, to side arrays (masked key, extraction
+//      index; key, value, position); the rest of the extraction capacity padded with the largest key.
+//   3. the extracted elements sorted by the library's own LSD passes (gated on the device), stably:
+//      equal masked keys keep position order.
+//   4. k_ns_bounds: for every tile of positions, how many extracted elements go before its first
+//      remainder element (binary search in the sorted extraction).
+//   5. k_ns_merge: every tile writes its remainder elements and the extracted elements that fall
+//      among them, merged by (masked key, position) - the stable order - to a plan buffer; the merged
+//      output of a tile is one contiguous range.
+//   6. k_ns_copy: the plan buffer back to the caller's arrays (the merge cannot run in place: its
+//      output of a tile overlaps the input of its neighbours).
+// The radix path is still enqueued behind and finds the caller's data in order (its own order
+// check on the histogram read: k_msd_plan then gates every pass off); its histogram read is
+// skipped when this path has sorted (k_hist16_in's `skip`).  Result: the stable sort, as on the
+// radix path.  Bytes per key (nearly sorted input): 4 (mark) + 16 (merge) + 16 (copy) + ~0 (the
+// extraction, n / 1000-ish keys) against the radix path's 52-80.
+#pragma once
+#include "rs_kernels.hpp"
+
+namespace rs {
+
+constexpr uint32_t kNsHalo = 64;           // keys of context on each side of a tile
+constexpr uint32_t kNsWin = 4096;          // a tile's window in k_ns_mark: 256 threads x 16 keys
+constexpr uint32_t kNsTile = kNsWin - 2 * kNsHalo;   // keys per tile (3968: 124 bitmap words)
+constexpr uint32_t kNsIter = 16;           // marking rounds per tile before giving up
+constexpr uint32_t kNsBChunk = 512;        // extracted elements per LDS chunk in the merge
+// control words (ctl): [1] a tile failed, [3] a tile was dense (the path is off), [4] m (marked
+// total), [5] done (the path sorted: the radix path's histogram read is skipped), [8 .. 8 + 16)
+// gate words
+constexpr uint32_t kNsCtlWords = 32;
+constexpr uint32_t kNsGate = 8;
+
+// masked key of element i of a layout (KEYS / SOA: keys[i]; AOS: keys[2i])
+template <int L>
+__device__ __forceinline__ uint32_t ns_key(const uint32_t* keys, uint64_t i) {
+    return keys[(L == LAYOUT_AOS ? 2ull : 1ull) * i];
+}
+
+// Persistent grid: workgroup g takes tiles g, g + grid, ... in order, with the next tile's window
+// loaded into registers while this one is marked.  Thread g holds window group g (16 consecutive
+// keys) in registers; the marks live in LDS as one 16-bit word per group.  A tile with more than
+// kNsDense descents of its own is not nearly sorted: it turns the path off (ctl[3]) and every
+// workgroup stops after its current tile (random input is read for about one tile per workgroup).
+// No same-address atomics per tile: the counts go to tcnt, k_ns_decide adds them.
+constexpr uint32_t kNsDense = 256;
+template <int L>
+__global__ __launch_bounds__(256) void k_ns_mark(const uint32_t* __restrict__ keys, uint32_t n, uint32_t fmask,
+                                                 uint32_t* __restrict__ bitmap, uint32_t* __restrict__ tcnt,
+                                                 uint32_t* __restrict__ tbnd, uint32_t* ctl) {
+    constexpr uint32_t G = 16, NG = kNsWin / G, W = kNsWin, HALO = kNsHalo;
+    constexpr uint32_t NWD = kNsTile / 32;
+    constexpr uint32_t ESZ = L == LAYOUT_AOS ? 8u : 4u;
+    static_assert(NG == 256 && NWD <= 256, "one group per thread");
+    __shared__ __attribute__((aligned(16))) uint32_t s_k[W + 4];   // the window's masked keys (+ a pad group read past the end)
+    __shared__ uint32_t s_mw[NG + 1];      // marks: bit j of word g = window position 16 g + j
+    __shared__ uint32_t s_desc[4], s_cnt[4];
+    __shared__ uint32_t s_first, s_last, s_stop;
+    const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+    const uint32_t ntiles = (n + kNsTile - 1) / kNsTile;
+    if (tid == 0) {
+        s_mw[NG] = 0u;
+        s_k[W] = 0u;
+    }
+    // window group `tid` of tile t into r (zeros outside the array)
+    auto load = [&](uint32_t t, uint32_t (&r)[G]) {
+        const int64_t w0 = (int64_t)t * kNsTile - (int64_t)HALO;
+        const int64_t lo = w0 > 0 ? w0 : 0, hi = w0 + W < (int64_t)n ? w0 + W : (int64_t)n;
+        const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(keys + (L == LAYOUT_AOS ? 2 : 1) * lo), (short)0, (int)((hi - lo) * ESZ), 0x00020000);
+        // (tile 0: the window starts HALO keys before the array; those offsets wrap past the range)
+        uint32_t off = (uint32_t)((int64_t)tid * G + (w0 - lo)) * ESZ;
+        asm volatile("" : "+v"(off));
+#pragma unroll
+        for (uint32_t j = 0; j < G; ++j)
+            r[j] = __builtin_amdgcn_raw_buffer_load_b32(rk, (int)(off + j * ESZ), 0, 0) & fmask;
+    };
+    uint32_t k[G], kn[G];
+    uint32_t t = blockIdx.x;
+    if (t < ntiles) load(t, k);
+    for (; t < ntiles; t += gridDim.x) {
+        const uint64_t t0 = (uint64_t)t * kNsTile;
+        const uint32_t nown = (uint32_t)((t0 + kNsTile < n ? t0 + kNsTile : (uint64_t)n) - t0);
+        const int64_t w0 = (int64_t)t0 - (int64_t)HALO;
+        // window index i is array position w0 + i; pairs (i, i + 1) count when both are in the array
+        const int64_t pg = w0 + (int64_t)tid * G;    // this group's first position
+#pragma unroll
+        for (uint32_t j = 0; j < G; j += 4)
+            *reinterpret_cast<uint4*>(&s_k[tid * G + j]) = make_uint4(k[j], k[j + 1], k[j + 2], k[j + 3]);
+        if (tid == 0) {
+            s_first = 0xFFFFFFFFu;
+            s_last = 0u;
+        }
+        if (t + gridDim.x < ntiles) load(t + gridDim.x, kn);   // the next tile's window, in flight
+        __syncthreads();
+        // descents of this group's 16 pairs (pair 15: with the next group's first key)
+        const uint32_t nx = s_k[tid * G + G];
+        uint32_t d = 0;
+#pragma unroll
+        for (uint32_t j = 0; j + 1 < G; ++j) d |= (k[j] > k[j + 1] ? 1u : 0u) << j;
+        d |= (tid + 1 < NG && k[G - 1] > nx ? 1u : 0u) << (G - 1);
+        // pairs with both positions in [0, n)
+        const int64_t jlo = -pg, jhi = (int64_t)n - 1 - pg;   // valid j: jlo <= j < jhi
+        uint32_t vmask = 0xFFFFu;
+        if (jlo > 0) vmask &= jlo >= (int64_t)G ? 0u : (0xFFFFu << jlo) & 0xFFFFu;
+        if (jhi < (int64_t)G) vmask &= jhi <= 0 ? 0u : (1u << jhi) - 1u;
+        d &= vmask;
+        // the previous group's pair 15 marks this group's position 0
+        const bool pd = tid > 0 && pg - 1 >= 0 && pg < (int64_t)n && s_k[tid * G - 1] > k[0];
+        const uint32_t m = (d | (d << 1) | (pd ? 1u : 0u)) & 0xFFFFu;
+        s_mw[tid] = m;
+        // this tile's own descents (pair's first position owned)
+        const int64_t olo = (int64_t)HALO - (int64_t)tid * G, ohi = olo + nown;   // owned j: olo <= j < ohi
+        uint32_t omask = 0xFFFFu;
+        if (olo > 0) omask &= olo >= (int64_t)G ? 0u : (0xFFFFu << olo) & 0xFFFFu;
+        if (ohi < (int64_t)G) omask &= ohi <= 0 ? 0u : (1u << ohi) - 1u;
+        const uint32_t own = wave_sum((uint32_t)__popc(d & omask));
+        if (lane == 0) s_desc[w] = own;
+        const int any = __syncthreads_or(m != 0u);
+        if (s_desc[0] + s_desc[1] + s_desc[2] + s_desc[3] > kNsDense) {   // (uniform)
+            if (tid == 0) __hip_atomic_store(ctl + 3, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+        }
+        bool fail = false;   // (thread 0's)
+        if (any) {
+            // rounds: the last unmarked element before every marked run against the first after it
+            for (uint32_t round = 0;; ++round) {
+                const uint32_t mm = s_mw[tid], m1 = s_mw[tid + 1];
+                const uint32_t ext = mm | ((m1 & 1u) << G);
+                uint32_t starts = ~ext & (ext >> 1) & 0xFFFFu;   // i unmarked, i + 1 marked
+                bool changed = false;
+                while (starts) {
+                    const uint32_t i = (uint32_t)__builtin_ctz(starts);
+                    starts &= starts - 1u;
+                    if (pg + i < 0) continue;              // (before the array: no predecessor)
+                    uint32_t jj = W;                       // first unmarked after the run
+                    const uint32_t rest = ~mm & (0xFFFFu << (i + 1u)) & 0xFFFFu;
+                    if (rest) {
+                        jj = tid * G + (uint32_t)__builtin_ctz(rest);
+                    } else {
+                        for (uint32_t q = tid + 1; q < NG; ++q) {
+                            const uint32_t uq = ~s_mw[q] & 0xFFFFu;
+                            if (uq) {
+                                jj = q * G + (uint32_t)__builtin_ctz(uq);
+                                break;
+                            }
+                        }
+                    }
+                    // the run reaches the array's end, or the window's: its successor is the next
+                    // tile's first remainder element (k_ns_decide checks that pair)
+                    if (jj >= W || w0 + (int64_t)jj >= (int64_t)n) continue;
+                    const uint32_t ii = tid * G + i;
+                    if (s_k[ii] > s_k[jj]) {
+                        atomicOr(&s_mw[tid], 1u << i);
+                        atomicOr(&s_mw[jj / G], 1u << (jj % G));
+                        changed = true;
+                    }
+                }
+                if (!__syncthreads_or(changed ? 1 : 0)) break;
+                if (round + 1 == kNsIter) {   // not settled: give up
+                    fail = true;
+                    break;
+                }
+            }
+        }
+        // owned marks: bitmap word q (threads q < 124) = window groups 4 + 2q and 5 + 2q; count;
+        // first / last unmarked owned position
+        uint32_t cnt = 0;
+        if (tid < NWD && tid * 32u < nown) {
+            const uint32_t hg = HALO / G;
+            uint32_t wd = s_mw[hg + 2 * tid] | (s_mw[hg + 2 * tid + 1] << G);
+            const uint32_t valid = nown - tid * 32u >= 32u ? 0xFFFFFFFFu : (1u << (nown - tid * 32u)) - 1u;
+            wd &= valid;
+            bitmap[(t0 >> 5) + tid] = wd;
+            cnt = (uint32_t)__popc(wd);
+            const uint32_t un = ~wd & valid;
+            if (un) {
+                atomicMin(&s_first, tid * 32u + (uint32_t)__builtin_ctz(un));
+                atomicMax(&s_last, tid * 32u + 31u - (uint32_t)__builtin_clz(un));
+            }
+        }
+        cnt = wave_sum(cnt);
+        if (lane == 0) s_cnt[w] = cnt;
+        __syncthreads();
+        if (tid == 0) {
+            tcnt[t] = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
+            uint32_t f = s_first, l = s_last;
+            if (f == 0xFFFFFFFFu) {   // no remainder element: no boundary keys
+                fail = true;
+                f = l = 0u;
+            }
+            tbnd[2 * t] = s_k[HALO + f];
+            tbnd[2 * t + 1] = s_k[HALO + l];
+            if (fail) atomicOr(ctl + 1, 1u);
+            s_stop = __hip_atomic_load(ctl + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __syncthreads();   // (also: every reader of this tile's s_k / s_mw is done)
+        if (s_stop) break;
+#pragma unroll
+        for (uint32_t j = 0; j < G; ++j) k[j] = kn[j];
+    }
+}
+
+// The path's decision, in two launches.  k_ns_decide_a (one 1024-thread workgroup per 1024 tiles):
+// the tiles' offsets into the extraction relative to their chunk (toff) and the chunk totals (csum);
+// an inversion between two tiles' remainders (the last remainder key of a tile against the first of
+// the next) sets ctl[2].  k_ns_decide_b (one workgroup): the chunks' offsets (coff) and the decision
+// - on iff no tile failed (ctl[1]), none was dense (ctl[3]), the remainder is in order across every
+// tile boundary (ctl[2]) and 0 < marked <= cap.  On: m = ctl[4], every gate word 1.  Off: gate
+// words 0 (the radix path runs as without this path).  A tile's offset: ns_toff().
+__global__ __launch_bounds__(1024) void k_ns_decide_a(const uint32_t* __restrict__ tcnt,
+                                                      const uint32_t* __restrict__ tbnd, uint32_t ntiles,
+                                                      uint32_t* __restrict__ toff, uint32_t* __restrict__ csum,
+                                                      uint32_t* ctl) {
+    __shared__ uint32_t s_scratch[16];
+    if (ctl[1] || ctl[3]) return;   // (uniform: the path is off)
+    const uint32_t t = blockIdx.x * 1024u + threadIdx.x;
+    const uint32_t c = t < ntiles ? tcnt[t] : 0u;
+    const bool bad = t + 1 < ntiles && tbnd[2 * t + 1] > tbnd[2 * t + 2];
+    uint32_t tot;
+    const uint32_t ex = block_excl_scan_n<16>(c, s_scratch, tot);
+    if (t < ntiles) toff[t] = ex;
+    if (threadIdx.x == 0) csum[blockIdx.x] = tot;
+    if (__syncthreads_or(bad ? 1 : 0) && threadIdx.x == 0) atomicOr(ctl + 2, 1u);
+}
+
+__global__ __launch_bounds__(1024) void k_ns_decide_b(const uint32_t* __restrict__ csum, uint32_t ntiles,
+                                                      uint32_t cap, uint32_t* __restrict__ toff,
+                                                      uint32_t* __restrict__ coff, uint32_t* ctl) {
+    __shared__ uint32_t s_scratch[16];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t nch = (ntiles + 1023u) / 1024u;   // <= 1024 (n < 2^32)
+    bool on = !ctl[1] && !ctl[2] && !ctl[3];         // (uniform)
+    uint32_t total = 0;
+    if (on) {
+        const uint32_t ex = block_excl_scan_n<16>(tid < nch ? csum[tid] : 0u, s_scratch, total);
+        if (tid <= nch) coff[tid] = ex;
+        on = total != 0u && total <= cap;           // sorted already, or too many marked
+        // toff[ntiles] such that ns_toff(ntiles) = m
+        __syncthreads();
+        if (tid == 0) toff[ntiles] = total - coff[ntiles >> 10];
+    }
+    if (tid == 0) ctl[4] = on ? total : 0u;
+    if (tid < 16u) ctl[kNsGate + tid] = on ? 1u : 0u;
+}
+
+// Tile t's offset into the extraction (the marked elements of tiles before it); t == ntiles: m.
+__device__ __forceinline__ uint32_t ns_toff(const uint32_t* toff, const uint32_t* coff, uint32_t t) {
+    return coff[t >> 10] + toff[t];
+}
+
+// The marked elements of every tile, in position order, to the extraction: ek = masked key, ei =
+// extraction index (the LSD passes sort (ek, ei) stably), sk / sv / sp = key, value, position in
+// extraction order.  Past m: pads (the largest key, after every real one in a stable sort).  One
+// 128-thread workgroup per tile, a bitmap word per thread.
+template <int L>
+__global__ __launch_bounds__(128) void k_ns_extract(const uint32_t* __restrict__ keys,
+                                                    const uint32_t* __restrict__ vals, uint32_t n,
+                                                    uint32_t fmask, uint32_t cap,
+                                                    const uint32_t* __restrict__ bitmap,
+                                                    const uint32_t* __restrict__ toff,
+                                                    const uint32_t* __restrict__ coff, const uint32_t* ctl,
+                                                    uint32_t* __restrict__ ek, uint32_t* __restrict__ ei,
+                                                    uint32_t* __restrict__ sk, uint32_t* __restrict__ sv,
+                                                    uint32_t* __restrict__ sp) {
+    __shared__ uint32_t s_scratch[2];
+    if (!ctl[kNsGate]) return;
+    const uint32_t tid = threadIdx.x, t = blockIdx.x;
+    const uint32_t m = ctl[4];
+    // pads (grid-stride over the extraction's tail)
+    for (uint64_t e = (uint64_t)m + (uint64_t)t * 128u + tid; e < cap; e += (uint64_t)gridDim.x * 128u) {
+        ek[e] = 0xFFFFFFFFu;
+        ei[e] = (uint32_t)e;
+    }
+    const uint64_t t0 = (uint64_t)t * kNsTile;
+    const uint32_t nown = (uint32_t)((t0 + kNsTile < n ? t0 + kNsTile : n) - t0);
+    const uint32_t nwords = (nown + 31u) / 32u;   // <= 124
+    uint32_t bits = tid < nwords ? bitmap[(t0 >> 5) + tid] : 0u;
+    uint32_t total;
+    uint32_t e = ns_toff(toff, coff, t) + block_excl_scan_n<2>((uint32_t)__popc(bits), s_scratch, total);
+    while (bits) {
+        const uint32_t b = (uint32_t)__builtin_ctz(bits);
+        bits &= bits - 1u;
+        const uint64_t p = t0 + tid * 32u + b;
+        const uint32_t key = ns_key<L>(keys, p);
+        ek[e] = key & fmask;
+        ei[e] = e;
+        sk[e] = key;
+        sv[e] = L == LAYOUT_KEYS ? 0u : (L == LAYOUT_AOS ? keys[2 * p + 1] : vals[p]);
+        sp[e] = (uint32_t)p;
+        ++e;
+    }
+}
+
+// (masked key, position) order
+__device__ __forceinline__ bool ns_less(uint32_t ka, uint32_t pa, uint32_t kb, uint32_t pb) {
+    return ka < kb || (ka == kb && pa < pb);
+}
+
+// Threads j < m: the sorted extraction's positions (bp, gathered through the extraction index; the
+// sorted masked keys bm are the sorted ek itself).
+__global__ __launch_bounds__(256) void k_ns_gather(const uint32_t* __restrict__ ei, const uint32_t* __restrict__ sp,
+                                                   const uint32_t* ctl, uint32_t* __restrict__ bp) {
+    if (!ctl[kNsGate]) return;
+    const uint32_t m = ctl[4];
+    for (uint32_t j = blockIdx.x * 256u + threadIdx.x; j < m; j += gridDim.x * 256u) bp[j] = sp[ei[j]];
+}
+
+// Threads t <= ntiles: blo[t] = the extracted elements ordered before tile t's first remainder
+// element: those before the last remainder element ahead of the tile (bit-scanned back, searched
+// in the sorted extraction); blo[0] = 0, blo[ntiles] = m.
+template <int L>
+__global__ __launch_bounds__(256) void k_ns_bounds(const uint32_t* __restrict__ keys, uint32_t n, uint32_t fmask,
+                                                   const uint32_t* __restrict__ bitmap, uint32_t ntiles,
+                                                   const uint32_t* __restrict__ bm, const uint32_t* __restrict__ bp,
+                                                   const uint32_t* ctl, uint32_t* __restrict__ blo) {
+    if (!ctl[kNsGate]) return;
+    const uint32_t t = blockIdx.x * 256u + threadIdx.x;
+    if (t > ntiles) return;
+    const uint32_t m = ctl[4];
+    if (t == 0) { blo[0] = 0u; return; }
+    if (t == ntiles) { blo[ntiles] = m; return; }
+    // the last unmarked position q < t0 (k_ns_mark failed the path when a whole tile is marked, so
+    // the previous tile holds one)
+    uint64_t q = (uint64_t)t * kNsTile - 1u;
+    while ((bitmap[q >> 5] >> (q & 31u)) & 1u) --q;
+    const uint32_t kq = ns_key<L>(keys, q) & fmask;
+    // count of extracted elements (bm, bp) < (kq, q)
+    uint32_t lo = 0, hi = m;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (ns_less(bm[mid], bp[mid], kq, (uint32_t)q)) lo = mid + 1;
+        else hi = mid;
+    }
+    blo[t] = lo;
+}
+
+// Tile t's output range [olo, ohi): the merge writes the tile's remainder elements and the
+// extracted elements [blo[t], blo[t + 1]) there (the ranges of all tiles partition [0, n)).
+__device__ __forceinline__ void ns_out_range(const uint32_t* toff, const uint32_t* coff, const uint32_t* blo,
+                                             uint32_t t, uint32_t ntiles, uint32_t n, int64_t& olo, int64_t& ohi) {
+    const int64_t t0 = (int64_t)t * kNsTile;
+    const int64_t t1 = t + 1 < ntiles ? t0 + kNsTile : (int64_t)n;
+    olo = t0 - (int64_t)ns_toff(toff, coff, t) + blo[t];
+    ohi = t1 - (int64_t)ns_toff(toff, coff, t + 1) + blo[t + 1];
+}
+
+// The merge runs in place: a tile reads the positions of its own output range straight from the
+// caller's arrays (nobody else writes them, and it writes them only after its reads); every other
+// position of its input - the part another tile's output covers - is saved first, here, to the same
+// position of the plan buffer tmp (records; keys only: keys).  One workgroup per tile.
+template <int L>
+__global__ __launch_bounds__(256) void k_ns_save(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals,
+                                                 uint32_t n, const uint32_t* __restrict__ toff,
+                                                 const uint32_t* __restrict__ coff, const uint32_t* __restrict__ blo,
+                                                 const uint32_t* ctl, uint32_t* __restrict__ tmp) {
+    if (!ctl[kNsGate]) return;
+    const uint32_t t = blockIdx.x, tid = threadIdx.x;
+    const uint32_t ntiles = (n + kNsTile - 1) / kNsTile;
+    const int64_t t0 = (int64_t)t * kNsTile;
+    const int64_t t1 = t + 1 < ntiles ? t0 + kNsTile : (int64_t)n;
+    int64_t olo, ohi;
+    ns_out_range(toff, coff, blo, t, ntiles, n, olo, ohi);
+    const int64_t a1 = olo < t1 ? olo : t1;    // [t0, a1) and [b0, t1): outside the own range
+    const int64_t b0 = ohi > t0 ? ohi : t0;
+    auto save = [&](int64_t lo, int64_t hi) {
+        for (int64_t p = lo + tid; p < hi; p += 256) {
+            if (L == LAYOUT_KEYS) {
+                tmp[p] = keys[p];
+            } else if (L == LAYOUT_AOS) {
+                reinterpret_cast<uint2*>(tmp)[p] = reinterpret_cast<const uint2*>(keys)[p];
+            } else {
+                reinterpret_cast<uint2*>(tmp)[p] = make_uint2(keys[p], vals[p]);
+            }
+        }
+    };
+    save(t0, a1);
+    save(b0 > a1 ? b0 : a1, t1);
+}
+
+// Tile t: its remainder elements (positions [t0, t0 + kNsTile) not in the bitmap) and the
+// extracted elements [blo[t], blo[t + 1]) merged by (masked key, position) - the stable order -
+// into the caller's arrays at the tile's output range (in place, see k_ns_save).  Element e of the
+// tile is thread e % 256's slot e / 256 (coalesced loads; consecutive remainder elements are
+// written by consecutive lanes).
+template <int L>
+__global__ __launch_bounds__(256, 4) void k_ns_merge(uint32_t* keys, uint32_t* vals, uint32_t n, uint32_t fmask,
+                                                     const uint32_t* __restrict__ bitmap,
+                                                     const uint32_t* __restrict__ toff,
+                                                     const uint32_t* __restrict__ coff,
+                                                     const uint32_t* __restrict__ blo,
+                                                     const uint32_t* __restrict__ ei, const uint32_t* __restrict__ bm,
+                                                     const uint32_t* __restrict__ bp, const uint32_t* __restrict__ sk,
+                                                     const uint32_t* __restrict__ sv, const uint32_t* ctl,
+                                                     const uint32_t* __restrict__ tmp) {
+    constexpr uint32_t KPT = (kNsTile + 255) / 256;
+    constexpr uint32_t NWD = kNsTile / 32;
+    __shared__ uint32_t s_ak[kNsTile];        // the tile's remainder, in order: masked keys, positions
+    __shared__ uint32_t s_ap[kNsTile];
+    __shared__ uint32_t s_bk[kNsBChunk];      // a chunk of the tile's extracted elements
+    __shared__ uint32_t s_bp[kNsBChunk];
+    __shared__ uint32_t s_w[NWD], s_wpre[NWD];   // the tile's bitmap words, marks before each word
+    __shared__ uint32_t s_scratch[4];
+    if (!ctl[kNsGate]) return;
+    const uint32_t ntiles = (n + kNsTile - 1) / kNsTile;
+    for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    // (per-slot positions recomputed each tile from an opaque copy of the thread index: hoisted out
+    // of the tile loop they take a register each)
+    uint32_t tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    const uint64_t t0 = (uint64_t)t * kNsTile;
+    const uint32_t nown = (uint32_t)((t0 + kNsTile < n ? t0 + kNsTile : n) - t0);
+    const uint32_t nwd = (nown + 31u) / 32u;
+    uint32_t nmarked;
+    __syncthreads();   // the previous tile's readers of s_ak / s_bk are done
+    {   // bitmap words and their exclusive popcount prefix (threads 0 .. 123)
+        const uint32_t wv = tid < nwd ? bitmap[(t0 >> 5) + tid] : 0u;
+        const uint32_t pre = block_excl_scan_n<4>((uint32_t)__popc(wv), s_scratch, nmarked);
+        if (tid < NWD) { s_w[tid] = wv; s_wpre[tid] = pre; }
+    }
+    __syncthreads();
+    const uint32_t natot = nown - nmarked;
+    int64_t olo, ohi;
+    ns_out_range(toff, coff, blo, t, ntiles, n, olo, ohi);
+    const uint32_t b0 = blo[t], b1 = blo[t + 1];
+    const bool hasb = b1 > b0;   // (most tiles: no extracted element falls among theirs)
+    // the positions [alo, ahi) of the tile (relative) lie in its own output range: read in place;
+    // the rest from tmp, where k_ns_save put them.  Buffer loads over the tile: one offset register,
+    // slot offsets immediate, zeros past the end.
+    const uint32_t alo = (uint32_t)(olo - (int64_t)t0 < 0 ? 0 : (olo - (int64_t)t0 > nown ? nown : olo - (int64_t)t0));
+    const uint32_t ahi = (uint32_t)(ohi - (int64_t)t0 < 0 ? 0 : (ohi - (int64_t)t0 > nown ? nown : ohi - (int64_t)t0));
+    constexpr uint32_t ESZ = L == LAYOUT_AOS ? 8u : 4u;
+    constexpr uint32_t TSZ = L == LAYOUT_KEYS ? 4u : 8u;   // tmp: keys, or records
+    uint32_t lo = tid * 4u;
+    asm volatile("" : "+v"(lo));
+    const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(keys + (L == LAYOUT_AOS ? 2ull : 1ull) * t0), (short)0, (int)(nown * ESZ), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(L == LAYOUT_SOA ? vals + t0 : keys), (short)0, (int)(nown * 4u), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rt = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(tmp + (TSZ / 4u) * t0), (short)0, (int)(nown * TSZ), 0x00020000);
+    uint32_t fk[KPT], fv[KPT], ao[KPT];
+    uint32_t valid = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < KPT; ++j) {
+        const uint32_t i = j * 256u + tid;
+        if (i >= alo && i < ahi) {
+            if constexpr (L == LAYOUT_AOS) {
+                const auto q = __builtin_amdgcn_raw_buffer_load_b64(rk, (int)(2u * lo + j * 256u * 8u), 0, 0);
+                fk[j] = q[0];
+                fv[j] = q[1];
+            } else {
+                fk[j] = __builtin_amdgcn_raw_buffer_load_b32(rk, (int)(lo + j * 1024u), 0, 0);
+                fv[j] = L == LAYOUT_SOA ? __builtin_amdgcn_raw_buffer_load_b32(rv, (int)(lo + j * 1024u), 0, 0) : 0u;
+            }
+        } else {
+            if constexpr (L == LAYOUT_KEYS) {
+                fk[j] = __builtin_amdgcn_raw_buffer_load_b32(rt, (int)(lo + j * 1024u), 0, 0);
+                fv[j] = 0u;
+            } else {
+                const auto q = __builtin_amdgcn_raw_buffer_load_b64(rt, (int)(2u * lo + j * 256u * 8u), 0, 0);
+                fk[j] = q[0];
+                fv[j] = q[1];
+            }
+        }
+    }
+    // every load of the workgroup has landed before any thread writes (in place)
+#pragma unroll
+    for (uint32_t j = 0; j < KPT; ++j) asm volatile("" ::"v"(fk[j]), "v"(fv[j]));
+#pragma unroll
+    for (uint32_t j = 0; j < KPT; ++j) {
+        const uint32_t i = j * 256u + tid;
+        const bool in = i < nown;
+        const uint32_t wv = in ? s_w[i >> 5] : 0xFFFFFFFFu;
+        const bool ok = in && !((wv >> (i & 31u)) & 1u);
+        ao[j] = i - (s_wpre[i >> 5 < NWD ? i >> 5 : NWD - 1] + (uint32_t)__popc(wv & ((1u << (i & 31u)) - 1u)));
+        valid |= ok ? (1u << j) : 0u;
+        if (hasb && ok) {
+            s_ak[ao[j]] = fk[j] & fmask;
+            s_ap[ao[j]] = (uint32_t)t0 + i;
+        }
+    }
+    __syncthreads();
+    const uint32_t obase = (uint32_t)olo;   // = arank0 + b0: the tile's first output position
+    const uint32_t arank0 = obase - b0;
+    for (uint32_t c0 = b0; c0 < b1; c0 += kNsBChunk) {
+        const uint32_t cn = b1 - c0 < kNsBChunk ? b1 - c0 : kNsBChunk;
+        if (c0 != b0) __syncthreads();   // the previous chunk's readers are done
+        for (uint32_t i = tid; i < cn; i += 256) {
+            s_bk[i] = bm[c0 + i];
+            s_bp[i] = bp[c0 + i];
+        }
+        __syncthreads();
+        // the chunk's elements: output = extraction rank + remainder elements of the tile before them
+        for (uint32_t i = tid; i < cn; i += 256) {
+            const uint32_t kb = s_bk[i], pb = s_bp[i];
+            uint32_t l = 0, h = natot;
+            while (l < h) {
+                const uint32_t mid = (l + h) >> 1;
+                if (ns_less(s_ak[mid], s_ap[mid], kb, pb)) l = mid + 1;
+                else h = mid;
+            }
+            const uint32_t o = c0 + i + arank0 + l;
+            const uint32_t e = ei[c0 + i];
+            if (L == LAYOUT_KEYS) {
+                keys[o] = sk[e];
+            } else if (L == LAYOUT_AOS) {
+                reinterpret_cast<uint2*>(keys)[o] = make_uint2(sk[e], sv[e]);
+            } else {
+                keys[o] = sk[e];
+                vals[o] = sv[e];
+            }
+        }
+        // this thread's remainder elements: the chunk's elements before each
+#pragma unroll
+        for (uint32_t j = 0; j < KPT; ++j) {
+            if (!((valid >> j) & 1u)) continue;
+            const uint32_t ka = fk[j] & fmask, pa = (uint32_t)t0 + j * 256u + tid;
+            uint32_t l = 0, h = cn;
+            while (l < h) {
+                const uint32_t mid = (l + h) >> 1;
+                if (ns_less(s_bk[mid], s_bp[mid], ka, pa)) l = mid + 1;
+                else h = mid;
+            }
+            ao[j] += l;
+        }
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < KPT; ++j) {
+        if (!((valid >> j) & 1u)) continue;
+        const uint32_t o = obase + ao[j];
+        if (L == LAYOUT_KEYS) {
+            keys[o] = fk[j];
+        } else if (L == LAYOUT_AOS) {
+            reinterpret_cast<uint2*>(keys)[o] = make_uint2(fk[j], fv[j]);
+        } else {
+            keys[o] = fk[j];
+            vals[o] = fv[j];
+        }
+    }
+    }
+}
+
+// ctl[5] = 1 when this path sorted (read by k_hist16_in's skip): set by the last kernel of the path.
+__global__ void k_ns_done(uint32_t* ctl) {
+    if (threadIdx.x == 0) ctl[5] = ctl[kNsGate];
+}
+
+}  // namespace rs

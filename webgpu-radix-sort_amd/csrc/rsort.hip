@@ -28,6 +28,7 @@
 #include "../../include/rsort.h"
 #include "rs_internal.h"
 #include "rs_kernels.hpp"
+#include "rs_presorted.hpp"
 
 #define RS_EXPORT extern "C" __attribute__((visibility("default")))
 
@@ -233,7 +234,7 @@ struct KernelTimer {
     void run(int kind, hipStream_t s, F&& launch, const char* label = nullptr) {
         static const char* const names[RS_KERNEL_KINDS] = {"rsort.histogram", "rsort.scan", "rsort.scatter",
                                                            "rsort.check", "rsort.bucket", "rsort.fallback",
-                                                           "rsort.split"};
+                                                           "rsort.split", "rsort.presorted"};
         RoctxRange range(label ? label : names[kind]);
         if (!enabled || !((mask >> kind) & 1u)) { launch(); return; }
         Rec r{kind, get(), get()};
@@ -312,6 +313,10 @@ struct rs_plan {
     bool split_on = true;            // split over-full buckets (rs_plan_debug.split = 0: the LSD fallback)
     bool last_hybrid = false;        // the last sort enqueued the hybrid path (rs_plan_last_path)
     bool last_split = false;         // ... with the bucket split's launches (rs_plan_last_split)
+    uint32_t* ns = nullptr;          // the presorted path's workspace (check_order plans of the hybrid
+    uint32_t ns_cap = 0;             // path; ns_words()): its extraction capacity
+    bool ns_on = true;               // the presorted path where it applies (rs_plan_debug.presorted = 0: off)
+    bool last_ns = false;            // the last sort enqueued the presorted path (rs_plan_last_path)
     bool path_none = false;          // the last sort moved nothing (n <= 1): rs_plan_last_path NONE
     int scatter_kind = RS_KERNEL_SCATTER;   // timer kind of the pass launches being enqueued
     uint32_t* host_err = nullptr;  // host-mapped error word: set by a timed-out look-back wait,
@@ -564,20 +569,22 @@ rs_status run_pass_cfg(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint3
     if constexpr (SR != 1) {
         return fail(RS_ERR_INVALID_ARG, "staging rounds are one-sweep only");
     } else {
-        // the gated LSD fallback of the hybrid MSD path times all its launches as one kind
-        const bool fb = p->scatter_kind == RS_KERNEL_FALLBACK;
-        p->timer.run(fb ? RS_KERNEL_FALLBACK : RS_KERNEL_HISTOGRAM, s, [&] {
+        // the gated LSD fallback of the hybrid MSD path (and the presorted path's sort of its
+        // extraction) times all its launches as one kind
+        const bool fb = p->scatter_kind != RS_KERNEL_SCATTER;
+        const int fk = p->scatter_kind;
+        p->timer.run(fb ? fk : RS_KERNEL_HISTOGRAM, s, [&] {
             launch_histogram<R, TILE>(L, ik, n, shift, mask, ntiles, p->counts, gate, pass, s);
         });
         HIP_TRY(hipGetLastError());
-        p->timer.run(fb ? RS_KERNEL_FALLBACK : RS_KERNEL_SCAN, s, [&] {
+        p->timer.run(fb ? fk : RS_KERNEL_SCAN, s, [&] {
             hipLaunchKernelGGL(rs::k_scan_rows, dim3(1u << R), dim3(rs::kBlock), 0, s, p->counts,
                                ntiles, p->totals, gate, pass);
         });
         HIP_TRY(hipGetLastError());
         // The scatter always stages the tile through LDS (the local shuffle,
         // RadixSortLocalShuffle.ts:94-116): it is what makes the writes coalesced.
-        p->timer.run(fb ? RS_KERNEL_FALLBACK : RS_KERNEL_SCATTER, s, [&] {
+        p->timer.run(fb ? fk : RS_KERNEL_SCATTER, s, [&] {
             if constexpr (KEYS_ONLY)
                 launch_scatter_l<R, BLOCK, KPT, rs::LAYOUT_KEYS>(p->rank_mode, ik, iv, ok, ov, n, shift, mask,
                                                                  ntiles, grid, p->counts, p->totals, gate, pass, s);
@@ -758,6 +765,50 @@ RS_EXPORT const char* rs_status_string(rs_status s) {
 
 RS_EXPORT uint32_t rs_version(void) { return (RSORT_VERSION_MAJOR << 16) | RSORT_VERSION_MINOR; }
 
+// The presorted path's workspace (rs_presorted.hpp): control words, per-tile counts / boundary keys /
+// offsets / bounds, the mark bitmap, and eight arrays of the extraction capacity (masked key and
+// extraction index twice - the ping-pong of its sort - then key, value, position, and the sorted
+// positions).  Sized for min(capacity, kMsdMax) keys: the hybrid path never sorts more.
+struct NsWs {
+    uint32_t *ctl, *tcnt, *tbnd, *toff, *blo, *csum, *coff, *bitmap, *ek, *ei, *ek2, *ei2, *sk, *sv, *sp, *bp;
+};
+uint64_t ns_keys(uint64_t capacity) { return std::min<uint64_t>(capacity, kMsdMax); }
+// extraction capacity for n keys: n / 128 (config 4's n / 1000 transpositions mark ~n / 500), at
+// least 64K, in whole 16K-key tiles of its sort
+uint32_t ns_cap_for(uint64_t n) {
+    return (uint32_t)std::max<uint64_t>(65536u, (n / 128u + 16383u) / 16384u * 16384u);
+}
+NsWs ns_layout(uint32_t* q, uint64_t capacity) {
+    const uint64_t nt = (ns_keys(capacity) + rs::kNsTile - 1) / rs::kNsTile;
+    const uint64_t cap = ns_cap_for(ns_keys(capacity));
+    NsWs w;
+    w.ctl = q;
+    q += rs::kNsCtlWords;
+    w.tcnt = q;
+    q += nt;
+    w.tbnd = q;
+    q += 2 * nt;
+    w.toff = q;
+    q += nt + 1;
+    w.blo = q;
+    q += nt + 1;
+    w.csum = q;                       // per 1024 tiles (k_ns_decide_a / _b)
+    q += nt / 1024 + 1;
+    w.coff = q;
+    q += nt / 1024 + 2;
+    w.bitmap = q;
+    q += nt * (rs::kNsTile / 32);
+    uint32_t** arr[8] = {&w.ek, &w.ei, &w.ek2, &w.ei2, &w.sk, &w.sv, &w.sp, &w.bp};
+    for (uint32_t** a : arr) {
+        *a = q;
+        q += cap;
+    }
+    return w;
+}
+uint64_t ns_words(uint64_t capacity) {
+    return (uint64_t)(ns_layout(nullptr, capacity).bp - (uint32_t*)nullptr) + ns_cap_for(ns_keys(capacity));
+}
+
 RS_EXPORT rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out) {
     if (!desc || !out) return fail(RS_ERR_INVALID_ARG, "rs_plan_create: null argument");
     *out = nullptr;
@@ -879,6 +930,11 @@ RS_EXPORT rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out) {
             return cleanup(fail(e == hipErrorOutOfMemory ? RS_ERR_OUT_OF_MEMORY : RS_ERR_HIP,
                                 "rs_plan_create: hipMalloc failed: %s", hipGetErrorString(e)));
     }
+    // check_order (sorts of >= kMsdMin keys): the presorted path's workspace
+    if (sorts && p->check_order && d.count >= kMsdMin &&
+        (e = alloc(&p->ns, 4ull * ns_words(d.count))) != hipSuccess)
+        return cleanup(fail(e == hipErrorOutOfMemory ? RS_ERR_OUT_OF_MEMORY : RS_ERR_HIP,
+                            "rs_plan_create: hipMalloc failed: %s", hipGetErrorString(e)));
     p->tickets = p->ptot + rs::kTotalsMax;   // [16] tickets, [16] error word
 
     if ((e = hipHostMalloc((void**)&p->host_err, 4, hipHostMallocMapped)) != hipSuccess ||
@@ -907,6 +963,7 @@ RS_EXPORT void rs_plan_destroy(rs_plan* p) {
     (void)hipFree(p->status);
     (void)hipFree(p->msd);
     (void)hipFree(p->split);
+    (void)hipFree(p->ns);
     if (p->host_err) (void)hipHostFree(p->host_err);
     if (p->done) (void)hipEventDestroy(p->done);
     delete p;
@@ -1015,6 +1072,86 @@ static rs_status enqueue_split(rs_plan* p, const rs::SplitWs& sw, bool keys, boo
     return RS_OK;
 }
 
+// The presorted path (rs_presorted.hpp) of a check_order sort, in place on the caller's data (uk /
+// uv: arrays, keys, or records in uk): mark -> decide -> extract -> the extraction's sort (four 8-bit
+// LSD passes of the histogram path, gated on the device) -> bounds -> save -> merge in place.  Every
+// launch after k_ns_decide_b exits at once unless the device found the input nearly sorted;
+// k_ns_done then makes the radix path's order check find the data in order (the hybrid path's
+// histogram read is skipped outright: k_hist16_in's `skip`).
+static rs_status enqueue_presorted(rs_plan* p, uint32_t* uk, uint32_t* uv, uint32_t n, hipStream_t s) {
+    constexpr int K = rs::LAYOUT_KEYS, S = rs::LAYOUT_SOA, A = rs::LAYOUT_AOS;
+    const NsWs w = ns_layout(p->ns, p->capacity);
+    const uint32_t cap = ns_cap_for(n);
+    if (n > ns_keys(p->capacity) || cap > ns_cap_for(ns_keys(p->capacity)))
+        return fail(RS_ERR_INVALID_ARG, "internal: %u keys exceed the presorted workspace", n);
+    const uint32_t ntiles = (n + rs::kNsTile - 1) / rs::kNsTile;
+    const uint32_t fm = full_mask(p->bit_count);
+    const int L = p->layout;
+    const uint32_t* gate = w.ctl + rs::kNsGate;
+    p->last_ns = true;
+    HIP_TRY(hipMemsetAsync(w.ctl, 0, 4 * rs::kNsCtlWords, s));
+    // persistent grids: as many workgroups as are resident, tiles taken in order
+    auto resident = [&](auto kern, uint32_t units) {
+        static const uint32_t per_cu = resident_per_cu(kern, 256);
+        return std::max(1u, std::min<uint32_t>(units, p->cus * per_cu));
+    };
+    p->timer.run(RS_KERNEL_PRESORTED, s, [&] {
+        auto mark = [&](auto kern) {
+            hipLaunchKernelGGL(kern, dim3(resident(kern, ntiles)), dim3(256), 0, s, (const uint32_t*)uk, n, fm,
+                               w.bitmap, w.tcnt, w.tbnd, w.ctl);
+        };
+        L == A ? mark(rs::k_ns_mark<A>) : mark(rs::k_ns_mark<S>);   // (keys only reads as SOA)
+        hipLaunchKernelGGL(rs::k_ns_decide_a, dim3((ntiles + 1023u) / 1024u), dim3(1024), 0, s,
+                           (const uint32_t*)w.tcnt, (const uint32_t*)w.tbnd, ntiles, w.toff, w.csum, w.ctl);
+        hipLaunchKernelGGL(rs::k_ns_decide_b, dim3(1), dim3(1024), 0, s, (const uint32_t*)w.csum, ntiles, cap, w.toff,
+                           w.coff, w.ctl);
+        auto extract = [&](auto kern) {
+            hipLaunchKernelGGL(kern, dim3(ntiles), dim3(128), 0, s, (const uint32_t*)uk, (const uint32_t*)uv, n, fm,
+                               cap, (const uint32_t*)w.bitmap, (const uint32_t*)w.toff, (const uint32_t*)w.coff,
+                               (const uint32_t*)w.ctl, w.ek, w.ei, w.sk, w.sv, w.sp);
+        };
+        L == A ? extract(rs::k_ns_extract<A>) : L == S ? extract(rs::k_ns_extract<S>) : extract(rs::k_ns_extract<K>);
+    }, "rsort.presorted.mark");
+    HIP_TRY(hipGetLastError());
+    // the extraction (masked key, extraction index) sorted stably: ek / ei -> ek2 / ei2 -> ... -> ek / ei
+    p->scatter_kind = RS_KERNEL_PRESORTED;
+    rs_status st = RS_OK;
+    for (uint32_t i = 0; i < 4 && st == RS_OK; ++i) {
+        const bool odd = i & 1u;
+        st = run_pass(p, odd ? w.ek2 : w.ek, odd ? w.ei2 : w.ei, odd ? w.ek : w.ek2, odd ? w.ei : w.ei2, cap, 8 * i, 8,
+                      layout_pair(S, S), gate, (int)i, s, /*onesweep=*/false);
+    }
+    p->scatter_kind = RS_KERNEL_SCATTER;
+    if (st != RS_OK) return st;
+    p->timer.run(RS_KERNEL_PRESORTED, s, [&] {
+        hipLaunchKernelGGL(rs::k_ns_gather, dim3(std::min<uint32_t>(cap / 256u, 4u * p->cus)), dim3(256), 0, s,
+                           (const uint32_t*)w.ei, (const uint32_t*)w.sp, (const uint32_t*)w.ctl, w.bp);
+        auto bounds = [&](auto kern) {
+            hipLaunchKernelGGL(kern, dim3((ntiles + 1u + 255u) / 256u), dim3(256), 0, s, (const uint32_t*)uk, n, fm,
+                               (const uint32_t*)w.bitmap, ntiles, (const uint32_t*)w.ek, (const uint32_t*)w.bp,
+                               (const uint32_t*)w.ctl, w.blo);
+        };
+        L == A ? bounds(rs::k_ns_bounds<A>) : bounds(rs::k_ns_bounds<S>);
+        auto save = [&](auto kern) {
+            hipLaunchKernelGGL(kern, dim3(ntiles), dim3(256), 0, s, (const uint32_t*)uk, (const uint32_t*)uv, n,
+                               (const uint32_t*)w.toff, (const uint32_t*)w.coff, (const uint32_t*)w.blo,
+                               (const uint32_t*)w.ctl, p->tmp_k);
+        };
+        L == A ? save(rs::k_ns_save<A>) : L == S ? save(rs::k_ns_save<S>) : save(rs::k_ns_save<K>);
+        auto merge = [&](auto kern) {
+            hipLaunchKernelGGL(kern, dim3(resident(kern, ntiles)), dim3(256), 0, s, uk, uv, n, fm,
+                               (const uint32_t*)w.bitmap, (const uint32_t*)w.toff, (const uint32_t*)w.coff,
+                               (const uint32_t*)w.blo, (const uint32_t*)w.ei, (const uint32_t*)w.ek,
+                               (const uint32_t*)w.bp, (const uint32_t*)w.sk, (const uint32_t*)w.sv,
+                               (const uint32_t*)w.ctl, (const uint32_t*)p->tmp_k);
+        };
+        L == A ? merge(rs::k_ns_merge<A>) : L == S ? merge(rs::k_ns_merge<S>) : merge(rs::k_ns_merge<K>);
+        hipLaunchKernelGGL(rs::k_ns_done, dim3(1), dim3(64), 0, s, w.ctl);
+    }, "rsort.presorted.merge");
+    HIP_TRY(hipGetLastError());
+    return RS_OK;
+}
+
 // The hybrid MSD path (rs_kernels.hpp, "hybrid MSD path"): the 16-bit bucket histogram of the
 // input and the device's choice first, then top-byte pass -> segmented next-byte pass -> in-LDS
 // bucket sort; the LSD passes on the input enqueued behind, gated the other way (skewed keys).
@@ -1108,6 +1245,7 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
         return fail(RS_ERR_INVALID_ARG, "internal: %u segmented tiles exceed the plan's %llu status words",
                     ntiles + 257, (unsigned long long)p->status_words);
     p->last_hybrid = true;
+    p->last_ns = false;
     // the pass totals, tickets and error word are zeroed by k_hist16_reduce (nothing reads them before)
     // 16-bit buckets: a tile sized to the mean bucket + 4 sigma of a uniform population takes
     // every bucket that fits it (at 2^28 keys: 4352 records, ~2 buckets over it), the large tile
@@ -1164,6 +1302,13 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
         return fail(RS_ERR_CAPACITY, "%llu keys over %u histogram rows (at most 2^27 keys per row)",
                     (unsigned long long)n, hrows);
     if (chk) HIP_TRY(hipMemsetAsync(p->flags, 0, 16 * 4, s));
+    // check_order: the presorted path first (nearly-sorted input is sorted there; the histogram
+    // read is then skipped and finds nothing to do)
+    const uint32_t* ns_skip = nullptr;
+    if (chk && p->ns && p->ns_on) {
+        if (rs_status st = enqueue_presorted(p, uk, uv, n32, s)) return st;
+        ns_skip = p->ns + 5;
+    }
     p->timer.run(RS_KERNEL_HISTOGRAM, s, [&] {
         if (region) {   // the senders counted: one row, their table
             hipLaunchKernelGGL(rs::k_region_rows, dim3(256), dim3(256), 0, s, region_hist, p->tmp_k, over, big,
@@ -1181,7 +1326,7 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
         const bool full = !generic && kbase == 0u && vbits == 32u;
         auto go = [&](auto kern) {
             hipLaunchKernelGGL(kern, dim3(hrows), dim3(1024), 0, s, sk, n32, p->tmp_k, kbase, range, vbits - 16,
-                               over, big, chk ? p->flags : (uint32_t*)nullptr, b0rows, sw.huge);
+                               over, big, chk ? p->flags : (uint32_t*)nullptr, b0rows, sw.huge, ns_skip);
         };
         if (chk && b0rows) {   // check_order: the order check and the fallback's byte-0 totals ride along
             if (in_aos && !narrow && ((uintptr_t)sk & 15u) == 0) go(rs::k_hist16_in<A, true, true, 2>);
@@ -1203,7 +1348,7 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
         hipLaunchKernelGGL(rs::k_hist16_reduce, dim3(256), dim3(1024), 0, s, (const uint32_t*)p->tmp_k,
                            hrows, hist16, top_tot, range_bad, base16, small_cap, kBucketCap, over, big,
                            p->ptot, (uint32_t)(rs::kTotalsMax + kTicketWords), (const uint32_t*)b0rows,
-                           static_p0 ? cbase : (uint32_t*)nullptr, sw.huge, p->smax2);
+                           static_p0 ? cbase : (uint32_t*)nullptr, sw.huge, p->smax2, ns_skip);
     }, region ? "rsort.msd.region_table" : "rsort.msd.hist16");
     HIP_TRY(hipGetLastError());
     p->timer.run(RS_KERNEL_SCAN, s, [&] {
@@ -1466,6 +1611,7 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
 // caller's input is only read, the result lands in uk / uv; check_order not supported).
 static rs_status enqueue_sort(rs_plan* p, uint32_t* uk, uint32_t* uv, uint64_t n, hipStream_t s,
                               const uint32_t* in_k0 = nullptr, const uint32_t* in_v0 = nullptr) {
+    p->last_ns = false;
     if (use_msd(p, n)) {
         const bool aos = p->layout == rs::LAYOUT_AOS;
         return enqueue_sort_msd(p, in_k0 ? in_k0 : uk, aos ? nullptr : (in_k0 ? in_v0 : uv), aos, uk, uv, aos, n, s);
@@ -1474,6 +1620,10 @@ static rs_status enqueue_sort(rs_plan* p, uint32_t* uk, uint32_t* uv, uint64_t n
     const uint32_t n32 = (uint32_t)n;
     const uint32_t* gate = p->check_order ? p->flags : nullptr;
     if (p->check_order) HIP_TRY(hipMemsetAsync(p->flags, 0, 16 * 4, s));
+    // check_order in place: the presorted path first (nearly-sorted input is sorted there, and the
+    // order check before pass 0 then gates every pass off)
+    if (p->check_order && !in_k0 && p->ns && p->ns_on && n >= kMsdMin && n <= ns_keys(p->capacity))
+        if (rs_status st = enqueue_presorted(p, uk, uv, (uint32_t)n, s)) return st;
     const bool onesweep = use_onesweep(p, n);
     if (onesweep) {
         // totals, tickets and the device error word (a timeout never outlives its sort)
@@ -1644,6 +1794,14 @@ RS_EXPORT rs_status rs_plan_last_path(rs_plan* p, uint32_t* path) {
     *path = RS_PATH_NONE;
     if (!p->done_recorded || p->path_none) return RS_OK;
     HIP_TRY(hipEventSynchronize(p->done));
+    if (p->last_ns) {   // the presorted path's done word (ctl[5])
+        uint32_t done = 0u;
+        HIP_TRY(hipMemcpy(&done, p->ns + 5, 4, hipMemcpyDeviceToHost));
+        if (done) {
+            *path = RS_PATH_PRESORTED;
+            return RS_OK;
+        }
+    }
     if (!p->last_hybrid) {
         *path = RS_PATH_LSD;
         return RS_OK;
@@ -1913,7 +2071,8 @@ RS_EXPORT rs_status rs_plan_hist16(rs_plan* p, const void* keys, uint64_t n, voi
         uint32_t* z = p->tmp_k + (size_t)hrows * 65536u;
         auto go = [&](auto kern) {
             hipLaunchKernelGGL(kern, dim3(hrows), dim3(1024), 0, s, (const uint32_t*)keys, (uint32_t)n, p->tmp_k, 0u,
-                               0xFFFFFFFFu, 16u, z, z, (uint32_t*)nullptr, (uint32_t*)nullptr, (uint32_t*)nullptr);
+                               0xFFFFFFFFu, 16u, z, z, (uint32_t*)nullptr, (uint32_t*)nullptr, (uint32_t*)nullptr,
+                               (const uint32_t*)nullptr);
         };
         if (aos && ((uintptr_t)keys & 15u) == 0) go(rs::k_hist16_in<rs::LAYOUT_AOS, true, true>);
         else if (aos) go(rs::k_hist16_in<rs::LAYOUT_AOS, false, true>);
@@ -2016,7 +2175,7 @@ RS_EXPORT rs_status rs_plan_set_debug(rs_plan* p, const rs_plan_debug* d) {
     auto tri = [](int32_t v, int hi) { return v >= -1 && v <= hi; };
     if (!tri(d->rank, 1) || !tri(d->tile, 1) || !tri(d->onesweep, 1) || !tri(d->msd, 1) ||
         !tri(d->keys_cfg, 1) || !tri(d->msd_keys_cfg, 2) || !tri(d->kbucket_wave, 1) ||
-        !tri(d->selftest_fail, 1) || !tri(d->split, 1))
+        !tri(d->selftest_fail, 1) || !tri(d->split, 1) || !tri(d->presorted, 1))
         return fail(RS_ERR_INVALID_ARG, "rs_plan_set_debug: every field must be -1 or a listed choice");
     if (d->selftest_fail == 1) {
         p->selftest = 0;
@@ -2030,6 +2189,7 @@ RS_EXPORT rs_status rs_plan_set_debug(rs_plan* p, const rs_plan_debug* d) {
     if (d->msd_keys_cfg >= 0) p->msd_keys_cfg = d->msd_keys_cfg;
     if (d->kbucket_wave >= 0) p->kbucket_wave = d->kbucket_wave == 1;
     if (d->split >= 0) p->split_on = d->split == 1;
+    if (d->presorted >= 0) p->ns_on = d->presorted == 1;
     return RS_OK;
 }
 

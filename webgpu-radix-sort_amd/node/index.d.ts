@@ -115,7 +115,7 @@ export declare class RadixSortKernel {
   /** Waits for the last sort; throws if a sort failed on the device since the last check. */
   check(): void;
   /** The path the last sort took (waits for it; rs_plan_last_path). */
-  lastPath(): "none" | "lsd" | "hybrid" | "hybrid_fallback" | "in_order";
+  lastPath(): "none" | "lsd" | "hybrid" | "hybrid_fallback" | "in_order" | "presorted";
   /** How deep the last hybrid sort split over-full 16-bit buckets: 0, 2 or 3 (rs_plan_last_split). */
   lastSplit(): 0 | 2 | 3;
   destroy(): void;
@@ -142,7 +142,7 @@ export declare class RadixSortTextureKernel {
   readonly info: PlanInfo;
   dispatch(pass?: ComputePass): void;
   check(): void;
-  lastPath(): "none" | "lsd" | "hybrid" | "hybrid_fallback" | "in_order";
+  lastPath(): "none" | "lsd" | "hybrid" | "hybrid_fallback" | "in_order" | "presorted";
   lastSplit(): 0 | 2 | 3;
   destroy(): void;
 }

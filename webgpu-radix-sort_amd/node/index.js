@@ -335,7 +335,8 @@ class RadixSortKernel {
    * last check (its output is invalid; rs_plan_check). */
   check() { if (this._plan) addon.planCheck(this._plan); }
 
-  /** The path the last sort took (waits for it): "lsd", "hybrid", "hybrid_fallback", "in_order". */
+  /** The path the last sort took (waits for it): "lsd", "hybrid", "hybrid_fallback", "in_order",
+   *  "presorted". */
   lastPath() { return addon.planLastPath(this._plan); }
 
   /** How deep the last hybrid sort split over-full 16-bit buckets (skewed keys): 0, 2 or 3. */

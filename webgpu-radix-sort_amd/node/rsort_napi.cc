@@ -461,7 +461,7 @@ napi_value PlanCheck(napi_env env, napi_callback_info info) {
 }
 
 // planLastPath(plan): the path the plan's last sort took ("none", "lsd", "hybrid",
-// "hybrid_fallback", "in_order"; rs_plan_last_path, waits for it)
+// "hybrid_fallback", "in_order", "presorted"; rs_plan_last_path, waits for it)
 napi_value PlanLastPath(napi_env env, napi_callback_info info) {
     napi_value a[1];
     if (!args(env, info, a)) return nullptr;
@@ -469,7 +469,7 @@ napi_value PlanLastPath(napi_env env, napi_callback_info info) {
     if (!b || !b->plan) return napi_throw_error(env, nullptr, "plan destroyed"), nullptr;
     uint32_t path = 0;
     RS_CALL(env, rs_plan_last_path(b->plan, &path), "lastPath");
-    static const char* const names[] = {"none", "lsd", "hybrid", "hybrid_fallback", "in_order"};
+    static const char* const names[] = {"none", "lsd", "hybrid", "hybrid_fallback", "in_order", "presorted"};
     napi_value v;
     napi_create_string_utf8(env, path < 5 ? names[path] : "unknown", NAPI_AUTO_LENGTH, &v);
     return v;

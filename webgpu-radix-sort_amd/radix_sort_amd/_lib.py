@@ -30,11 +30,11 @@ RS_FLAG_AVOID_BANK_CONFLICTS = 0x8
 RS_FLAG_INTERLEAVED = 0x10
 
 (RS_KERNEL_HISTOGRAM, RS_KERNEL_SCAN, RS_KERNEL_SCATTER, RS_KERNEL_CHECK, RS_KERNEL_BUCKET,
- RS_KERNEL_FALLBACK, RS_KERNEL_SPLIT) = range(7)
-RS_KERNEL_KINDS = 7
-KERNEL_NAMES = ("histogram", "scan", "scatter", "check", "bucket", "fallback", "split")
+ RS_KERNEL_FALLBACK, RS_KERNEL_SPLIT, RS_KERNEL_PRESORTED) = range(8)
+RS_KERNEL_KINDS = 8
+KERNEL_NAMES = ("histogram", "scan", "scatter", "check", "bucket", "fallback", "split", "presorted")
 # rs_plan_last_path
-PATH_NAMES = ("none", "lsd", "hybrid", "hybrid_fallback", "in_order")
+PATH_NAMES = ("none", "lsd", "hybrid", "hybrid_fallback", "in_order", "presorted")
 
 
 class RadixSortError(RuntimeError):
@@ -57,7 +57,7 @@ class PlanDebug(ctypes.Structure):
     _fields_ = [("rank", ctypes.c_int32), ("tile", ctypes.c_int32), ("onesweep", ctypes.c_int32),
                 ("msd", ctypes.c_int32), ("keys_cfg", ctypes.c_int32), ("msd_keys_cfg", ctypes.c_int32),
                 ("kbucket_wave", ctypes.c_int32), ("selftest_fail", ctypes.c_int32),
-                ("split", ctypes.c_int32)]
+                ("split", ctypes.c_int32), ("presorted", ctypes.c_int32)]
 
 
 # Path overrides applied to every plan the Python wrappers create (tests select kernels with

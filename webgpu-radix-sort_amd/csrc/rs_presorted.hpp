@@ -4,34 +4,33 @@
 // order: the reference checks the order between its passes and skips the rest once the data is
 // sorted.  Input that is NEARLY in order - sorted data with a few displaced elements, BASELINE
 // config 4's "nearly sorted" f32 keys - still pays every pass there (and here, on the radix path:
-// 80 B/key for config 4's skewed floats).  This path sorts such input in O(n) traffic instead:
+// 52-80 B/key for config 4's skewed floats).  This path sorts such input in O(n) traffic instead:
 //
 //   1. k_ns_mark: the descents (i, i + 1: key[i] > key[i + 1] under the bit_count mask) mark both
 //      their elements; the unmarked remainder is then re-checked around every marked run (the last
 //      unmarked element before a run against the first after it) and both ends of any inversion
-//      marked, until the remainder is in order.  Tiles of 4096 keys iterate in LDS with a 64-key
-//      halo of context on each side (marks in the halo are the neighbour's business: any marking
-//      whose remainder is in order is a valid one, and a pair of remainder elements in two tiles is
-//      checked by k_ns_decide).  More than 16 rounds, too many descents, or a tile marked whole
-//      sends the sort to the radix path (decided on the device: k_ns_decide).  Workgroups stop
-//      reading once the running descent count exceeds half the extraction capacity (random input
-//      costs a few million keys of reading, not a pass).
-//   2. k_ns_extract: the marked elements, in position order, to side arrays (masked key, extraction
+//      marked, until the remainder is in order.  Tiles of 3968 keys iterate in LDS inside a window
+//      with 64 keys of context on each side (marks in the context are the neighbour's business: any
+//      marking whose remainder is in order is a valid one, and a pair of remainder elements in two
+//      tiles is checked by k_ns_decide).  More than 16 rounds, a tile with more than 256 descents,
+//      or a tile marked whole sends the sort to the radix path.  Output: a mark bitmap, per-tile
+//      mark counts and first / last remainder keys.
+//   2. k_ns_decide: the decision on the device (every later launch is gated on it) and the tiles'
+//      offsets into the extraction.
+//   3. k_ns_extract: the marked elements, in position order, to side arrays (masked key, extraction
 //      index; key, value, position); the rest of the extraction capacity padded with the largest key.
-//   3. the extracted elements sorted by the library's own LSD passes (gated on the device), stably:
-//      equal masked keys keep position order.
-//   4. k_ns_bounds: for every tile of positions, how many extracted elements go before its first
-//      remainder element (binary search in the sorted extraction).
-//   5. k_ns_merge: every tile writes its remainder elements and the extracted elements that fall
-//      among them, merged by (masked key, position) - the stable order - to a plan buffer; the merged
-//      output of a tile is one contiguous range.
-//   6. k_ns_copy: the plan buffer back to the caller's arrays (the merge cannot run in place: its
-//      output of a tile overlaps the input of its neighbours).
+//   4. the extraction sorted stably by (masked key, extraction index): k_ns_totals (every pass's
+//      digit totals) and four 8-bit one-sweep passes (k_onesweep) - equal keys keep position order.
+//   5. k_ns_gather / k_ns_bounds: the sorted positions, and for every tile how many extracted
+//      elements go before its first remainder element (binary search in the sorted extraction).
+//   6. k_ns_save / k_ns_merge: every tile writes its remainder elements and the extracted elements
+//      that fall among them, merged by (masked key, position) - the stable order - to its output
+//      range, in place; the input positions another tile's output covers are saved to the plan
+//      buffer first (a few hundred keys per tile boundary for config 4).
 // The radix path is still enqueued behind and finds the caller's data in order (its own order
-// check on the histogram read: k_msd_plan then gates every pass off); its histogram read is
-// skipped when this path has sorted (k_hist16_in's `skip`).  Result: the stable sort, as on the
-// radix path.  Bytes per key (nearly sorted input): 4 (mark) + 16 (merge) + 16 (copy) + ~0 (the
-// extraction, n / 1000-ish keys) against the radix path's 52-80.
+// check: every pass gated off); the hybrid path skips even its histogram read when this path has
+// sorted (k_hist16_in's `skip`).  Result: the stable sort, as on the radix path.  Bytes per key
+// (config 4): 4 (mark) + 16 (merge) + ~1 (save) + the extraction (~n / 250 keys, sorted).
 #pragma once
 #include "rs_kernels.hpp"
 
@@ -72,7 +71,7 @@ __global__ __launch_bounds__(256) void k_ns_mark(const uint32_t* __restrict__ ke
     __shared__ __attribute__((aligned(16))) uint32_t s_k[W + 4];   // the window's masked keys (+ a pad group read past the end)
     __shared__ uint32_t s_mw[NG + 1];      // marks: bit j of word g = window position 16 g + j
     __shared__ uint32_t s_desc[4], s_cnt[4];
-    __shared__ uint32_t s_first, s_last, s_stop;
+    __shared__ uint32_t s_fw[4], s_lw[4], s_stop;
     const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
     const uint32_t ntiles = (n + kNsTile - 1) / kNsTile;
     if (tid == 0) {
@@ -104,10 +103,10 @@ __global__ __launch_bounds__(256) void k_ns_mark(const uint32_t* __restrict__ ke
 #pragma unroll
         for (uint32_t j = 0; j < G; j += 4)
             *reinterpret_cast<uint4*>(&s_k[tid * G + j]) = make_uint4(k[j], k[j + 1], k[j + 2], k[j + 3]);
-        if (tid == 0) {
-            s_first = 0xFFFFFFFFu;
-            s_last = 0u;
-        }
+        // thread 0: the path-off flag, read now and looked at after this tile (its wait then covers
+        // only this load: it is issued before the next window's)
+        uint32_t stop = 0;
+        if (tid == 0) stop = __hip_atomic_load(ctl + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (t + gridDim.x < ntiles) load(t + gridDim.x, kn);   // the next tile's window, in flight
         __syncthreads();
         // descents of this group's 16 pairs (pair 15: with the next group's first key)
@@ -182,7 +181,7 @@ __global__ __launch_bounds__(256) void k_ns_mark(const uint32_t* __restrict__ ke
         }
         // owned marks: bitmap word q (threads q < 124) = window groups 4 + 2q and 5 + 2q; count;
         // first / last unmarked owned position
-        uint32_t cnt = 0;
+        uint32_t cnt = 0, un = 0;
         if (tid < NWD && tid * 32u < nown) {
             const uint32_t hg = HALO / G;
             uint32_t wd = s_mw[hg + 2 * tid] | (s_mw[hg + 2 * tid + 1] << G);
@@ -190,18 +189,29 @@ __global__ __launch_bounds__(256) void k_ns_mark(const uint32_t* __restrict__ ke
             wd &= valid;
             bitmap[(t0 >> 5) + tid] = wd;
             cnt = (uint32_t)__popc(wd);
-            const uint32_t un = ~wd & valid;
-            if (un) {
-                atomicMin(&s_first, tid * 32u + (uint32_t)__builtin_ctz(un));
-                atomicMax(&s_last, tid * 32u + 31u - (uint32_t)__builtin_clz(un));
-            }
+            un = ~wd & valid;
         }
         cnt = wave_sum(cnt);
-        if (lane == 0) s_cnt[w] = cnt;
+        {   // the wave's first / last unmarked position: its first / last lane with one
+            const uint64_t b = __ballot(un != 0u);
+            const uint32_t fl = tid * 32u + (uint32_t)__builtin_ctz(un | 0x80000000u);
+            const uint32_t ll = tid * 32u + 31u - (uint32_t)__builtin_clz(un | 1u);
+            const uint32_t f = __shfl(fl, b ? (int)__builtin_ctzll(b) : 0, 64);
+            const uint32_t l = __shfl(ll, b ? 63 - (int)__builtin_clzll(b) : 0, 64);
+            if (lane == 0) {
+                s_cnt[w] = cnt;
+                s_fw[w] = b ? f : 0xFFFFFFFFu;
+                s_lw[w] = b ? l : 0xFFFFFFFFu;
+            }
+        }
         __syncthreads();
         if (tid == 0) {
             tcnt[t] = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
-            uint32_t f = s_first, l = s_last;
+            uint32_t f = 0xFFFFFFFFu, l = 0xFFFFFFFFu;
+            for (uint32_t q = 0; q < 4u; ++q) {
+                if (f == 0xFFFFFFFFu) f = s_fw[q];
+                if (s_lw[q] != 0xFFFFFFFFu) l = s_lw[q];
+            }
             if (f == 0xFFFFFFFFu) {   // no remainder element: no boundary keys
                 fail = true;
                 f = l = 0u;
@@ -209,7 +219,7 @@ __global__ __launch_bounds__(256) void k_ns_mark(const uint32_t* __restrict__ ke
             tbnd[2 * t] = s_k[HALO + f];
             tbnd[2 * t + 1] = s_k[HALO + l];
             if (fail) atomicOr(ctl + 1, 1u);
-            s_stop = __hip_atomic_load(ctl + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_stop = stop;
         }
         __syncthreads();   // (also: every reader of this tile's s_k / s_mw is done)
         if (s_stop) break;
@@ -218,44 +228,58 @@ __global__ __launch_bounds__(256) void k_ns_mark(const uint32_t* __restrict__ ke
     }
 }
 
-// The path's decision, in two launches.  k_ns_decide_a (one 1024-thread workgroup per 1024 tiles):
-// the tiles' offsets into the extraction relative to their chunk (toff) and the chunk totals (csum);
-// an inversion between two tiles' remainders (the last remainder key of a tile against the first of
-// the next) sets ctl[2].  k_ns_decide_b (one workgroup): the chunks' offsets (coff) and the decision
-// - on iff no tile failed (ctl[1]), none was dense (ctl[3]), the remainder is in order across every
-// tile boundary (ctl[2]) and 0 < marked <= cap.  On: m = ctl[4], every gate word 1.  Off: gate
-// words 0 (the radix path runs as without this path).  A tile's offset: ns_toff().
-__global__ __launch_bounds__(1024) void k_ns_decide_a(const uint32_t* __restrict__ tcnt,
-                                                      const uint32_t* __restrict__ tbnd, uint32_t ntiles,
-                                                      uint32_t* __restrict__ toff, uint32_t* __restrict__ csum,
-                                                      uint32_t* ctl) {
+// The path's decision: one 1024-thread workgroup per 1024 tiles writes the tiles' offsets into the
+// extraction relative to their chunk (toff) and the chunk total (csum); an inversion between two
+// tiles' remainders (the last remainder key of a tile against the first of the next) sets ctl[2].
+// The last workgroup to finish (arrival count ctl[6]) then scans the chunk totals into coff and
+// decides - on iff no tile failed (ctl[1]), none was dense (ctl[3]), the remainder is in order
+// across every tile boundary (ctl[2]) and 0 < marked <= cap.  On: m = ctl[4], every gate word 1,
+// the extraction sort's digit totals and tickets (sub) zeroed.  Off: gate words 0 (the radix path
+// runs as without this path).  A tile's offset: ns_toff().
+constexpr uint32_t kNsSubWords = 4 * 256 + 32;   // the extraction sort's totals [4][256], tickets, error
+__global__ __launch_bounds__(1024) void k_ns_decide(const uint32_t* __restrict__ tcnt,
+                                                    const uint32_t* __restrict__ tbnd, uint32_t ntiles,
+                                                    uint32_t cap, uint32_t* __restrict__ toff,
+                                                    uint32_t* __restrict__ csum, uint32_t* __restrict__ coff,
+                                                    uint32_t* __restrict__ sub, uint32_t* ctl) {
     __shared__ uint32_t s_scratch[16];
-    if (ctl[1] || ctl[3]) return;   // (uniform: the path is off)
-    const uint32_t t = blockIdx.x * 1024u + threadIdx.x;
-    const uint32_t c = t < ntiles ? tcnt[t] : 0u;
-    const bool bad = t + 1 < ntiles && tbnd[2 * t + 1] > tbnd[2 * t + 2];
-    uint32_t tot;
-    const uint32_t ex = block_excl_scan_n<16>(c, s_scratch, tot);
-    if (t < ntiles) toff[t] = ex;
-    if (threadIdx.x == 0) csum[blockIdx.x] = tot;
-    if (__syncthreads_or(bad ? 1 : 0) && threadIdx.x == 0) atomicOr(ctl + 2, 1u);
-}
-
-__global__ __launch_bounds__(1024) void k_ns_decide_b(const uint32_t* __restrict__ csum, uint32_t ntiles,
-                                                      uint32_t cap, uint32_t* __restrict__ toff,
-                                                      uint32_t* __restrict__ coff, uint32_t* ctl) {
-    __shared__ uint32_t s_scratch[16];
+    __shared__ uint32_t s_last;
     const uint32_t tid = threadIdx.x;
-    const uint32_t nch = (ntiles + 1023u) / 1024u;   // <= 1024 (n < 2^32)
-    bool on = !ctl[1] && !ctl[2] && !ctl[3];         // (uniform)
+    const uint32_t nch = gridDim.x;   // (ntiles + 1023) / 1024 <= 1024 (n < 2^32)
+    bool on = !ctl[1] && !ctl[3];     // (uniform)
+    if (on) {
+        const uint32_t t = blockIdx.x * 1024u + tid;
+        const uint32_t c = t < ntiles ? tcnt[t] : 0u;
+        const bool bad = t + 1 < ntiles && tbnd[2 * t + 1] > tbnd[2 * t + 2];
+        uint32_t tot;
+        const uint32_t ex = block_excl_scan_n<16>(c, s_scratch, tot);
+        if (t < ntiles) toff[t] = ex;
+        const int anybad = __syncthreads_or(bad ? 1 : 0);
+        if (tid == 0) {
+            csum[blockIdx.x] = tot;
+            if (anybad) atomicOr(ctl + 2, 1u);
+            __threadfence();
+            s_last = atomicAdd(ctl + 6, 1u) == nch - 1u ? 1u : 0u;
+        }
+        __syncthreads();
+        if (!s_last) return;
+        __threadfence();
+        on = !__hip_atomic_load(ctl + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else if (blockIdx.x != 0) {
+        return;
+    }
+    // one workgroup from here: the last to arrive, or workgroup 0 when the path is off
     uint32_t total = 0;
     if (on) {
-        const uint32_t ex = block_excl_scan_n<16>(tid < nch ? csum[tid] : 0u, s_scratch, total);
+        const uint32_t ex = block_excl_scan_n<16>(tid < nch ? __hip_atomic_load(csum + tid, __ATOMIC_RELAXED,
+                                                                                  __HIP_MEMORY_SCOPE_AGENT)
+                                                            : 0u,
+                                                  s_scratch, total);
         if (tid <= nch) coff[tid] = ex;
-        on = total != 0u && total <= cap;           // sorted already, or too many marked
-        // toff[ntiles] such that ns_toff(ntiles) = m
+        on = total != 0u && total <= cap;   // sorted already, or too many marked
         __syncthreads();
-        if (tid == 0) toff[ntiles] = total - coff[ntiles >> 10];
+        if (tid == 0) toff[ntiles] = total - coff[ntiles >> 10];   // ns_toff(ntiles) = m
+        for (uint32_t i = tid; i < kNsSubWords; i += 1024) sub[i] = 0u;
     }
     if (tid == 0) ctl[4] = on ? total : 0u;
     if (tid < 16u) ctl[kNsGate + tid] = on ? 1u : 0u;
@@ -314,6 +338,27 @@ __device__ __forceinline__ bool ns_less(uint32_t ka, uint32_t pa, uint32_t kb, u
     return ka < kb || (ka == kb && pa < pb);
 }
 
+// Every pass's digit totals of the extraction sort (sub[256 p + d], they do not depend on the
+// order): the m extracted keys counted in LDS, then the cap - m pads (digit 255 of every pass).
+__global__ __launch_bounds__(256) void k_ns_totals(const uint32_t* __restrict__ ek, uint32_t cap,
+                                                   const uint32_t* ctl, uint32_t* __restrict__ sub) {
+    __shared__ uint32_t h[4 * 256];
+    if (!ctl[kNsGate]) return;
+    const uint32_t m = ctl[4], tid = threadIdx.x;
+    for (uint32_t i = tid; i < 4 * 256; i += 256) h[i] = 0u;
+    __syncthreads();
+    for (uint32_t j = blockIdx.x * 256u + tid; j < m; j += gridDim.x * 256u) {
+        const uint32_t k = ek[j];
+#pragma unroll
+        for (uint32_t p = 0; p < 4; ++p) atomicAdd(&h[256 * p + ((k >> (8 * p)) & 255u)], 1u);
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < 4 * 256; i += 256) {
+        const uint32_t c = h[i] + (blockIdx.x == 0 && (i & 255u) == 255u ? cap - m : 0u);
+        if (c) atomicAdd(&sub[i], c);
+    }
+}
+
 // Threads j < m: the sorted extraction's positions (bp, gathered through the extraction index; the
 // sorted masked keys bm are the sorted ek itself).
 __global__ __launch_bounds__(256) void k_ns_gather(const uint32_t* __restrict__ ei, const uint32_t* __restrict__ sp,
@@ -324,8 +369,9 @@ __global__ __launch_bounds__(256) void k_ns_gather(const uint32_t* __restrict__ 
 }
 
 // Threads t <= ntiles: blo[t] = the extracted elements ordered before tile t's first remainder
-// element: those before the last remainder element ahead of the tile (bit-scanned back, searched
-// in the sorted extraction); blo[0] = 0, blo[ntiles] = m.
+// element - those before the last remainder element ahead of the tile (bit-scanned back; k_ns_mark
+// failed the path when a tile is marked whole, so the previous tile holds one), searched in the
+// sorted extraction (bm, bp); blo[0] = 0, blo[ntiles] = m.
 template <int L>
 __global__ __launch_bounds__(256) void k_ns_bounds(const uint32_t* __restrict__ keys, uint32_t n, uint32_t fmask,
                                                    const uint32_t* __restrict__ bitmap, uint32_t ntiles,
@@ -337,12 +383,9 @@ __global__ __launch_bounds__(256) void k_ns_bounds(const uint32_t* __restrict__ 
     const uint32_t m = ctl[4];
     if (t == 0) { blo[0] = 0u; return; }
     if (t == ntiles) { blo[ntiles] = m; return; }
-    // the last unmarked position q < t0 (k_ns_mark failed the path when a whole tile is marked, so
-    // the previous tile holds one)
     uint64_t q = (uint64_t)t * kNsTile - 1u;
     while ((bitmap[q >> 5] >> (q & 31u)) & 1u) --q;
     const uint32_t kq = ns_key<L>(keys, q) & fmask;
-    // count of extracted elements (bm, bp) < (kq, q)
     uint32_t lo = 0, hi = m;
     while (lo < hi) {
         const uint32_t mid = (lo + hi) >> 1;
@@ -408,7 +451,7 @@ __global__ __launch_bounds__(256, 4) void k_ns_merge(uint32_t* keys, uint32_t* v
                                                      const uint32_t* __restrict__ blo,
                                                      const uint32_t* __restrict__ ei, const uint32_t* __restrict__ bm,
                                                      const uint32_t* __restrict__ bp, const uint32_t* __restrict__ sk,
-                                                     const uint32_t* __restrict__ sv, const uint32_t* ctl,
+                                                     const uint32_t* __restrict__ sv, uint32_t* ctl,
                                                      const uint32_t* __restrict__ tmp) {
     constexpr uint32_t KPT = (kNsTile + 255) / 256;
     constexpr uint32_t NWD = kNsTile / 32;
@@ -416,9 +459,13 @@ __global__ __launch_bounds__(256, 4) void k_ns_merge(uint32_t* keys, uint32_t* v
     __shared__ uint32_t s_ap[kNsTile];
     __shared__ uint32_t s_bk[kNsBChunk];      // a chunk of the tile's extracted elements
     __shared__ uint32_t s_bp[kNsBChunk];
+    __shared__ uint32_t s_be[kNsBChunk];
     __shared__ uint32_t s_w[NWD], s_wpre[NWD];   // the tile's bitmap words, marks before each word
     __shared__ uint32_t s_scratch[4];
     if (!ctl[kNsGate]) return;
+    // the path has sorted once every workgroup is done (read by the radix path's histogram read,
+    // a later launch: k_hist16_in's skip)
+    if (blockIdx.x == 0 && threadIdx.x == 0) ctl[5] = 1u;
     const uint32_t ntiles = (n + kNsTile - 1) / kNsTile;
     for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
     // (per-slot positions recomputed each tile from an opaque copy of the thread index: hoisted out
@@ -428,19 +475,25 @@ __global__ __launch_bounds__(256, 4) void k_ns_merge(uint32_t* keys, uint32_t* v
     const uint64_t t0 = (uint64_t)t * kNsTile;
     const uint32_t nown = (uint32_t)((t0 + kNsTile < n ? t0 + kNsTile : n) - t0);
     const uint32_t nwd = (nown + 31u) / 32u;
-    uint32_t nmarked;
-    __syncthreads();   // the previous tile's readers of s_ak / s_bk are done
-    {   // bitmap words and their exclusive popcount prefix (threads 0 .. 123)
-        const uint32_t wv = tid < nwd ? bitmap[(t0 >> 5) + tid] : 0u;
-        const uint32_t pre = block_excl_scan_n<4>((uint32_t)__popc(wv), s_scratch, nmarked);
-        if (tid < NWD) { s_w[tid] = wv; s_wpre[tid] = pre; }
-    }
-    __syncthreads();
-    const uint32_t natot = nown - nmarked;
     int64_t olo, ohi;
     ns_out_range(toff, coff, blo, t, ntiles, n, olo, ohi);
     const uint32_t b0 = blo[t], b1 = blo[t + 1];
     const bool hasb = b1 > b0;   // (most tiles: no extracted element falls among theirs)
+    const uint32_t cn0 = b1 - b0 < kNsBChunk ? b1 - b0 : kNsBChunk;
+    __syncthreads();   // the previous tile's readers of the LDS arrays are done
+    // the bitmap word (threads 0 .. 123) and the first chunk of extracted elements, loaded before
+    // the tile's elements: loads complete in order, so the scan below waits for these only
+    const uint32_t wv = tid < nwd ? bitmap[(t0 >> 5) + tid] : 0u;
+    uint32_t qk[2], qe[2], qp[2];
+#pragma unroll
+    for (uint32_t r = 0; r < 2; ++r) {
+        const uint32_t i = tid + 256u * r;
+        if (i < cn0) {
+            qk[r] = bm[b0 + i];
+            qe[r] = ei[b0 + i];
+            qp[r] = bp[b0 + i];
+        }
+    }
     // the positions [alo, ahi) of the tile (relative) lie in its own output range: read in place;
     // the rest from tmp, where k_ns_save put them.  Buffer loads over the tile: one offset register,
     // slot offsets immediate, zeros past the end.
@@ -481,6 +534,23 @@ __global__ __launch_bounds__(256, 4) void k_ns_merge(uint32_t* keys, uint32_t* v
             }
         }
     }
+    // while they are in flight: the bitmap words' exclusive popcount prefix, the first chunk to LDS
+    uint32_t nmarked;
+    {
+        const uint32_t pre = block_excl_scan_n<4>((uint32_t)__popc(wv), s_scratch, nmarked);
+        if (tid < NWD) { s_w[tid] = wv; s_wpre[tid] = pre; }
+#pragma unroll
+        for (uint32_t r = 0; r < 2; ++r) {
+            const uint32_t i = tid + 256u * r;
+            if (i < cn0) {
+                s_bk[i] = qk[r];
+                s_be[i] = qe[r];
+                s_bp[i] = qp[r];
+            }
+        }
+    }
+    __syncthreads();
+    const uint32_t natot = nown - nmarked;
     // every load of the workgroup has landed before any thread writes (in place)
 #pragma unroll
     for (uint32_t j = 0; j < KPT; ++j) asm volatile("" ::"v"(fk[j]), "v"(fv[j]));
@@ -488,9 +558,9 @@ __global__ __launch_bounds__(256, 4) void k_ns_merge(uint32_t* keys, uint32_t* v
     for (uint32_t j = 0; j < KPT; ++j) {
         const uint32_t i = j * 256u + tid;
         const bool in = i < nown;
-        const uint32_t wv = in ? s_w[i >> 5] : 0xFFFFFFFFu;
-        const bool ok = in && !((wv >> (i & 31u)) & 1u);
-        ao[j] = i - (s_wpre[i >> 5 < NWD ? i >> 5 : NWD - 1] + (uint32_t)__popc(wv & ((1u << (i & 31u)) - 1u)));
+        const uint32_t wvi = in ? s_w[i >> 5] : 0xFFFFFFFFu;
+        const bool ok = in && !((wvi >> (i & 31u)) & 1u);
+        ao[j] = i - (s_wpre[i >> 5 < NWD ? i >> 5 : NWD - 1] + (uint32_t)__popc(wvi & ((1u << (i & 31u)) - 1u)));
         valid |= ok ? (1u << j) : 0u;
         if (hasb && ok) {
             s_ak[ao[j]] = fk[j] & fmask;
@@ -502,12 +572,15 @@ __global__ __launch_bounds__(256, 4) void k_ns_merge(uint32_t* keys, uint32_t* v
     const uint32_t arank0 = obase - b0;
     for (uint32_t c0 = b0; c0 < b1; c0 += kNsBChunk) {
         const uint32_t cn = b1 - c0 < kNsBChunk ? b1 - c0 : kNsBChunk;
-        if (c0 != b0) __syncthreads();   // the previous chunk's readers are done
-        for (uint32_t i = tid; i < cn; i += 256) {
-            s_bk[i] = bm[c0 + i];
-            s_bp[i] = bp[c0 + i];
+        if (c0 != b0) {   // (the first chunk is in LDS already)
+            __syncthreads();   // the previous chunk's readers are done
+            for (uint32_t i = tid; i < cn; i += 256) {
+                s_bk[i] = bm[c0 + i];
+                s_be[i] = ei[c0 + i];
+                s_bp[i] = bp[c0 + i];
+            }
+            __syncthreads();
         }
-        __syncthreads();
         // the chunk's elements: output = extraction rank + remainder elements of the tile before them
         for (uint32_t i = tid; i < cn; i += 256) {
             const uint32_t kb = s_bk[i], pb = s_bp[i];
@@ -518,7 +591,7 @@ __global__ __launch_bounds__(256, 4) void k_ns_merge(uint32_t* keys, uint32_t* v
                 else h = mid;
             }
             const uint32_t o = c0 + i + arank0 + l;
-            const uint32_t e = ei[c0 + i];
+            const uint32_t e = s_be[i];
             if (L == LAYOUT_KEYS) {
                 keys[o] = sk[e];
             } else if (L == LAYOUT_AOS) {
@@ -556,11 +629,6 @@ __global__ __launch_bounds__(256, 4) void k_ns_merge(uint32_t* keys, uint32_t* v
         }
     }
     }
-}
-
-// ctl[5] = 1 when this path sorted (read by k_hist16_in's skip): set by the last kernel of the path.
-__global__ void k_ns_done(uint32_t* ctl) {
-    if (threadIdx.x == 0) ctl[5] = ctl[kNsGate];
 }
 
 }  // namespace rs

@@ -766,11 +766,11 @@ RS_EXPORT const char* rs_status_string(rs_status s) {
 RS_EXPORT uint32_t rs_version(void) { return (RSORT_VERSION_MAJOR << 16) | RSORT_VERSION_MINOR; }
 
 // The presorted path's workspace (rs_presorted.hpp): control words, per-tile counts / boundary keys /
-// offsets / bounds, the mark bitmap, and eight arrays of the extraction capacity (masked key and
-// extraction index twice - the ping-pong of its sort - then key, value, position, and the sorted
-// positions).  Sized for min(capacity, kMsdMax) keys: the hybrid path never sorts more.
+// offsets / bounds, the chunk sums, the extraction sort's totals, the mark bitmap, and eight arrays
+// of the extraction capacity (masked key and extraction index twice - the ping-pong of its sort -
+// then key, value, position, and the sorted positions).  Sized for min(capacity, kMsdMax) keys: the hybrid path never sorts more.
 struct NsWs {
-    uint32_t *ctl, *tcnt, *tbnd, *toff, *blo, *csum, *coff, *bitmap, *ek, *ei, *ek2, *ei2, *sk, *sv, *sp, *bp;
+    uint32_t *ctl, *tcnt, *tbnd, *toff, *blo, *csum, *coff, *sub, *bitmap, *ek, *ei, *ek2, *ei2, *sk, *sv, *sp, *bp;
 };
 uint64_t ns_keys(uint64_t capacity) { return std::min<uint64_t>(capacity, kMsdMax); }
 // extraction capacity for n keys: n / 128 (config 4's n / 1000 transpositions mark ~n / 500), at
@@ -796,6 +796,8 @@ NsWs ns_layout(uint32_t* q, uint64_t capacity) {
     q += nt / 1024 + 1;
     w.coff = q;
     q += nt / 1024 + 2;
+    w.sub = q;                        // the extraction sort's digit totals, tickets, error word
+    q += rs::kNsSubWords;
     w.bitmap = q;
     q += nt * (rs::kNsTile / 32);
     uint32_t** arr[8] = {&w.ek, &w.ei, &w.ek2, &w.ei2, &w.sk, &w.sv, &w.sp, &w.bp};
@@ -1073,11 +1075,11 @@ static rs_status enqueue_split(rs_plan* p, const rs::SplitWs& sw, bool keys, boo
 }
 
 // The presorted path (rs_presorted.hpp) of a check_order sort, in place on the caller's data (uk /
-// uv: arrays, keys, or records in uk): mark -> decide -> extract -> the extraction's sort (four 8-bit
-// LSD passes of the histogram path, gated on the device) -> bounds -> save -> merge in place.  Every
-// launch after k_ns_decide_b exits at once unless the device found the input nearly sorted;
-// k_ns_done then makes the radix path's order check find the data in order (the hybrid path's
-// histogram read is skipped outright: k_hist16_in's `skip`).
+// uv: arrays, keys, or records in uk): mark -> decide -> extract -> the extraction's sort (its four
+// 8-bit digit totals from one read, then four one-sweep passes) -> gather -> bounds -> save ->
+// merge in place: 12 launches.  Every launch after k_ns_decide exits at once unless the device found the input nearly
+// sorted; k_ns_merge then flags the data sorted (ctl[5]) and the radix path enqueued behind finds
+// it in order (the hybrid path's histogram read is skipped outright: k_hist16_in's `skip`).
 static rs_status enqueue_presorted(rs_plan* p, uint32_t* uk, uint32_t* uv, uint32_t n, hipStream_t s) {
     constexpr int K = rs::LAYOUT_KEYS, S = rs::LAYOUT_SOA, A = rs::LAYOUT_AOS;
     const NsWs w = ns_layout(p->ns, p->capacity);
@@ -1088,41 +1090,58 @@ static rs_status enqueue_presorted(rs_plan* p, uint32_t* uk, uint32_t* uv, uint3
     const uint32_t fm = full_mask(p->bit_count);
     const int L = p->layout;
     const uint32_t* gate = w.ctl + rs::kNsGate;
+    // the extraction sort: 16K-key tiles (cap is a whole number of them), one look-back status word
+    // per (tile, digit)
+    const uint32_t stiles = cap / (uint32_t)kLarge.tile;
+    if ((uint64_t)stiles * 256u > p->status_words)
+        return fail(RS_ERR_INVALID_ARG, "internal: %u extraction tiles exceed the plan's status words", stiles);
     p->last_ns = true;
     HIP_TRY(hipMemsetAsync(w.ctl, 0, 4 * rs::kNsCtlWords, s));
     // persistent grids: as many workgroups as are resident, tiles taken in order
-    auto resident = [&](auto kern, uint32_t units) {
-        static const uint32_t per_cu = resident_per_cu(kern, 256);
+    auto resident = [&](auto kern, uint32_t units, uint32_t block) {
+        static const uint32_t per_cu = resident_per_cu(kern, (int)block);
         return std::max(1u, std::min<uint32_t>(units, p->cus * per_cu));
     };
     p->timer.run(RS_KERNEL_PRESORTED, s, [&] {
         auto mark = [&](auto kern) {
-            hipLaunchKernelGGL(kern, dim3(resident(kern, ntiles)), dim3(256), 0, s, (const uint32_t*)uk, n, fm,
+            hipLaunchKernelGGL(kern, dim3(resident(kern, ntiles, 256)), dim3(256), 0, s, (const uint32_t*)uk, n, fm,
                                w.bitmap, w.tcnt, w.tbnd, w.ctl);
         };
         L == A ? mark(rs::k_ns_mark<A>) : mark(rs::k_ns_mark<S>);   // (keys only reads as SOA)
-        hipLaunchKernelGGL(rs::k_ns_decide_a, dim3((ntiles + 1023u) / 1024u), dim3(1024), 0, s,
-                           (const uint32_t*)w.tcnt, (const uint32_t*)w.tbnd, ntiles, w.toff, w.csum, w.ctl);
-        hipLaunchKernelGGL(rs::k_ns_decide_b, dim3(1), dim3(1024), 0, s, (const uint32_t*)w.csum, ntiles, cap, w.toff,
-                           w.coff, w.ctl);
+        hipLaunchKernelGGL(rs::k_ns_decide, dim3((ntiles + 1023u) / 1024u), dim3(1024), 0, s, (const uint32_t*)w.tcnt,
+                           (const uint32_t*)w.tbnd, ntiles, cap, w.toff, w.csum, w.coff, w.sub, w.ctl);
         auto extract = [&](auto kern) {
             hipLaunchKernelGGL(kern, dim3(ntiles), dim3(128), 0, s, (const uint32_t*)uk, (const uint32_t*)uv, n, fm,
                                cap, (const uint32_t*)w.bitmap, (const uint32_t*)w.toff, (const uint32_t*)w.coff,
                                (const uint32_t*)w.ctl, w.ek, w.ei, w.sk, w.sv, w.sp);
         };
         L == A ? extract(rs::k_ns_extract<A>) : L == S ? extract(rs::k_ns_extract<S>) : extract(rs::k_ns_extract<K>);
+        // the extraction (masked key, extraction index) sorted stably, ek / ei -> ek2 / ei2 -> ... ->
+        // ek / ei: every pass's digit totals from one read (they do not depend on the order), then
+        // the passes (16K-key tiles, decoupled look-back)
+        hipLaunchKernelGGL(rs::k_ns_totals, dim3(std::min<uint32_t>(cap / 2048u, p->cus)), dim3(256), 0, s,
+                           (const uint32_t*)w.ek, cap, (const uint32_t*)w.ctl, w.sub);
     }, "rsort.presorted.mark");
     HIP_TRY(hipGetLastError());
-    // the extraction (masked key, extraction index) sorted stably: ek / ei -> ek2 / ei2 -> ... -> ek / ei
-    p->scatter_kind = RS_KERNEL_PRESORTED;
-    rs_status st = RS_OK;
-    for (uint32_t i = 0; i < 4 && st == RS_OK; ++i) {
+    const bool ballot = p->rank_mode == rs::RANK_BALLOT;
+    for (uint32_t i = 0; i < 4; ++i) {
+        if (rs_status st = next_epoch(p, s)) return st;
         const bool odd = i & 1u;
-        st = run_pass(p, odd ? w.ek2 : w.ek, odd ? w.ei2 : w.ei, odd ? w.ek : w.ek2, odd ? w.ei : w.ei2, cap, 8 * i, 8,
-                      layout_pair(S, S), gate, (int)i, s, /*onesweep=*/false);
+        p->timer.run(RS_KERNEL_PRESORTED, s, [&] {
+            auto go = [&](auto kern) {
+                hipLaunchKernelGGL(kern, dim3(resident(kern, stiles, kLarge.block)), dim3(kLarge.block), 0, s,
+                                   (const uint32_t*)(odd ? w.ek2 : w.ek), (const uint32_t*)(odd ? w.ei2 : w.ei),
+                                   odd ? w.ek : w.ek2, odd ? w.ei : w.ei2, cap, 8u * i, 255u, stiles,
+                                   (const uint32_t*)(w.sub + 256u * i), p->status, w.sub + 1024u + i,
+                                   w.sub + 1024u + 16u, (uint32_t*)nullptr, 0u, 0u, p->epoch, gate, (int)i,
+                                   (uint32_t*)nullptr, 0xFFFFFFFFu, p->spin_max, p->host_err_dev,
+                                   (const uint32_t*)nullptr, (const uint32_t*)nullptr, 0u, 0xFFFFFFFFu);
+            };
+            constexpr int B = kLarge.block, KP = kLarge.kpt;
+            ballot ? go(rs::k_onesweep<8, B, KP, S, rs::RANK_BALLOT>) : go(rs::k_onesweep<8, B, KP, S, rs::RANK_LDS_ATOMIC>);
+        }, "rsort.presorted.sort");
+        HIP_TRY(hipGetLastError());
     }
-    p->scatter_kind = RS_KERNEL_SCATTER;
-    if (st != RS_OK) return st;
     p->timer.run(RS_KERNEL_PRESORTED, s, [&] {
         hipLaunchKernelGGL(rs::k_ns_gather, dim3(std::min<uint32_t>(cap / 256u, 4u * p->cus)), dim3(256), 0, s,
                            (const uint32_t*)w.ei, (const uint32_t*)w.sp, (const uint32_t*)w.ctl, w.bp);
@@ -1139,14 +1158,13 @@ static rs_status enqueue_presorted(rs_plan* p, uint32_t* uk, uint32_t* uv, uint3
         };
         L == A ? save(rs::k_ns_save<A>) : L == S ? save(rs::k_ns_save<S>) : save(rs::k_ns_save<K>);
         auto merge = [&](auto kern) {
-            hipLaunchKernelGGL(kern, dim3(resident(kern, ntiles)), dim3(256), 0, s, uk, uv, n, fm,
+            hipLaunchKernelGGL(kern, dim3(resident(kern, ntiles, 256)), dim3(256), 0, s, uk, uv, n, fm,
                                (const uint32_t*)w.bitmap, (const uint32_t*)w.toff, (const uint32_t*)w.coff,
                                (const uint32_t*)w.blo, (const uint32_t*)w.ei, (const uint32_t*)w.ek,
-                               (const uint32_t*)w.bp, (const uint32_t*)w.sk, (const uint32_t*)w.sv,
-                               (const uint32_t*)w.ctl, (const uint32_t*)p->tmp_k);
+                               (const uint32_t*)w.bp, (const uint32_t*)w.sk, (const uint32_t*)w.sv, w.ctl,
+                               (const uint32_t*)p->tmp_k);
         };
         L == A ? merge(rs::k_ns_merge<A>) : L == S ? merge(rs::k_ns_merge<S>) : merge(rs::k_ns_merge<K>);
-        hipLaunchKernelGGL(rs::k_ns_done, dim3(1), dim3(64), 0, s, w.ctl);
     }, "rsort.presorted.merge");
     HIP_TRY(hipGetLastError());
     return RS_OK;

@@ -443,8 +443,8 @@ __global__ __launch_bounds__(256) void k_ns_save(const uint32_t* __restrict__ ke
 // into the caller's arrays at the tile's output range (in place, see k_ns_save).  Element e of the
 // tile is thread e % 256's slot e / 256 (coalesced loads; consecutive remainder elements are
 // written by consecutive lanes).
-template <int L>
-__global__ __launch_bounds__(256, 4) void k_ns_merge(uint32_t* keys, uint32_t* vals, uint32_t n, uint32_t fmask,
+template <int L, uint32_t NT = 512>
+__global__ __launch_bounds__(NT) void k_ns_merge(uint32_t* keys, uint32_t* vals, uint32_t n, uint32_t fmask,
                                                      const uint32_t* __restrict__ bitmap,
                                                      const uint32_t* __restrict__ toff,
                                                      const uint32_t* __restrict__ coff,
@@ -453,7 +453,7 @@ __global__ __launch_bounds__(256, 4) void k_ns_merge(uint32_t* keys, uint32_t* v
                                                      const uint32_t* __restrict__ bp, const uint32_t* __restrict__ sk,
                                                      const uint32_t* __restrict__ sv, uint32_t* ctl,
                                                      const uint32_t* __restrict__ tmp) {
-    constexpr uint32_t KPT = (kNsTile + 255) / 256;
+    constexpr uint32_t KPT = (kNsTile + NT - 1) / NT;
     constexpr uint32_t NWD = kNsTile / 32;
     __shared__ uint32_t s_ak[kNsTile];        // the tile's remainder, in order: masked keys, positions
     __shared__ uint32_t s_ap[kNsTile];
@@ -461,7 +461,7 @@ __global__ __launch_bounds__(256, 4) void k_ns_merge(uint32_t* keys, uint32_t* v
     __shared__ uint32_t s_bp[kNsBChunk];
     __shared__ uint32_t s_be[kNsBChunk];
     __shared__ uint32_t s_w[NWD], s_wpre[NWD];   // the tile's bitmap words, marks before each word
-    __shared__ uint32_t s_scratch[4];
+    __shared__ uint32_t s_scratch[NT / 64];
     if (!ctl[kNsGate]) return;
     // the path has sorted once every workgroup is done (read by the radix path's histogram read,
     // a later launch: k_hist16_in's skip)
@@ -484,10 +484,11 @@ __global__ __launch_bounds__(256, 4) void k_ns_merge(uint32_t* keys, uint32_t* v
     // the bitmap word (threads 0 .. 123) and the first chunk of extracted elements, loaded before
     // the tile's elements: loads complete in order, so the scan below waits for these only
     const uint32_t wv = tid < nwd ? bitmap[(t0 >> 5) + tid] : 0u;
-    uint32_t qk[2], qe[2], qp[2];
+    constexpr uint32_t QR = (kNsBChunk + NT - 1) / NT;
+    uint32_t qk[QR], qe[QR], qp[QR];
 #pragma unroll
-    for (uint32_t r = 0; r < 2; ++r) {
-        const uint32_t i = tid + 256u * r;
+    for (uint32_t r = 0; r < QR; ++r) {
+        const uint32_t i = tid + NT * r;
         if (i < cn0) {
             qk[r] = bm[b0 + i];
             qe[r] = ei[b0 + i];
@@ -513,22 +514,22 @@ __global__ __launch_bounds__(256, 4) void k_ns_merge(uint32_t* keys, uint32_t* v
     uint32_t valid = 0;
 #pragma unroll
     for (uint32_t j = 0; j < KPT; ++j) {
-        const uint32_t i = j * 256u + tid;
+        const uint32_t i = j * NT + tid;
         if (i >= alo && i < ahi) {
             if constexpr (L == LAYOUT_AOS) {
-                const auto q = __builtin_amdgcn_raw_buffer_load_b64(rk, (int)(2u * lo + j * 256u * 8u), 0, 0);
+                const auto q = __builtin_amdgcn_raw_buffer_load_b64(rk, (int)(2u * lo + j * NT * 8u), 0, 0);
                 fk[j] = q[0];
                 fv[j] = q[1];
             } else {
-                fk[j] = __builtin_amdgcn_raw_buffer_load_b32(rk, (int)(lo + j * 1024u), 0, 0);
-                fv[j] = L == LAYOUT_SOA ? __builtin_amdgcn_raw_buffer_load_b32(rv, (int)(lo + j * 1024u), 0, 0) : 0u;
+                fk[j] = __builtin_amdgcn_raw_buffer_load_b32(rk, (int)(lo + j * NT * 4u), 0, 0);
+                fv[j] = L == LAYOUT_SOA ? __builtin_amdgcn_raw_buffer_load_b32(rv, (int)(lo + j * NT * 4u), 0, 0) : 0u;
             }
         } else {
             if constexpr (L == LAYOUT_KEYS) {
-                fk[j] = __builtin_amdgcn_raw_buffer_load_b32(rt, (int)(lo + j * 1024u), 0, 0);
+                fk[j] = __builtin_amdgcn_raw_buffer_load_b32(rt, (int)(lo + j * NT * 4u), 0, 0);
                 fv[j] = 0u;
             } else {
-                const auto q = __builtin_amdgcn_raw_buffer_load_b64(rt, (int)(2u * lo + j * 256u * 8u), 0, 0);
+                const auto q = __builtin_amdgcn_raw_buffer_load_b64(rt, (int)(2u * lo + j * NT * 8u), 0, 0);
                 fk[j] = q[0];
                 fv[j] = q[1];
             }
@@ -537,11 +538,11 @@ __global__ __launch_bounds__(256, 4) void k_ns_merge(uint32_t* keys, uint32_t* v
     // while they are in flight: the bitmap words' exclusive popcount prefix, the first chunk to LDS
     uint32_t nmarked;
     {
-        const uint32_t pre = block_excl_scan_n<4>((uint32_t)__popc(wv), s_scratch, nmarked);
+        const uint32_t pre = block_excl_scan_n<NT / 64>((uint32_t)__popc(wv), s_scratch, nmarked);
         if (tid < NWD) { s_w[tid] = wv; s_wpre[tid] = pre; }
 #pragma unroll
-        for (uint32_t r = 0; r < 2; ++r) {
-            const uint32_t i = tid + 256u * r;
+        for (uint32_t r = 0; r < QR; ++r) {
+            const uint32_t i = tid + NT * r;
             if (i < cn0) {
                 s_bk[i] = qk[r];
                 s_be[i] = qe[r];
@@ -556,7 +557,7 @@ __global__ __launch_bounds__(256, 4) void k_ns_merge(uint32_t* keys, uint32_t* v
     for (uint32_t j = 0; j < KPT; ++j) asm volatile("" ::"v"(fk[j]), "v"(fv[j]));
 #pragma unroll
     for (uint32_t j = 0; j < KPT; ++j) {
-        const uint32_t i = j * 256u + tid;
+        const uint32_t i = j * NT + tid;
         const bool in = i < nown;
         const uint32_t wvi = in ? s_w[i >> 5] : 0xFFFFFFFFu;
         const bool ok = in && !((wvi >> (i & 31u)) & 1u);
@@ -574,7 +575,7 @@ __global__ __launch_bounds__(256, 4) void k_ns_merge(uint32_t* keys, uint32_t* v
         const uint32_t cn = b1 - c0 < kNsBChunk ? b1 - c0 : kNsBChunk;
         if (c0 != b0) {   // (the first chunk is in LDS already)
             __syncthreads();   // the previous chunk's readers are done
-            for (uint32_t i = tid; i < cn; i += 256) {
+            for (uint32_t i = tid; i < cn; i += NT) {
                 s_bk[i] = bm[c0 + i];
                 s_be[i] = ei[c0 + i];
                 s_bp[i] = bp[c0 + i];
@@ -582,7 +583,7 @@ __global__ __launch_bounds__(256, 4) void k_ns_merge(uint32_t* keys, uint32_t* v
             __syncthreads();
         }
         // the chunk's elements: output = extraction rank + remainder elements of the tile before them
-        for (uint32_t i = tid; i < cn; i += 256) {
+        for (uint32_t i = tid; i < cn; i += NT) {
             const uint32_t kb = s_bk[i], pb = s_bp[i];
             uint32_t l = 0, h = natot;
             while (l < h) {
@@ -605,7 +606,7 @@ __global__ __launch_bounds__(256, 4) void k_ns_merge(uint32_t* keys, uint32_t* v
 #pragma unroll
         for (uint32_t j = 0; j < KPT; ++j) {
             if (!((valid >> j) & 1u)) continue;
-            const uint32_t ka = fk[j] & fmask, pa = (uint32_t)t0 + j * 256u + tid;
+            const uint32_t ka = fk[j] & fmask, pa = (uint32_t)t0 + j * NT + tid;
             uint32_t l = 0, h = cn;
             while (l < h) {
                 const uint32_t mid = (l + h) >> 1;

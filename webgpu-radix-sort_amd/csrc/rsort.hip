@@ -1158,7 +1158,7 @@ static rs_status enqueue_presorted(rs_plan* p, uint32_t* uk, uint32_t* uv, uint3
         };
         L == A ? save(rs::k_ns_save<A>) : L == S ? save(rs::k_ns_save<S>) : save(rs::k_ns_save<K>);
         auto merge = [&](auto kern) {
-            hipLaunchKernelGGL(kern, dim3(resident(kern, ntiles, 256)), dim3(256), 0, s, uk, uv, n, fm,
+            hipLaunchKernelGGL(kern, dim3(resident(kern, ntiles, 512)), dim3(512), 0, s, uk, uv, n, fm,
                                (const uint32_t*)w.bitmap, (const uint32_t*)w.toff, (const uint32_t*)w.coff,
                                (const uint32_t*)w.blo, (const uint32_t*)w.ei, (const uint32_t*)w.ek,
                                (const uint32_t*)w.bp, (const uint32_t*)w.sk, (const uint32_t*)w.sv, w.ctl,

@@ -293,44 +293,50 @@ __device__ __forceinline__ uint32_t ns_toff(const uint32_t* toff, const uint32_t
 // The marked elements of every tile, in position order, to the extraction: ek = masked key, ei =
 // extraction index (the LSD passes sort (ek, ei) stably), sk / sv / sp = key, value, position in
 // extraction order.  Past m: pads (the largest key, after every real one in a stable sort).  One
-// 128-thread workgroup per tile, a bitmap word per thread.
+// wave per tile (no barrier): lane l takes bitmap words 2l and 2l + 1.
 template <int L>
-__global__ __launch_bounds__(128) void k_ns_extract(const uint32_t* __restrict__ keys,
-                                                    const uint32_t* __restrict__ vals, uint32_t n,
-                                                    uint32_t fmask, uint32_t cap,
-                                                    const uint32_t* __restrict__ bitmap,
-                                                    const uint32_t* __restrict__ toff,
-                                                    const uint32_t* __restrict__ coff, const uint32_t* ctl,
-                                                    uint32_t* __restrict__ ek, uint32_t* __restrict__ ei,
-                                                    uint32_t* __restrict__ sk, uint32_t* __restrict__ sv,
-                                                    uint32_t* __restrict__ sp) {
-    __shared__ uint32_t s_scratch[2];
+__global__ __launch_bounds__(64) void k_ns_extract(const uint32_t* __restrict__ keys,
+                                                   const uint32_t* __restrict__ vals, uint32_t n,
+                                                   uint32_t fmask, uint32_t cap,
+                                                   const uint32_t* __restrict__ bitmap,
+                                                   const uint32_t* __restrict__ toff,
+                                                   const uint32_t* __restrict__ coff, const uint32_t* ctl,
+                                                   uint32_t* __restrict__ ek, uint32_t* __restrict__ ei,
+                                                   uint32_t* __restrict__ sk, uint32_t* __restrict__ sv,
+                                                   uint32_t* __restrict__ sp) {
+    static_assert(kNsTile / 32 <= 128, "two bitmap words per lane");
     if (!ctl[kNsGate]) return;
-    const uint32_t tid = threadIdx.x, t = blockIdx.x;
+    const uint32_t lane = threadIdx.x, t = blockIdx.x;
     const uint32_t m = ctl[4];
     // pads (grid-stride over the extraction's tail)
-    for (uint64_t e = (uint64_t)m + (uint64_t)t * 128u + tid; e < cap; e += (uint64_t)gridDim.x * 128u) {
+    for (uint64_t e = (uint64_t)m + (uint64_t)t * 64u + lane; e < cap; e += (uint64_t)gridDim.x * 64u) {
         ek[e] = 0xFFFFFFFFu;
         ei[e] = (uint32_t)e;
     }
     const uint64_t t0 = (uint64_t)t * kNsTile;
     const uint32_t nown = (uint32_t)((t0 + kNsTile < n ? t0 + kNsTile : n) - t0);
     const uint32_t nwords = (nown + 31u) / 32u;   // <= 124
-    uint32_t bits = tid < nwords ? bitmap[(t0 >> 5) + tid] : 0u;
-    uint32_t total;
-    uint32_t e = ns_toff(toff, coff, t) + block_excl_scan_n<2>((uint32_t)__popc(bits), s_scratch, total);
-    while (bits) {
-        const uint32_t b = (uint32_t)__builtin_ctz(bits);
-        bits &= bits - 1u;
-        const uint64_t p = t0 + tid * 32u + b;
-        const uint32_t key = ns_key<L>(keys, p);
-        ek[e] = key & fmask;
-        ei[e] = e;
-        sk[e] = key;
-        sv[e] = L == LAYOUT_KEYS ? 0u : (L == LAYOUT_AOS ? keys[2 * p + 1] : vals[p]);
-        sp[e] = (uint32_t)p;
-        ++e;
-    }
+    const uint32_t w0 = 2u * lane, w1 = w0 + 1u;
+    uint32_t b0 = w0 < nwords ? bitmap[(t0 >> 5) + w0] : 0u;
+    uint32_t b1 = w1 < nwords ? bitmap[(t0 >> 5) + w1] : 0u;
+    const uint32_t c = (uint32_t)__popc(b0) + (uint32_t)__popc(b1);
+    uint32_t e = ns_toff(toff, coff, t) + wave_incl_scan(c) - c;
+    auto take = [&](uint32_t bits, uint32_t word) {
+        while (bits) {
+            const uint32_t b = (uint32_t)__builtin_ctz(bits);
+            bits &= bits - 1u;
+            const uint64_t p = t0 + word * 32u + b;
+            const uint32_t key = ns_key<L>(keys, p);
+            ek[e] = key & fmask;
+            ei[e] = e;
+            sk[e] = key;
+            sv[e] = L == LAYOUT_KEYS ? 0u : (L == LAYOUT_AOS ? keys[2 * p + 1] : vals[p]);
+            sp[e] = (uint32_t)p;
+            ++e;
+        }
+    };
+    take(b0, w0);
+    take(b1, w1);
 }
 
 // (masked key, position) order
@@ -510,11 +516,19 @@ __global__ __launch_bounds__(NT) void k_ns_merge(uint32_t* keys, uint32_t* vals,
         (void*)(L == LAYOUT_SOA ? vals + t0 : keys), (short)0, (int)(nown * 4u), 0x00020000);
     const __amdgpu_buffer_rsrc_t rt = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(tmp + (TSZ / 4u) * t0), (short)0, (int)(nown * TSZ), 0x00020000);
+    // Only the elements whose output position differs from their input position are written (for
+    // config 4 - transposed pairs - few remainder elements move at all): the keys are read first,
+    // the values (separate arrays) then for the movers only; a tile with more than one chunk of
+    // extracted elements reads every value up front (allv) and writes its extracted elements chunk
+    // by chunk.
+    constexpr bool SPLITV = L == LAYOUT_SOA;
+    const bool allv = b1 - b0 > kNsBChunk;
     uint32_t fk[KPT], fv[KPT], ao[KPT];
     uint32_t valid = 0;
 #pragma unroll
     for (uint32_t j = 0; j < KPT; ++j) {
         const uint32_t i = j * NT + tid;
+        fv[j] = 0u;
         if (i >= alo && i < ahi) {
             if constexpr (L == LAYOUT_AOS) {
                 const auto q = __builtin_amdgcn_raw_buffer_load_b64(rk, (int)(2u * lo + j * NT * 8u), 0, 0);
@@ -522,16 +536,18 @@ __global__ __launch_bounds__(NT) void k_ns_merge(uint32_t* keys, uint32_t* vals,
                 fv[j] = q[1];
             } else {
                 fk[j] = __builtin_amdgcn_raw_buffer_load_b32(rk, (int)(lo + j * NT * 4u), 0, 0);
-                fv[j] = L == LAYOUT_SOA ? __builtin_amdgcn_raw_buffer_load_b32(rv, (int)(lo + j * NT * 4u), 0, 0) : 0u;
+                if (SPLITV && allv) fv[j] = __builtin_amdgcn_raw_buffer_load_b32(rv, (int)(lo + j * NT * 4u), 0, 0);
             }
         } else {
             if constexpr (L == LAYOUT_KEYS) {
                 fk[j] = __builtin_amdgcn_raw_buffer_load_b32(rt, (int)(lo + j * NT * 4u), 0, 0);
-                fv[j] = 0u;
-            } else {
+            } else if constexpr (L == LAYOUT_AOS) {
                 const auto q = __builtin_amdgcn_raw_buffer_load_b64(rt, (int)(2u * lo + j * NT * 8u), 0, 0);
                 fk[j] = q[0];
                 fv[j] = q[1];
+            } else {
+                fk[j] = __builtin_amdgcn_raw_buffer_load_b32(rt, (int)(2u * lo + j * NT * 8u), 0, 0);
+                if (allv) fv[j] = __builtin_amdgcn_raw_buffer_load_b32(rt, (int)(2u * lo + j * NT * 8u + 4u), 0, 0);
             }
         }
     }
@@ -552,9 +568,6 @@ __global__ __launch_bounds__(NT) void k_ns_merge(uint32_t* keys, uint32_t* vals,
     }
     __syncthreads();
     const uint32_t natot = nown - nmarked;
-    // every load of the workgroup has landed before any thread writes (in place)
-#pragma unroll
-    for (uint32_t j = 0; j < KPT; ++j) asm volatile("" ::"v"(fk[j]), "v"(fv[j]));
 #pragma unroll
     for (uint32_t j = 0; j < KPT; ++j) {
         const uint32_t i = j * NT + tid;
@@ -568,9 +581,16 @@ __global__ __launch_bounds__(NT) void k_ns_merge(uint32_t* keys, uint32_t* vals,
             s_ap[ao[j]] = (uint32_t)t0 + i;
         }
     }
+    // (allv: every load has landed before the first write, which comes in the chunk loop)
+    if (allv) {
+#pragma unroll
+        for (uint32_t j = 0; j < KPT; ++j) asm volatile("" ::"v"(fk[j]), "v"(fv[j]));
+    }
     __syncthreads();
     const uint32_t obase = (uint32_t)olo;   // = arank0 + b0: the tile's first output position
     const uint32_t arank0 = obase - b0;
+    uint32_t bo = 0, be = 0;   // (one chunk: this thread's extracted element, written at the end)
+    bool bhas = false;
     for (uint32_t c0 = b0; c0 < b1; c0 += kNsBChunk) {
         const uint32_t cn = b1 - c0 < kNsBChunk ? b1 - c0 : kNsBChunk;
         if (c0 != b0) {   // (the first chunk is in LDS already)
@@ -593,13 +613,19 @@ __global__ __launch_bounds__(NT) void k_ns_merge(uint32_t* keys, uint32_t* vals,
             }
             const uint32_t o = c0 + i + arank0 + l;
             const uint32_t e = s_be[i];
-            if (L == LAYOUT_KEYS) {
-                keys[o] = sk[e];
-            } else if (L == LAYOUT_AOS) {
-                reinterpret_cast<uint2*>(keys)[o] = make_uint2(sk[e], sv[e]);
+            if (allv) {
+                if (L == LAYOUT_KEYS) {
+                    keys[o] = sk[e];
+                } else if (L == LAYOUT_AOS) {
+                    reinterpret_cast<uint2*>(keys)[o] = make_uint2(sk[e], sv[e]);
+                } else {
+                    keys[o] = sk[e];
+                    vals[o] = sv[e];
+                }
             } else {
-                keys[o] = sk[e];
-                vals[o] = sv[e];
+                bo = o;
+                be = e;
+                bhas = true;
             }
         }
         // this thread's remainder elements: the chunk's elements before each
@@ -616,9 +642,29 @@ __global__ __launch_bounds__(NT) void k_ns_merge(uint32_t* keys, uint32_t* vals,
             ao[j] += l;
         }
     }
+    // the movers: remainder elements whose output position is not their input position
+    uint32_t mv = 0;
 #pragma unroll
     for (uint32_t j = 0; j < KPT; ++j) {
-        if (!((valid >> j) & 1u)) continue;
+        const uint32_t i = j * NT + tid;
+        mv |= (((valid >> j) & 1u) && obase + ao[j] != (uint32_t)t0 + i) ? (1u << j) : 0u;
+    }
+    if (SPLITV && !allv) {   // their values
+#pragma unroll
+        for (uint32_t j = 0; j < KPT; ++j) {
+            if (!((mv >> j) & 1u)) continue;
+            const uint32_t i = j * NT + tid;
+            fv[j] = (i >= alo && i < ahi) ? __builtin_amdgcn_raw_buffer_load_b32(rv, (int)(lo + j * NT * 4u), 0, 0)
+                                          : __builtin_amdgcn_raw_buffer_load_b32(rt, (int)(2u * lo + j * NT * 8u + 4u), 0, 0);
+        }
+    }
+    // every load of the workgroup has landed before any thread writes (in place)
+#pragma unroll
+    for (uint32_t j = 0; j < KPT; ++j) asm volatile("" ::"v"(fk[j]), "v"(fv[j]));
+    __syncthreads();
+#pragma unroll
+    for (uint32_t j = 0; j < KPT; ++j) {
+        if (!((mv >> j) & 1u)) continue;
         const uint32_t o = obase + ao[j];
         if (L == LAYOUT_KEYS) {
             keys[o] = fk[j];
@@ -627,6 +673,16 @@ __global__ __launch_bounds__(NT) void k_ns_merge(uint32_t* keys, uint32_t* vals,
         } else {
             keys[o] = fk[j];
             vals[o] = fv[j];
+        }
+    }
+    if (bhas) {
+        if (L == LAYOUT_KEYS) {
+            keys[bo] = sk[be];
+        } else if (L == LAYOUT_AOS) {
+            reinterpret_cast<uint2*>(keys)[bo] = make_uint2(sk[be], sv[be]);
+        } else {
+            keys[bo] = sk[be];
+            vals[bo] = sv[be];
         }
     }
     }

@@ -1090,8 +1090,8 @@ static rs_status enqueue_presorted(rs_plan* p, uint32_t* uk, uint32_t* uv, uint3
     const uint32_t fm = full_mask(p->bit_count);
     const int L = p->layout;
     const uint32_t* gate = w.ctl + rs::kNsGate;
-    // the extraction sort: 16K-key tiles (cap is a whole number of them), one look-back status word
-    // per (tile, digit)
+    // the extraction sort: 16K-key tiles (cap is a whole number of them; 4K-key tiles measured
+    // slower: 27 vs 20 us per pass at config 4's 2M), one look-back status word per (tile, digit)
     const uint32_t stiles = cap / (uint32_t)kLarge.tile;
     if ((uint64_t)stiles * 256u > p->status_words)
         return fail(RS_ERR_INVALID_ARG, "internal: %u extraction tiles exceed the plan's status words", stiles);
@@ -1111,7 +1111,7 @@ static rs_status enqueue_presorted(rs_plan* p, uint32_t* uk, uint32_t* uv, uint3
         hipLaunchKernelGGL(rs::k_ns_decide, dim3((ntiles + 1023u) / 1024u), dim3(1024), 0, s, (const uint32_t*)w.tcnt,
                            (const uint32_t*)w.tbnd, ntiles, cap, w.toff, w.csum, w.coff, w.sub, w.ctl);
         auto extract = [&](auto kern) {
-            hipLaunchKernelGGL(kern, dim3(ntiles), dim3(128), 0, s, (const uint32_t*)uk, (const uint32_t*)uv, n, fm,
+            hipLaunchKernelGGL(kern, dim3(ntiles), dim3(64), 0, s, (const uint32_t*)uk, (const uint32_t*)uv, n, fm,
                                cap, (const uint32_t*)w.bitmap, (const uint32_t*)w.toff, (const uint32_t*)w.coff,
                                (const uint32_t*)w.ctl, w.ek, w.ei, w.sk, w.sv, w.sp);
         };

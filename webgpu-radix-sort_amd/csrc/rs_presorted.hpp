@@ -63,7 +63,8 @@ constexpr uint32_t kNsDense = 256;
 template <int L>
 __global__ __launch_bounds__(256) void k_ns_mark(const uint32_t* __restrict__ keys, uint32_t n, uint32_t fmask,
                                                  uint32_t* __restrict__ bitmap, uint32_t* __restrict__ tcnt,
-                                                 uint32_t* __restrict__ tbnd, uint32_t* ctl) {
+                                                 uint32_t* __restrict__ tbnd, uint2* __restrict__ samp,
+                                                 uint32_t* ctl) {
     constexpr uint32_t G = 16, NG = kNsWin / G, W = kNsWin, HALO = kNsHalo;
     constexpr uint32_t NWD = kNsTile / 32;
     constexpr uint32_t ESZ = L == LAYOUT_AOS ? 8u : 4u;
@@ -190,6 +191,10 @@ __global__ __launch_bounds__(256) void k_ns_mark(const uint32_t* __restrict__ ke
             bitmap[(t0 >> 5) + tid] = wd;
             cnt = (uint32_t)__popc(wd);
             un = ~wd & valid;
+            // the word's sample (k_ns_rank): its first unmarked position, as (masked key, position);
+            // none: position ~0
+            const uint32_t f = tid * 32u + (uint32_t)__builtin_ctz(un | 0x80000000u);
+            samp[(t0 >> 5) + tid] = un ? make_uint2(s_k[HALO + f], (uint32_t)t0 + f) : make_uint2(0u, 0xFFFFFFFFu);
         }
         cnt = wave_sum(cnt);
         {   // the wave's first / last unmarked position: its first / last lane with one
@@ -303,7 +308,7 @@ __global__ __launch_bounds__(64) void k_ns_extract(const uint32_t* __restrict__ 
                                                    const uint32_t* __restrict__ coff, const uint32_t* ctl,
                                                    uint32_t* __restrict__ ek, uint32_t* __restrict__ ei,
                                                    uint32_t* __restrict__ sk, uint32_t* __restrict__ sv,
-                                                   uint32_t* __restrict__ sp) {
+                                                   uint32_t* __restrict__ sp, uint32_t* __restrict__ wpre) {
     static_assert(kNsTile / 32 <= 128, "two bitmap words per lane");
     if (!ctl[kNsGate]) return;
     const uint32_t lane = threadIdx.x, t = blockIdx.x;
@@ -320,7 +325,10 @@ __global__ __launch_bounds__(64) void k_ns_extract(const uint32_t* __restrict__ 
     uint32_t b0 = w0 < nwords ? bitmap[(t0 >> 5) + w0] : 0u;
     uint32_t b1 = w1 < nwords ? bitmap[(t0 >> 5) + w1] : 0u;
     const uint32_t c = (uint32_t)__popc(b0) + (uint32_t)__popc(b1);
-    uint32_t e = ns_toff(toff, coff, t) + wave_incl_scan(c) - c;
+    const uint32_t ex = wave_incl_scan(c) - c;   // marks of the tile before word w0
+    if (w0 < nwords) wpre[(t0 >> 5) + w0] = ex;
+    if (w1 < nwords) wpre[(t0 >> 5) + w1] = ex + (uint32_t)__popc(b0);
+    uint32_t e = ns_toff(toff, coff, t) + ex;
     auto take = [&](uint32_t bits, uint32_t word) {
         while (bits) {
             const uint32_t b = (uint32_t)__builtin_ctz(bits);
@@ -365,13 +373,20 @@ __global__ __launch_bounds__(256) void k_ns_totals(const uint32_t* __restrict__ 
     }
 }
 
-// Threads j < m: the sorted extraction's positions (bp, gathered through the extraction index; the
-// sorted masked keys bm are the sorted ek itself).
+// Threads j < m: the sorted extraction's positions, keys and values (bp, bk, bv: gathered through
+// the extraction index; the sorted masked keys bm are the sorted ek itself).
 __global__ __launch_bounds__(256) void k_ns_gather(const uint32_t* __restrict__ ei, const uint32_t* __restrict__ sp,
-                                                   const uint32_t* ctl, uint32_t* __restrict__ bp) {
+                                                   const uint32_t* __restrict__ sk, const uint32_t* __restrict__ sv,
+                                                   const uint32_t* ctl, uint32_t* __restrict__ bp,
+                                                   uint32_t* __restrict__ bk, uint32_t* __restrict__ bv) {
     if (!ctl[kNsGate]) return;
     const uint32_t m = ctl[4];
-    for (uint32_t j = blockIdx.x * 256u + threadIdx.x; j < m; j += gridDim.x * 256u) bp[j] = sp[ei[j]];
+    for (uint32_t j = blockIdx.x * 256u + threadIdx.x; j < m; j += gridDim.x * 256u) {
+        const uint32_t e = ei[j];
+        bp[j] = sp[e];
+        bk[j] = sk[e];
+        bv[j] = sv[e];
+    }
 }
 
 // Threads t <= ntiles: blo[t] = the extracted elements ordered before tile t's first remainder
@@ -419,7 +434,8 @@ template <int L>
 __global__ __launch_bounds__(256) void k_ns_save(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals,
                                                  uint32_t n, const uint32_t* __restrict__ toff,
                                                  const uint32_t* __restrict__ coff, const uint32_t* __restrict__ blo,
-                                                 const uint32_t* ctl, uint32_t* __restrict__ tmp) {
+                                                 const uint32_t* ctl, uint32_t* __restrict__ tmp,
+                                                 uint32_t* __restrict__ tileof) {
     if (!ctl[kNsGate]) return;
     const uint32_t t = blockIdx.x, tid = threadIdx.x;
     const uint32_t ntiles = (n + kNsTile - 1) / kNsTile;
@@ -442,30 +458,83 @@ __global__ __launch_bounds__(256) void k_ns_save(const uint32_t* __restrict__ ke
     };
     save(t0, a1);
     save(b0 > a1 ? b0 : a1, t1);
+    for (uint32_t j = blo[t] + tid; j < blo[t + 1]; j += 256) tileof[j] = t;   // (for k_ns_rank)
 }
 
-// Tile t: its remainder elements (positions [t0, t0 + kNsTile) not in the bitmap) and the
-// extracted elements [blo[t], blo[t + 1]) merged by (masked key, position) - the stable order -
-// into the caller's arrays at the tile's output range (in place, see k_ns_save).  Element e of the
-// tile is thread e % 256's slot e / 256 (coalesced loads; consecutive remainder elements are
-// written by consecutive lanes).
+// Threads j < m: rank[j] = the remainder elements of sorted extracted element j's tile (tileof,
+// from k_ns_save) ordered before it.  The remainder of a tile is in (key, position) order, so a
+// binary search over the tile's word samples (k_ns_mark: the first remainder element of every
+// 32-position word, as (masked key, position); a probe on a word without one moves to the next
+// word with one) finds the last word whose sample is before the element; that word's own
+// remainder elements are compared, and the words before it counted whole (wpre: the tile's marks
+// before each word).
+template <int L>
+__global__ __launch_bounds__(256) void k_ns_rank(const uint32_t* __restrict__ keys, uint32_t n, uint32_t fmask,
+                                                 const uint32_t* __restrict__ bitmap,
+                                                 const uint32_t* __restrict__ wpre, const uint2* __restrict__ samp,
+                                                 const uint32_t* __restrict__ tileof,
+                                                 const uint32_t* __restrict__ bm, const uint32_t* __restrict__ bp,
+                                                 const uint32_t* ctl, uint32_t* __restrict__ rank) {
+    if (!ctl[kNsGate]) return;
+    const uint32_t m = ctl[4];
+    for (uint32_t j = blockIdx.x * 256u + threadIdx.x; j < m; j += gridDim.x * 256u) {
+        const uint32_t t = tileof[j];
+        const uint64_t t0 = (uint64_t)t * kNsTile;
+        const uint32_t nown = (uint32_t)((t0 + kNsTile < n ? t0 + kNsTile : n) - t0);
+        const uint32_t nwd = (nown + 31u) / 32u;
+        const uint32_t kb = bm[j], pb = bp[j];
+        const uint2* sw = samp + (t0 >> 5);
+        // the number of words whose sample is before (kb, pb)
+        uint32_t lo = 0, hi = nwd;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            uint32_t wq = mid;
+            uint2 q = sw[mid];
+            while (q.y == 0xFFFFFFFFu && ++wq < hi) q = sw[wq];   // (a word marked whole)
+            if (wq >= hi) hi = mid;
+            else if (ns_less(q.x, q.y, kb, pb)) lo = wq + 1;
+            else hi = mid;
+        }
+        uint32_t r = 0;
+        if (lo > 0) {
+            const uint32_t wd = lo - 1;   // the last such word: holds its own sample
+            const uint32_t bits = bitmap[(t0 >> 5) + wd];
+            r = wd * 32u - wpre[(t0 >> 5) + wd];
+            const uint64_t p0 = t0 + wd * 32u;
+            const uint32_t cnt = nown - wd * 32u < 32u ? nown - wd * 32u : 32u;
+            // the word's 32 keys at once (one or two cache lines), then counted
+            uint32_t k[32];
+#pragma unroll
+            for (uint32_t i = 0; i < 32u; ++i) k[i] = i < cnt ? ns_key<L>(keys, p0 + i) : 0u;
+#pragma unroll
+            for (uint32_t i = 0; i < 32u; ++i)
+                r += (i < cnt && !((bits >> i) & 1u) && ns_less(k[i] & fmask, (uint32_t)(p0 + i), kb, pb)) ? 1u : 0u;
+        }
+        rank[j] = r;
+    }
+}
+
+// Tile t: its remainder elements (positions [t0, t0 + kNsTile) not in the bitmap) go to the tile's
+// first output position + their remainder index + the tile's extracted elements ordered before them
+// (those whose rank is at most that index); the extracted elements [blo[t], blo[t + 1]) go to the
+// tile's first output position + their rank + their index in the tile's list.  Only the elements
+// whose output position differs from their input position are read and written (for config 4 -
+// transposed pairs - few remainder elements move at all), in place (see k_ns_save: a tile reads
+// only its own output range from the caller's arrays, and writes after every thread of the
+// workgroup has read).  Element e of the tile is thread e % NT's slot e / NT.
 template <int L, uint32_t NT = 512>
-__global__ __launch_bounds__(NT) void k_ns_merge(uint32_t* keys, uint32_t* vals, uint32_t n, uint32_t fmask,
-                                                     const uint32_t* __restrict__ bitmap,
-                                                     const uint32_t* __restrict__ toff,
-                                                     const uint32_t* __restrict__ coff,
-                                                     const uint32_t* __restrict__ blo,
-                                                     const uint32_t* __restrict__ ei, const uint32_t* __restrict__ bm,
-                                                     const uint32_t* __restrict__ bp, const uint32_t* __restrict__ sk,
-                                                     const uint32_t* __restrict__ sv, uint32_t* ctl,
-                                                     const uint32_t* __restrict__ tmp) {
+__global__ __launch_bounds__(NT) void k_ns_merge(uint32_t* keys, uint32_t* vals, uint32_t n,
+                                                 const uint32_t* __restrict__ bitmap,
+                                                 const uint32_t* __restrict__ toff,
+                                                 const uint32_t* __restrict__ coff,
+                                                 const uint32_t* __restrict__ blo,
+                                                 const uint32_t* __restrict__ rank, const uint32_t* __restrict__ bk,
+                                                 const uint32_t* __restrict__ bv, uint32_t* ctl,
+                                                 const uint32_t* __restrict__ tmp) {
     constexpr uint32_t KPT = (kNsTile + NT - 1) / NT;
     constexpr uint32_t NWD = kNsTile / 32;
-    __shared__ uint32_t s_ak[kNsTile];        // the tile's remainder, in order: masked keys, positions
-    __shared__ uint32_t s_ap[kNsTile];
-    __shared__ uint32_t s_bk[kNsBChunk];      // a chunk of the tile's extracted elements
-    __shared__ uint32_t s_bp[kNsBChunk];
-    __shared__ uint32_t s_be[kNsBChunk];
+    constexpr uint32_t BC = 2 * NT;           // extracted elements per LDS chunk
+    __shared__ uint32_t s_r[BC];              // a chunk of the tile's extracted elements' ranks
     __shared__ uint32_t s_w[NWD], s_wpre[NWD];   // the tile's bitmap words, marks before each word
     __shared__ uint32_t s_scratch[NT / 64];
     if (!ctl[kNsGate]) return;
@@ -484,90 +553,32 @@ __global__ __launch_bounds__(NT) void k_ns_merge(uint32_t* keys, uint32_t* vals,
     int64_t olo, ohi;
     ns_out_range(toff, coff, blo, t, ntiles, n, olo, ohi);
     const uint32_t b0 = blo[t], b1 = blo[t + 1];
-    const bool hasb = b1 > b0;   // (most tiles: no extracted element falls among theirs)
-    const uint32_t cn0 = b1 - b0 < kNsBChunk ? b1 - b0 : kNsBChunk;
+    const uint32_t cn0 = b1 - b0 < BC ? b1 - b0 : BC;
     __syncthreads();   // the previous tile's readers of the LDS arrays are done
-    // the bitmap word (threads 0 .. 123) and the first chunk of extracted elements, loaded before
-    // the tile's elements: loads complete in order, so the scan below waits for these only
     const uint32_t wv = tid < nwd ? bitmap[(t0 >> 5) + tid] : 0u;
-    constexpr uint32_t QR = (kNsBChunk + NT - 1) / NT;
-    uint32_t qk[QR], qe[QR], qp[QR];
-#pragma unroll
-    for (uint32_t r = 0; r < QR; ++r) {
-        const uint32_t i = tid + NT * r;
-        if (i < cn0) {
-            qk[r] = bm[b0 + i];
-            qe[r] = ei[b0 + i];
-            qp[r] = bp[b0 + i];
-        }
+    const uint32_t r0 = tid < cn0 ? rank[b0 + tid] : 0u;
+    const uint32_t r1 = tid + NT < cn0 ? rank[b0 + tid + NT] : 0u;
+    // the extracted elements (the first chunk's, this thread's two): their data
+    uint32_t xk0 = 0, xv0 = 0, xk1 = 0, xv1 = 0;
+    if (tid < cn0) {
+        xk0 = bk[b0 + tid];
+        if (L != LAYOUT_KEYS) xv0 = bv[b0 + tid];
     }
-    // the positions [alo, ahi) of the tile (relative) lie in its own output range: read in place;
-    // the rest from tmp, where k_ns_save put them.  Buffer loads over the tile: one offset register,
-    // slot offsets immediate, zeros past the end.
-    const uint32_t alo = (uint32_t)(olo - (int64_t)t0 < 0 ? 0 : (olo - (int64_t)t0 > nown ? nown : olo - (int64_t)t0));
-    const uint32_t ahi = (uint32_t)(ohi - (int64_t)t0 < 0 ? 0 : (ohi - (int64_t)t0 > nown ? nown : ohi - (int64_t)t0));
-    constexpr uint32_t ESZ = L == LAYOUT_AOS ? 8u : 4u;
-    constexpr uint32_t TSZ = L == LAYOUT_KEYS ? 4u : 8u;   // tmp: keys, or records
-    uint32_t lo = tid * 4u;
-    asm volatile("" : "+v"(lo));
-    const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(keys + (L == LAYOUT_AOS ? 2ull : 1ull) * t0), (short)0, (int)(nown * ESZ), 0x00020000);
-    const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(L == LAYOUT_SOA ? vals + t0 : keys), (short)0, (int)(nown * 4u), 0x00020000);
-    const __amdgpu_buffer_rsrc_t rt = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(tmp + (TSZ / 4u) * t0), (short)0, (int)(nown * TSZ), 0x00020000);
-    // Only the elements whose output position differs from their input position are written (for
-    // config 4 - transposed pairs - few remainder elements move at all): the keys are read first,
-    // the values (separate arrays) then for the movers only; a tile with more than one chunk of
-    // extracted elements reads every value up front (allv) and writes its extracted elements chunk
-    // by chunk.
-    constexpr bool SPLITV = L == LAYOUT_SOA;
-    const bool allv = b1 - b0 > kNsBChunk;
-    uint32_t fk[KPT], fv[KPT], ao[KPT];
-    uint32_t valid = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < KPT; ++j) {
-        const uint32_t i = j * NT + tid;
-        fv[j] = 0u;
-        if (i >= alo && i < ahi) {
-            if constexpr (L == LAYOUT_AOS) {
-                const auto q = __builtin_amdgcn_raw_buffer_load_b64(rk, (int)(2u * lo + j * NT * 8u), 0, 0);
-                fk[j] = q[0];
-                fv[j] = q[1];
-            } else {
-                fk[j] = __builtin_amdgcn_raw_buffer_load_b32(rk, (int)(lo + j * NT * 4u), 0, 0);
-                if (SPLITV && allv) fv[j] = __builtin_amdgcn_raw_buffer_load_b32(rv, (int)(lo + j * NT * 4u), 0, 0);
-            }
-        } else {
-            if constexpr (L == LAYOUT_KEYS) {
-                fk[j] = __builtin_amdgcn_raw_buffer_load_b32(rt, (int)(lo + j * NT * 4u), 0, 0);
-            } else if constexpr (L == LAYOUT_AOS) {
-                const auto q = __builtin_amdgcn_raw_buffer_load_b64(rt, (int)(2u * lo + j * NT * 8u), 0, 0);
-                fk[j] = q[0];
-                fv[j] = q[1];
-            } else {
-                fk[j] = __builtin_amdgcn_raw_buffer_load_b32(rt, (int)(2u * lo + j * NT * 8u), 0, 0);
-                if (allv) fv[j] = __builtin_amdgcn_raw_buffer_load_b32(rt, (int)(2u * lo + j * NT * 8u + 4u), 0, 0);
-            }
-        }
+    if (tid + NT < cn0) {
+        xk1 = bk[b0 + tid + NT];
+        if (L != LAYOUT_KEYS) xv1 = bv[b0 + tid + NT];
     }
-    // while they are in flight: the bitmap words' exclusive popcount prefix, the first chunk to LDS
-    uint32_t nmarked;
     {
+        uint32_t nmarked;
         const uint32_t pre = block_excl_scan_n<NT / 64>((uint32_t)__popc(wv), s_scratch, nmarked);
         if (tid < NWD) { s_w[tid] = wv; s_wpre[tid] = pre; }
-#pragma unroll
-        for (uint32_t r = 0; r < QR; ++r) {
-            const uint32_t i = tid + NT * r;
-            if (i < cn0) {
-                s_bk[i] = qk[r];
-                s_be[i] = qe[r];
-                s_bp[i] = qp[r];
-            }
-        }
+        if (tid < cn0) s_r[tid] = r0;
+        if (tid + NT < cn0) s_r[tid + NT] = r1;
     }
     __syncthreads();
-    const uint32_t natot = nown - nmarked;
+    // remainder index of every slot, then the extracted elements before it, chunk by chunk
+    uint32_t ao[KPT];
+    uint32_t valid = 0;
 #pragma unroll
     for (uint32_t j = 0; j < KPT; ++j) {
         const uint32_t i = j * NT + tid;
@@ -576,115 +587,84 @@ __global__ __launch_bounds__(NT) void k_ns_merge(uint32_t* keys, uint32_t* vals,
         const bool ok = in && !((wvi >> (i & 31u)) & 1u);
         ao[j] = i - (s_wpre[i >> 5 < NWD ? i >> 5 : NWD - 1] + (uint32_t)__popc(wvi & ((1u << (i & 31u)) - 1u)));
         valid |= ok ? (1u << j) : 0u;
-        if (hasb && ok) {
-            s_ak[ao[j]] = fk[j] & fmask;
-            s_ap[ao[j]] = (uint32_t)t0 + i;
-        }
     }
-    // (allv: every load has landed before the first write, which comes in the chunk loop)
-    if (allv) {
+    uint32_t bef[KPT];
 #pragma unroll
-        for (uint32_t j = 0; j < KPT; ++j) asm volatile("" ::"v"(fk[j]), "v"(fv[j]));
-    }
-    __syncthreads();
-    const uint32_t obase = (uint32_t)olo;   // = arank0 + b0: the tile's first output position
-    const uint32_t arank0 = obase - b0;
-    uint32_t bo = 0, be = 0;   // (one chunk: this thread's extracted element, written at the end)
-    bool bhas = false;
-    for (uint32_t c0 = b0; c0 < b1; c0 += kNsBChunk) {
-        const uint32_t cn = b1 - c0 < kNsBChunk ? b1 - c0 : kNsBChunk;
+    for (uint32_t j = 0; j < KPT; ++j) bef[j] = 0u;
+    for (uint32_t c0 = b0; c0 < b1; c0 += BC) {
+        const uint32_t cn = b1 - c0 < BC ? b1 - c0 : BC;
         if (c0 != b0) {   // (the first chunk is in LDS already)
-            __syncthreads();   // the previous chunk's readers are done
-            for (uint32_t i = tid; i < cn; i += NT) {
-                s_bk[i] = bm[c0 + i];
-                s_be[i] = ei[c0 + i];
-                s_bp[i] = bp[c0 + i];
-            }
+            __syncthreads();
+            for (uint32_t i = tid; i < cn; i += NT) s_r[i] = rank[c0 + i];
             __syncthreads();
         }
-        // the chunk's elements: output = extraction rank + remainder elements of the tile before them
-        for (uint32_t i = tid; i < cn; i += NT) {
-            const uint32_t kb = s_bk[i], pb = s_bp[i];
-            uint32_t l = 0, h = natot;
-            while (l < h) {
-                const uint32_t mid = (l + h) >> 1;
-                if (ns_less(s_ak[mid], s_ap[mid], kb, pb)) l = mid + 1;
-                else h = mid;
-            }
-            const uint32_t o = c0 + i + arank0 + l;
-            const uint32_t e = s_be[i];
-            if (allv) {
-                if (L == LAYOUT_KEYS) {
-                    keys[o] = sk[e];
-                } else if (L == LAYOUT_AOS) {
-                    reinterpret_cast<uint2*>(keys)[o] = make_uint2(sk[e], sv[e]);
-                } else {
-                    keys[o] = sk[e];
-                    vals[o] = sv[e];
-                }
-            } else {
-                bo = o;
-                be = e;
-                bhas = true;
-            }
-        }
-        // this thread's remainder elements: the chunk's elements before each
 #pragma unroll
-        for (uint32_t j = 0; j < KPT; ++j) {
-            if (!((valid >> j) & 1u)) continue;
-            const uint32_t ka = fk[j] & fmask, pa = (uint32_t)t0 + j * NT + tid;
+        for (uint32_t j = 0; j < KPT; ++j) {   // upper bound of the remainder index in the ranks
             uint32_t l = 0, h = cn;
             while (l < h) {
                 const uint32_t mid = (l + h) >> 1;
-                if (ns_less(s_bk[mid], s_bp[mid], ka, pa)) l = mid + 1;
+                if (s_r[mid] <= ao[j]) l = mid + 1;
                 else h = mid;
             }
-            ao[j] += l;
+            bef[j] += l;
         }
     }
-    // the movers: remainder elements whose output position is not their input position
-    uint32_t mv = 0;
+    // the movers: read (own output range in place, the rest from tmp, where k_ns_save put them)
+    const uint32_t obase = (uint32_t)olo;
+    const uint32_t alo = (uint32_t)(olo - (int64_t)t0 < 0 ? 0 : (olo - (int64_t)t0 > nown ? nown : olo - (int64_t)t0));
+    const uint32_t ahi = (uint32_t)(ohi - (int64_t)t0 < 0 ? 0 : (ohi - (int64_t)t0 > nown ? nown : ohi - (int64_t)t0));
+    uint32_t fk[KPT], fv[KPT], mv = 0;
 #pragma unroll
     for (uint32_t j = 0; j < KPT; ++j) {
         const uint32_t i = j * NT + tid;
-        mv |= (((valid >> j) & 1u) && obase + ao[j] != (uint32_t)t0 + i) ? (1u << j) : 0u;
-    }
-    if (SPLITV && !allv) {   // their values
-#pragma unroll
-        for (uint32_t j = 0; j < KPT; ++j) {
-            if (!((mv >> j) & 1u)) continue;
-            const uint32_t i = j * NT + tid;
-            fv[j] = (i >= alo && i < ahi) ? __builtin_amdgcn_raw_buffer_load_b32(rv, (int)(lo + j * NT * 4u), 0, 0)
-                                          : __builtin_amdgcn_raw_buffer_load_b32(rt, (int)(2u * lo + j * NT * 8u + 4u), 0, 0);
+        const uint32_t o = obase + ao[j] + bef[j];
+        ao[j] = o;
+        fk[j] = 0u;
+        fv[j] = 0u;
+        if (((valid >> j) & 1u) && o != (uint32_t)t0 + i) {
+            mv |= 1u << j;
+            const uint64_t p = t0 + i;
+            if (i >= alo && i < ahi) {
+                if (L == LAYOUT_AOS) {
+                    const uint2 q = reinterpret_cast<const uint2*>(keys)[p];
+                    fk[j] = q.x;
+                    fv[j] = q.y;
+                } else {
+                    fk[j] = keys[p];
+                    if (L == LAYOUT_SOA) fv[j] = vals[p];
+                }
+            } else {
+                if (L == LAYOUT_KEYS) {
+                    fk[j] = tmp[p];
+                } else {
+                    const uint2 q = reinterpret_cast<const uint2*>(tmp)[p];
+                    fk[j] = q.x;
+                    fv[j] = q.y;
+                }
+            }
         }
     }
     // every load of the workgroup has landed before any thread writes (in place)
 #pragma unroll
     for (uint32_t j = 0; j < KPT; ++j) asm volatile("" ::"v"(fk[j]), "v"(fv[j]));
     __syncthreads();
+    auto put = [&](uint32_t o, uint32_t k, uint32_t v) {
+        if (L == LAYOUT_KEYS) {
+            keys[o] = k;
+        } else if (L == LAYOUT_AOS) {
+            reinterpret_cast<uint2*>(keys)[o] = make_uint2(k, v);
+        } else {
+            keys[o] = k;
+            vals[o] = v;
+        }
+    };
 #pragma unroll
-    for (uint32_t j = 0; j < KPT; ++j) {
-        if (!((mv >> j) & 1u)) continue;
-        const uint32_t o = obase + ao[j];
-        if (L == LAYOUT_KEYS) {
-            keys[o] = fk[j];
-        } else if (L == LAYOUT_AOS) {
-            reinterpret_cast<uint2*>(keys)[o] = make_uint2(fk[j], fv[j]);
-        } else {
-            keys[o] = fk[j];
-            vals[o] = fv[j];
-        }
-    }
-    if (bhas) {
-        if (L == LAYOUT_KEYS) {
-            keys[bo] = sk[be];
-        } else if (L == LAYOUT_AOS) {
-            reinterpret_cast<uint2*>(keys)[bo] = make_uint2(sk[be], sv[be]);
-        } else {
-            keys[bo] = sk[be];
-            vals[bo] = sv[be];
-        }
-    }
+    for (uint32_t j = 0; j < KPT; ++j)
+        if ((mv >> j) & 1u) put(ao[j], fk[j], fv[j]);
+    if (tid < cn0) put(obase + r0 + tid, xk0, xv0);
+    if (tid + NT < cn0) put(obase + r1 + tid + NT, xk1, xv1);
+    for (uint32_t jj = b0 + BC + tid; jj < b1; jj += NT)   // (more than one chunk)
+        put(obase + rank[jj] + (jj - b0), bk[jj], L == LAYOUT_KEYS ? 0u : bv[jj]);
     }
 }
 

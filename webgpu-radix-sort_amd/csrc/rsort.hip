@@ -766,11 +766,13 @@ RS_EXPORT const char* rs_status_string(rs_status s) {
 RS_EXPORT uint32_t rs_version(void) { return (RSORT_VERSION_MAJOR << 16) | RSORT_VERSION_MINOR; }
 
 // The presorted path's workspace (rs_presorted.hpp): control words, per-tile counts / boundary keys /
-// offsets / bounds, the chunk sums, the extraction sort's totals, the mark bitmap, and eight arrays
-// of the extraction capacity (masked key and extraction index twice - the ping-pong of its sort -
-// then key, value, position, and the sorted positions).  Sized for min(capacity, kMsdMax) keys: the hybrid path never sorts more.
+// offsets / bounds, the chunk sums, the extraction sort's totals, the mark bitmap with its per-word
+// mark prefix and samples, and twelve arrays of the extraction capacity (masked key and extraction
+// index twice - the ping-pong of its sort - then key, value, position; the sorted positions, keys
+// and values; ranks and tiles).  Sized for min(capacity, kMsdMax) keys: the hybrid path never sorts more.
 struct NsWs {
-    uint32_t *ctl, *tcnt, *tbnd, *toff, *blo, *csum, *coff, *sub, *bitmap, *ek, *ei, *ek2, *ei2, *sk, *sv, *sp, *bp;
+    uint32_t *ctl, *tcnt, *tbnd, *toff, *blo, *csum, *coff, *sub, *bitmap, *wpre, *samp, *ek, *ei, *ek2, *ei2, *sk,
+        *sv, *sp, *bp, *bk, *bv, *rank, *tileof;
 };
 uint64_t ns_keys(uint64_t capacity) { return std::min<uint64_t>(capacity, kMsdMax); }
 // extraction capacity for n keys: n / 128 (config 4's n / 1000 transpositions mark ~n / 500), at
@@ -800,7 +802,11 @@ NsWs ns_layout(uint32_t* q, uint64_t capacity) {
     q += rs::kNsSubWords;
     w.bitmap = q;
     q += nt * (rs::kNsTile / 32);
-    uint32_t** arr[8] = {&w.ek, &w.ei, &w.ek2, &w.ei2, &w.sk, &w.sv, &w.sp, &w.bp};
+    w.wpre = q;                       // per bitmap word: the tile's marks before it
+    q += nt * (rs::kNsTile / 32);
+    w.samp = q;                       // per bitmap word: (key, position) sample (k_ns_mark, k_ns_rank)
+    q += 2 * nt * (rs::kNsTile / 32);
+    uint32_t** arr[12] = {&w.ek, &w.ei, &w.ek2, &w.ei2, &w.sk, &w.sv, &w.sp, &w.bp, &w.bk, &w.bv, &w.rank, &w.tileof};
     for (uint32_t** a : arr) {
         *a = q;
         q += cap;
@@ -808,7 +814,7 @@ NsWs ns_layout(uint32_t* q, uint64_t capacity) {
     return w;
 }
 uint64_t ns_words(uint64_t capacity) {
-    return (uint64_t)(ns_layout(nullptr, capacity).bp - (uint32_t*)nullptr) + ns_cap_for(ns_keys(capacity));
+    return (uint64_t)(ns_layout(nullptr, capacity).tileof - (uint32_t*)nullptr) + ns_cap_for(ns_keys(capacity));
 }
 
 RS_EXPORT rs_status rs_plan_create(const rs_plan_desc* desc, rs_plan** out) {
@@ -1077,7 +1083,7 @@ static rs_status enqueue_split(rs_plan* p, const rs::SplitWs& sw, bool keys, boo
 // The presorted path (rs_presorted.hpp) of a check_order sort, in place on the caller's data (uk /
 // uv: arrays, keys, or records in uk): mark -> decide -> extract -> the extraction's sort (its four
 // 8-bit digit totals from one read, then four one-sweep passes) -> gather -> bounds -> save ->
-// merge in place: 12 launches.  Every launch after k_ns_decide exits at once unless the device found the input nearly
+// rank -> merge in place: 13 launches.  Every launch after k_ns_decide exits at once unless the device found the input nearly
 // sorted; k_ns_merge then flags the data sorted (ctl[5]) and the radix path enqueued behind finds
 // it in order (the hybrid path's histogram read is skipped outright: k_hist16_in's `skip`).
 static rs_status enqueue_presorted(rs_plan* p, uint32_t* uk, uint32_t* uv, uint32_t n, hipStream_t s) {
@@ -1105,7 +1111,7 @@ static rs_status enqueue_presorted(rs_plan* p, uint32_t* uk, uint32_t* uv, uint3
     p->timer.run(RS_KERNEL_PRESORTED, s, [&] {
         auto mark = [&](auto kern) {
             hipLaunchKernelGGL(kern, dim3(resident(kern, ntiles, 256)), dim3(256), 0, s, (const uint32_t*)uk, n, fm,
-                               w.bitmap, w.tcnt, w.tbnd, w.ctl);
+                               w.bitmap, w.tcnt, w.tbnd, reinterpret_cast<uint2*>(w.samp), w.ctl);
         };
         L == A ? mark(rs::k_ns_mark<A>) : mark(rs::k_ns_mark<S>);   // (keys only reads as SOA)
         hipLaunchKernelGGL(rs::k_ns_decide, dim3((ntiles + 1023u) / 1024u), dim3(1024), 0, s, (const uint32_t*)w.tcnt,
@@ -1113,7 +1119,7 @@ static rs_status enqueue_presorted(rs_plan* p, uint32_t* uk, uint32_t* uv, uint3
         auto extract = [&](auto kern) {
             hipLaunchKernelGGL(kern, dim3(ntiles), dim3(64), 0, s, (const uint32_t*)uk, (const uint32_t*)uv, n, fm,
                                cap, (const uint32_t*)w.bitmap, (const uint32_t*)w.toff, (const uint32_t*)w.coff,
-                               (const uint32_t*)w.ctl, w.ek, w.ei, w.sk, w.sv, w.sp);
+                               (const uint32_t*)w.ctl, w.ek, w.ei, w.sk, w.sv, w.sp, w.wpre);
         };
         L == A ? extract(rs::k_ns_extract<A>) : L == S ? extract(rs::k_ns_extract<S>) : extract(rs::k_ns_extract<K>);
         // the extraction (masked key, extraction index) sorted stably, ek / ei -> ek2 / ei2 -> ... ->
@@ -1144,7 +1150,8 @@ static rs_status enqueue_presorted(rs_plan* p, uint32_t* uk, uint32_t* uv, uint3
     }
     p->timer.run(RS_KERNEL_PRESORTED, s, [&] {
         hipLaunchKernelGGL(rs::k_ns_gather, dim3(std::min<uint32_t>(cap / 256u, 4u * p->cus)), dim3(256), 0, s,
-                           (const uint32_t*)w.ei, (const uint32_t*)w.sp, (const uint32_t*)w.ctl, w.bp);
+                           (const uint32_t*)w.ei, (const uint32_t*)w.sp, (const uint32_t*)w.sk, (const uint32_t*)w.sv,
+                           (const uint32_t*)w.ctl, w.bp, w.bk, w.bv);
         auto bounds = [&](auto kern) {
             hipLaunchKernelGGL(kern, dim3((ntiles + 1u + 255u) / 256u), dim3(256), 0, s, (const uint32_t*)uk, n, fm,
                                (const uint32_t*)w.bitmap, ntiles, (const uint32_t*)w.ek, (const uint32_t*)w.bp,
@@ -1154,15 +1161,21 @@ static rs_status enqueue_presorted(rs_plan* p, uint32_t* uk, uint32_t* uv, uint3
         auto save = [&](auto kern) {
             hipLaunchKernelGGL(kern, dim3(ntiles), dim3(256), 0, s, (const uint32_t*)uk, (const uint32_t*)uv, n,
                                (const uint32_t*)w.toff, (const uint32_t*)w.coff, (const uint32_t*)w.blo,
-                               (const uint32_t*)w.ctl, p->tmp_k);
+                               (const uint32_t*)w.ctl, p->tmp_k, w.tileof);
         };
         L == A ? save(rs::k_ns_save<A>) : L == S ? save(rs::k_ns_save<S>) : save(rs::k_ns_save<K>);
+        auto rank = [&](auto kern) {
+            hipLaunchKernelGGL(kern, dim3(cap / 256u), dim3(256), 0, s, (const uint32_t*)uk, n, fm,
+                               (const uint32_t*)w.bitmap, (const uint32_t*)w.wpre,
+                               reinterpret_cast<const uint2*>(w.samp), (const uint32_t*)w.tileof,
+                               (const uint32_t*)w.ek, (const uint32_t*)w.bp, (const uint32_t*)w.ctl, w.rank);
+        };
+        L == A ? rank(rs::k_ns_rank<A>) : rank(rs::k_ns_rank<S>);
         auto merge = [&](auto kern) {
-            hipLaunchKernelGGL(kern, dim3(resident(kern, ntiles, 512)), dim3(512), 0, s, uk, uv, n, fm,
+            hipLaunchKernelGGL(kern, dim3(resident(kern, ntiles, 512)), dim3(512), 0, s, uk, uv, n,
                                (const uint32_t*)w.bitmap, (const uint32_t*)w.toff, (const uint32_t*)w.coff,
-                               (const uint32_t*)w.blo, (const uint32_t*)w.ei, (const uint32_t*)w.ek,
-                               (const uint32_t*)w.bp, (const uint32_t*)w.sk, (const uint32_t*)w.sv, w.ctl,
-                               (const uint32_t*)p->tmp_k);
+                               (const uint32_t*)w.blo, (const uint32_t*)w.rank, (const uint32_t*)w.bk,
+                               (const uint32_t*)w.bv, w.ctl, (const uint32_t*)p->tmp_k);
         };
         L == A ? merge(rs::k_ns_merge<A>) : L == S ? merge(rs::k_ns_merge<S>) : merge(rs::k_ns_merge<K>);
     }, "rsort.presorted.merge");

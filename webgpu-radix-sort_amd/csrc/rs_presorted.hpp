@@ -542,6 +542,36 @@ __global__ __launch_bounds__(NT) void k_ns_merge(uint32_t* keys, uint32_t* vals,
     // a later launch: k_hist16_in's skip)
     if (blockIdx.x == 0 && threadIdx.x == 0) ctl[5] = 1u;
     const uint32_t ntiles = (n + kNsTile - 1) / kNsTile;
+    // a tile's own loads - its output range, extracted-element range, bitmap word (threads 0 .. 123),
+    // the first chunk's ranks and data (this thread's two) - issued one tile ahead
+    struct Meta {
+        int64_t olo, ohi;
+        uint32_t b0, b1, wv, r0, r1, xk0, xv0, xk1, xv1;
+    };
+    auto fetch = [&](uint32_t t, Meta& q) {
+        const uint32_t tid = threadIdx.x;
+        const uint64_t t0 = (uint64_t)t * kNsTile;
+        const uint32_t nown = (uint32_t)((t0 + kNsTile < n ? t0 + kNsTile : n) - t0);
+        const uint32_t nwd = (nown + 31u) / 32u;
+        ns_out_range(toff, coff, blo, t, ntiles, n, q.olo, q.ohi);
+        q.b0 = blo[t];
+        q.b1 = blo[t + 1];
+        const uint32_t cn0 = q.b1 - q.b0 < BC ? q.b1 - q.b0 : BC;
+        q.wv = tid < nwd ? bitmap[(t0 >> 5) + tid] : 0u;
+        q.r0 = tid < cn0 ? rank[q.b0 + tid] : 0u;
+        q.r1 = tid + NT < cn0 ? rank[q.b0 + tid + NT] : 0u;
+        q.xk0 = q.xv0 = q.xk1 = q.xv1 = 0u;
+        if (tid < cn0) {
+            q.xk0 = bk[q.b0 + tid];
+            if (L != LAYOUT_KEYS) q.xv0 = bv[q.b0 + tid];
+        }
+        if (tid + NT < cn0) {
+            q.xk1 = bk[q.b0 + tid + NT];
+            if (L != LAYOUT_KEYS) q.xv1 = bv[q.b0 + tid + NT];
+        }
+    };
+    Meta cur;
+    if (blockIdx.x < ntiles) fetch(blockIdx.x, cur);
     for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
     // (per-slot positions recomputed each tile from an opaque copy of the thread index: hoisted out
     // of the tile loop they take a register each)
@@ -549,25 +579,11 @@ __global__ __launch_bounds__(NT) void k_ns_merge(uint32_t* keys, uint32_t* vals,
     asm volatile("" : "+v"(tid));
     const uint64_t t0 = (uint64_t)t * kNsTile;
     const uint32_t nown = (uint32_t)((t0 + kNsTile < n ? t0 + kNsTile : n) - t0);
-    const uint32_t nwd = (nown + 31u) / 32u;
-    int64_t olo, ohi;
-    ns_out_range(toff, coff, blo, t, ntiles, n, olo, ohi);
-    const uint32_t b0 = blo[t], b1 = blo[t + 1];
+    const int64_t olo = cur.olo, ohi = cur.ohi;
+    const uint32_t b0 = cur.b0, b1 = cur.b1, wv = cur.wv, r0 = cur.r0, r1 = cur.r1;
+    const uint32_t xk0 = cur.xk0, xv0 = cur.xv0, xk1 = cur.xk1, xv1 = cur.xv1;
     const uint32_t cn0 = b1 - b0 < BC ? b1 - b0 : BC;
     __syncthreads();   // the previous tile's readers of the LDS arrays are done
-    const uint32_t wv = tid < nwd ? bitmap[(t0 >> 5) + tid] : 0u;
-    const uint32_t r0 = tid < cn0 ? rank[b0 + tid] : 0u;
-    const uint32_t r1 = tid + NT < cn0 ? rank[b0 + tid + NT] : 0u;
-    // the extracted elements (the first chunk's, this thread's two): their data
-    uint32_t xk0 = 0, xv0 = 0, xk1 = 0, xv1 = 0;
-    if (tid < cn0) {
-        xk0 = bk[b0 + tid];
-        if (L != LAYOUT_KEYS) xv0 = bv[b0 + tid];
-    }
-    if (tid + NT < cn0) {
-        xk1 = bk[b0 + tid + NT];
-        if (L != LAYOUT_KEYS) xv1 = bv[b0 + tid + NT];
-    }
     {
         uint32_t nmarked;
         const uint32_t pre = block_excl_scan_n<NT / 64>((uint32_t)__popc(wv), s_scratch, nmarked);
@@ -644,6 +660,8 @@ __global__ __launch_bounds__(NT) void k_ns_merge(uint32_t* keys, uint32_t* vals,
             }
         }
     }
+    // the next tile's loads, in flight while this one writes
+    if (t + gridDim.x < ntiles) fetch(t + gridDim.x, cur);
     // every load of the workgroup has landed before any thread writes (in place)
 #pragma unroll
     for (uint32_t j = 0; j < KPT; ++j) asm volatile("" ::"v"(fk[j]), "v"(fv[j]));

@@ -465,8 +465,10 @@ def main() -> None:
         # inside the timed region HIP events bracket only the pass launches (the roofline's kernel:
         # the scatter passes, or the LSD passes of the device's fallback); every other launch group
         # runs back to back, as it does unprofiled
+        # (check_order: the presorted path's order scan too, the "check" kind: its roofline kernel)
+        timed_kinds = ("scatter", "fallback") + (("check",) if wl["check_order"] else ())
         for k in kernels:
-            k.set_profiling(True, kinds=("scatter", "fallback"))
+            k.set_profiling(True, kinds=timed_kinds)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for i in range(K):
@@ -492,7 +494,7 @@ def main() -> None:
             kern.dispatch()
         torch.cuda.synchronize()
         for name, v in kern.kernel_times(reset=True).items():
-            if name not in ("scatter", "fallback"):
+            if name not in timed_kinds:
                 # per-sort times of the untimed runs, scaled to K sorts (reported per step below)
                 kernel_ms[name] = {"ms": v["ms"] / nbd * K, "launches": round(v["launches"] / nbd * K)}
         kern.set_profiling(False)
@@ -625,6 +627,7 @@ def main() -> None:
         extra["bucket_split"] = {"levels": split_levels, "ms_per_sort": round(sp["ms"] / max(K, 1), 4)}
     if device_path == "hybrid_fallback":
         sc = fb        # the device took the LSD fallback: its passes are the pass launches
+    presorted = device_path == "presorted"
     # one-sweep path: one digit-count launch per sort instead of one per pass
     onesweep = msd or 0 < hist_launches < sc["launches"]
     bytes_per_key = 16 if wl["values"] else 8
@@ -639,9 +642,29 @@ def main() -> None:
             "ms_per_sort": round(bk["ms"] / max(K, 1), 4),
             "achieved_GBs": round(bucket_keys * bytes_per_key / (bk["ms"] / max(K, 1) / 1e3) / 1e9, 1),
             "frac": round(bucket_keys * bytes_per_key / (bk["ms"] / max(K, 1) / 1e3) / 1e9 / HBM_PEAK_GBS, 4)}
+    elif presorted:
+        # check_order, nearly sorted input: no radix pass ran (their launches are gated off)
+        ck = kernel_ms.get("check", {"ms": 0.0, "launches": 0})
+        ps = kernel_ms.get("presorted", {"ms": 0.0, "launches": 0})
+        extra["path"] = ("presorted: order scan marking the displaced keys (k_ns_mark), their extraction "
+                         "and stable sort, in-place merge of the movers (k_ns_merge); the radix "
+                         "launches behind it gated off")
+        extra["presorted_path"] = {"order_scan_ms_per_sort": round(ck["ms"] / max(K, 1), 4),
+                                   "rest_ms_per_sort": round(ps["ms"] / max(K, 1), 4)}
     elif bk["launches"]:
         extra["path"] = "LSD one-sweep passes (the hybrid MSD path's device-side fallback: skewed keys)"
-    if sc["launches"]:
+    if presorted:
+        # the roofline kernel: the order scan, the path's one full read (4 B per key)
+        ck = kernel_ms.get("check", {"ms": 0.0, "launches": 0})
+        if ck["launches"]:
+            avg_ms = ck["ms"] / ck["launches"]
+            achieved = n * 4 / (avg_ms / 1e3) / 1e9
+            roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                    "kernel": "k_ns_mark (order scan: every key read once, descents and their runs marked)",
+                    "avg_launch_ms": round(avg_ms, 4), "algorithmic_bytes_per_launch": n * 4,
+                    "lib_sha16": _lib_sha16(), "traffic_lib_sha16": None}
+    elif sc["launches"]:
         avg_ms = sc["ms"] / sc["launches"]
         achieved = scatter_keys * bytes_per_key / (avg_ms / 1e3) / 1e9
         # PMC traffic (tools/pmc_traffic.py, separate rocprofv3 passes): used only when it was
@@ -673,6 +696,10 @@ def main() -> None:
     hist_reads = max(1, round(hist / max(K, 1))) if hist else passes
     if use_dist and hist:
         hist_reads = 1   # one totals read per group sort: each key once per step
+    if presorted:
+        # no radix pass: one read of the keys (the order scan); the moved records are few
+        passes = 0
+        hist_reads = 1
     if msd:
         # MSD pass 0, MSD pass 1, bucket pass; one read of the input for the 16-bit histogram
         # (4 B/key arrays; records are read whole: 8 B/key = two 4-byte key reads)

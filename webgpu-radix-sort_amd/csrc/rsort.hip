@@ -1108,12 +1108,17 @@ static rs_status enqueue_presorted(rs_plan* p, uint32_t* uk, uint32_t* uv, uint3
         static const uint32_t per_cu = resident_per_cu(kern, (int)block);
         return std::max(1u, std::min<uint32_t>(units, p->cus * per_cu));
     };
-    p->timer.run(RS_KERNEL_PRESORTED, s, [&] {
+    // the order scan (k_ns_mark) is timed as the order check it is (RS_KERNEL_CHECK), the rest of the
+    // path as RS_KERNEL_PRESORTED
+    p->timer.run(RS_KERNEL_CHECK, s, [&] {
         auto mark = [&](auto kern) {
             hipLaunchKernelGGL(kern, dim3(resident(kern, ntiles, 256)), dim3(256), 0, s, (const uint32_t*)uk, n, fm,
                                w.bitmap, w.tcnt, w.tbnd, reinterpret_cast<uint2*>(w.samp), w.ctl);
         };
         L == A ? mark(rs::k_ns_mark<A>) : mark(rs::k_ns_mark<S>);   // (keys only reads as SOA)
+    }, "rsort.presorted.mark");
+    HIP_TRY(hipGetLastError());
+    p->timer.run(RS_KERNEL_PRESORTED, s, [&] {
         hipLaunchKernelGGL(rs::k_ns_decide, dim3((ntiles + 1023u) / 1024u), dim3(1024), 0, s, (const uint32_t*)w.tcnt,
                            (const uint32_t*)w.tbnd, ntiles, cap, w.toff, w.csum, w.coff, w.sub, w.ctl);
         auto extract = [&](auto kern) {
@@ -1127,7 +1132,7 @@ static rs_status enqueue_presorted(rs_plan* p, uint32_t* uk, uint32_t* uv, uint3
         // the passes (16K-key tiles, decoupled look-back)
         hipLaunchKernelGGL(rs::k_ns_totals, dim3(std::min<uint32_t>(cap / 2048u, p->cus)), dim3(256), 0, s,
                            (const uint32_t*)w.ek, cap, (const uint32_t*)w.ctl, w.sub);
-    }, "rsort.presorted.mark");
+    }, "rsort.presorted.extract");
     HIP_TRY(hipGetLastError());
     const bool ballot = p->rank_mode == rs::RANK_BALLOT;
     for (uint32_t i = 0; i < 4; ++i) {

@@ -1086,6 +1086,11 @@ static rs_status enqueue_split(rs_plan* p, const rs::SplitWs& sw, bool keys, boo
 // rank -> merge in place: 13 launches.  Every launch after k_ns_decide exits at once unless the device found the input nearly
 // sorted; k_ns_merge then flags the data sorted (ctl[5]) and the radix path enqueued behind finds
 // it in order (the hybrid path's histogram read is skipped outright: k_hist16_in's `skip`).
+#if !RS_KNOB_OPEN || !defined(RS_NS_MERGE_NT)
+#undef RS_NS_MERGE_NT
+#define RS_NS_MERGE_NT 512   // k_ns_merge threads per workgroup (one tile each)
+#endif
+constexpr uint32_t kNsMergeNT = RS_NS_MERGE_NT;
 static rs_status enqueue_presorted(rs_plan* p, uint32_t* uk, uint32_t* uv, uint32_t n, hipStream_t s) {
     constexpr int K = rs::LAYOUT_KEYS, S = rs::LAYOUT_SOA, A = rs::LAYOUT_AOS;
     const NsWs w = ns_layout(p->ns, p->capacity);
@@ -1177,12 +1182,13 @@ static rs_status enqueue_presorted(rs_plan* p, uint32_t* uk, uint32_t* uv, uint3
         };
         L == A ? rank(rs::k_ns_rank<A>) : rank(rs::k_ns_rank<S>);
         auto merge = [&](auto kern) {
-            hipLaunchKernelGGL(kern, dim3(resident(kern, ntiles, 512)), dim3(512), 0, s, uk, uv, n,
+            hipLaunchKernelGGL(kern, dim3(resident(kern, ntiles, kNsMergeNT)), dim3(kNsMergeNT), 0, s, uk, uv, n,
                                (const uint32_t*)w.bitmap, (const uint32_t*)w.toff, (const uint32_t*)w.coff,
                                (const uint32_t*)w.blo, (const uint32_t*)w.rank, (const uint32_t*)w.bk,
                                (const uint32_t*)w.bv, w.ctl, (const uint32_t*)p->tmp_k);
         };
-        L == A ? merge(rs::k_ns_merge<A>) : L == S ? merge(rs::k_ns_merge<S>) : merge(rs::k_ns_merge<K>);
+        L == A ? merge(rs::k_ns_merge<A, kNsMergeNT>) : L == S ? merge(rs::k_ns_merge<S, kNsMergeNT>)
+               : merge(rs::k_ns_merge<K, kNsMergeNT>);
     }, "rsort.presorted.merge");
     HIP_TRY(hipGetLastError());
     return RS_OK;

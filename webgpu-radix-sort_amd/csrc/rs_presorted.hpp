@@ -53,6 +53,24 @@ __device__ __forceinline__ uint32_t ns_key(const uint32_t* keys, uint64_t i) {
     return keys[(L == LAYOUT_AOS ? 2ull : 1ull) * i];
 }
 
+// A sample of the order before any tile is read: kNsProbe adjacent pairs, one at a pseudo-random
+// place in each of kNsProbe equal strides.  More than 1/16 of them descending (random input: about
+// half; the count in ctl[7]) turns the path off, so that k_ns_mark's workgroups stop at once.
+// Nearly sorted input (config 4: 0.2 % descents) is far below that.  A sample per thread.
+constexpr uint32_t kNsProbe = 16384;
+__device__ __forceinline__ bool ns_probe_off(const uint32_t* ctl) { return ctl[7] > kNsProbe / 16u; }
+template <int L>
+__global__ __launch_bounds__(256) void k_ns_probe(const uint32_t* __restrict__ keys, uint32_t n, uint32_t fmask,
+                                                  uint32_t* ctl) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;   // (grid: kNsProbe / 256)
+    const uint64_t step = (uint64_t)(n - 1) / kNsProbe;   // (n >= 12M: step >= 1)
+    // (jittered inside its stride: a periodic pattern in the input must not alias the samples)
+    const uint64_t p = (uint64_t)i * step + ((i * 0x9E3779B9u) >> 8) % step;
+    uint32_t c = (ns_key<L>(keys, p) & fmask) > (ns_key<L>(keys, p + 1) & fmask) ? 1u : 0u;
+    c = wave_sum(c);
+    if (lane_id() == 0 && c) atomicAdd(ctl + 7, c);
+}
+
 // Persistent grid: workgroup g takes tiles g, g + grid, ... in order, with the next tile's window
 // loaded into registers while this one is marked.  Thread g holds window group g (16 consecutive
 // keys) in registers; the marks live in LDS as one 16-bit word per group.  A tile with more than
@@ -92,6 +110,7 @@ __global__ __launch_bounds__(256) void k_ns_mark(const uint32_t* __restrict__ ke
         for (uint32_t j = 0; j < G; ++j)
             r[j] = __builtin_amdgcn_raw_buffer_load_b32(rk, (int)(off + j * ESZ), 0, 0) & fmask;
     };
+    if (ns_probe_off(ctl)) return;   // the probe found the input far from sorted
     uint32_t k[G], kn[G];
     uint32_t t = blockIdx.x;
     if (t < ntiles) load(t, k);
@@ -237,7 +256,8 @@ __global__ __launch_bounds__(256) void k_ns_mark(const uint32_t* __restrict__ ke
 // extraction relative to their chunk (toff) and the chunk total (csum); an inversion between two
 // tiles' remainders (the last remainder key of a tile against the first of the next) sets ctl[2].
 // The last workgroup to finish (arrival count ctl[6]) then scans the chunk totals into coff and
-// decides - on iff no tile failed (ctl[1]), none was dense (ctl[3]), the remainder is in order
+// decides - on iff the probe's sample was nearly sorted (ctl[7]), no tile failed (ctl[1]), none
+// was dense (ctl[3]), the remainder is in order
 // across every tile boundary (ctl[2]) and 0 < marked <= cap.  On: m = ctl[4], every gate word 1,
 // the extraction sort's digit totals and tickets (sub) zeroed.  Off: gate words 0 (the radix path
 // runs as without this path).  A tile's offset: ns_toff().
@@ -251,7 +271,7 @@ __global__ __launch_bounds__(1024) void k_ns_decide(const uint32_t* __restrict__
     __shared__ uint32_t s_last;
     const uint32_t tid = threadIdx.x;
     const uint32_t nch = gridDim.x;   // (ntiles + 1023) / 1024 <= 1024 (n < 2^32)
-    bool on = !ctl[1] && !ctl[3];     // (uniform)
+    bool on = !ctl[1] && !ctl[3] && !ns_probe_off(ctl);   // (uniform)
     if (on) {
         const uint32_t t = blockIdx.x * 1024u + tid;
         const uint32_t c = t < ntiles ? tcnt[t] : 0u;
@@ -297,10 +317,11 @@ __device__ __forceinline__ uint32_t ns_toff(const uint32_t* toff, const uint32_t
 
 // The marked elements of every tile, in position order, to the extraction: ek = masked key, ei =
 // extraction index (the LSD passes sort (ek, ei) stably), sk / sv / sp = key, value, position in
-// extraction order.  Past m: pads (the largest key, after every real one in a stable sort).  One
-// wave per tile (no barrier): lane l takes bitmap words 2l and 2l + 1.
+// extraction order.  Past m: pads (the largest key, after every real one in a stable sort).  A
+// grid-stride loop of waves, launched a wave per tile (no barrier): lane l takes bitmap words 2l and
+// 2l + 1.
 template <int L>
-__global__ __launch_bounds__(64) void k_ns_extract(const uint32_t* __restrict__ keys,
+__global__ __launch_bounds__(256) void k_ns_extract(const uint32_t* __restrict__ keys,
                                                    const uint32_t* __restrict__ vals, uint32_t n,
                                                    uint32_t fmask, uint32_t cap,
                                                    const uint32_t* __restrict__ bitmap,
@@ -311,13 +332,17 @@ __global__ __launch_bounds__(64) void k_ns_extract(const uint32_t* __restrict__ 
                                                    uint32_t* __restrict__ sp, uint32_t* __restrict__ wpre) {
     static_assert(kNsTile / 32 <= 128, "two bitmap words per lane");
     if (!ctl[kNsGate]) return;
-    const uint32_t lane = threadIdx.x, t = blockIdx.x;
+    const uint32_t lane = lane_id(), gw = blockIdx.x * (blockDim.x / 64u) + (threadIdx.x >> 6);
+    const uint32_t nw = gridDim.x * (blockDim.x / 64u);   // waves in the grid
     const uint32_t m = ctl[4];
     // pads (grid-stride over the extraction's tail)
-    for (uint64_t e = (uint64_t)m + (uint64_t)t * 64u + lane; e < cap; e += (uint64_t)gridDim.x * 64u) {
+    for (uint64_t e = (uint64_t)m + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < cap;
+         e += (uint64_t)gridDim.x * blockDim.x) {
         ek[e] = 0xFFFFFFFFu;
         ei[e] = (uint32_t)e;
     }
+    const uint32_t ntiles = (n + kNsTile - 1) / kNsTile;
+    for (uint32_t t = gw; t < ntiles; t += nw) {
     const uint64_t t0 = (uint64_t)t * kNsTile;
     const uint32_t nown = (uint32_t)((t0 + kNsTile < n ? t0 + kNsTile : n) - t0);
     const uint32_t nwords = (nown + 31u) / 32u;   // <= 124
@@ -345,6 +370,7 @@ __global__ __launch_bounds__(64) void k_ns_extract(const uint32_t* __restrict__ 
     };
     take(b0, w0);
     take(b1, w1);
+    }
 }
 
 // (masked key, position) order
@@ -429,7 +455,8 @@ __device__ __forceinline__ void ns_out_range(const uint32_t* toff, const uint32_
 // The merge runs in place: a tile reads the positions of its own output range straight from the
 // caller's arrays (nobody else writes them, and it writes them only after its reads); every other
 // position of its input - the part another tile's output covers - is saved first, here, to the same
-// position of the plan buffer tmp (records; keys only: keys).  One workgroup per tile.
+// position of the plan buffer tmp (records; keys only: keys).  A persistent grid, a workgroup per
+// tile at a time.
 template <int L>
 __global__ __launch_bounds__(256) void k_ns_save(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals,
                                                  uint32_t n, const uint32_t* __restrict__ toff,
@@ -437,8 +464,9 @@ __global__ __launch_bounds__(256) void k_ns_save(const uint32_t* __restrict__ ke
                                                  const uint32_t* ctl, uint32_t* __restrict__ tmp,
                                                  uint32_t* __restrict__ tileof) {
     if (!ctl[kNsGate]) return;
-    const uint32_t t = blockIdx.x, tid = threadIdx.x;
+    const uint32_t tid = threadIdx.x;
     const uint32_t ntiles = (n + kNsTile - 1) / kNsTile;
+    for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
     const int64_t t0 = (int64_t)t * kNsTile;
     const int64_t t1 = t + 1 < ntiles ? t0 + kNsTile : (int64_t)n;
     int64_t olo, ohi;
@@ -459,6 +487,7 @@ __global__ __launch_bounds__(256) void k_ns_save(const uint32_t* __restrict__ ke
     save(t0, a1);
     save(b0 > a1 ? b0 : a1, t1);
     for (uint32_t j = blo[t] + tid; j < blo[t + 1]; j += 256) tileof[j] = t;   // (for k_ns_rank)
+    }
 }
 
 // Threads j < m: rank[j] = the remainder elements of sorted extracted element j's tile (tileof,

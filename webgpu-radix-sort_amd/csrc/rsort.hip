@@ -1116,6 +1116,10 @@ static rs_status enqueue_presorted(rs_plan* p, uint32_t* uk, uint32_t* uv, uint3
     // the order scan (k_ns_mark) is timed as the order check it is (RS_KERNEL_CHECK), the rest of the
     // path as RS_KERNEL_PRESORTED
     p->timer.run(RS_KERNEL_CHECK, s, [&] {
+        auto probe = [&](auto kern) {
+            hipLaunchKernelGGL(kern, dim3(rs::kNsProbe / 256u), dim3(256), 0, s, (const uint32_t*)uk, n, fm, w.ctl);
+        };
+        L == A ? probe(rs::k_ns_probe<A>) : probe(rs::k_ns_probe<S>);
         auto mark = [&](auto kern) {
             hipLaunchKernelGGL(kern, dim3(resident(kern, ntiles, 256)), dim3(256), 0, s, (const uint32_t*)uk, n, fm,
                                w.bitmap, w.tcnt, w.tbnd, reinterpret_cast<uint2*>(w.samp), w.ctl);
@@ -1127,7 +1131,9 @@ static rs_status enqueue_presorted(rs_plan* p, uint32_t* uk, uint32_t* uv, uint3
         hipLaunchKernelGGL(rs::k_ns_decide, dim3((ntiles + 1023u) / 1024u), dim3(1024), 0, s, (const uint32_t*)w.tcnt,
                            (const uint32_t*)w.tbnd, ntiles, cap, w.toff, w.csum, w.coff, w.sub, w.ctl);
         auto extract = [&](auto kern) {
-            hipLaunchKernelGGL(kern, dim3(ntiles), dim3(64), 0, s, (const uint32_t*)uk, (const uint32_t*)uv, n, fm,
+            // (a wave per tile: a persistent grid measured slower, 75 vs 63 us at config 4)
+            hipLaunchKernelGGL(kern, dim3((ntiles + 3u) / 4u), dim3(256), 0, s,
+                               (const uint32_t*)uk, (const uint32_t*)uv, n, fm,
                                cap, (const uint32_t*)w.bitmap, (const uint32_t*)w.toff, (const uint32_t*)w.coff,
                                (const uint32_t*)w.ctl, w.ek, w.ei, w.sk, w.sv, w.sp, w.wpre);
         };
@@ -1169,8 +1175,9 @@ static rs_status enqueue_presorted(rs_plan* p, uint32_t* uk, uint32_t* uv, uint3
         };
         L == A ? bounds(rs::k_ns_bounds<A>) : bounds(rs::k_ns_bounds<S>);
         auto save = [&](auto kern) {
-            hipLaunchKernelGGL(kern, dim3(ntiles), dim3(256), 0, s, (const uint32_t*)uk, (const uint32_t*)uv, n,
-                               (const uint32_t*)w.toff, (const uint32_t*)w.coff, (const uint32_t*)w.blo,
+            hipLaunchKernelGGL(kern, dim3(resident(kern, ntiles, 256)), dim3(256), 0, s, (const uint32_t*)uk,
+                               (const uint32_t*)uv, n, (const uint32_t*)w.toff, (const uint32_t*)w.coff,
+                               (const uint32_t*)w.blo,
                                (const uint32_t*)w.ctl, p->tmp_k, w.tileof);
         };
         L == A ? save(rs::k_ns_save<A>) : L == S ? save(rs::k_ns_save<S>) : save(rs::k_ns_save<K>);

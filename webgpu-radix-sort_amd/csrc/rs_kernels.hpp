@@ -358,6 +358,46 @@ struct Slots<KPT, true> {
 // published digit count (rank_tile's npad), the next-pass totals and the scatter exclude them.
 constexpr uint32_t kPadKey = 0xFFFFFFFFu;
 
+// A bucket's records (KV: 8-byte records, key then value; else keys) into slots j of lane l of the
+// wave at wbase: position wbase + 64 j + l, pads (kPadKey) from cnt on.  Buffer loads bounded to the
+// bucket (past cnt they return 0): no per-slot branch.  (load_tile's per-slot `if` compiles, in the
+// larger bucket tiles - 256 x 34, 1024 x 17 - to a branch per slot whose load waits for itself
+// before the branch joins: one memory latency per slot.)
+template <int KPT, bool KV>
+__device__ __forceinline__ void load_bucket(const uint32_t* src, uint32_t wbase, uint32_t cnt, uint32_t (&k)[KPT],
+                                            uint32_t (&v)[KV ? KPT : 1]) {
+    constexpr uint32_t ESZ = KV ? 8u : 4u;
+    const uint32_t lane = lane_id();
+    // (src and cnt are the workgroup's bucket: uniform, made scalar - a descriptor the compiler cannot
+    // prove uniform is issued in a loop over the lanes' distinct values)
+    // (readfirstlane returns int: each half goes through uint32_t, else the low half's bit 31 would
+    // sign-extend over the high half)
+    cnt = (uint32_t)__builtin_amdgcn_readfirstlane(cnt);
+    const uint64_t sa = reinterpret_cast<uint64_t>(src);
+    const uint32_t sa_hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(sa >> 32));
+    const uint32_t sa_lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)sa);
+    src = reinterpret_cast<const uint32_t*>(((uint64_t)sa_hi << 32) | (uint64_t)sa_lo);
+    const int lim = (int)cnt - (int)(wbase + lane);
+    const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, (int)(cnt * ESZ), 0x00020000);
+    uint32_t lo = (wbase + lane) * ESZ;   // (one offset register, immediate slot offsets)
+    asm volatile("" : "+v"(lo));
+#pragma unroll
+    for (int j = 0; j < KPT; ++j) {
+        uint32_t kk;
+        if constexpr (KV) {
+            const auto q = __builtin_amdgcn_raw_buffer_load_b64(rr, (int)(lo + j * 64 * ESZ), 0, 0);
+            kk = q[0];
+            v[j] = q[1];
+        } else {
+            kk = __builtin_amdgcn_raw_buffer_load_b32(rr, (int)(lo + j * 64 * ESZ), 0, 0);
+        }
+        // (the pad mask opaque: a select on the loaded word would become a branch again)
+        uint32_t m = j * 64 < lim ? 0xFFFFFFFFu : 0u;
+        asm volatile("" : "+v"(m));
+        k[j] = (kk & m) | (kPadKey & ~m);
+    }
+}
+
 template <int KPT, int L, bool CLAMP = false>
 __device__ __forceinline__ void load_tile(const uint32_t* __restrict__ in_k,
                                           const uint32_t* __restrict__ in_v, uint64_t wbase,
@@ -2466,7 +2506,9 @@ __global__ __launch_bounds__(BLOCK, MW) void k_bucket_sort8(const uint32_t* rec,
         if (cnt == 0u || cnt > (uint32_t)TILE) continue;        // (never: the lists' bounds)
         if ((uint64_t)base + cnt > sw.n) continue;              // (never: a counting fault, reported)
         uint32_t k[KPT], v[KV ? KPT : 1];
-        load_tile<KPT, LI>(rec + (KV ? 2ull : 1ull) * base, nullptr, wbase, cnt, false, k, v);
+        // (branch-free, load_bucket; 256 x 17 records: load_tile, whose code there has no per-slot wait)
+        if constexpr (!KV || KPT > 24) load_bucket<KPT, KV>(rec + (KV ? 2ull : 1ull) * base, wbase, cnt, k, v);
+        else load_tile<KPT, LI>(rec + (KV ? 2ull : 1ull) * base, nullptr, wbase, cnt, false, k, v);
         if (cnt > 1u) {
             for (uint32_t p = 0, shift = 0; p < (LISTED ? 1u : 2u); ++p, shift += 8u) {
                 Slots<KPT, PACK> rank;
@@ -2585,7 +2627,14 @@ __global__ __launch_bounds__(BLOCK, MW) void k_bucket_sort(const uint32_t* rec,
     if (it >= nb) return;
     uint32_t k[KPT], v[KV ? KPT : 1];
     uint32_t k2[PF ? KPT : 1], v2[PF && KV ? KPT : 1];
-    load_tile<KPT, LI>(rec + (KV ? 2ull : 1ull) * rstart(bucket_of(it)), nullptr, wbase, cnt, false, k, v);
+    // keys and the larger tiles load branch-free (load_bucket); the 256 x (<= 24) record tiles keep
+    // load_tile, whose code for them has no per-slot wait
+    constexpr bool BUF = !KV || KPT > 24 || BLOCK > 256;
+    auto load = [&](const uint32_t* src, uint32_t c, uint32_t (&kk)[KPT], uint32_t (&vv)[KV ? KPT : 1]) {
+        if constexpr (BUF) load_bucket<KPT, KV>(src, wbase, c, kk, vv);
+        else load_tile<KPT, LI>(src, nullptr, wbase, c, false, kk, vv);
+    };
+    load(rec + (KV ? 2ull : 1ull) * rstart(bucket_of(it)), cnt, k, v);
     while (true) {
         const uint32_t b = bucket_of(it);
         const uint32_t base = bstart(b);
@@ -2593,8 +2642,7 @@ __global__ __launch_bounds__(BLOCK, MW) void k_bucket_sort(const uint32_t* rec,
         const uint32_t nit = next_valid(it + gridDim.x, ncnt);
         if constexpr (PF != 0) {
             if (nit < nb)
-                load_tile<KPT, LI>(rec + (KV ? 2ull : 1ull) * rstart(bucket_of(nit)), nullptr, wbase,
-                                   ncnt, false, k2, v2);
+                load(rec + (KV ? 2ull : 1ull) * rstart(bucket_of(nit)), ncnt, k2, v2);
         }
         if (cnt > 1u) {
             for (uint32_t p = 0, shift = 0; p < 2u; ++p, shift += 8u) {
@@ -2654,7 +2702,7 @@ __global__ __launch_bounds__(BLOCK, MW) void k_bucket_sort(const uint32_t* rec,
                 if constexpr (KV) v[j] = v2[j];
             }
         } else {
-            load_tile<KPT, LI>(rec + (KV ? 2ull : 1ull) * rstart(bucket_of(it)), nullptr, wbase, cnt, false, k, v);
+            load(rec + (KV ? 2ull : 1ull) * rstart(bucket_of(it)), cnt, k, v);
         }
     }
 }
@@ -2723,21 +2771,27 @@ __global__ __launch_bounds__(BLOCK, MW) void k_bucket_sort_wide(const uint32_t* 
     };
     auto src_of = [&](uint32_t b) { return rec + (KV ? 2ull : 1ull) * ((sstart[b >> 8] + base16[b]) & rmask); };
     // w = (low 16 bits of the key) << 16 | position (KV), or the key (keys only); pads kPadKey
+    // Branch-free buffer loads over the bucket's records (lanes past cnt read 0): a load under a
+    // per-slot branch waits for itself before the branch joins, one memory latency per slot.
+    constexpr uint32_t ESZ = KV ? 8u : 4u;
+    auto bucket_rsrc = [](const uint32_t* src, uint32_t cnt) {
+        return __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, (int)(cnt * ESZ), 0x00020000);
+    };
     auto load_words = [&](const uint32_t* src, uint32_t cnt, uint32_t (&xx)[KPT], uint32_t (&vv)[VR ? KPT : 1]) {
         const int lim = (int)cnt - (int)(wbase + lane);
-        const uint2* sr = reinterpret_cast<const uint2*>(src) + wbase + lane;
-        const uint32_t* sk = src + wbase + lane;
+        const __amdgpu_buffer_rsrc_t rr = bucket_rsrc(src, cnt);
+        uint32_t lo = (wbase + lane) * ESZ;   // (one offset register, immediate slot offsets)
+        asm volatile("" : "+v"(lo));
 #pragma unroll
         for (int j = 0; j < KPT; ++j) {
-            if (VR) {
-                const uint2 r = j * 64 < lim ? sr[j * 64] : make_uint2(0u, 0u);
-                xx[j] = j * 64 < lim ? ((r.x & 0xFFFFu) << 16) | (wbase + (uint32_t)j * 64u + lane) : kPadKey;
-                vv[VR ? j : 0] = r.y;
-            } else if (KV) {
-                xx[j] = j * 64 < lim ? ((sr[j * 64].x & 0xFFFFu) << 16) | (wbase + (uint32_t)j * 64u + lane) : kPadKey;
-            } else {
-                xx[j] = j * 64 < lim ? sk[j * 64] : kPadKey;
-            }
+            const uint32_t kw = __builtin_amdgcn_raw_buffer_load_b32(rr, (int)(lo + j * 64 * ESZ), 0, 0);
+            if (VR) vv[VR ? j : 0] = __builtin_amdgcn_raw_buffer_load_b32(rr, (int)(lo + j * 64 * ESZ + 4), 0, 0);
+            // (the pad mask opaque: a select on the loaded word becomes a branch with the load sunk
+            // into it, and the wait with it)
+            uint32_t m = j * 64 < lim ? 0xFFFFFFFFu : 0u;
+            asm volatile("" : "+v"(m));
+            const uint32_t wd = KV ? ((kw & 0xFFFFu) << 16) | (wbase + (uint32_t)j * 64u + lane) : kw;
+            xx[j] = (wd & m) | (kPadKey & ~m);
         }
     };
     uint32_t cnt = 0;
@@ -2774,12 +2828,14 @@ __global__ __launch_bounds__(BLOCK, MW) void k_bucket_sort_wide(const uint32_t* 
         // sorted slot reads its value straight from the record instead (no LDS round).
         constexpr bool GATHER = RS_WIDE_GATHER && KV && !VR && LO == LAYOUT_SOA;
         if (KV && !GATHER) {
-            const int lim = (int)cnt - (int)(wbase + lane);
-            const uint2* sr = reinterpret_cast<const uint2*>(src) + wbase + lane;
+            // (unconditional: a slot past cnt writes the 0 its load returned to an unused position)
+            const __amdgpu_buffer_rsrc_t rr = bucket_rsrc(src, cnt);
+            uint32_t lo = (wbase + lane) * ESZ + 4u;
+            asm volatile("" : "+v"(lo));
             uint32_t* sw = s_w + wbase + lane;
 #pragma unroll
             for (int j = 0; j < KPT; ++j)
-                if (j * 64 < lim) sw[j * 64] = VR ? v[VR ? j : 0] : sr[j * 64].y;
+                sw[j * 64] = VR ? v[VR ? j : 0] : __builtin_amdgcn_raw_buffer_load_b32(rr, (int)(lo + j * 64 * ESZ), 0, 0);
             __syncthreads();
         }
         const uint32_t hi = b << bshift;

@@ -661,9 +661,19 @@ def main() -> None:
             achieved = n * 4 / (avg_ms / 1e3) / 1e9
             roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                    "kernel": "k_ns_mark (order scan: every key read once, descents and their runs marked)",
+                    "kernel": "k_ns_mark (order scan: every key read once, descents and their runs "
+                              "marked; timed with the 16K-pair k_ns_probe before it, ~4 us)",
                     "avg_launch_ms": round(avg_ms, 4), "algorithmic_bytes_per_launch": n * 4,
                     "lib_sha16": _lib_sha16(), "traffic_lib_sha16": None}
+            # PMC traffic of k_ns_mark (tools/r05/pmc_kernels.py), when measured on this very library
+            try:
+                with open(args.traffic_json) as f:
+                    tj = json.load(f).get(args.workload) or {}
+                roof["traffic_lib_sha16"] = tj.get("lib_sha16")
+                if "mark_bytes_per_launch" in tj and tj.get("lib_sha16") == roof["lib_sha16"] and not use_dist:
+                    roof["traffic"] = tj["mark_bytes_per_launch"]
+            except (OSError, ValueError):
+                pass
     elif sc["launches"]:
         avg_ms = sc["ms"] / sc["launches"]
         achieved = scatter_keys * bytes_per_key / (avg_ms / 1e3) / 1e9

@@ -2627,9 +2627,11 @@ __global__ __launch_bounds__(BLOCK, MW) void k_bucket_sort(const uint32_t* rec,
     if (it >= nb) return;
     uint32_t k[KPT], v[KV ? KPT : 1];
     uint32_t k2[PF ? KPT : 1], v2[PF && KV ? KPT : 1];
-    // keys and the larger tiles load branch-free (load_bucket); the 256 x (<= 24) record tiles keep
-    // load_tile, whose code for them has no per-slot wait
-    constexpr bool BUF = !KV || KPT > 24 || BLOCK > 256;
+    // branch-free loads (load_bucket) but for the 256 x (<= 24) tiles writing records (texture
+    // layout), whose load_tile code has no per-slot wait: measured at config 3, separate arrays
+    // 0.845 -> 0.770 ms per bucket pass with load_bucket, records 0.851 -> 0.879
+    // (profiles/r05/ab_bucket_buf/)
+    constexpr bool BUF = LO != LAYOUT_AOS || KPT > 24 || BLOCK > 256;
     auto load = [&](const uint32_t* src, uint32_t c, uint32_t (&kk)[KPT], uint32_t (&vv)[KV ? KPT : 1]) {
         if constexpr (BUF) load_bucket<KPT, KV>(src, wbase, c, kk, vv);
         else load_tile<KPT, LI>(src, nullptr, wbase, c, false, kk, vv);

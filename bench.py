@@ -372,6 +372,8 @@ def main() -> None:
     ap.add_argument("--rank", default="lds", choices=["lds", "ballot"],
                     help="in-wave ranking: lane-ordered LDS atomics (default, self-tested per device) or "
                          "the architecture-guaranteed ballot ranking (rs_plan_debug.rank = 1)")
+    ap.add_argument("--plan-debug", default="",
+                    help="A/B diagnostics: rs_plan_debug overrides for every plan, e.g. 'xcd=0,presorted=0'")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--distributed", action="store_true",
                     help="use the bucket-exchange path even at world size 1 (testing)")
@@ -401,6 +403,9 @@ def main() -> None:
     from radix_sort_amd import RadixSortKernel, RadixSortTextureKernel, _lib, ops
     if args.rank == "ballot":   # every plan of this process ranks by ballot
         _lib.plan_debug(rank="ballot").__enter__()
+    if args.plan_debug:         # e.g. xcd=0: every plan of this process (A/B runs; marked in the line)
+        fields = dict(kv.split("=", 1) for kv in args.plan_debug.split(","))
+        _lib.plan_debug(**{k: int(v) for k, v in fields.items()}).__enter__()
     from radix_sort_amd.distributed import (HipLocalOps, StepTimeline, distributed_sort,
                                             summarize_timelines, timeline_record)
 
@@ -750,6 +755,8 @@ def main() -> None:
             "rccl_ranks": dist.get_world_size() if use_dist and backend == "nccl" else 0,
             "roofline": roof, "cpu_baseline": cpu, **extra,
         }
+        if args.plan_debug:
+            out["plan_debug"] = args.plan_debug   # an A/B run with path overrides, not the default build
         if args.share_gpu:
             out["rehearsal"] = (f"{world} gloo ranks sharing GPU 0, exchange through host copies: "
                                 "tests the N-rank code path, NOT a measurement")

@@ -26,7 +26,7 @@ extern "C" {
 #endif
 
 #define RSORT_VERSION_MAJOR 0
-#define RSORT_VERSION_MINOR 5
+#define RSORT_VERSION_MINOR 6
 
 typedef enum rs_status {
     RS_OK = 0,
@@ -239,6 +239,14 @@ typedef struct rs_plan_debug {
                                them (default), 0 take the LSD fallback for the whole sort */
     int32_t presorted;      /* hybrid path with check_order: 1 the nearly-sorted path where the
                                device finds it applies (default), 0 never (the radix passes) */
+    int32_t xcd;            /* hybrid MSD passes with values: XCD-local tile streams on 1 both passes,
+                               2 pass 0 only, 3 pass 1 only; 0 one global tile counter (the default;
+                               added in 0.6) */
+    int32_t high_half;      /* test hook: 1 the hybrid path's bucket kernels read records buffers
+                               placed at an address whose low 32 bits are >= 2^31 (needs spare plan
+                               capacity: n + 2^28 records; RS_ERR_CAPACITY otherwise) (0.6) */
+    int32_t msd_db;         /* hybrid MSD passes with values: 1 double-buffered tiles (the next
+                               tile's loads in flight during the whole tile), 0 single (0.6) */
 } rs_plan_debug;
 rs_status rs_plan_set_debug(rs_plan* plan, const rs_plan_debug* debug);
 void      rs_plan_destroy(rs_plan* plan);     /* frees the workspace (reference quirk Q9) */

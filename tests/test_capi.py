@@ -20,7 +20,7 @@ def test_library_exports_every_header_symbol():
 
 def test_version_and_status_strings():
     L = _lib.load()
-    assert L.rs_version() == (0 << 16) | 5
+    assert L.rs_version() == (0 << 16) | 6
     assert L.rs_status_string(_lib.RS_ERR_NOT_POW2).decode().startswith("workgroup")
     assert "device-side failure" in L.rs_status_string(_lib.RS_ERR_DEVICE).decode()
 
@@ -84,7 +84,7 @@ def test_debug_struct_and_kernel_kinds_match_the_header():
     body = hdr[hdr.index("typedef struct rs_plan_debug"):hdr.index("} rs_plan_debug;")]
     fields = re.findall(r"int32_t\s+(\w+);", body)
     assert [f for f, _ in _lib.PlanDebug._fields_] == fields
-    assert fields[-1] == "presorted"
+    assert fields[-1] == "msd_db"
     assert re.search(r"RS_KERNEL_SPLIT = 6", hdr) and re.search(r"RS_KERNEL_PRESORTED = 7", hdr)
     assert re.search(r"RS_KERNEL_KINDS = 8", hdr)
     assert _lib.RS_KERNEL_KINDS == 8 and _lib.KERNEL_NAMES[_lib.RS_KERNEL_SPLIT] == "split"

@@ -181,3 +181,72 @@ def test_presorted_on_the_lsd_path_with_bit_count(plan_debug, bits):
     assert kern.last_path() == "presorted"
     kern.destroy()
     assert np.array_equal(_np(kt), ek) and np.array_equal(_np(vt), ev)
+
+
+# ---- seeded randomized search (round 6) --------------------------------------------------------
+# Beyond the hand-made shapes above: every case draws its size (>= the 12M-key minimum of the path),
+# bit_count, duplicate ratio and a mix of perturbations (transpositions near and far, reversed and
+# rotated runs of 2-300 keys) at a density from n / 10^5 to n / 50, then sorts it on all three
+# layouts, compared word for word with the oracle's stable sort.  Both outcomes of the device's
+# decision are exercised: low densities take the presorted path, high ones the radix path.
+def _random_nearly(seed: int):
+    r = _rng(1000 + seed)
+    n = int(r.integers(12 << 20, 17 << 20)) | int(r.integers(0, 2))   # odd sizes too
+    bits = int(r.choice([16, 28, 32]))
+    mask = np.uint32((1 << bits) - 1 if bits < 32 else 0xFFFFFFFF)
+    distinct = int(r.choice([n, n // 10, 1000, 3]))
+    pool = np.sort(O.gen_u32_c(seed, distinct) & mask)
+    keys = np.sort(pool[r.integers(0, distinct, n)])                  # sorted masked keys, duplicates
+    if bits < 32:   # bits above the mask: carried along, ignored by the order (random)
+        keys |= r.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32) & ~mask
+    density = float(np.exp(r.uniform(np.log(1e-5), np.log(1 / 50))))
+    ops = max(1, int(n * density))
+    kinds = r.integers(0, 4, ops)
+    for kind, at in zip(kinds.tolist(), r.integers(0, n - 301, ops).tolist()):
+        ln = int(r.integers(2, 301))
+        if kind == 0:                                   # transposition at distance 1..300
+            b = at + ln - 1
+            keys[at], keys[b] = keys[b], keys[at]
+        elif kind == 1:                                 # far transposition
+            b = int(r.integers(0, n))
+            keys[at], keys[b] = keys[b], keys[at]
+        elif kind == 2:                                 # reversed run
+            keys[at:at + ln] = keys[at:at + ln][::-1].copy()
+        else:                                           # rotated run
+            keys[at:at + ln] = np.roll(keys[at:at + ln], int(r.integers(1, ln)))
+    return n, bits, density, keys
+
+
+def test_presorted_seeded_random_search():
+    paths = []
+    for seed in range(10):
+        n, bits, density, keys = _random_nearly(seed)
+        vals = np.arange(n, dtype=np.uint32)
+        ek, ev = O.stable_sort_masked_c(keys, vals, bits)
+        tag = (seed, n, bits, round(density * n))
+        kt, vt = _t(keys), _t(vals)
+        kern = RadixSortKernel(keys=kt, values=vt, count=n, check_order=True, bit_count=bits)
+        kern.dispatch()
+        kern.check()
+        paths.append(kern.last_path())
+        kern.destroy()
+        assert np.array_equal(_np(kt), ek) and np.array_equal(_np(vt), ev), (tag, paths[-1])
+        del kt, vt
+        kt = _t(keys)
+        kern = RadixSortKernel(keys=kt, count=n, check_order=True, bit_count=bits)
+        kern.dispatch()
+        kern.check()
+        kern.destroy()
+        assert np.array_equal(_np(kt), ek), (tag, "keys only")
+        del kt
+        rt = _t(np.stack([keys, vals], axis=-1).reshape(-1)).view(-1, 2)
+        kern = RadixSortTextureKernel(texture=rt, count=n, check_order=True, bit_count=bits)
+        kern.dispatch()
+        kern.check()
+        kern.destroy()
+        out = _np(rt).reshape(-1, 2)
+        assert np.array_equal(out[:, 0], ek) and np.array_equal(out[:, 1], ev), (tag, "records")
+        del rt
+    print("paths:", paths)
+    # the search reaches both sides of the device's decision
+    assert paths.count("presorted") >= 3 and len(set(paths) - {"presorted"}) >= 1, paths

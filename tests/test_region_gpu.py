@@ -55,3 +55,75 @@ def test_region_large_buckets_with_tiny_ones(mean, top_lo, ntop):
     ek, ev = O.stable_sort_masked(keys, vals, 32)
     assert (ok.cpu().numpy().view(np.uint32) == ek).all()
     assert (ov.cpu().numpy().view(np.uint32) == ev).all()
+
+
+# ---- buckets at high addresses (round 6) --------------------------------------------------------
+# Round 5's fault: load_bucket rebuilt a bucket's base address from two readfirstlane halves and the
+# low half's bit 31 sign-extended over the high half - wrong only when the bucket's address has bit 31
+# of its low word set, i.e. only for some placements of the records buffer.  rs_plan_debug.high_half
+# places the buffers the bucket kernels read (R2, and the split's R3) at a 2^31 low address word, so
+# every tile kind below meets such buckets on every run, whatever the allocator does.
+SPARE = (1 << 28) + (1 << 17)   # the shift needs up to 2^31 + 8n bytes of spare plan capacity
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mean,top_lo,ntop,huge", [
+    (3900, 0x21, 1, 0),        # 256 x 17 (the config-3 tile; separate arrays: load_bucket)
+    (7000, 0xF0, 2, 0),        # 256 x 34
+    (12000, 0x10, 1, 0),       # 1024 x 17
+    (20000, 0x42, 1, 0),       # the wide kernel over every bucket
+    (3900, 0x80, 1, 3),        # a bucket over the widest tile: the split (512 x 34 sub-bucket tiles)
+])
+def test_region_buckets_at_high_addresses(plan_debug, mean, top_lo, ntop, huge):
+    keys, vals, hist = _region(mean, top_lo, ntop, seed=7 * mean + ntop + huge)
+    if huge:   # bucket 9 of the region: `huge` times the widest tile, its low bits random
+        extra = ((np.uint32((top_lo << 8) + 9) << np.uint32(16)) |
+                 np.random.default_rng(5).integers(0, 1 << 16, huge * WIDE_CAP, dtype=np.uint32))
+        keys = np.concatenate([keys, extra])
+        vals = np.random.default_rng(6).permutation(keys.size).astype(np.uint32)
+        order = np.argsort(keys >> np.uint32(24), kind="stable")
+        keys, vals = keys[order], vals[order]
+        hist = np.zeros(65536, dtype=np.int32)
+        np.add.at(hist, keys >> np.uint32(16), 1)
+    n = keys.size
+    rec = keys.astype(np.uint64) | (vals.astype(np.uint64) << np.uint64(32))
+    rt = torch.from_numpy(rec.view(np.int64)).cuda()
+    ht = torch.from_numpy(hist).cuda()
+    ok = torch.empty(n, dtype=torch.int32, device="cuda")
+    ov = torch.empty(n, dtype=torch.int32, device="cuda")
+    plan_debug(high_half=1)
+    plan = SortPlan(0, 2 * n + SPARE, True)
+    try:
+        plan.set_profiling(True)
+        plan.sort_region(rt, ok, ov, n, ht, top_lo, top_lo + ntop)
+        plan.check()
+        assert plan.kernel_times()["bucket"]["launches"] > 0
+        assert plan.last_path() == "hybrid"
+        if huge:
+            assert plan.last_split() >= 2
+    finally:
+        plan.destroy()
+    ek, ev = O.stable_sort_masked(keys, vals, 32)
+    assert (ok.cpu().numpy().view(np.uint32) == ek).all()
+    assert (ov.cpu().numpy().view(np.uint32) == ev).all()
+
+
+@pytest.mark.gpu
+def test_whole_sort_buckets_at_high_addresses(plan_debug):
+    """The whole-array hybrid sort (separate arrays) with its R2 - the plan's second records buffer -
+    at a 2^31 low address word."""
+    n = (16 << 20) + 77
+    keys = O.gen_u32_c(21, n)
+    vals = np.arange(n, dtype=np.uint32)
+    ek, ev = O.stable_sort_masked_c(keys, vals, 32)
+    plan_debug(high_half=1)
+    kt = torch.from_numpy(keys.view(np.int32).copy()).cuda()
+    vt = torch.from_numpy(vals.view(np.int32).copy()).cuda()
+    plan = SortPlan(0, 2 * n + SPARE, True)
+    try:
+        plan.sort(kt, vt, n)
+        plan.check()
+        assert plan.last_path() == "hybrid"
+    finally:
+        plan.destroy()
+    assert (kt.cpu().numpy().view(np.uint32) == ek).all() and (vt.cpu().numpy().view(np.uint32) == ev).all()

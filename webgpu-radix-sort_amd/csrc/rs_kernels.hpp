@@ -1284,14 +1284,43 @@ __global__ __launch_bounds__(BLOCK, pass_min_waves(BLOCK, KPT)) void k_onesweep(
 // No order check, no next-pass totals, no staging rounds (k_onesweep keeps those for the LSD passes).
 // L: input layout (SOA arrays: pass 0 of separate arrays; AOS records: R1, or a texture), LO: output
 // layout (AOS: R1 / R2 records; SOA: arrays).  KB: range-relative keys (key - kbase) as in k_onesweep.
-template <int L, int LO, int SEG, bool KB = false, int RANK = RANK_LDS_ATOMIC>
+//
+// XC (round 6): XCD-local tile streams.  A line where two consecutive tiles' runs of one digit meet
+// is written partly by each tile; when the two tiles run on different XCDs the line reaches memory
+// as two partial writes from two L2s (the pass's 1.085x traffic and most of its time over a linear
+// copy: tools/run_probe.hip).  With XC every XCD claims the tiles of its own contiguous tile range
+// from its own ticket counter, and no look-back chain crosses two ranges, so consecutive tiles -
+// and the lines they share - are (almost always) written through one L2 and the chains never wait
+// on another XCD's claims (round 5's XCD-grouped claims over one global chain did, and lost 4 %):
+//   SEG = 1: the ranges are runs of whole top-byte segments (every segment has its own chain
+//            already), cut at the segment boundary nearest to each eighth of the tiles;
+//   SEG = 0: the input is cut into 8 chunks at k_hist16_in row boundaries (rows [x hrows / 8,
+//            (x + 1) hrows / 8) for XCD x), each chunk a segment with its own chain, whose digit-d
+//            output starts at the digit's start + cbase[row][d] (k_hist16_reduce: the keys of digit d
+//            in the rows before) - the per-chunk bases the histogram read gives for free.
+// A workgroup whose range is exhausted takes tiles from the next XCDs' counters (balance; claims of
+// one counter stay in tile order, so every look-back still waits only on tiles claimed earlier by
+// running workgroups).  The XCD is read from HW_REG_XCC_ID: placement only, never correctness.
+// Measured on config 3 (profiles/r06/xcd_claims/): pass 0 1.003 vs 0.993 ms, pass 1 1.045 vs 0.993 -
+// slower, like round 5's grouped claims, so the product keeps one counter per pass (rs_plan_debug.xcd
+// = 0); the seam lines are not what bounds the real pass (its per-tile phases are).
+__device__ __forceinline__ uint32_t xcc_id() {
+    uint32_t x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+    return x & 7u;
+}
+
+template <int L, int LO, int SEG, bool KB = false, int RANK = RANK_LDS_ATOMIC, bool XC = false>
 __global__ __launch_bounds__(1024, 4) void k_msd_pass(
     const uint32_t* __restrict__ in_k, const uint32_t* __restrict__ in_v,
     uint32_t* __restrict__ out_k, uint32_t* __restrict__ out_v, uint32_t n, uint32_t shift,
     uint32_t ntiles, const uint32_t* __restrict__ dtot, unsigned long long* status,
     uint32_t* ticket, uint32_t* err, uint32_t epoch, const uint32_t* gate, int gate_pass,
     uint32_t spin_max, uint32_t* host_err, const uint32_t* __restrict__ segtab,
-    const uint32_t* __restrict__ base16, uint32_t kbase) {
+    const uint32_t* __restrict__ base16, uint32_t kbase,
+    const uint32_t* __restrict__ cbase = nullptr, uint32_t hrows = 0) {
+    // XC: ticket = 8 counters (one per XCD); SEG = 0 also cbase (k_hist16_reduce's [row][top byte]
+    // chunk starts) and hrows (k_hist16_in's grid: its chunk formula cuts the input here too)
     static_assert(L != LAYOUT_KEYS && LO != LAYOUT_KEYS, "with values");
     static_assert(SEG == 0 || SEG == 1, "the two MSD passes");
     constexpr int BLOCK = 1024, KPT = 16, R = 8, RADIX = 256, NW = BLOCK / 64;
@@ -1305,23 +1334,90 @@ __global__ __launch_bounds__(1024, 4) void k_msd_pass(
     __shared__ uint32_t s_next;
     __shared__ uint2 s_kv[TILE];
     __shared__ uint32_t s_seg[SEG == 1 ? 769 : 1];
+    __shared__ uint32_t s_xf[XC ? 9 : 1];                  // XC: XCD x's tiles [s_xf[x], s_xf[x + 1])
+    __shared__ uint32_t s_xs[XC && SEG == 0 ? 9 : 1];      // XC, SEG = 0: chunk x's first record
+    __shared__ uint32_t s_xr[XC && SEG == 0 ? 9 : 1];      // ... and first histogram row
 
     if (gated_off(gate, gate_pass)) return;
     const uint32_t tid = threadIdx.x, w = tid >> 6, lane = lane_id();
     if (SEG == 1)
         for (uint32_t i = tid; i < 769u; i += BLOCK) s_seg[i] = segtab[i];
+    if (XC && SEG == 0 && tid <= 8u) {
+        // chunk x: k_hist16_in rows [x hrows / 8, (x + 1) hrows / 8), row r = records [r chunk, (r + 1) chunk)
+        const uint64_t chunk = (((uint64_t)n + hrows - 1) / hrows + 3u) & ~3ull;
+        auto start = [&](uint32_t x) -> uint32_t {
+            const uint64_t s = (uint64_t)(x * hrows / 8u) * chunk;
+            return s < n ? (uint32_t)s : n;
+        };
+        uint32_t f = 0;
+        for (uint32_t x = 0; x < tid; ++x) f += (start(x + 1) - start(x) + TILE - 1) / (uint32_t)TILE;
+        s_xf[tid] = f;
+        s_xs[tid] = start(tid);
+        s_xr[tid] = tid * hrows / 8u;
+    }
+    uint32_t dglob = 0;   // XC, SEG = 0, thread d < 256: digit d's first output position
     {   // first output position of every digit (SEG = 0; SEG = 1 per segment, below)
         const uint32_t c = (SEG == 0 && tid < (uint32_t)RADIX) ? dtot[tid] : 0u;
         uint32_t all;
         const uint32_t ex = block_excl_scan_n<NW>(c, s_scratch, all);
         if (tid < (uint32_t)RADIX) s_dbase[tid] = ex;
-        if (tid == 0) s_next = atomicAdd(ticket, 1u);
+        dglob = ex;
+        if (XC && SEG == 1 && tid <= 8u) {
+            // (s_seg is visible: the scan's barriers) XCD x's range starts at the first segment whose
+            // first tile is at or after x/8 of the tiles
+            const uint32_t ntt = s_seg[256];
+            const uint32_t target = (uint32_t)((uint64_t)tid * ntt / 8u);
+            uint32_t lo = 0, hi = 256;   // the first s with s_seg[s] >= target (s_seg[256] = ntt >= target)
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (s_seg[mid] >= target) hi = mid;
+                else lo = mid + 1;
+            }
+            s_xf[tid] = tid == 8u ? ntt : s_seg[lo];
+        }
+        if (!XC && tid == 0) s_next = atomicAdd(ticket, 1u);
+        __syncthreads();
+    }
+    // XC claims (thread 0): own XCD's counter first, then the next XCDs' in turn once exhausted;
+    // nt when every counter is
+    const uint32_t xid = XC ? xcc_id() : 0u;
+    uint32_t xcur = 0;
+    const uint32_t nt = XC ? s_xf[8] : (SEG == 1 ? s_seg[SEG == 1 ? 256 : 0] : ntiles);
+    auto claim = [&]() -> uint32_t {
+        // a lane-varying address as far as the compiler knows: its atomic optimizer would turn a
+        // uniform-address add into a wave-aggregated one whose result is broadcast at once
+        uint32_t z = 0;
+        asm volatile("" : "+v"(z));
+        if constexpr (XC) {
+            for (; xcur < 8u; ++xcur) {
+                const uint32_t x = (xid + xcur) & 7u;
+                const uint32_t lo = s_xf[x], hi = s_xf[x + 1];
+                if (lo < hi) {
+                    const uint32_t t = atomicAdd(ticket + x + z, 1u);
+                    if (t < hi - lo) return lo + t;
+                }
+            }
+            return nt;
+        } else {
+            return atomicAdd(ticket + z, 1u);
+        }
+    };
+    if (XC) {
+        if (tid == 0) s_next = claim();
         __syncthreads();
     }
     uint32_t T = s_next;
-    const uint32_t nt = SEG == 1 ? s_seg[SEG == 1 ? 256 : 0] : ntiles;
     auto geom = [&](uint32_t t, uint32_t& t0, uint32_t& tend, uint32_t& seg, uint32_t& first) {
-        if (SEG == 1) {
+        if (XC && SEG == 0) {
+            uint32_t x = 0;   // s_xf[x] <= t < s_xf[x + 1] (empty chunks skipped)
+#pragma unroll
+            for (int i = 1; i < 8; ++i) x += s_xf[i] <= t ? 1u : 0u;
+            seg = x;
+            first = s_xf[x];
+            t0 = s_xs[x] + (t - first) * (uint32_t)TILE;
+            const uint32_t e = s_xs[x + 1];
+            tend = e - t0 < (uint32_t)TILE ? e : t0 + (uint32_t)TILE;
+        } else if (SEG == 1) {
             uint32_t lo = 0, hi = 256;                   // s_seg[lo] <= t < s_seg[hi]
             while (hi - lo > 1) {
                 const uint32_t mid = (lo + hi) >> 1;
@@ -1374,6 +1470,7 @@ __global__ __launch_bounds__(1024, 4) void k_msd_pass(
         }
         // (loaded with the tile: read at the top of a tile it would wait for every store before it)
         if (SEG == 1) nb16 = base16[(sg << 8) | (tid & 255u)];
+        if (XC && SEG == 0) nb16 = t < nt ? cbase[(size_t)s_xr[sg] * 256u + (tid & 255u)] : 0u;
     };
     load(T);
     // the first tile's registers used (waited for) here, so that the loop top's state - which the
@@ -1382,21 +1479,16 @@ __global__ __launch_bounds__(1024, 4) void k_msd_pass(
     // stores after them drain (an explicit s_waitcnt is dropped by the compiler's own wait pass)
 #pragma unroll
     for (int j = 0; j < KPT; ++j) asm volatile("" ::"v"(k[j]), "v"(v[j]));
-    if (SEG == 1) asm volatile("" ::"v"(nb16));
+    if (SEG == 1 || XC) asm volatile("" ::"v"(nb16));
     uint32_t Tq = 0;   // thread 0: the next tile's ticket, requested at the top of this tile
     while (T < nt) {
-        if (tid == 0) {
-            // a lane-varying address as far as the compiler knows: its atomic optimizer would turn a
-            // uniform-address add into a wave-aggregated one whose result is broadcast at once
-            uint32_t z = 0;
-            asm volatile("" : "+v"(z));
-            Tq = atomicAdd(ticket + z, 1u);
-        }
+        if (tid == 0) Tq = claim();
         uint32_t tile0, tend, seg, seg_first;
         geom(T, tile0, tend, seg, seg_first);
         const uint32_t nvalid = tend - tile0;
         const bool first_tile = T == seg_first;   // publishes an inclusive prefix at once
         if (SEG == 1 && tid < (uint32_t)RADIX) s_dbase[tid] = s_seg[257 + seg] + nb16;
+        if (XC && SEG == 0 && tid < (uint32_t)RADIX) s_dbase[tid] = dglob + nb16;
         {   // slots past the tile's end become pads (kPadKey: after every real key); KB: relative keys
             const uint32_t wb = w * (uint32_t)WAVE_KEYS + lane;
 #pragma unroll
@@ -1488,6 +1580,214 @@ __global__ __launch_bounds__(1024, 4) void k_msd_pass(
         }
         __syncthreads();
         T = Tn;
+    }
+}
+
+// ---- k_msd_pass_db: the MSD pass with the next tile's loads in flight during the whole tile -------
+// k_msd_pass issues tile T+1's loads after staging tile T (its registers are free only then), so
+// tile T+1's rank waits for loads issued a look-back and a scatter earlier, and the HBM pipe idles
+// while T+1 ranks, publishes and stages (~1/3 of a tile: the phase stamps of docs/design_history.md
+// §12).  Here the tile data is double-buffered in registers: tile T+1's loads are issued at the TOP of
+// tile T (tickets are claimed two tiles ahead), so they arrive while T ranks, publishes, stages,
+// walks back and scatters, and T's stores drain while T+1 ranks.  Ranks are kept as 16-bit pairs
+// (tile positions < 2^14) so both tiles' keys and values fit the 128 VGPRs of a 1024-thread
+// workgroup.  Everything else - geometry, pads, rank, publish, local shuffle, look-back, fixed-count
+// scatter - is k_msd_pass's, so the output is the same stable partition.
+template <int L, int LO, int SEG, bool KB = false, int RANK = RANK_LDS_ATOMIC>
+__global__ __launch_bounds__(1024, 4) void k_msd_pass_db(
+    const uint32_t* __restrict__ in_k, const uint32_t* __restrict__ in_v,
+    uint32_t* __restrict__ out_k, uint32_t* __restrict__ out_v, uint32_t n, uint32_t shift,
+    uint32_t ntiles, const uint32_t* __restrict__ dtot, unsigned long long* status,
+    uint32_t* ticket, uint32_t* err, uint32_t epoch, const uint32_t* gate, int gate_pass,
+    uint32_t spin_max, uint32_t* host_err, const uint32_t* __restrict__ segtab,
+    const uint32_t* __restrict__ base16, uint32_t kbase, const uint32_t* = nullptr, uint32_t = 0) {
+    // (the last two: k_msd_pass's XC arguments, unused: one launch signature for both kernels)
+    static_assert(L != LAYOUT_KEYS && LO != LAYOUT_KEYS, "with values");
+    static_assert(SEG == 0 || SEG == 1, "the two MSD passes");
+    constexpr int BLOCK = 1024, KPT = 16, R = 8, RADIX = 256, NW = BLOCK / 64;
+    constexpr int TILE = BLOCK * KPT, WAVE_KEYS = 64 * KPT;
+    constexpr uint32_t mask = RADIX - 1;
+    constexpr uint32_t ESZ = L == LAYOUT_AOS ? 8u : 4u;
+    __shared__ uint32_t s_whist[NW][RADIX];
+    __shared__ uint32_t s_gdelta[RADIX];
+    __shared__ uint32_t s_dbase[RADIX];
+    __shared__ uint32_t s_scratch[NW];
+    __shared__ uint32_t s_next[2];
+    __shared__ uint2 s_kv[TILE];
+    __shared__ uint32_t s_seg[SEG == 1 ? 769 : 1];
+
+    if (gated_off(gate, gate_pass)) return;
+    const uint32_t tid = threadIdx.x, w = tid >> 6, lane = lane_id();
+    if (SEG == 1)
+        for (uint32_t i = tid; i < 769u; i += BLOCK) s_seg[i] = segtab[i];
+    auto claim = [&]() -> uint32_t {
+        uint32_t z = 0;   // (a lane-varying address to the compiler: no wave-aggregated atomic)
+        asm volatile("" : "+v"(z));
+        return atomicAdd(ticket + z, 1u);
+    };
+    {
+        const uint32_t c = (SEG == 0 && tid < (uint32_t)RADIX) ? dtot[tid] : 0u;
+        uint32_t all;
+        const uint32_t ex = block_excl_scan_n<NW>(c, s_scratch, all);
+        if (tid < (uint32_t)RADIX) s_dbase[tid] = ex;
+        if (tid == 0) {
+            s_next[0] = claim();
+            s_next[1] = claim();
+        }
+        __syncthreads();
+    }
+    uint32_t T = s_next[0], Tn = s_next[1];
+    const uint32_t nt = SEG == 1 ? s_seg[SEG == 1 ? 256 : 0] : ntiles;
+    auto geom = [&](uint32_t t, uint32_t& t0, uint32_t& tend, uint32_t& seg, uint32_t& first) {
+        if (SEG == 1) {
+            uint32_t lo = 0, hi = 256;
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (s_seg[mid] <= t) lo = mid;
+                else hi = mid;
+            }
+            seg = lo;
+            first = s_seg[lo];
+            t0 = s_seg[257 + lo] + (t - first) * (uint32_t)TILE;
+            const uint32_t e = s_seg[513 + lo];
+            tend = e - t0 < (uint32_t)TILE ? e : t0 + (uint32_t)TILE;
+        } else {
+            seg = 0;
+            first = 0;
+            t0 = t * (uint32_t)TILE;
+            tend = (uint64_t)t0 + TILE <= n ? t0 + (uint32_t)TILE : n;
+        }
+    };
+    const uint32_t lofs = (w * (uint32_t)WAVE_KEYS + lane) * ESZ;
+    auto load = [&](uint32_t t, uint32_t (&k)[KPT], uint32_t (&v)[KPT], uint32_t& nb) {
+        uint32_t t0 = 0, tend = 0, sg = 0, fi;
+        if (t < nt) geom(t, t0, tend, sg, fi);
+        const uint32_t nbytes = (tend - t0) * ESZ;
+        uint32_t lo = lofs;
+        asm volatile("" : "+v"(lo));
+        if constexpr (L == LAYOUT_AOS) {
+            const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+                (void*)(in_k + 2ull * t0), (short)0, (int)nbytes, 0x00020000);
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) {
+                const auto q = __builtin_amdgcn_raw_buffer_load_b64(rr, (int)(lo + j * 64 * 8), 0, 0);
+                k[j] = q[0];
+                v[j] = q[1];
+            }
+        } else {
+            const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(
+                (void*)(in_k + t0), (short)0, (int)nbytes, 0x00020000);
+            const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(
+                (void*)(in_v + t0), (short)0, (int)nbytes, 0x00020000);
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) k[j] = __builtin_amdgcn_raw_buffer_load_b32(rk, (int)(lo + j * 256), 0, 0);
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) v[j] = __builtin_amdgcn_raw_buffer_load_b32(rv, (int)(lo + j * 256), 0, 0);
+        }
+        if (SEG == 1) nb = base16[(sg << 8) | (tid & 255u)];
+    };
+    uint32_t ka[KPT], va[KPT], kb[KPT], vb[KPT];
+    uint32_t nba = 0, nbb = 0;
+    load(T, ka, va, nba);
+    // one tile: (kc, vc) hold tile T (loaded); tile Tn's loads go to (kn, vn) at once
+    auto tile = [&](uint32_t (&kc)[KPT], uint32_t (&vc)[KPT], uint32_t& nbc, uint32_t (&kn)[KPT],
+                    uint32_t (&vn)[KPT], uint32_t& nbn) {
+        load(Tn, kn, vn, nbn);   // in flight during this whole tile
+        uint32_t Tq = 0;
+        if (tid == 0) Tq = claim();   // the tile after Tn (read after staging)
+        uint32_t tile0, tend, seg, seg_first;
+        geom(T, tile0, tend, seg, seg_first);
+        const uint32_t nvalid = tend - tile0;
+        const bool first_tile = T == seg_first;
+        if (SEG == 1 && tid < (uint32_t)RADIX) s_dbase[tid] = s_seg[257 + seg] + nbc;
+        {
+            const uint32_t wb = w * (uint32_t)WAVE_KEYS + lane;
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) {
+                const bool ok = wb + j * 64u < nvalid;
+                kc[j] = ok ? (KB ? kc[j] - kbase : kc[j]) : kPadKey;
+            }
+        }
+        Slots<KPT, true> rank;
+        uint32_t c;
+        const uint32_t tstart = rank_tile<R, NW, KPT, RANK>(kc, rank, s_whist, s_scratch, shift, mask,
+                                                            (uint32_t)TILE - nvalid, c);
+        unsigned long long* st = status + (size_t)T * RADIX + tid;
+        if (tid < (uint32_t)RADIX) {
+            if (first_tile) st_store(st, (epoch << 2) | kStInclusive, s_dbase[tid] + c);
+            else st_store(st, (epoch << 2) | kStAggregate, c);
+            set_wave_offsets<R, NW>(s_whist, tstart);
+        }
+        __syncthreads();
+        stage_tile<KPT, true, TILE>(kc, vc, rank, s_whist[w], nullptr, s_kv, shift, mask, nullptr, 0u, 0u);
+        if (tid == 0) s_next[0] = Tq;
+        __syncthreads();
+        const uint32_t Tnn = s_next[0];
+        if (tid < (uint32_t)RADIX) {
+            uint32_t excl = s_dbase[tid];
+            if (!first_tile) {
+                excl = 0;
+                uint32_t j = T - 1;
+                uint32_t spins = 0;
+                for (;;) {
+                    unsigned long long sv[kLookback];
+#pragma unroll
+                    for (int i = 0; i < kLookback; ++i)
+                        sv[i] = (j >= (uint32_t)i) ? st_load(status + (size_t)(j - i) * RADIX + tid) : 0ull;
+                    uint32_t used = 0;
+                    bool done = false;
+#pragma unroll
+                    for (int i = 0; i < kLookback; ++i) {
+                        if (done || used != (uint32_t)i) break;
+                        const uint32_t f = (uint32_t)(sv[i] >> 32);
+                        if ((f >> 2) != epoch || j < (uint32_t)i) break;
+                        excl += (uint32_t)sv[i];
+                        ++used;
+                        done = (f & 3u) == kStInclusive;
+                    }
+                    if (done) break;
+                    j -= used;
+                    if (used == 0u) {
+                        ++spins;
+                        if (spins > spin_max ||
+                            ((spins & 255u) == 0u &&
+                             __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+                            atomicOr(err, 1u);
+                            if (host_err)
+                                __hip_atomic_fetch_or(host_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(1);
+                    }
+                }
+                st_store(st, (epoch << 2) | kStInclusive, excl + c);
+            }
+            s_gdelta[tid] = excl - tstart;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) {
+            const uint32_t i0 = (uint32_t)j * BLOCK + tid;
+            const uint32_t i = i0 < nvalid ? i0 : nvalid - 1u;
+            const uint2 kv = s_kv[i];
+            uint32_t pos = s_gdelta[(kv.x >> shift) & mask] + i;
+            pos = pos < n ? pos : n - 1u;
+            if constexpr (LO == LAYOUT_AOS) {
+                reinterpret_cast<uint2*>(out_k)[pos] = kv;
+            } else {
+                out_k[pos] = kv.x;
+                out_v[pos] = kv.y;
+            }
+        }
+        // (no barrier here: the next writers of s_kv / s_gdelta / s_whist come after the next
+        // tile's rank barriers)
+        T = Tn;
+        Tn = Tnn;
+    };
+    while (T < nt) {
+        tile(ka, va, nba, kb, vb, nbb);
+        if (T >= nt) break;
+        tile(kb, vb, nbb, ka, va, nba);
     }
 }
 

@@ -94,8 +94,10 @@ struct TileCfg {
     uint32_t max_grid;
 };
 constexpr TileCfg kLarge{1024, 16, 16384, 512};
-// Words after the digit totals: [16] tile tickets (one per k_onesweep launch slot), [16] error words
-constexpr uint32_t kTicketWords = 32;
+// Words after the digit totals: [16] tile tickets (one per k_onesweep launch slot), [16] error words,
+// then [2][8] the hybrid MSD passes' per-XCD tile counters (k_msd_pass XC) and 16 spare
+constexpr uint32_t kTicketWords = 64;
+constexpr uint32_t kXcdTickets = 32;
 #if !RS_KNOB_OPEN || !defined(RS_MSD_LEAN)
 #undef RS_MSD_LEAN
 #define RS_MSD_LEAN 1    // the MSD passes with values on k_msd_pass (0: k_onesweep)
@@ -305,6 +307,11 @@ struct rs_plan {
                                      // (32K-key tiles for pass 0 only: no faster, r03_keys_pass0_tiles_ab)
     bool kbucket_wave = true;        // one wave per 16-bit bucket (rs_plan_debug.kbucket_wave = 0: workgroups)
     bool kbucket_pf = false;         // workgroup kernel on a persistent prefetching grid (sweep: RSORT_KBUCKET_PF=1)
+    bool msd_db = false;             // the MSD passes double-buffered (k_msd_pass_db; rs_plan_debug.msd_db)
+    bool high_half = false;          // test hook (rs_plan_debug.high_half): R2 / R3 at a 2^31 low address word
+    int xcd_claims = 0;              // hybrid MSD passes with values: XCD-local tile streams (k_msd_pass XC;
+                                     // rs_plan_debug.xcd: 0 none (default: XC measured slower, 1.00 / 1.04
+                                     // vs 0.99 ms per pass), 1 both passes, 2 pass 0 only, 3 pass 1 only)
     bool static_passes = false;      // hybrid MSD passes over static splits (sweep only, RSORT_STATIC=1: measured
                                      // slower than the look-back passes)
     uint32_t* msd = nullptr;         // its workspace: hist16 | base16 | segtab | gates | mtot
@@ -459,7 +466,9 @@ template <int L, int LO, int SEG, bool KB = false, int BLOCK = kLarge.block, int
 void launch_msd_pass(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint32_t* ok, uint32_t* ov,
                      uint32_t n, uint32_t shift, uint32_t ntiles, const uint32_t* dtot, uint32_t* ticket,
                      const uint32_t* gate, const uint32_t* segtab, const uint32_t* base16,
-                     hipStream_t s, uint32_t kbase = 0, uint32_t pmask = 0xFFFFFFFFu) {
+                     hipStream_t s, uint32_t kbase = 0, uint32_t pmask = 0xFFFFFFFFu,
+                     const uint32_t* cbase = nullptr, uint32_t hrows = 0) {
+    // cbase / hrows (SEG = 0): the histogram rows' chunk starts, for XCD-local claims (k_msd_pass XC)
     static_assert(BLOCK * KPT == kLarge.tile || BLOCK * KPT == 2 * kLarge.tile, "k_msd_plan tile sizes");
     static_assert(SR == 1 || SEG == 0, "staging rounds: the top-byte pass only");
     auto go = [&](auto kern) {
@@ -474,15 +483,28 @@ void launch_msd_pass(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint32_
                           KPT == kLarge.kpt;
     if constexpr (LEAN) {
         if (pmask == 0xFFFFFFFFu) {   // (the ring experiment keeps k_onesweep)
+            // XCD-local claims (rs_plan_debug.xcd): 8 counters per pass after the per-pass tickets
+            const bool xc = (p->xcd_claims == 1 || p->xcd_claims == (SEG == 0 ? 2 : 3)) && (SEG == 1 || (cbase && hrows));
             auto lean = [&](auto kern) {
                 static const uint32_t per_cu = resident_per_cu(kern, BLOCK);
-                const uint32_t grid = std::min<uint32_t>(ntiles, p->cus * per_cu);
-                hipLaunchKernelGGL(kern, dim3(grid), dim3(BLOCK), 0, s, ik, iv, ok, ov, n, shift, ntiles, dtot,
-                                   p->status, ticket, p->tickets + 16, p->epoch, gate, SEG, p->spin_max,
-                                   p->host_err_dev, segtab, base16, kbase);
+                // (XC, SEG = 0: up to one partial tile per chunk on top)
+                const uint32_t bound = xc && SEG == 0 ? ntiles + 8u : ntiles;
+                const uint32_t grid = std::min<uint32_t>(bound, p->cus * per_cu);
+                hipLaunchKernelGGL(kern, dim3(grid), dim3(BLOCK), 0, s, ik, iv, ok, ov, n, shift, bound, dtot,
+                                   p->status, xc ? p->tickets + kXcdTickets + 8 * SEG : ticket, p->tickets + 16,
+                                   p->epoch, gate, SEG, p->spin_max, p->host_err_dev, segtab, base16, kbase, cbase,
+                                   hrows);
             };
-            if (p->rank_mode == rs::RANK_BALLOT) lean(rs::k_msd_pass<L, LO, SEG, KB, rs::RANK_BALLOT>);
-            else lean(rs::k_msd_pass<L, LO, SEG, KB, rs::RANK_LDS_ATOMIC>);
+            if (p->msd_db && !xc) {
+                if (p->rank_mode == rs::RANK_BALLOT) lean(rs::k_msd_pass_db<L, LO, SEG, KB, rs::RANK_BALLOT>);
+                else lean(rs::k_msd_pass_db<L, LO, SEG, KB, rs::RANK_LDS_ATOMIC>);
+            } else if (xc) {
+                if (p->rank_mode == rs::RANK_BALLOT) lean(rs::k_msd_pass<L, LO, SEG, KB, rs::RANK_BALLOT, true>);
+                else lean(rs::k_msd_pass<L, LO, SEG, KB, rs::RANK_LDS_ATOMIC, true>);
+            } else {
+                if (p->rank_mode == rs::RANK_BALLOT) lean(rs::k_msd_pass<L, LO, SEG, KB, rs::RANK_BALLOT>);
+                else lean(rs::k_msd_pass<L, LO, SEG, KB, rs::RANK_LDS_ATOMIC>);
+            }
             return;
         }
     }
@@ -1249,6 +1271,27 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
     const bool strict = split && !region;
     p->last_split = split;
     uint32_t* r3 = region ? p->tmp2 : r1;
+    if (p->high_half) {
+        // test hook (rs_plan_debug.high_half): the records buffers the bucket kernels read (R2, and the
+        // split's R3) start where the low 32 bits of the address are 2^31, so that the buckets' base
+        // addresses have bit 31 of their low word set (round 5's sign-extension fault in load_bucket);
+        // the plan's spare capacity holds the shift
+        const uint64_t rbytes = 8ull * ((p->capacity + kRecPad - 1) / kRecPad * kRecPad);
+        auto high = [&](uint32_t*& buf) -> bool {
+            if (buf != p->tmp_k && buf != p->tmp2) return true;   // the caller's buffer: left alone
+            const uint64_t a = (uint64_t)(uintptr_t)buf & 0xFFFFFFFFull, need = 8ull * (n + kRecPad);
+            // already wholly in the upper half of a 4 GiB window: no shift; else up to 2^31 + need bytes
+            const uint64_t o = (a >= 0x80000000ull && a + need <= 0x100000000ull) ? 0ull
+                             : (0x80000000ull - a) & 0xFFFFFFFFull;   // (a multiple of 4)
+            if (o + need > rbytes) return false;
+            buf += o / 4u;
+            return true;
+        };
+        const bool r3_own = r3 != r1;   // (whole sorts: R3 is R1, shifted with it below only if separate)
+        if (!high(r2) || (r3_own && !high(r3)))
+            return fail(RS_ERR_CAPACITY, "rs_plan_debug.high_half: the plan's capacity (%llu) leaves no room to "
+                        "shift %llu records to a 2^31 address", (unsigned long long)p->capacity, (unsigned long long)n);
+    }
     rs::SplitWs sw{};
     if (split) {
         uint32_t* q = p->split;
@@ -1345,6 +1388,9 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
     // workgroups per CU).
     const bool static_p0 = !region && !keys && p->static_passes && hrows <= rs::kMaxRows;
     const bool static_p1 = !keys && p->static_passes;
+    // XCD-local claims of MSD pass 0 (k_msd_pass XC): its chunks' digit bases from the histogram rows
+    // (k_hist16_reduce's cbase); the keys-only passes (k_onesweep) keep one counter
+    const uint32_t* xc_cbase = (!region && !keys && (p->xcd_claims == 1 || p->xcd_claims == 2) && hrows <= rs::kMaxRows) ? cbase : nullptr;
     // (the fallback's byte-0 totals: only where a fallback is enqueued)
     uint32_t* b0rows = (chk && !strict) ? p->tmp_k + (size_t)hrows * 65537u : nullptr;
     if (!region && (uint64_t)n / hrows >= (uint64_t)rs::kEvMax * rs::kHalfT)   // k_hist16_in's crossing log
@@ -1397,7 +1443,7 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
         hipLaunchKernelGGL(rs::k_hist16_reduce, dim3(256), dim3(1024), 0, s, (const uint32_t*)p->tmp_k,
                            hrows, hist16, top_tot, range_bad, base16, small_cap, kBucketCap, over, big,
                            p->ptot, (uint32_t)(rs::kTotalsMax + kTicketWords), (const uint32_t*)b0rows,
-                           static_p0 ? cbase : (uint32_t*)nullptr, sw.huge, p->smax2, ns_skip);
+                           (static_p0 || xc_cbase) ? cbase : (uint32_t*)nullptr, sw.huge, p->smax2, ns_skip);
     }, region ? "rsort.msd.region_table" : "rsort.msd.hist16");
     HIP_TRY(hipGetLastError());
     p->timer.run(RS_KERNEL_SCAN, s, [&] {
@@ -1447,13 +1493,15 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
 #endif
         else if (in_aos && kbase)
             launch_msd_pass<A, A, 0, true>(p, sk, nullptr, r1, nullptr, n32, vbits - 8, ntiles, top_tot,
-                                           p->tickets + 4, g_msd, nullptr, nullptr, s, kbase);
+                                           p->tickets + 4, g_msd, nullptr, nullptr, s, kbase, 0xFFFFFFFFu, xc_cbase,
+                                           hrows);
         else if (in_aos)
             launch_msd_pass<A, A, 0>(p, sk, nullptr, r1, nullptr, n32, vbits - 8, ntiles, top_tot,
-                                     p->tickets + 4, g_msd, nullptr, nullptr, s);
+                                     p->tickets + 4, g_msd, nullptr, nullptr, s, 0u, 0xFFFFFFFFu, xc_cbase, hrows);
         else if (kbase)
             launch_msd_pass<S, A, 0, true>(p, sk, sv, r1, nullptr, n32, vbits - 8, ntiles, top_tot,
-                                           p->tickets + 4, g_msd, nullptr, nullptr, s, kbase);
+                                           p->tickets + 4, g_msd, nullptr, nullptr, s, kbase, 0xFFFFFFFFu, xc_cbase,
+                                           hrows);
 #if RS_P0_SR2
         else   // 32K-record tiles staged in two rounds: 128-record digit runs (tools/run_probe.hip)
             launch_msd_pass<S, A, 0, false, kLarge.block, 2 * kLarge.kpt, 2>(
@@ -1462,7 +1510,7 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
 #else
         else
             launch_msd_pass<S, A, 0>(p, sk, sv, r1, nullptr, n32, vbits - 8, ntiles, top_tot, p->tickets + 4,
-                                     g_msd, nullptr, nullptr, s);
+                                     g_msd, nullptr, nullptr, s, 0u, 0xFFFFFFFFu, xc_cbase, hrows);
 #endif
     }, "rsort.msd.pass0");
     HIP_TRY(hipGetLastError());
@@ -2224,7 +2272,8 @@ RS_EXPORT rs_status rs_plan_set_debug(rs_plan* p, const rs_plan_debug* d) {
     auto tri = [](int32_t v, int hi) { return v >= -1 && v <= hi; };
     if (!tri(d->rank, 1) || !tri(d->tile, 1) || !tri(d->onesweep, 1) || !tri(d->msd, 1) ||
         !tri(d->keys_cfg, 1) || !tri(d->msd_keys_cfg, 2) || !tri(d->kbucket_wave, 1) ||
-        !tri(d->selftest_fail, 1) || !tri(d->split, 1) || !tri(d->presorted, 1))
+        !tri(d->selftest_fail, 1) || !tri(d->split, 1) || !tri(d->presorted, 1) || !tri(d->xcd, 3) ||
+        !tri(d->high_half, 1) || !tri(d->msd_db, 1))
         return fail(RS_ERR_INVALID_ARG, "rs_plan_set_debug: every field must be -1 or a listed choice");
     if (d->selftest_fail == 1) {
         p->selftest = 0;
@@ -2239,6 +2288,9 @@ RS_EXPORT rs_status rs_plan_set_debug(rs_plan* p, const rs_plan_debug* d) {
     if (d->kbucket_wave >= 0) p->kbucket_wave = d->kbucket_wave == 1;
     if (d->split >= 0) p->split_on = d->split == 1;
     if (d->presorted >= 0) p->ns_on = d->presorted == 1;
+    if (d->xcd >= 0) p->xcd_claims = d->xcd;
+    if (d->high_half >= 0) p->high_half = d->high_half == 1;
+    if (d->msd_db >= 0) p->msd_db = d->msd_db == 1;
     return RS_OK;
 }
 

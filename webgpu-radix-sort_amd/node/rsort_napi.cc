@@ -471,7 +471,7 @@ napi_value PlanLastPath(napi_env env, napi_callback_info info) {
     RS_CALL(env, rs_plan_last_path(b->plan, &path), "lastPath");
     static const char* const names[] = {"none", "lsd", "hybrid", "hybrid_fallback", "in_order", "presorted"};
     napi_value v;
-    napi_create_string_utf8(env, path < 5 ? names[path] : "unknown", NAPI_AUTO_LENGTH, &v);
+    napi_create_string_utf8(env, path < sizeof(names) / sizeof(names[0]) ? names[path] : "unknown", NAPI_AUTO_LENGTH, &v);
     return v;
 }
 

@@ -11,7 +11,7 @@ for (const name of ['RadixSortKernel', 'RadixSortBufferKernel', 'RadixSortTextur
 }
 assert.strictEqual(typeof rs.addon.planCreate, 'function');
 assert.strictEqual(rs.addon.FLAG_INTERLEAVED, 0x10);
-assert.strictEqual(rs.addon.version(), 5);
+assert.strictEqual(rs.addon.version(), 6);
 for (const f of ['planCheck', 'scanPlanRunIndirect', 'scanPlanDispatchChain']) {
   assert.strictEqual(typeof rs.addon[f], 'function', f);
 }

@@ -168,6 +168,34 @@ async function testSkewedFloatKeys(device, rand) {
   for (const b of [keysBuffer, valuesBuffer]) b.destroy();
 }
 
+// Nearly-sorted keys with checkOrder (>= 12M): the presorted path sorts them, and lastPath() names
+// it "presorted" (the addon's path-name table covers every RS_PATH_* value).
+async function testPresortedPath(device, rand) {
+  const n = 12 * 1024 * 1024 + 5;
+  const keys = new Uint32Array(n);
+  for (let i = 0; i < n; i += 1) keys[i] = i * 3;
+  for (let s = 0; s < 2000; s += 1) {   // transpositions of neighbours a few places apart
+    const i = Math.floor(rand() * (n - 8));
+    const j = i + 1 + Math.floor(rand() * 6);
+    const t = keys[i]; keys[i] = keys[j]; keys[j] = t;
+  }
+  const [keysBuffer, keysBufferMapped] = createBuffers(device, keys);
+  const kernel = new RadixSortKernel({ device, data: { keys: keysBuffer }, count: n, bitCount: 32, checkOrder: true });
+  const encoder = device.createCommandEncoder();
+  const pass = encoder.beginComputePass();
+  kernel.dispatch(pass);
+  pass.end();
+  encoder.copyBufferToBuffer(kernel.buffers.keys, 0, keysBufferMapped, 0, n * 4);
+  device.queue.submit([encoder.finish()]);
+  await keysBufferMapped.mapAsync(GPUMapMode.READ);
+  const kr = new Uint32Array(keysBufferMapped.getMappedRange().slice());
+  keysBufferMapped.unmap();
+  assert.strictEqual(kernel.lastPath(), 'presorted');
+  for (let i = 0; i < n; i += 1) assert.strictEqual(kr[i], i * 3, `presorted key @${i}`);
+  kernel.destroy();
+  keysBuffer.destroy();
+}
+
 (async () => {
   const adapter = await gpu.requestAdapter();
   assert.ok(adapter, 'no HIP device');
@@ -178,5 +206,6 @@ async function testSkewedFloatKeys(device, rand) {
   const c = await testTextureSort(device, rand);
   await testPrefixSum(device, rand);
   await testSkewedFloatKeys(device, rand);
-  console.log(`node sort checks ok (${a + b} sort cases, ${c} texture cases, prefix sum, skewed f32 hybrid split)`);
+  await testPresortedPath(device, rand);
+  console.log(`node sort checks ok (${a + b} sort cases, ${c} texture cases, prefix sum, skewed f32 hybrid split, presorted path)`);
 })().catch((e) => { console.error(e); process.exit(1); });

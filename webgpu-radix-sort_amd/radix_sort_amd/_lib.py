@@ -57,7 +57,9 @@ class PlanDebug(ctypes.Structure):
     _fields_ = [("rank", ctypes.c_int32), ("tile", ctypes.c_int32), ("onesweep", ctypes.c_int32),
                 ("msd", ctypes.c_int32), ("keys_cfg", ctypes.c_int32), ("msd_keys_cfg", ctypes.c_int32),
                 ("kbucket_wave", ctypes.c_int32), ("selftest_fail", ctypes.c_int32),
-                ("split", ctypes.c_int32), ("presorted", ctypes.c_int32)]
+                ("split", ctypes.c_int32), ("presorted", ctypes.c_int32),
+                ("xcd", ctypes.c_int32), ("high_half", ctypes.c_int32),
+                ("msd_db", ctypes.c_int32)]
 
 
 # Path overrides applied to every plan the Python wrappers create (tests select kernels with

@@ -659,26 +659,26 @@ def main() -> None:
     elif bk["launches"]:
         extra["path"] = "LSD one-sweep passes (the hybrid MSD path's device-side fallback: skewed keys)"
     if presorted:
-        # the roofline kernel: the order scan, the path's one full read (4 B per key)
+        # the roofline is the whole presorted path (round 6; round 5 named its order scan, a minor
+        # kernel): algorithmic bytes = every key read once by the order scan (4 B) + every element
+        # the merge moved read and written once (16 B with values, 8 keys only), over the path's
+        # time per sort (order scan + the rest, HIP events)
         ck = kernel_ms.get("check", {"ms": 0.0, "launches": 0})
+        ps = kernel_ms.get("presorted", {"ms": 0.0, "launches": 0})
         if ck["launches"]:
-            avg_ms = ck["ms"] / ck["launches"]
-            achieved = n * 4 / (avg_ms / 1e3) / 1e9
+            counts = kernels[last].presorted_counts()
+            path_ms = (ck["ms"] + ps["ms"]) / max(K, 1)
+            alg = n * 4 + counts["moved"] * bytes_per_key
+            achieved = alg / (path_ms / 1e3) / 1e9
             roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                    "kernel": "k_ns_mark (order scan: every key read once, descents and their runs "
-                              "marked; timed with the 16K-pair k_ns_probe before it, ~4 us)",
-                    "avg_launch_ms": round(avg_ms, 4), "algorithmic_bytes_per_launch": n * 4,
+                    "kernel": "the presorted path (order scan k_ns_mark, extraction and its sort, "
+                              "k_ns_merge of the movers): 4 B per key + %d B per moved element" % bytes_per_key,
+                    "avg_launch_ms": round(path_ms, 4), "algorithmic_bytes_per_launch": alg,
+                    "marked": counts["marked"], "moved": counts["moved"],
                     "lib_sha16": _lib_sha16(), "traffic_lib_sha16": None}
-            # PMC traffic of k_ns_mark (tools/r05/pmc_kernels.py), when measured on this very library
-            try:
-                with open(args.traffic_json) as f:
-                    tj = json.load(f).get(args.workload) or {}
-                roof["traffic_lib_sha16"] = tj.get("lib_sha16")
-                if "mark_bytes_per_launch" in tj and tj.get("lib_sha16") == roof["lib_sha16"] and not use_dist:
-                    roof["traffic"] = tj["mark_bytes_per_launch"]
-            except (OSError, ValueError):
-                pass
+            scan_ms = ck["ms"] / ck["launches"]
+            extra["presorted_path"]["order_scan_frac"] = round(n * 4 / (scan_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)
     elif sc["launches"]:
         avg_ms = sc["ms"] / sc["launches"]
         achieved = scatter_keys * bytes_per_key / (avg_ms / 1e3) / 1e9

@@ -196,6 +196,10 @@ enum {
                                      were extracted, sorted and merged back (no radix pass) */
 };
 rs_status rs_plan_last_path(rs_plan* plan, uint32_t* path);
+/* The presorted path of the plan's last sort (waits for it): *marked = the elements its order scan
+ * marked and extracted, *moved = the elements its merge wrote (each read and written once); both 0
+ * when that sort did not take the path (0.6). */
+rs_status rs_plan_presorted_counts(rs_plan* plan, uint64_t* marked, uint64_t* moved);
 /* How deep the hybrid path's last sort split over-full 16-bit buckets (skewed keys, e.g. f32 in
  * [0, 1) or few distinct keys): 0 not at all, 2 by byte 1 (24-bit sub-buckets sorted in LDS), 3 some
  * sub-buckets by byte 0 as well.  Waits for the sort.  Diagnostics: the result never depends on it. */
@@ -245,8 +249,6 @@ typedef struct rs_plan_debug {
     int32_t high_half;      /* test hook: 1 the hybrid path's bucket kernels read records buffers
                                placed at an address whose low 32 bits are >= 2^31 (needs spare plan
                                capacity: n + 2^28 records; RS_ERR_CAPACITY otherwise) (0.6) */
-    int32_t msd_db;         /* hybrid MSD passes with values: 1 double-buffered tiles (the next
-                               tile's loads in flight during the whole tile), 0 single (0.6) */
 } rs_plan_debug;
 rs_status rs_plan_set_debug(rs_plan* plan, const rs_plan_debug* debug);
 void      rs_plan_destroy(rs_plan* plan);     /* frees the workspace (reference quirk Q9) */

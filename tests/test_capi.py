@@ -84,7 +84,7 @@ def test_debug_struct_and_kernel_kinds_match_the_header():
     body = hdr[hdr.index("typedef struct rs_plan_debug"):hdr.index("} rs_plan_debug;")]
     fields = re.findall(r"int32_t\s+(\w+);", body)
     assert [f for f, _ in _lib.PlanDebug._fields_] == fields
-    assert fields[-1] == "msd_db"
+    assert fields[-1] == "high_half"
     assert re.search(r"RS_KERNEL_SPLIT = 6", hdr) and re.search(r"RS_KERNEL_PRESORTED = 7", hdr)
     assert re.search(r"RS_KERNEL_KINDS = 8", hdr)
     assert _lib.RS_KERNEL_KINDS == 8 and _lib.KERNEL_NAMES[_lib.RS_KERNEL_SPLIT] == "split"

@@ -250,3 +250,32 @@ def test_presorted_seeded_random_search():
     print("paths:", paths)
     # the search reaches both sides of the device's decision
     assert paths.count("presorted") >= 3 and len(set(paths) - {"presorted"}) >= 1, paths
+
+
+@pytest.mark.parametrize("n", [15753718, (12 << 20) + 5, 14447713])
+def test_presorted_at_sizes_where_the_probe_overflowed(n):
+    """Sizes at which round 5's probe sampled past the array (tests/test_presorted_probe.py): the
+    nearly-sorted path on all three layouts, word for word against the oracle."""
+    keys = O.nearly_sorted_f32_bits(n, 5)
+    vals = np.arange(n, dtype=np.uint32)
+    ek, ev = O.stable_sort_masked_c(keys, vals, 32)
+    kt, vt = _t(keys), _t(vals)
+    kern = RadixSortKernel(keys=kt, values=vt, count=n, check_order=True)
+    kern.dispatch()
+    kern.check()
+    assert kern.last_path() == "presorted"
+    kern.destroy()
+    assert np.array_equal(_np(kt), ek) and np.array_equal(_np(vt), ev)
+    kt = _t(keys)
+    kern = RadixSortKernel(keys=kt, count=n, check_order=True)
+    kern.dispatch()
+    kern.check()
+    kern.destroy()
+    assert np.array_equal(_np(kt), ek)
+    rt = _t(np.stack([keys, vals], axis=-1).reshape(-1)).view(-1, 2)
+    kern = RadixSortTextureKernel(texture=rt, count=n, check_order=True)
+    kern.dispatch()
+    kern.check()
+    kern.destroy()
+    out = _np(rt).reshape(-1, 2)
+    assert np.array_equal(out[:, 0], ek) and np.array_equal(out[:, 1], ev)

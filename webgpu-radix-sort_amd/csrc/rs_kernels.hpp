@@ -61,6 +61,13 @@
 #define RS_STAGE_BATCH 1     // stage_tile: all slots' offsets read before the staging writes
 #endif
 
+#if !RS_KNOB_OPEN || !defined(RS_MSD_TAILBAR)
+#undef RS_MSD_TAILBAR
+#define RS_MSD_TAILBAR 0     // k_msd_pass: a barrier after the scatter (1: round 5's; 0: none - the next
+                             // writers of the staging area and the digit deltas come after the next
+                             // rank's barriers; 0.962 vs 0.986 ms per pass, profiles/r06/tailbar)
+#endif
+
 #if !RS_KNOB_OPEN || !defined(RS_STAMPS)
 #undef RS_STAMPS
 #define RS_STAMPS 0          // diagnostic build: per-tile phase timestamps of k_onesweep
@@ -1482,6 +1489,8 @@ __global__ __launch_bounds__(1024, 4) void k_msd_pass(
     if (SEG == 1 || XC) asm volatile("" ::"v"(nb16));
     uint32_t Tq = 0;   // thread 0: the next tile's ticket, requested at the top of this tile
     while (T < nt) {
+        RS_STAMP(gate_pass, ntiles, T, 0, __builtin_amdgcn_s_memtime());
+        RS_STAMP(gate_pass, ntiles, T, 7, blockIdx.x);
         if (tid == 0) Tq = claim();
         uint32_t tile0, tend, seg, seg_first;
         geom(T, tile0, tend, seg, seg_first);
@@ -1501,6 +1510,7 @@ __global__ __launch_bounds__(1024, 4) void k_msd_pass(
         uint32_t c;
         const uint32_t tstart = rank_tile<R, NW, KPT, RANK>(k, rank, s_whist, s_scratch, shift, mask,
                                                             (uint32_t)TILE - nvalid, c);
+        RS_STAMP(gate_pass, ntiles, T, 1, __builtin_amdgcn_s_memtime());
         unsigned long long* st = status + (size_t)T * RADIX + tid;
         if (tid < (uint32_t)RADIX) {
             if (first_tile) st_store(st, (epoch << 2) | kStInclusive, s_dbase[tid] + c);
@@ -1508,9 +1518,11 @@ __global__ __launch_bounds__(1024, 4) void k_msd_pass(
             set_wave_offsets<R, NW>(s_whist, tstart);
         }
         __syncthreads();
+        RS_STAMP(gate_pass, ntiles, T, 2, __builtin_amdgcn_s_memtime());
         stage_tile<KPT, true, TILE>(k, v, rank, s_whist[w], nullptr, s_kv, shift, mask, nullptr, 0u, 0u);
         if (tid == 0) s_next = Tq;
         __syncthreads();
+        RS_STAMP(gate_pass, ntiles, T, 3, __builtin_amdgcn_s_memtime());
         const uint32_t Tn = s_next;
         // the look-back's first status words, then the next tile's loads behind them
         const bool lb = tid < (uint32_t)RADIX && !first_tile;
@@ -1562,6 +1574,7 @@ __global__ __launch_bounds__(1024, 4) void k_msd_pass(
             s_gdelta[tid] = excl - tstart;
         }
         __syncthreads();
+        RS_STAMP(gate_pass, ntiles, T, 4, __builtin_amdgcn_s_memtime());
         // the scatter: a fixed KPT stores per thread (staged positions past the tile's end repeat the
         // last record: the same value to the same address), while the next tile's loads arrive
 #pragma unroll
@@ -1578,216 +1591,9 @@ __global__ __launch_bounds__(1024, 4) void k_msd_pass(
                 out_v[pos] = kv.y;
             }
         }
-        __syncthreads();
+        if (RS_MSD_TAILBAR) __syncthreads();
+        RS_STAMP(gate_pass, ntiles, T, 5, __builtin_amdgcn_s_memtime());
         T = Tn;
-    }
-}
-
-// ---- k_msd_pass_db: the MSD pass with the next tile's loads in flight during the whole tile -------
-// k_msd_pass issues tile T+1's loads after staging tile T (its registers are free only then), so
-// tile T+1's rank waits for loads issued a look-back and a scatter earlier, and the HBM pipe idles
-// while T+1 ranks, publishes and stages (~1/3 of a tile: the phase stamps of docs/design_history.md
-// §12).  Here the tile data is double-buffered in registers: tile T+1's loads are issued at the TOP of
-// tile T (tickets are claimed two tiles ahead), so they arrive while T ranks, publishes, stages,
-// walks back and scatters, and T's stores drain while T+1 ranks.  Ranks are kept as 16-bit pairs
-// (tile positions < 2^14) so both tiles' keys and values fit the 128 VGPRs of a 1024-thread
-// workgroup.  Everything else - geometry, pads, rank, publish, local shuffle, look-back, fixed-count
-// scatter - is k_msd_pass's, so the output is the same stable partition.
-template <int L, int LO, int SEG, bool KB = false, int RANK = RANK_LDS_ATOMIC>
-__global__ __launch_bounds__(1024, 4) void k_msd_pass_db(
-    const uint32_t* __restrict__ in_k, const uint32_t* __restrict__ in_v,
-    uint32_t* __restrict__ out_k, uint32_t* __restrict__ out_v, uint32_t n, uint32_t shift,
-    uint32_t ntiles, const uint32_t* __restrict__ dtot, unsigned long long* status,
-    uint32_t* ticket, uint32_t* err, uint32_t epoch, const uint32_t* gate, int gate_pass,
-    uint32_t spin_max, uint32_t* host_err, const uint32_t* __restrict__ segtab,
-    const uint32_t* __restrict__ base16, uint32_t kbase, const uint32_t* = nullptr, uint32_t = 0) {
-    // (the last two: k_msd_pass's XC arguments, unused: one launch signature for both kernels)
-    static_assert(L != LAYOUT_KEYS && LO != LAYOUT_KEYS, "with values");
-    static_assert(SEG == 0 || SEG == 1, "the two MSD passes");
-    constexpr int BLOCK = 1024, KPT = 16, R = 8, RADIX = 256, NW = BLOCK / 64;
-    constexpr int TILE = BLOCK * KPT, WAVE_KEYS = 64 * KPT;
-    constexpr uint32_t mask = RADIX - 1;
-    constexpr uint32_t ESZ = L == LAYOUT_AOS ? 8u : 4u;
-    __shared__ uint32_t s_whist[NW][RADIX];
-    __shared__ uint32_t s_gdelta[RADIX];
-    __shared__ uint32_t s_dbase[RADIX];
-    __shared__ uint32_t s_scratch[NW];
-    __shared__ uint32_t s_next[2];
-    __shared__ uint2 s_kv[TILE];
-    __shared__ uint32_t s_seg[SEG == 1 ? 769 : 1];
-
-    if (gated_off(gate, gate_pass)) return;
-    const uint32_t tid = threadIdx.x, w = tid >> 6, lane = lane_id();
-    if (SEG == 1)
-        for (uint32_t i = tid; i < 769u; i += BLOCK) s_seg[i] = segtab[i];
-    auto claim = [&]() -> uint32_t {
-        uint32_t z = 0;   // (a lane-varying address to the compiler: no wave-aggregated atomic)
-        asm volatile("" : "+v"(z));
-        return atomicAdd(ticket + z, 1u);
-    };
-    {
-        const uint32_t c = (SEG == 0 && tid < (uint32_t)RADIX) ? dtot[tid] : 0u;
-        uint32_t all;
-        const uint32_t ex = block_excl_scan_n<NW>(c, s_scratch, all);
-        if (tid < (uint32_t)RADIX) s_dbase[tid] = ex;
-        if (tid == 0) {
-            s_next[0] = claim();
-            s_next[1] = claim();
-        }
-        __syncthreads();
-    }
-    uint32_t T = s_next[0], Tn = s_next[1];
-    const uint32_t nt = SEG == 1 ? s_seg[SEG == 1 ? 256 : 0] : ntiles;
-    auto geom = [&](uint32_t t, uint32_t& t0, uint32_t& tend, uint32_t& seg, uint32_t& first) {
-        if (SEG == 1) {
-            uint32_t lo = 0, hi = 256;
-            while (hi - lo > 1) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (s_seg[mid] <= t) lo = mid;
-                else hi = mid;
-            }
-            seg = lo;
-            first = s_seg[lo];
-            t0 = s_seg[257 + lo] + (t - first) * (uint32_t)TILE;
-            const uint32_t e = s_seg[513 + lo];
-            tend = e - t0 < (uint32_t)TILE ? e : t0 + (uint32_t)TILE;
-        } else {
-            seg = 0;
-            first = 0;
-            t0 = t * (uint32_t)TILE;
-            tend = (uint64_t)t0 + TILE <= n ? t0 + (uint32_t)TILE : n;
-        }
-    };
-    const uint32_t lofs = (w * (uint32_t)WAVE_KEYS + lane) * ESZ;
-    auto load = [&](uint32_t t, uint32_t (&k)[KPT], uint32_t (&v)[KPT], uint32_t& nb) {
-        uint32_t t0 = 0, tend = 0, sg = 0, fi;
-        if (t < nt) geom(t, t0, tend, sg, fi);
-        const uint32_t nbytes = (tend - t0) * ESZ;
-        uint32_t lo = lofs;
-        asm volatile("" : "+v"(lo));
-        if constexpr (L == LAYOUT_AOS) {
-            const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
-                (void*)(in_k + 2ull * t0), (short)0, (int)nbytes, 0x00020000);
-#pragma unroll
-            for (int j = 0; j < KPT; ++j) {
-                const auto q = __builtin_amdgcn_raw_buffer_load_b64(rr, (int)(lo + j * 64 * 8), 0, 0);
-                k[j] = q[0];
-                v[j] = q[1];
-            }
-        } else {
-            const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(
-                (void*)(in_k + t0), (short)0, (int)nbytes, 0x00020000);
-            const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(
-                (void*)(in_v + t0), (short)0, (int)nbytes, 0x00020000);
-#pragma unroll
-            for (int j = 0; j < KPT; ++j) k[j] = __builtin_amdgcn_raw_buffer_load_b32(rk, (int)(lo + j * 256), 0, 0);
-#pragma unroll
-            for (int j = 0; j < KPT; ++j) v[j] = __builtin_amdgcn_raw_buffer_load_b32(rv, (int)(lo + j * 256), 0, 0);
-        }
-        if (SEG == 1) nb = base16[(sg << 8) | (tid & 255u)];
-    };
-    uint32_t ka[KPT], va[KPT], kb[KPT], vb[KPT];
-    uint32_t nba = 0, nbb = 0;
-    load(T, ka, va, nba);
-    // one tile: (kc, vc) hold tile T (loaded); tile Tn's loads go to (kn, vn) at once
-    auto tile = [&](uint32_t (&kc)[KPT], uint32_t (&vc)[KPT], uint32_t& nbc, uint32_t (&kn)[KPT],
-                    uint32_t (&vn)[KPT], uint32_t& nbn) {
-        load(Tn, kn, vn, nbn);   // in flight during this whole tile
-        uint32_t Tq = 0;
-        if (tid == 0) Tq = claim();   // the tile after Tn (read after staging)
-        uint32_t tile0, tend, seg, seg_first;
-        geom(T, tile0, tend, seg, seg_first);
-        const uint32_t nvalid = tend - tile0;
-        const bool first_tile = T == seg_first;
-        if (SEG == 1 && tid < (uint32_t)RADIX) s_dbase[tid] = s_seg[257 + seg] + nbc;
-        {
-            const uint32_t wb = w * (uint32_t)WAVE_KEYS + lane;
-#pragma unroll
-            for (int j = 0; j < KPT; ++j) {
-                const bool ok = wb + j * 64u < nvalid;
-                kc[j] = ok ? (KB ? kc[j] - kbase : kc[j]) : kPadKey;
-            }
-        }
-        Slots<KPT, true> rank;
-        uint32_t c;
-        const uint32_t tstart = rank_tile<R, NW, KPT, RANK>(kc, rank, s_whist, s_scratch, shift, mask,
-                                                            (uint32_t)TILE - nvalid, c);
-        unsigned long long* st = status + (size_t)T * RADIX + tid;
-        if (tid < (uint32_t)RADIX) {
-            if (first_tile) st_store(st, (epoch << 2) | kStInclusive, s_dbase[tid] + c);
-            else st_store(st, (epoch << 2) | kStAggregate, c);
-            set_wave_offsets<R, NW>(s_whist, tstart);
-        }
-        __syncthreads();
-        stage_tile<KPT, true, TILE>(kc, vc, rank, s_whist[w], nullptr, s_kv, shift, mask, nullptr, 0u, 0u);
-        if (tid == 0) s_next[0] = Tq;
-        __syncthreads();
-        const uint32_t Tnn = s_next[0];
-        if (tid < (uint32_t)RADIX) {
-            uint32_t excl = s_dbase[tid];
-            if (!first_tile) {
-                excl = 0;
-                uint32_t j = T - 1;
-                uint32_t spins = 0;
-                for (;;) {
-                    unsigned long long sv[kLookback];
-#pragma unroll
-                    for (int i = 0; i < kLookback; ++i)
-                        sv[i] = (j >= (uint32_t)i) ? st_load(status + (size_t)(j - i) * RADIX + tid) : 0ull;
-                    uint32_t used = 0;
-                    bool done = false;
-#pragma unroll
-                    for (int i = 0; i < kLookback; ++i) {
-                        if (done || used != (uint32_t)i) break;
-                        const uint32_t f = (uint32_t)(sv[i] >> 32);
-                        if ((f >> 2) != epoch || j < (uint32_t)i) break;
-                        excl += (uint32_t)sv[i];
-                        ++used;
-                        done = (f & 3u) == kStInclusive;
-                    }
-                    if (done) break;
-                    j -= used;
-                    if (used == 0u) {
-                        ++spins;
-                        if (spins > spin_max ||
-                            ((spins & 255u) == 0u &&
-                             __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
-                            atomicOr(err, 1u);
-                            if (host_err)
-                                __hip_atomic_fetch_or(host_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                            break;
-                        }
-                        __builtin_amdgcn_s_sleep(1);
-                    }
-                }
-                st_store(st, (epoch << 2) | kStInclusive, excl + c);
-            }
-            s_gdelta[tid] = excl - tstart;
-        }
-        __syncthreads();
-#pragma unroll
-        for (int j = 0; j < KPT; ++j) {
-            const uint32_t i0 = (uint32_t)j * BLOCK + tid;
-            const uint32_t i = i0 < nvalid ? i0 : nvalid - 1u;
-            const uint2 kv = s_kv[i];
-            uint32_t pos = s_gdelta[(kv.x >> shift) & mask] + i;
-            pos = pos < n ? pos : n - 1u;
-            if constexpr (LO == LAYOUT_AOS) {
-                reinterpret_cast<uint2*>(out_k)[pos] = kv;
-            } else {
-                out_k[pos] = kv.x;
-                out_v[pos] = kv.y;
-            }
-        }
-        // (no barrier here: the next writers of s_kv / s_gdelta / s_whist come after the next
-        // tile's rank barriers)
-        T = Tn;
-        Tn = Tnn;
-    };
-    while (T < nt) {
-        tile(ka, va, nba, kb, vb, nbb);
-        if (T >= nt) break;
-        tile(kb, vb, nbb, ka, va, nba);
     }
 }
 
@@ -2914,11 +2720,8 @@ __global__ __launch_bounds__(BLOCK, MW) void k_bucket_sort(const uint32_t* rec,
         for (; it < nb; it += gridDim.x) {
             cnt = hist16[bucket_of(it)];
             if (cnt == 0u || cnt <= min_cnt) continue;   // empty, or the smaller tile's launch took it
-            if (cnt > (uint32_t)TILE) {                   // the large-tile launch's (or: never, gated)
-                if (over && tid == 0) atomicOr(err, 8u);
-                continue;
-            }
-            break;
+            if (cnt > (uint32_t)TILE) continue;           // the next launch's (listed: the wide kernel's,
+            break;                                        // which flags any bucket over its own tile)
         }
         return it;
     };

@@ -43,7 +43,7 @@ constexpr uint32_t kNsIter = 16;           // marking rounds per tile before giv
 constexpr uint32_t kNsBChunk = 512;        // extracted elements per LDS chunk in the merge
 // control words (ctl): [1] a tile failed, [3] a tile was dense (the path is off), [4] m (marked
 // total), [5] done (the path sorted: the radix path's histogram read is skipped), [8 .. 8 + 16)
-// gate words
+// gate words, [24] the elements the merge moved (rs_plan_presorted_counts)
 constexpr uint32_t kNsCtlWords = 32;
 constexpr uint32_t kNsGate = 8;
 
@@ -64,8 +64,16 @@ __global__ __launch_bounds__(256) void k_ns_probe(const uint32_t* __restrict__ k
                                                   uint32_t* ctl) {
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;   // (grid: kNsProbe / 256)
     const uint64_t step = (uint64_t)(n - 1) / kNsProbe;   // (n >= 12M: step >= 1)
-    // (jittered inside its stride: a periodic pattern in the input must not alias the samples)
-    const uint64_t p = (uint64_t)i * step + ((i * 0x9E3779B9u) >> 8) % step;
+    // (jittered inside its stride: a periodic pattern in the input must not alias the samples).
+    // The jitter is the high word of hash x step - in [0, step) by construction.  Round 5 wrote
+    // ((hash >> 8) % step): both operands provably below 2^24, the compiler expanded the remainder
+    // into its float-reciprocal 24-bit form, whose quotient comes out one too large for some
+    // operands (n = 15753718: 5 of the 16384 samples), and the negative remainder, masked to 24
+    // bits, sent the sample ~2^24 keys past the array: a memory fault whenever that address was
+    // unmapped (tests/test_presorted_gpu.py's seeded search found it; test_probe_sample_positions
+    // pins the arithmetic).
+    const uint64_t jit = ((uint64_t)(i * 0x9E3779B9u) * step) >> 32;
+    const uint64_t p = (uint64_t)i * step + jit;
     uint32_t c = (ns_key<L>(keys, p) & fmask) > (ns_key<L>(keys, p + 1) & fmask) ? 1u : 0u;
     c = wave_sum(c);
     if (lane_id() == 0 && c) atomicAdd(ctl + 7, c);
@@ -605,6 +613,7 @@ __global__ __launch_bounds__(NT) void k_ns_merge(uint32_t* keys, uint32_t* vals,
     };
     Meta cur;
     if (blockIdx.x < ntiles) fetch(blockIdx.x, cur);
+    uint32_t moved = 0;   // elements this thread wrote (added to ctl[24] once, at the end)
     for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
     // (per-slot positions recomputed each tile from an opaque copy of the thread index: hoisted out
     // of the tile loop they take a register each)
@@ -716,7 +725,11 @@ __global__ __launch_bounds__(NT) void k_ns_merge(uint32_t* keys, uint32_t* vals,
     if (tid + NT < cn0) put(obase + r1 + tid + NT, xk1, xv1);
     for (uint32_t jj = b0 + BC + tid; jj < b1; jj += NT)   // (more than one chunk)
         put(obase + rank[jj] + (jj - b0), bk[jj], L == LAYOUT_KEYS ? 0u : bv[jj]);
+    moved += (uint32_t)__popc(mv) + (tid < cn0 ? 1u : 0u) + (tid + NT < cn0 ? 1u : 0u) +
+             (b1 - b0 > BC + tid ? (b1 - b0 - BC - tid + NT - 1u) / NT : 0u);
     }
+    moved = wave_sum(moved);
+    if (lane_id() == 0 && moved) atomicAdd(ctl + 24, moved);
 }
 
 }  // namespace rs

@@ -307,7 +307,6 @@ struct rs_plan {
                                      // (32K-key tiles for pass 0 only: no faster, r03_keys_pass0_tiles_ab)
     bool kbucket_wave = true;        // one wave per 16-bit bucket (rs_plan_debug.kbucket_wave = 0: workgroups)
     bool kbucket_pf = false;         // workgroup kernel on a persistent prefetching grid (sweep: RSORT_KBUCKET_PF=1)
-    bool msd_db = false;             // the MSD passes double-buffered (k_msd_pass_db; rs_plan_debug.msd_db)
     bool high_half = false;          // test hook (rs_plan_debug.high_half): R2 / R3 at a 2^31 low address word
     int xcd_claims = 0;              // hybrid MSD passes with values: XCD-local tile streams (k_msd_pass XC;
                                      // rs_plan_debug.xcd: 0 none (default: XC measured slower, 1.00 / 1.04
@@ -495,10 +494,7 @@ void launch_msd_pass(rs_plan* p, const uint32_t* ik, const uint32_t* iv, uint32_
                                    p->epoch, gate, SEG, p->spin_max, p->host_err_dev, segtab, base16, kbase, cbase,
                                    hrows);
             };
-            if (p->msd_db && !xc) {
-                if (p->rank_mode == rs::RANK_BALLOT) lean(rs::k_msd_pass_db<L, LO, SEG, KB, rs::RANK_BALLOT>);
-                else lean(rs::k_msd_pass_db<L, LO, SEG, KB, rs::RANK_LDS_ATOMIC>);
-            } else if (xc) {
+            if (xc) {
                 if (p->rank_mode == rs::RANK_BALLOT) lean(rs::k_msd_pass<L, LO, SEG, KB, rs::RANK_BALLOT, true>);
                 else lean(rs::k_msd_pass<L, LO, SEG, KB, rs::RANK_LDS_ATOMIC, true>);
             } else {
@@ -1065,8 +1061,11 @@ static rs_status enqueue_split(rs_plan* p, const rs::SplitWs& sw, bool keys, boo
                 constexpr int LO = decltype(lo)::value;
                 // one sub-bucket per workgroup (65536 of them: 256 huge buckets; more are taken
                 // grid-stride), so the hardware overlaps the workgroups' load latencies
+                // (a grid-stride over at most 24 workgroups per CU: gated off - no over-full bucket, the
+                // usual case - 65536 workgroups cost 16 us of dispatch, this grid ~4)
                 auto small = [&](auto kern) {
-                    const uint32_t grid = (uint32_t)std::min<uint64_t>(65536u, 256ull * sw.smax2);
+                    const uint32_t grid = (uint32_t)std::min<uint64_t>(std::min<uint64_t>(65536u, 256ull * sw.smax2),
+                                                                       24ull * p->cus);
                     hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, s, (const uint32_t*)r3, sw, uk, uv);
                 };
                 auto large = [&](auto kern) {   // the sub-buckets the first launch listed
@@ -1569,9 +1568,20 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
         // the wide kernel: every bucket (wide_all), or the listed buckets over the population-sized
         // tile on a small persistent grid (sweep: RSORT_OVER_GRID workgroups)
         const uint32_t over_grid = std::max(1u, (uint32_t)RS_KNOB("RSORT_OVER_GRID", 256));
+        // the listed buckets of at most 1024 x 8 records (at 2^28 uniform keys: the ~2 buckets just
+        // over the primary tile) go to a 1024 x 8 tile first: one such bucket alone on the wide
+        // kernel's 1024 x 34 slots took 0.034 ms, the length of the whole launch (profiles/r06/
+        // xcd_claims); the wide kernel then takes the listed rest (min_cnt = 8192)
+        const bool listed8 = !wide_all && small_cap < 8192u;
+        auto listed = [&](auto kern) {
+            hipLaunchKernelGGL(kern, dim3(over_grid), dim3(1024), 0, s, ring ? ring : r2, hist16, base16, uk, uv,
+                               g_msd, p->tickets + 16, small_cap, (const uint32_t*)over, kbase,
+                               (const uint32_t*)sstart, rmask, b_lo, b_cnt);
+        };
         auto large = [&](auto kern, uint32_t block) {
             hipLaunchKernelGGL(kern, dim3(wide_all ? b_cnt : over_grid), dim3(block), 0, s, ring ? ring : r2,
-                               hist16, base16, uk, uv, g_msd, p->tickets + 16, wide_all ? 0u : small_cap,
+                               hist16, base16, uk, uv, g_msd, p->tickets + 16,
+                               wide_all ? 0u : (listed8 ? 8192u : small_cap),
                                wide_all ? (const uint32_t*)nullptr : (const uint32_t*)over, kbase,
                                (const uint32_t*)sstart, rmask, vbits - 16, b_lo, b_cnt);
         };
@@ -1644,6 +1654,8 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
             // three workgroups per CU, 512 x 34: two, 1024 x 34: one)
             if (big_tile)
                 ballot ? big(rs::k_bucket_sort<1024, 17, B0, LO, 4>) : big(rs::k_bucket_sort<1024, 17, A0, LO, 4>);
+            if (listed8)
+                ballot ? listed(rs::k_bucket_sort<1024, 8, B0, LO, 1>) : listed(rs::k_bucket_sort<1024, 8, A0, LO, 1>);
             // the listed buckets over the primary tile (none for uniform keys), or every bucket
             // (wide_all); keys only: the smallest wide tile that holds the population's buckets
             // (512 x 18: three workgroups per CU, 512 x 34: two, 1024 x 34: one)
@@ -2267,13 +2279,33 @@ RS_EXPORT rs_status rs_plan_set_wait_limit(rs_plan* p, uint32_t sleeps) {
     return RS_OK;
 }
 
+// The presorted path's counts of the plan's last sort (waits for it): marked = the elements the
+// order scan marked and the path extracted, moved = the elements its merge wrote (each read and
+// written once: 16 B with values); both 0 when the last sort did not take the path.
+RS_EXPORT rs_status rs_plan_presorted_counts(rs_plan* p, uint64_t* marked, uint64_t* moved) {
+    if (!p || !marked || !moved) return fail(RS_ERR_INVALID_ARG, "rs_plan_presorted_counts: null argument");
+    *marked = 0;
+    *moved = 0;
+    if (!p->last_ns || !p->ns) return RS_OK;
+    DeviceGuard guard(p->desc.device);
+    if (p->done_recorded) HIP_TRY(hipEventSynchronize(p->done));
+    const NsWs w = ns_layout(p->ns, p->capacity);
+    uint32_t ctl[rs::kNsCtlWords];
+    HIP_TRY(hipMemcpy(ctl, w.ctl, sizeof(ctl), hipMemcpyDeviceToHost));
+    if (ctl[rs::kNsGate]) {   // the path was on
+        *marked = ctl[4];
+        *moved = ctl[24];
+    }
+    return RS_OK;
+}
+
 RS_EXPORT rs_status rs_plan_set_debug(rs_plan* p, const rs_plan_debug* d) {
     if (!p || !d) return fail(RS_ERR_INVALID_ARG, "rs_plan_set_debug: null argument");
     auto tri = [](int32_t v, int hi) { return v >= -1 && v <= hi; };
     if (!tri(d->rank, 1) || !tri(d->tile, 1) || !tri(d->onesweep, 1) || !tri(d->msd, 1) ||
         !tri(d->keys_cfg, 1) || !tri(d->msd_keys_cfg, 2) || !tri(d->kbucket_wave, 1) ||
         !tri(d->selftest_fail, 1) || !tri(d->split, 1) || !tri(d->presorted, 1) || !tri(d->xcd, 3) ||
-        !tri(d->high_half, 1) || !tri(d->msd_db, 1))
+        !tri(d->high_half, 1))
         return fail(RS_ERR_INVALID_ARG, "rs_plan_set_debug: every field must be -1 or a listed choice");
     if (d->selftest_fail == 1) {
         p->selftest = 0;
@@ -2290,7 +2322,6 @@ RS_EXPORT rs_status rs_plan_set_debug(rs_plan* p, const rs_plan_debug* d) {
     if (d->presorted >= 0) p->ns_on = d->presorted == 1;
     if (d->xcd >= 0) p->xcd_claims = d->xcd;
     if (d->high_half >= 0) p->high_half = d->high_half == 1;
-    if (d->msd_db >= 0) p->msd_db = d->msd_db == 1;
     return RS_OK;
 }
 

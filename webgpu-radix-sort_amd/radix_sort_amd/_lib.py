@@ -58,8 +58,7 @@ class PlanDebug(ctypes.Structure):
                 ("msd", ctypes.c_int32), ("keys_cfg", ctypes.c_int32), ("msd_keys_cfg", ctypes.c_int32),
                 ("kbucket_wave", ctypes.c_int32), ("selftest_fail", ctypes.c_int32),
                 ("split", ctypes.c_int32), ("presorted", ctypes.c_int32),
-                ("xcd", ctypes.c_int32), ("high_half", ctypes.c_int32),
-                ("msd_db", ctypes.c_int32)]
+                ("xcd", ctypes.c_int32), ("high_half", ctypes.c_int32)]
 
 
 # Path overrides applied to every plan the Python wrappers create (tests select kernels with
@@ -159,6 +158,7 @@ _SIGS = {
     "rs_plan_set_profiling": (ctypes.c_int, [_VP, ctypes.c_int]),
     "rs_plan_set_profiling_kinds": (ctypes.c_int, [_VP, ctypes.c_uint32]),
     "rs_plan_last_path": (ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_uint32)]),
+    "rs_plan_presorted_counts": (ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
     "rs_plan_last_split": (ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_uint32)]),
     "rs_plan_kernel_times": (ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_double),
                                             ctypes.POINTER(ctypes.c_uint64)]),

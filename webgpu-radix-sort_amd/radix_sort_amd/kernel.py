@@ -266,6 +266,14 @@ class RadixSortKernel:
         check(_lib.load().rs_plan_last_path(self._plan, ctypes.byref(v)), "last_path")
         return _lib.PATH_NAMES[v.value]
 
+    def presorted_counts(self) -> dict:
+        """The presorted path of the last dispatch (waits for it): the elements it marked and the
+        elements its merge moved (rs_plan_presorted_counts); zeros when it did not take the path."""
+        a, b = ctypes.c_uint64(), ctypes.c_uint64()
+        check(_lib.load().rs_plan_presorted_counts(self._plan, ctypes.byref(a), ctypes.byref(b)),
+              "presorted_counts")
+        return {"marked": int(a.value), "moved": int(b.value)}
+
     def last_split(self) -> int:
         """How deep the hybrid path's last dispatch split over-full 16-bit buckets (skewed keys):
         0, 2 (by byte 1) or 3 (some sub-buckets by byte 0 too) (rs_plan_last_split)."""

@@ -68,6 +68,13 @@
                              // rank's barriers; 0.962 vs 0.986 ms per pass, profiles/r06/tailbar)
 #endif
 
+#if !RS_KNOB_OPEN || !defined(RS_MSD_LBLATE)
+#undef RS_MSD_LBLATE
+#define RS_MSD_LBLATE 0      // k_msd_pass: the look-back waves (digits, tid < 256) issue their part of the
+                             // next tile's loads after their look-back, not before (a wave's re-read of
+                             // a status word otherwise waits for all 16 of its tile loads: vmcnt is in order)
+#endif
+
 #if !RS_KNOB_OPEN || !defined(RS_STAMPS)
 #undef RS_STAMPS
 #define RS_STAMPS 0          // diagnostic build: per-tile phase timestamps of k_onesweep
@@ -947,6 +954,10 @@ constexpr uint32_t kStAggregate = 1u, kStInclusive = 2u;
 // tile ahead (RS_AHEAD, within noise), and explicit vmcnt waits so that the next tile's rank runs
 // while this tile's stores drain (0.5 % slower).
 constexpr int kLookback = RS_LOOKBACK;   // predecessors read per look-back step
+#if !RS_KNOB_OPEN || !defined(RS_LB_FIRST)
+#undef RS_LB_FIRST
+#define RS_LB_FIRST RS_LOOKBACK   // k_msd_pass: predecessors read by the first look-back step
+#endif
 
 __device__ __forceinline__ unsigned long long st_load(const unsigned long long* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1526,25 +1537,37 @@ __global__ __launch_bounds__(1024, 4) void k_msd_pass(
         const uint32_t Tn = s_next;
         // the look-back's first status words, then the next tile's loads behind them
         const bool lb = tid < (uint32_t)RADIX && !first_tile;
-        unsigned long long sv[kLookback];
+        // (the first round may read a wider window, RS_LB_FIRST: it is issued before the tile loads)
+        constexpr int KW = RS_LB_FIRST > kLookback ? RS_LB_FIRST : kLookback;
+        unsigned long long sv[KW];
         if (lb) {
 #pragma unroll
-            for (int i = 0; i < kLookback; ++i)
-                sv[i] = (T - 1 >= (uint32_t)i) ? st_load(status + (size_t)(T - 1 - i) * RADIX + tid) : 0ull;
+            for (int i = 0; i < KW; ++i)
+                sv[i] = (i < RS_LB_FIRST && T - 1 >= (uint32_t)i) ? st_load(status + (size_t)(T - 1 - i) * RADIX + tid) : 0ull;
         }
-        load(Tn);
+        if (!RS_MSD_LBLATE || tid >= (uint32_t)RADIX) load(Tn);
         if (tid < (uint32_t)RADIX) {
             uint32_t excl = s_dbase[tid];
             if (lb) {
                 excl = 0;
                 uint32_t j = T - 1;                  // next predecessor to consume
                 uint32_t spins = 0;
+#if RS_STAMPS
+                uint32_t st_rounds = 0;
+#endif
+                int nwin = RS_LB_FIRST;   // this round's window
                 for (;;) {
+#if RS_STAMPS
+                    if (st_rounds++ == 0) {
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                        RS_STAMP(gate_pass, ntiles, T, 8, __builtin_amdgcn_s_memtime());
+                    }
+#endif
                     uint32_t used = 0;
                     bool done = false;
 #pragma unroll
-                    for (int i = 0; i < kLookback; ++i) {
-                        if (done || used != (uint32_t)i) break;
+                    for (int i = 0; i < KW; ++i) {
+                        if (i >= nwin || done || used != (uint32_t)i) break;
                         const uint32_t f = (uint32_t)(sv[i] >> 32);
                         if ((f >> 2) != epoch || j < (uint32_t)i) break;   // not yet published
                         excl += (uint32_t)sv[i];
@@ -1565,14 +1588,21 @@ __global__ __launch_bounds__(1024, 4) void k_msd_pass(
                         }
                         __builtin_amdgcn_s_sleep(1);
                     }
+                    nwin = kLookback;
 #pragma unroll
                     for (int i = 0; i < kLookback; ++i)
                         sv[i] = (j >= (uint32_t)i) ? st_load(status + (size_t)(j - i) * RADIX + tid) : 0ull;
                 }
                 st_store(st, (epoch << 2) | kStInclusive, excl + c);
+#if RS_STAMPS
+                RS_STAMP(gate_pass, ntiles, T, 9, st_rounds);
+                RS_STAMP(gate_pass, ntiles, T, 10, T - 1 - j);
+                RS_STAMP(gate_pass, ntiles, T, 11, spins);
+#endif
             }
             s_gdelta[tid] = excl - tstart;
         }
+        if (RS_MSD_LBLATE && tid < (uint32_t)RADIX) load(Tn);
         __syncthreads();
         RS_STAMP(gate_pass, ntiles, T, 4, __builtin_amdgcn_s_memtime());
         // the scatter: a fixed KPT stores per thread (staged positions past the tile's end repeat the

@@ -75,6 +75,12 @@
                              // a status word otherwise waits for all 16 of its tile loads: vmcnt is in order)
 #endif
 
+#if !RS_KNOB_OPEN || !defined(RS_H16_BATCH)
+#undef RS_H16_BATCH
+#define RS_H16_BATCH 1       // k_hist16_in: a group's adds all issued before their crossing checks
+                             // (with 3 loads per group: 0.232 vs 0.239 ms at config 3, profiles/r06/hist16)
+#endif
+
 #if !RS_KNOB_OPEN || !defined(RS_STAMPS)
 #undef RS_STAMPS
 #define RS_STAMPS 0          // diagnostic build: per-tile phase timestamps of k_onesweep
@@ -1859,7 +1865,7 @@ __global__ __launch_bounds__(1024) void k_hist16_in(const uint32_t* __restrict__
     // loads per thread per group; two groups in flight (the next one issued before this one is counted)
 #if !RS_KNOB_OPEN || !defined(RS_H16_FLY)
 #undef RS_H16_FLY
-#define RS_H16_FLY 6
+#define RS_H16_FLY 3
 #endif
     constexpr uint32_t FLY = CHECK ? 3 : RS_H16_FLY;
     using Vec = typename std::conditional<NARROW, uint2, uint4>::type;
@@ -1969,6 +1975,44 @@ __global__ __launch_bounds__(1024) void k_hist16_in(const uint32_t* __restrict__
         }
     };
     auto count_group = [&](uint64_t g0, const Vec (&q)[FLY]) {
+        if constexpr (FULL && !NARROW && !CHECK && RS_H16_BATCH) {
+            // (whole-range counts, no order check) a group in which no lane holds a load whose keys
+            // share one bucket - random keys: every group - issues all of its adds first and checks
+            // the returned halves for a crossing after: the adds' LDS round trips overlap instead
+            // of one per load (per-load grouping below otherwise)
+            constexpr int M = L == LAYOUT_AOS ? 2 : 4;
+            bool uni_any = false;
+#pragma unroll
+            for (uint32_t u = 0; u < FLY; ++u) {
+                const uint32_t ks[4] = {q[u].x, L == LAYOUT_AOS ? q[u].z : q[u].y, q[u].z, q[u].w};
+                bool uni = true;
+#pragma unroll
+                for (int j = 1; j < M; ++j) uni &= (ks[j] >> 16) == (ks[0] >> 16);
+                uni_any |= uni && g0 + (uint64_t)u * B + tid < nv;
+            }
+            if (__ballot(uni_any) == 0ull) {
+                uint32_t old[FLY * M];
+#pragma unroll
+                for (uint32_t u = 0; u < FLY; ++u) {
+                    const uint32_t ks[4] = {q[u].x, L == LAYOUT_AOS ? q[u].z : q[u].y, q[u].z, q[u].w};
+                    const bool ok = g0 + (uint64_t)u * B + tid < nv;
+#pragma unroll
+                    for (int j = 0; j < M; ++j) {
+                        const uint32_t b = ks[j] >> 16;
+                        old[u * M + j] = ok ? atomicAdd(&h[b >> 1], 1u << ((b & 1u) << 4)) : 0u;
+                    }
+                }
+#pragma unroll
+                for (uint32_t u = 0; u < FLY; ++u) {
+                    const uint32_t ks[4] = {q[u].x, L == LAYOUT_AOS ? q[u].z : q[u].y, q[u].z, q[u].w};
+                    const bool ok = g0 + (uint64_t)u * B + tid < nv;
+#pragma unroll
+                    for (int j = 0; j < M; ++j)
+                        if (ok) take_back(ks[j] >> 16, old[u * M + j], 1u);
+                }
+                return;
+            }
+        }
 #pragma unroll
         for (uint32_t u = 0; u < FLY; ++u) {
             const uint64_t i = g0 + (uint64_t)u * B + tid;

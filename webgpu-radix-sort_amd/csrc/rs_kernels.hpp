@@ -75,6 +75,12 @@
                              // a status word otherwise waits for all 16 of its tile loads: vmcnt is in order)
 #endif
 
+#if !RS_KNOB_OPEN || !defined(RS_OS_TAILBAR)
+#undef RS_OS_TAILBAR
+#define RS_OS_TAILBAR 0      // k_onesweep: a barrier after the last staging round's scatter (0: none,
+                             // config2 0.650 vs 0.654 ms, profiles/r06/ostb)
+#endif
+
 #if !RS_KNOB_OPEN || !defined(RS_H16_BATCH)
 #undef RS_H16_BATCH
 #define RS_H16_BATCH 1       // k_hist16_in: a group's adds all issued before their crossing checks
@@ -1271,7 +1277,10 @@ __global__ __launch_bounds__(BLOCK, pass_min_waves(BLOCK, KPT)) void k_onesweep(
                 scatter_tile<BLOCK, HAS_VALUES, LO>(s_keys, s_kv, s_gdelta, out_k, out_v, n,
                                                     nvalid - lo < (uint32_t)STAGE ? nvalid - lo : (uint32_t)STAGE,
                                                     tile0, shift, mask, lo, pmask);
-            __syncthreads();
+            // (after the last round: no barrier unless RS_OS_TAILBAR - as in k_msd_pass, the next
+            // writers of the staging area, the deltas and the counters come after the next tile's
+            // rank barriers, and the next-pass totals are complete before this tile's scatter)
+            if (h + 1 < SR || RS_OS_TAILBAR) __syncthreads();
         }
         RS_STAMP(pass, ntiles, T, 5, __builtin_amdgcn_s_memtime());
         T = Tn;

@@ -563,8 +563,16 @@ __global__ __launch_bounds__(256) void k_ns_rank(const uint32_t* __restrict__ ke
 // flight per CU), not bytes.  A wave-per-tile form that skips 64-position groups without movement
 // (32 tiles in flight per CU) measured 0.91 ms: its per-slot searches cost more than the latency
 // it hides (round 5, history).
+#if !RS_KNOB_OPEN || !defined(RS_NS_SPEC)
+#undef RS_NS_SPEC
+#define RS_NS_SPEC 0       // k_ns_merge: every slot's element loaded at the top of the tile (movers or not)
+#endif
+#if !RS_KNOB_OPEN || !defined(RS_NS_MINB)
+#undef RS_NS_MINB
+#define RS_NS_MINB 1       // k_ns_merge: workgroups per CU the register budget must allow
+#endif
 template <int L, uint32_t NT = 512>
-__global__ __launch_bounds__(NT) void k_ns_merge(uint32_t* keys, uint32_t* vals, uint32_t n,
+__global__ __launch_bounds__(NT, RS_NS_MINB) void k_ns_merge(uint32_t* keys, uint32_t* vals, uint32_t n,
                                                  const uint32_t* __restrict__ bitmap,
                                                  const uint32_t* __restrict__ toff,
                                                  const uint32_t* __restrict__ coff,
@@ -625,6 +633,39 @@ __global__ __launch_bounds__(NT) void k_ns_merge(uint32_t* keys, uint32_t* vals,
     const uint32_t b0 = cur.b0, b1 = cur.b1, wv = cur.wv, r0 = cur.r0, r1 = cur.r1;
     const uint32_t xk0 = cur.xk0, xv0 = cur.xv0, xk1 = cur.xk1, xv1 = cur.xv1;
     const uint32_t cn0 = b1 - b0 < BC ? b1 - b0 : BC;
+    const uint32_t alo = (uint32_t)(olo - (int64_t)t0 < 0 ? 0 : (olo - (int64_t)t0 > nown ? nown : olo - (int64_t)t0));
+    const uint32_t ahi = (uint32_t)(ohi - (int64_t)t0 < 0 ? 0 : (ohi - (int64_t)t0 > nown ? nown : ohi - (int64_t)t0));
+    uint32_t fk[KPT], fv[KPT];
+    auto read_slot = [&](uint32_t j) {   // slot j's element: own output range in place, else the save
+        const uint32_t i = j * NT + tid;
+        const uint64_t p = t0 + i;
+        if (i >= alo && i < ahi) {
+            if (L == LAYOUT_AOS) {
+                const uint2 q = reinterpret_cast<const uint2*>(keys)[p];
+                fk[j] = q.x;
+                fv[j] = q.y;
+            } else {
+                fk[j] = keys[p];
+                if (L == LAYOUT_SOA) fv[j] = vals[p];
+            }
+        } else {
+            if (L == LAYOUT_KEYS) {
+                fk[j] = tmp[p];
+            } else {
+                const uint2 q = reinterpret_cast<const uint2*>(tmp)[p];
+                fk[j] = q.x;
+                fv[j] = q.y;
+            }
+        }
+    };
+    if (RS_NS_SPEC) {   // every slot of the tile, in flight through the scans and searches below
+#pragma unroll
+        for (uint32_t j = 0; j < KPT; ++j) {
+            fk[j] = 0u;
+            fv[j] = 0u;
+            if (j * NT + tid < nown) read_slot(j);
+        }
+    }
     __syncthreads();   // the previous tile's readers of the LDS arrays are done
     {
         uint32_t nmarked;
@@ -669,37 +710,19 @@ __global__ __launch_bounds__(NT) void k_ns_merge(uint32_t* keys, uint32_t* vals,
     }
     // the movers: read (own output range in place, the rest from tmp, where k_ns_save put them)
     const uint32_t obase = (uint32_t)olo;
-    const uint32_t alo = (uint32_t)(olo - (int64_t)t0 < 0 ? 0 : (olo - (int64_t)t0 > nown ? nown : olo - (int64_t)t0));
-    const uint32_t ahi = (uint32_t)(ohi - (int64_t)t0 < 0 ? 0 : (ohi - (int64_t)t0 > nown ? nown : ohi - (int64_t)t0));
-    uint32_t fk[KPT], fv[KPT], mv = 0;
+    uint32_t mv = 0;
 #pragma unroll
     for (uint32_t j = 0; j < KPT; ++j) {
         const uint32_t i = j * NT + tid;
         const uint32_t o = obase + ao[j] + bef[j];
         ao[j] = o;
-        fk[j] = 0u;
-        fv[j] = 0u;
+        if (!RS_NS_SPEC) {
+            fk[j] = 0u;
+            fv[j] = 0u;
+        }
         if (((valid >> j) & 1u) && o != (uint32_t)t0 + i) {
             mv |= 1u << j;
-            const uint64_t p = t0 + i;
-            if (i >= alo && i < ahi) {
-                if (L == LAYOUT_AOS) {
-                    const uint2 q = reinterpret_cast<const uint2*>(keys)[p];
-                    fk[j] = q.x;
-                    fv[j] = q.y;
-                } else {
-                    fk[j] = keys[p];
-                    if (L == LAYOUT_SOA) fv[j] = vals[p];
-                }
-            } else {
-                if (L == LAYOUT_KEYS) {
-                    fk[j] = tmp[p];
-                } else {
-                    const uint2 q = reinterpret_cast<const uint2*>(tmp)[p];
-                    fk[j] = q.x;
-                    fv[j] = q.y;
-                }
-            }
+            if (!RS_NS_SPEC) read_slot(j);
         }
     }
     // the next tile's loads, in flight while this one writes

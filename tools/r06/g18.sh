@@ -1,0 +1,23 @@
+# Round 6: packed histogram rows (k_hist16_in -> k_hist16_reduce / k_hist16_sum): tests, then A/B
+cd /tmp && export TMPDIR=/tmp; cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out/ab
+E=$PWD/webgpu-radix-sort_amd/lib/exp
+timeout -k 10 600 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu \
+    tests/test_msd_gpu.py tests/test_region_gpu.py tests/test_group_gpu.py tests/test_split_gpu.py \
+    tests/test_presorted_gpu.py tests/test_distributed.py > gpurun_out/ab/packed_tests.log 2>&1 || { tail -30 gpurun_out/ab/packed_tests.log; exit 1; }
+tail -2 gpurun_out/ab/packed_tests.log
+for r in 1 2; do for v in base packed; do
+  L=$E/librsort_$v.so
+  RSORT_LIB=$L timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/ab/pk_${v}_r$r -o p --output-format csv -- python3 bench.py --workload config3 --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/ab/pk_${v}_r$r.json 2> gpurun_out/ab/pk_${v}_r$r.err || exit 1
+  python3 - <<PY
+import csv,glob,json
+d=json.loads(open('gpurun_out/ab/pk_${v}_r$r.json').read().strip().splitlines()[-1]); print('$v', $r, d['ms_per_step'], d['kernel_ms_per_step'])
+f=glob.glob("gpurun_out/ab/pk_${v}_r$r/**/*kernel_stats.csv",recursive=True)[0]
+for r in csv.DictReader(open(f)):
+    if 'hist16' in r["Name"]:
+        print('  ', r["Name"][:50], r["Calls"], round(float(r["AverageNs"])/1e6,4))
+PY
+done; done
+for r in 1 2; do for v in base packed; do
+  RSORT_LIB=$E/librsort_$v.so timeout -k 10 300 python3 bench.py --workload config3 --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/ab/pkb_${v}_r$r.json 2>/dev/null || exit 1
+  python3 -c "import json;d=json.loads(open('gpurun_out/ab/pkb_${v}_r$r.json').read().strip().splitlines()[-1]);print('bench $v',$r,d['ms_per_step'],d['kernel_ms_per_step']['histogram'])"
+done; done

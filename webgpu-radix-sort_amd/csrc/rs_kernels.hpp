@@ -1832,7 +1832,8 @@ __device__ __forceinline__ void set_gate(uint32_t* g, uint32_t v) {
 // ds_add per key and the next loads are issued before the current ones are counted.  (Up to round 4
 // each thread folded its 32 words into 64 registers and cleared them every 60K keys: the folds cost
 // as many LDS operations as the counting, and the 64 registers left one group of loads in flight.)
-// The workgroup's 65536 counts go to rows[blockIdx.x] (k_hist16_reduce adds the rows).
+// The workgroup's 65536 counts go to rows[blockIdx.x] as the packed halves plus the crossing log
+// (kRowEv; k_hist16_reduce / k_hist16_sum add the rows and the logged kHalfT's).
 // Range form (the multi-GPU group sorts): the buckets are of key - kbase >> shift, and a key
 // outside [kbase, kbase + range] sets the workgroup's flag word (rows[gridDim.x * 65536 + block];
 // k_msd_plan then picks the LSD passes over the whole 32-bit keys).  Records load 8 bytes per lane
@@ -1848,6 +1849,8 @@ __device__ __forceinline__ void set_gate(uint32_t* g, uint32_t v) {
 constexpr uint32_t kHalfT = 1u << 15;   // a 16-bit LDS half is brought back under this
 constexpr uint32_t kEvMax = 4096;       // crossings logged per workgroup: chunk / kHalfT at most, so any
                                         // chunk of up to 2^27 keys (n < 2^32 over >= 32 workgroups)
+constexpr uint32_t kRowEv = 32768;      // a row (65536 words): 32768 packed count pairs, then the
+                                        // crossing log (count, buckets)
 template <int L, bool AOS_WIDE = false, bool FULL = false, int CHECK = 0>
 __global__ __launch_bounds__(1024) void k_hist16_in(const uint32_t* __restrict__ keys, uint32_t n,
                                                      uint32_t* __restrict__ rows, uint32_t kbase,
@@ -1878,7 +1881,7 @@ __global__ __launch_bounds__(1024) void k_hist16_in(const uint32_t* __restrict__
 #endif
     constexpr uint32_t FLY = CHECK ? 3 : RS_H16_FLY;
     using Vec = typename std::conditional<NARROW, uint2, uint4>::type;
-    __shared__ uint32_t h[W];
+    __shared__ __attribute__((aligned(16))) uint32_t h[W];
     __shared__ uint32_t s_b0[B0 ? 256 : 1];
     __shared__ uint32_t s_ev[kEvMax];
     __shared__ uint32_t s_nev;
@@ -2097,22 +2100,18 @@ __global__ __launch_bounds__(1024) void k_hist16_in(const uint32_t* __restrict__
         if (__ballot(inverted) != 0ull && lane_id() == 0) atomicOr(inv, 1u);
         if (B0 && tid < 256u) b0rows[(size_t)blockIdx.x * 256u + tid] = s_b0[tid];
     }
-    uint2* row = reinterpret_cast<uint2*>(rows + (size_t)blockIdx.x * 65536u);
+    // the row as counted: the packed halves (half the bytes of 32-bit counts to write here and to read
+    // in the reduction), then the logged crossings (kRowEv: their count, then the buckets, each worth
+    // kHalfT more; the reduction adds them)
+    uint32_t* row = rows + (size_t)blockIdx.x * 65536u;
 #pragma unroll
-    for (uint32_t i = 0; i < PER; ++i) {
-        const uint32_t x = h[tid + B * i];
-        row[tid + B * i] = make_uint2(x & 0xFFFFu, x >> 16);
-    }
-    // the logged crossings: kHalfT more for each, added to the row once every thread's stores have
-    // completed (device-scope atomics after a release fence and the barrier)
+    for (uint32_t i = 0; i < PER / 4; ++i)
+        reinterpret_cast<uint4*>(row)[tid + B * i] = reinterpret_cast<const uint4*>(h)[tid + B * i];
     const uint32_t nev = s_nev;   // uniform (read after the barrier above)
-    if (nev) {
-        if (nev > kEvMax) bad = true;   // (never: the hosts launch chunks of <= 2^27 keys) -> flagged
-        __threadfence();
-        __syncthreads();
-        for (uint32_t e = tid; e < nev && e < kEvMax; e += B)
-            atomicAdd(rows + (size_t)blockIdx.x * 65536u + s_ev[e], kHalfT);
-    }
+    if (nev > kEvMax) bad = true;   // (never: the hosts launch chunks of <= 2^27 keys) -> flagged
+    const uint32_t ne = nev < kEvMax ? nev : kEvMax;
+    if (tid == 0) row[kRowEv] = ne;
+    for (uint32_t e = tid; e < ne; e += B) row[kRowEv + 1u + e] = s_ev[e];
     const int any_bad = __syncthreads_or(bad ? 1 : 0);
     if (tid == 0) rows[(size_t)gridDim.x * 65536u + blockIdx.x] = any_bad ? 1u : 0u;
 }
@@ -2135,6 +2134,9 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
 }
+// PACKED: k_hist16_in's rows (packed halves + crossing log, kRowEv); else rows of 65536 32-bit counts
+// (a multi-GPU region's table, k_region_rows).
+template <bool PACKED>
 __global__ __launch_bounds__(1024) void k_hist16_reduce(const uint32_t* __restrict__ rows, uint32_t nrows,
                                                          uint32_t* __restrict__ hist16,
                                                          uint32_t* __restrict__ top_tot,
@@ -2171,8 +2173,19 @@ __global__ __launch_bounds__(1024) void k_hist16_reduce(const uint32_t* __restri
         const int bad = __syncthreads_or(tid < nrows && rows[(size_t)nrows * 65536u + tid] != 0u);
         if (tid == 0) *range_bad = bad ? 1u : 0u;
     }
+    // lane c: buckets 4c .. 4c + 3 of this top byte (PACKED: two packed words)
     const uint4* r4 = reinterpret_cast<const uint4*>(rows) + (size_t)blockIdx.x * 64u + c;
-    constexpr size_t RS = 65536 / 4;    // row stride in 16-byte words
+    const uint2* r2 = reinterpret_cast<const uint2*>(rows) + (size_t)blockIdx.x * 64u + c;
+    constexpr size_t RS = PACKED ? 65536 / 2 : 65536 / 4;    // row stride in 8- / 16-byte words
+    auto ld = [&](uint32_t row) -> uint4 {
+        if constexpr (PACKED) {
+            const uint2 x = r2[row * RS];
+            return make_uint4(x.x & 0xFFFFu, x.x >> 16, x.y & 0xFFFFu, x.y >> 16);
+        } else {
+            return r4[row * RS];
+        }
+    };
+    __shared__ uint32_t s_extra[PACKED ? 256 : 1];
     uint4 a = make_uint4(0u, 0u, 0u, 0u);
     auto add = [](uint4& x, const uint4 y) { x.x += y.x; x.y += y.y; x.z += y.z; x.w += y.w; };
     // wave g holds one row's 256 buckets of this top byte at a time: their sum is the row's
@@ -2185,16 +2198,32 @@ __global__ __launch_bounds__(1024) void k_hist16_reduce(const uint32_t* __restri
     };
     uint32_t r = g;
     for (; r + 48u < nrows; r += 64u) {
-        const uint4 q0 = r4[r * RS], q1 = r4[(r + 16u) * RS], q2 = r4[(r + 32u) * RS], q3 = r4[(r + 48u) * RS];
+        const uint4 q0 = ld(r), q1 = ld(r + 16u), q2 = ld(r + 32u), q3 = ld(r + 48u);
         add(a, q0); add(a, q1); add(a, q2); add(a, q3);
         rowsum(r, q0); rowsum(r + 16u, q1); rowsum(r + 32u, q2); rowsum(r + 48u, q3);
     }
     for (; r < nrows; r += 16u) {
-        const uint4 q = r4[r * RS];
+        const uint4 q = ld(r);
         add(a, q);
         rowsum(r, q);
     }
     s_part[g][c] = a;
+    if constexpr (PACKED) {
+        // the rows' logged crossings of this top byte: kHalfT more each (uniform keys: none)
+        if (tid < 256u) s_extra[tid] = 0u;
+        __syncthreads();
+        if (tid < nrows) {
+            const uint32_t* ev = rows + (size_t)tid * 65536u + kRowEv;
+            const uint32_t ne = ev[0];
+            for (uint32_t e = 0; e < ne; ++e) {
+                const uint32_t b = ev[1u + e];
+                if ((b >> 8) == blockIdx.x) {
+                    atomicAdd(&s_extra[b & 255u], kHalfT);
+                    if (cbase) s_rowsum[tid] += kHalfT;
+                }
+            }
+        }
+    }
     __syncthreads();
     if (cbase) {   // exclusive scan of the row sums (uniform branch: every thread takes part)
         uint32_t tot;
@@ -2205,6 +2234,8 @@ __global__ __launch_bounds__(1024) void k_hist16_reduce(const uint32_t* __restri
         uint4 t = s_part[0][tid];
 #pragma unroll
         for (int j = 1; j < 16; ++j) add(t, s_part[j][tid]);
+        if constexpr (PACKED)
+            add(t, make_uint4(s_extra[4u * tid], s_extra[4u * tid + 1u], s_extra[4u * tid + 2u], s_extra[4u * tid + 3u]));
         reinterpret_cast<uint4*>(hist16)[blockIdx.x * 64u + tid] = t;
         const uint32_t s4 = t.x + t.y + t.z + t.w;
         const uint32_t inc = wave_incl_scan(s4);
@@ -2238,7 +2269,12 @@ __global__ __launch_bounds__(256) void k_hist16_sum(const uint32_t* __restrict__
     __shared__ uint32_t s_scratch[kWaves];
     const uint32_t b = blockIdx.x * 256u + threadIdx.x;
     uint32_t c = 0;
-    for (uint32_t r = 0; r < nrows; ++r) c += rows[(size_t)r * 65536u + b];
+    for (uint32_t r = 0; r < nrows; ++r) {   // packed halves + the logged crossings (k_hist16_in)
+        const uint32_t* row = rows + (size_t)r * 65536u;
+        c += (row[b >> 1] >> ((b & 1u) << 4)) & 0xFFFFu;
+        const uint32_t ne = row[kRowEv];
+        for (uint32_t e = 0; e < ne; ++e) c += row[kRowEv + 1u + e] == b ? kHalfT : 0u;
+    }
     out[b] = c;
     uint32_t tot;
     block_excl_scan(c, s_scratch, tot);

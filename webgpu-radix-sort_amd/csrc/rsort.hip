@@ -1407,7 +1407,7 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
         if (region) {   // the senders counted: one row, their table
             hipLaunchKernelGGL(rs::k_region_rows, dim3(256), dim3(256), 0, s, region_hist, p->tmp_k, over, big,
                                sw.huge);
-            hipLaunchKernelGGL(rs::k_hist16_reduce, dim3(256), dim3(1024), 0, s, (const uint32_t*)p->tmp_k,
+            hipLaunchKernelGGL(rs::k_hist16_reduce<false>, dim3(256), dim3(1024), 0, s, (const uint32_t*)p->tmp_k,
                                1u, hist16, top_tot, range_bad, base16, small_cap, kBucketCap, over, big,
                                p->ptot, (uint32_t)(rs::kTotalsMax + kTicketWords), (const uint32_t*)nullptr,
                                (uint32_t*)nullptr, sw.huge, p->smax2);
@@ -1439,7 +1439,7 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
         }
         // the reduction also lays out every top byte's buckets (bases inside the segment, the
         // overflow list, the oversize flag): the plan kernel is left with the 256 segments
-        hipLaunchKernelGGL(rs::k_hist16_reduce, dim3(256), dim3(1024), 0, s, (const uint32_t*)p->tmp_k,
+        hipLaunchKernelGGL(rs::k_hist16_reduce<true>, dim3(256), dim3(1024), 0, s, (const uint32_t*)p->tmp_k,
                            hrows, hist16, top_tot, range_bad, base16, small_cap, kBucketCap, over, big,
                            p->ptot, (uint32_t)(rs::kTotalsMax + kTicketWords), (const uint32_t*)b0rows,
                            (static_p0 || xc_cbase) ? cbase : (uint32_t*)nullptr, sw.huge, p->smax2, ns_skip);

@@ -174,8 +174,10 @@ rs_status rs_plan_sort_records_range(rs_plan* plan, const void* records, void* k
  * d_hist16 (device, 65536 u32) = the region's count per 16-bit bucket, 0 outside
  * [top_lo << 8, top_hi << 8).  The top-byte pass is the senders' partition, so the region takes
  * only the next-byte pass (per top-byte segment) and the in-LDS bucket sort; a bucket larger than
- * the bucket tile, or counts that do not add up to n, make the device sort the region with the
- * LSD passes instead (the result is always the stable sort).  records[] is only read. */
+ * the largest bucket tile is split on the device (the bucket split).  A table that does not describe
+ * the records (counts that do not add up to n, counts outside [top_lo, top_hi)) is reported as
+ * RS_ERR_DEVICE by rs_plan_check / the next call; with the split off (rs_plan_debug.split = 0) the
+ * device sorts such a region with the LSD passes instead.  records[] is only read. */
 #define RS_HIST16_WORDS 65792u
 rs_status rs_plan_hist16(rs_plan* plan, const void* keys, uint64_t n, void* d_hist16, void* stream);
 rs_status rs_plan_sort_region(rs_plan* plan, const void* records, void* keys_out, void* values_out,

@@ -127,3 +127,36 @@ def test_whole_sort_buckets_at_high_addresses(plan_debug):
     finally:
         plan.destroy()
     assert (kt.cpu().numpy().view(np.uint32) == ek).all() and (vt.cpu().numpy().view(np.uint32) == ev).all()
+
+
+# ---- a table that does not describe the region (round 6) ----------------------------------------
+@pytest.mark.gpu
+@pytest.mark.parametrize("split", [1, 0])
+def test_region_table_mismatch(plan_debug, split):
+    """Counts that do not add up to n: with the bucket split (the default) no LSD fallback is enqueued
+    and the plan check reports a device error; with the split off the device sorts the region with
+    the LSD passes (the stable sort, as before round 6)."""
+    from radix_sort_amd._lib import RS_ERR_DEVICE, RadixSortError
+    keys, vals, hist = _region(3900, 0x21, 1, seed=99)
+    hist[(0x21 << 8) + 11] += 5           # five records the region does not hold
+    n = keys.size
+    rec = keys.astype(np.uint64) | (vals.astype(np.uint64) << np.uint64(32))
+    rt = torch.from_numpy(rec.view(np.int64)).cuda()
+    ht = torch.from_numpy(hist).cuda()
+    ok = torch.empty(n, dtype=torch.int32, device="cuda")
+    ov = torch.empty(n, dtype=torch.int32, device="cuda")
+    plan_debug(split=split)
+    plan = SortPlan(0, max(n, 13 << 20), True)
+    try:
+        plan.sort_region(rt, ok, ov, n, ht, 0x21, 0x22)
+        if split:
+            with pytest.raises(RadixSortError) as ei:
+                plan.check()
+            assert ei.value.status == RS_ERR_DEVICE
+            return
+        plan.check()
+    finally:
+        plan.destroy()
+    ek, ev = O.stable_sort_masked(keys, vals, 32)
+    assert (ok.cpu().numpy().view(np.uint32) == ek).all()
+    assert (ov.cpu().numpy().view(np.uint32) == ev).all()

@@ -47,7 +47,8 @@ def main():
             ops.fill_iota_u32(v)
         kern.dispatch()
     torch.cuda.synchronize()
-    assert ops.is_sorted(k)
+    # (RS_PROF_NOCHECK=1: a traffic-attribution build whose passes do not sort, rs_kernels.hpp RS_DIAG_*)
+    assert os.environ.get("RS_PROF_NOCHECK") == "1" or ops.is_sorted(k)
     print(f"prof_driver: {reps} sorts of {name} done")
 
 

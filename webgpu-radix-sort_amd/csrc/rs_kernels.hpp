@@ -75,6 +75,19 @@
                              // a status word otherwise waits for all 16 of its tile loads: vmcnt is in order)
 #endif
 
+// Traffic attribution (sweep builds only; the output is then NOT sorted - tools/pmc_traffic.py
+// with RS_PROF_NOCHECK): RS_DIAG_LB = 1 - no look-back status reads (every tile scatters as if it
+// were its segment's first); RS_DIAG_SEQ = 1 - every record is written to its own input position
+// (no digit runs, so no partial lines at run seams).  The pass kernels k_onesweep / k_msd_pass.
+#if !RS_KNOB_OPEN || !defined(RS_DIAG_LB)
+#undef RS_DIAG_LB
+#define RS_DIAG_LB 0
+#endif
+#if !RS_KNOB_OPEN || !defined(RS_DIAG_SEQ)
+#undef RS_DIAG_SEQ
+#define RS_DIAG_SEQ 0
+#endif
+
 #if !RS_KNOB_OPEN || !defined(RS_OS_TAILBAR)
 #undef RS_OS_TAILBAR
 #define RS_OS_TAILBAR 0      // k_onesweep: a barrier after the last staging round's scatter (0: none,
@@ -734,8 +747,7 @@ __device__ __forceinline__ void scatter_tile(const uint32_t* s_keys, const uint2
         } else {
             key = s_keys[i];
         }
-        const uint32_t pos = s_gdelta[(key >> shift) & mask] + pbase + i;
-        (void)tile0;
+        const uint32_t pos = RS_DIAG_SEQ ? tile0 + pbase + i : s_gdelta[(key >> shift) & mask] + pbase + i;
         if (pos < n) {  // never false for consistent offsets; keeps a bug from faulting
             const uint32_t q = pos & pmask;
             if (LO == LAYOUT_AOS) {
@@ -1194,7 +1206,7 @@ __global__ __launch_bounds__(BLOCK, pass_min_waves(BLOCK, KPT)) void k_onesweep(
         if (SR == 1 && Tn < nt) load(Tn);
         if (tid < (uint32_t)RADIX) {
             uint32_t excl = s_dbase[tid];
-            if (!first_tile) {
+            if (!first_tile && !RS_DIAG_LB) {
                 // windowed look-back: kLookback predecessors loaded at once, consumed in order
                 // (aggregates summed) up to the first inclusive prefix; a not-yet-published
                 // word stops the window and is re-read next round
@@ -1551,7 +1563,7 @@ __global__ __launch_bounds__(1024, 4) void k_msd_pass(
         RS_STAMP(gate_pass, ntiles, T, 3, __builtin_amdgcn_s_memtime());
         const uint32_t Tn = s_next;
         // the look-back's first status words, then the next tile's loads behind them
-        const bool lb = tid < (uint32_t)RADIX && !first_tile;
+        const bool lb = tid < (uint32_t)RADIX && !first_tile && !RS_DIAG_LB;
         // (the first round may read a wider window, RS_LB_FIRST: it is issued before the tile loads)
         constexpr int KW = RS_LB_FIRST > kLookback ? RS_LB_FIRST : kLookback;
         unsigned long long sv[KW];
@@ -1627,7 +1639,7 @@ __global__ __launch_bounds__(1024, 4) void k_msd_pass(
             const uint32_t i0 = (uint32_t)j * BLOCK + tid;
             const uint32_t i = i0 < nvalid ? i0 : nvalid - 1u;
             const uint2 kv = s_kv[i];
-            uint32_t pos = s_gdelta[(kv.x >> shift) & mask] + i;
+            uint32_t pos = RS_DIAG_SEQ ? tile0 + i : s_gdelta[(kv.x >> shift) & mask] + i;
             pos = pos < n ? pos : n - 1u;   // never clamps for consistent offsets (no fault on a bug)
             if constexpr (LO == LAYOUT_AOS) {
                 reinterpret_cast<uint2*>(out_k)[pos] = kv;   // (KB: the range-relative key)
@@ -2269,11 +2281,20 @@ __global__ __launch_bounds__(256) void k_hist16_sum(const uint32_t* __restrict__
     __shared__ uint32_t s_scratch[kWaves];
     const uint32_t b = blockIdx.x * 256u + threadIdx.x;
     uint32_t c = 0;
-    for (uint32_t r = 0; r < nrows; ++r) {   // packed halves + the logged crossings (k_hist16_in)
-        const uint32_t* row = rows + (size_t)r * 65536u;
-        c += (row[b >> 1] >> ((b & 1u) << 4)) & 0xFFFFu;
-        const uint32_t ne = row[kRowEv];
-        for (uint32_t e = 0; e < ne; ++e) c += row[kRowEv + 1u + e] == b ? kHalfT : 0u;
+    // the packed halves (independent loads, unrolled), then the logged crossings of the rows that
+    // have any (k_hist16_in; uniform keys: none)
+#pragma unroll 8
+    for (uint32_t r = 0; r < nrows; ++r)
+        c += (rows[(size_t)r * 65536u + (b >> 1)] >> ((b & 1u) << 4)) & 0xFFFFu;
+    for (uint32_t r0 = 0; r0 < nrows; r0 += 256u) {
+        const uint32_t r = r0 + threadIdx.x;
+        const bool any = __syncthreads_or(r < nrows && rows[(size_t)r * 65536u + kRowEv] != 0u);
+        if (!any) continue;   // (uniform)
+        for (uint32_t q = r0; q < nrows && q < r0 + 256u; ++q) {
+            const uint32_t* ev = rows + (size_t)q * 65536u + kRowEv;
+            const uint32_t ne = ev[0];
+            for (uint32_t e = 0; e < ne; ++e) c += ev[1u + e] == b ? kHalfT : 0u;
+        }
     }
     out[b] = c;
     uint32_t tot;

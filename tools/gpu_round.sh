@@ -27,4 +27,6 @@ step 11 && { timeout -k 10 400 python3 bench.py --gpus 2 --share-gpu --keys-per-
 # webgpu-radix-sort_amd/csrc asan; the binary and the asan library must not be gpurun-ignored
 # for this step)
 step 12 && { ASAN_OPTIONS=halt_on_error=1 LSAN_OPTIONS=suppressions=tools/lsan.supp:print_suppressions=1 UBSAN_OPTIONS=halt_on_error=1:print_stacktrace=1 timeout -k 10 400 ./tools/asan_driver > gpurun_out/asan_driver.log 2>&1 || exit 22; }
+# SQ / TCC counters per kernel (config 3 and a multi-GPU receiver's regions), one --pmc pass per group
+step 13 && { for w in config3 region; do timeout -k 10 600 python3 tools/pmc_sq.py $w gpurun_out/pmc_sq_$w > gpurun_out/pmc_sq_$w.log 2>&1 || exit 23; done; }
 exit 0

@@ -1401,7 +1401,8 @@ static rs_status enqueue_sort_msd(rs_plan* p, const uint32_t* sk, const uint32_t
     // check_order: the presorted path first (nearly-sorted input is sorted there; the histogram
     // read is then skipped and finds nothing to do)
     const uint32_t* ns_skip = nullptr;
-    if (chk && p->ns && p->ns_on) {
+    if (chk && p->ns && p->ns_on && n <= ns_keys(p->capacity)) {   // (the LSD caller's pre-check: an
+        // input over the workspace skips the optional path instead of failing the sort)
         if (rs_status st = enqueue_presorted(p, uk, uv, n32, s)) return st;
         ns_skip = p->ns + 5;
     }

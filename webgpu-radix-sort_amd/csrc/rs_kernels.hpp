@@ -579,8 +579,13 @@ __device__ __forceinline__ void count_slots(const uint32_t (&k)[KPT], uint32_t* 
 }
 
 // Stable in-wave ranks of the KPT slots (see RankMode); counters in `whist` (this wave's row).
-// Every slot is ranked (pads included, see kPadKey).
-template <int R, int KPT, int RANK, class RK>
+// Every slot is ranked (pads included, see kPadKey).  PR: a slot holding pads (kPadKey: the
+// bucket's tail, lanes in a row with one digit) is ranked by runs - one add per run instead of up
+// to 64 returning adds to one address, which the LDS serialises.  Measured (profiles/r06/pad_runs):
+// the keys-only wave bucket sort 0.183 -> 0.161 ms (its 1152-key tile holds ~128 pads: two slots);
+// the KV bucket sort and the pass kernels slower (the per-slot test costs more than their pads), so
+// only the wave bucket sort sets it.
+template <int R, int KPT, int RANK, bool PR = false, class RK>
 __device__ __forceinline__ void rank_slots(const uint32_t (&k)[KPT], RK& rank,
                                            uint32_t* whist, uint32_t shift, uint32_t mask) {
     const uint32_t lane = lane_id();
@@ -595,7 +600,10 @@ __device__ __forceinline__ void rank_slots(const uint32_t (&k)[KPT], RK& rank,
         } else {
 #pragma unroll
             for (int j = 0; j < KPT; ++j) {
-                const uint32_t r = atomicAdd(&whist[(k[j] >> shift) & mask], 1u);
+                const uint32_t d = (k[j] >> shift) & mask;
+                uint32_t r;
+                if (PR && __ballot(k[j] == kPadKey) != 0ull) r = rank_add_runs(whist, d);
+                else r = atomicAdd(&whist[d], 1u);
                 if (j & 1) rank.set2(j - 1, rank.get(j - 1), r);
                 else rank.set(j, r);
             }
@@ -3179,7 +3187,7 @@ __global__ __launch_bounds__(64 * WPB, MW) void k_bucket_sort_keys_wave(uint32_t
             for (int i = 0; i < 4; ++i) h[lane * 4 + i] = 0u;
             wave_sync();
             Slots<KPT, RS_KWAVE_PACK != 0> rank;
-            rank_slots<8, KPT, RANK>(k, rank, h, shift, 255u);
+            rank_slots<8, KPT, RANK, true>(k, rank, h, shift, 255u);   // (its ~128 pads by runs)
             wave_sync();
             // exclusive scan of the 256 counters: lane l owns digits 4l .. 4l + 3
             const uint4 c = *reinterpret_cast<const uint4*>(h + lane * 4);
